@@ -1,0 +1,218 @@
+"""Headline benchmark: GRF kernel matrices / s on a 100k-node, 1M-edge graph, m = 128.
+
+One step = one full pass of the hot path with the adjacency CSR already resident
+in HBM: normalised Laplacian -> 12.8M Philox random walks (L = 8, p_halt = 0.1)
+-> Phi = sum_l f_l M_l (diffusion modulator, beta = 1) -> K = Phi Phi^T as a
+dense float32 N x N matrix in HBM (40 GB at N = 100k).  With --gpus N (launched
+by torch.distributed.run) every rank walks its source range, the Phi rows are
+all-gathered over RCCL and each rank writes its row block of K (strong scaling:
+one K per step for the whole job).
+
+Prints ONE JSON line on rank 0 (contract in the task description) with a
+`roofline` object for the dominant kernel (gram_sparse) and a `cpu_baseline`
+object (the C oracle -- a restatement of the reference's CPU algorithm -- on the
+host cores, bounded sample, extrapolated; rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import scipy.sparse as sp
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "efficient-gaussian-process-on-graphs_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def er_graph_exact_edges(n: int, n_edges: int, seed: int = 0) -> sp.csr_matrix:
+    """Undirected Erdos-Renyi graph with exactly n_edges distinct edges, unit weights, no self-loops."""
+    rng = np.random.default_rng(seed)
+    keys = np.empty(0, np.int64)
+    while keys.size < n_edges:
+        k = n_edges - keys.size
+        u = rng.integers(0, n, int(k * 1.2) + 16)
+        v = rng.integers(0, n, int(k * 1.2) + 16)
+        lo, hi = np.minimum(u, v), np.maximum(u, v)
+        cand = (lo * n + hi)[lo != hi]
+        keys = np.concatenate([keys, cand])
+        _, first = np.unique(keys, return_index=True)
+        keys = keys[np.sort(first)]
+    keys = keys[:n_edges]
+    u, v = keys // n, keys % n
+    A = sp.coo_matrix((np.ones(2 * n_edges), (np.r_[u, v], np.r_[v, u])), shape=(n, n)).tocsr()
+    A.sort_indices()
+    return A
+
+
+def diffusion_modulator(L: int, beta: float = 1.0) -> np.ndarray:
+    import math
+    return np.array([(-beta) ** l / (2 ** l * math.factorial(l)) for l in range(L)])
+
+
+def cpu_baseline(A, f, m, p, L, budget_rows: int, n_threads: int):
+    """Reference algorithm on the host (C oracle, PCG64 reference stream), bounded sample."""
+    from oracle import oracle as O
+
+    n = A.shape[0]
+    t0 = time.perf_counter()
+    Ls, _ = O.laplacian_sparse(A)
+    t1 = time.perf_counter()
+    ip, ix, dx = O._csr_arrays(Ls)
+    node, load = O.walk_slots(ip, ix, dx, m, p, L, rng=O.RNG_PCG64, n_chunks=n_threads, seed=42,
+                              n_threads=n_threads)
+    t2 = time.perf_counter()
+    mats = O.reduce_steps(node, load, O.NORM_MUL_RECIP, n_threads=n_threads)
+    del node, load
+    phi = O.phi_sparse(mats, f, n_threads=n_threads)
+    del mats
+    t3 = time.perf_counter()
+    rows = min(budget_rows, n)
+    O.gram_rows(phi, 0, rows, n_threads=n_threads)
+    t4 = time.perf_counter()
+    t_full = (t1 - t0) + (t2 - t1) + (t3 - t2) + (t4 - t3) * n / rows
+    return {
+        "value": 1.0 / t_full,
+        "unit": "K-matrices/s",
+        "cores": n_threads,
+        "kind": "port",
+        "sample": (f"C oracle (reference algorithm: PCG64 stream, {n_threads} chunks) on {n_threads} host threads: "
+                   f"full Laplacian+walks+step reduction+Phi ({t3 - t0:.2f} s) + K rows 0..{rows} "
+                   f"({t4 - t3:.2f} s) extrapolated x{n / rows:.1f} to all {n} rows; fp64"),
+        "stages_s": {"laplacian": t1 - t0, "walks": t2 - t1, "phi": t3 - t2, "gram_extrapolated": (t4 - t3) * n / rows},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--edges", type=int, default=1_000_000)
+    ap.add_argument("--walks", type=int, default=128)
+    ap.add_argument("--length", type=int, default=8)
+    ap.add_argument("--p-halt", type=float, default=0.1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=2048)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from grf_amd import _lib as C
+    from grf_amd.dist import allgather_csr_rows, shard_range
+    from grf_amd.engine import DeviceCSR, GRFEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    eng = GRFEngine(f"cuda:{local_rank}")
+    dev = eng.device
+
+    n, m, L, p = args.n, args.walks, args.length, args.p_halt
+    A = er_graph_exact_edges(n, args.edges, seed=0)
+    f = diffusion_modulator(L, 1.0)
+    A_dev = DeviceCSR.from_scipy(A, dev)
+    b, e = shard_range(n, rank, world)
+    ldk = eng.leading_dim(n)
+    K = torch.empty((e - b, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    gram_ms = []
+    nnz_phi = [0]
+
+    def step(record: bool):
+        G = eng.laplacian(A_dev)
+        slots = eng.walk(G, m, p, L, rng=C.RNG_PHILOX, seed=42, src_begin=b, src_end=e)
+        local = eng.compact(eng.features(slots, f), want64=False, want32=True)
+        del slots
+        if world > 1:
+            ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32)
+            phi = DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))
+        else:
+            phi = DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
+        tr = eng.transpose_banded(phi)
+        if record:
+            ev[0].record()
+        eng.gram_sparse(phi, tr, b, e, out=K)
+        if record:
+            ev[1].record()
+            ev[1].synchronize()
+            gram_ms.append(ev[0].elapsed_time(ev[1]))
+        nnz_phi[0] = phi.nnz
+        local_nnz = local.nnz
+        return local_nnz
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    local_nnz = 0
+    for _ in range(args.steps):
+        local_nnz = step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+        gm = torch.tensor([float(np.mean(gram_ms))], dtype=torch.float64, device=dev)
+        dist.all_reduce(gm, op=dist.ReduceOp.MAX)
+        gram_avg = float(gm.item())
+    else:
+        gram_avg = float(np.mean(gram_ms))
+
+    ms_per_step = 1000.0 * t / args.steps
+    # algorithmic bytes of one gram_sparse launch: write this rank's K rows once, read
+    # its Phi rows (col int32 + val fp32) and every Phi^T entry at least once
+    rows = e - b
+    alg_bytes = 4.0 * rows * n + 8.0 * local_nnz + 8.0 * nnz_phi[0]
+    achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
+    out = {
+        "metric": "GRF kernel-matrices/sec (N=100k graph, m=128 walks; + achieved HBM GB/s of the Gram kernel)",
+        "value": args.steps / t,
+        "unit": "K-matrices/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp64 walks/Phi, fp32 K",
+        "data": "synthetic Erdos-Renyi graph (seed 0), unit weights",
+        "config": {"workload": f"C4: ER N={n}, {args.edges} undirected edges, walks_per_node={m}, "
+                               f"max_walk_length={L}, p_halt={p}, diffusion modulator beta=1, Philox seed 42, "
+                               f"dense fp32 K resident in HBM",
+                   "n_nodes": n, "n_edges": args.edges, "walks_per_node": m, "max_walk_length": L,
+                   "parallelism": f"source-sharded x{world}, Phi all-gather, K row blocks"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "gram_sparse_kernel", "kernel_ms": gram_avg, "algorithmic_bytes": alg_bytes},
+        "nnz_phi": nnz_phi[0],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(A, f, m, p, L, args.cpu_rows, threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

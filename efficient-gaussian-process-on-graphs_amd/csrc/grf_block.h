@@ -1,0 +1,72 @@
+// grf_block.h -- wave64 / workgroup primitives (scan, bitonic sort) for gfx950.
+#pragma once
+#include "grf_common.h"
+
+namespace grf {
+
+// inclusive scan across the 64 lanes of a wave
+template <typename T>
+__device__ inline T wave_inclusive_scan(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        T o = __shfl_up(v, off, 64);
+        if (lane >= off) v += o;
+    }
+    return v;
+}
+
+template <typename T>
+__device__ inline T wave_sum(T v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Exclusive scan over the whole workgroup (blockDim.x multiple of 64, <= 1024).
+// `scratch` must hold blockDim.x/64 + 1 elements of T.  Returns the exclusive
+// prefix of this thread; *total receives the workgroup sum.  Contains barriers.
+template <typename T>
+__device__ inline T block_exclusive_scan(T v, T *scratch, T *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    T inc = wave_inclusive_scan(v);
+    __syncthreads();
+    if (lane == 63) scratch[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T run = 0;
+        for (int w = 0; w < nw; ++w) {
+            T t = scratch[w];
+            scratch[w] = run;
+            run += t;
+        }
+        scratch[nw] = run;
+    }
+    __syncthreads();
+    T res = scratch[wid] + inc - v;
+    *total = scratch[nw];
+    return res;
+}
+
+// In-LDS bitonic sort (ascending) of P = power-of-two 64-bit keys by the whole
+// workgroup.  Caller must __syncthreads() before (keys written) and after.
+__device__ inline void block_bitonic_sort(uint64_t *key, int P) {
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < (P >> 1); i += blockDim.x) {
+                // i-th compare/exchange pair of this (k, j) stage
+                int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+                int hi = lo | j;
+                bool asc = (lo & k) == 0;
+                uint64_t a = key[lo], b = key[hi];
+                if ((a > b) == asc) {
+                    key[lo] = b;
+                    key[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+}  // namespace grf

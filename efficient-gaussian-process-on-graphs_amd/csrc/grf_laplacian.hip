@@ -1,0 +1,256 @@
+// grf_laplacian.hip -- normalised graph Laplacians on the device, with the
+// exact floating-point semantics of the reference's numpy / scipy code so that
+// the walk matrix (and therefore every walk) is bit-identical.
+//
+//   GRF_LAP_SCIPY : efficient_graph_gp_sparse/utils_sparse/graph_utils.py:16-30
+//     deg  = A.sum(axis=1)  -> np.add.reduceat per row = a0 + pairwise(rest)
+//     dinv = 1/sqrt(deg), inf -> 0
+//     L    = (D_inv_sqrt @ (D - A)) @ D_inv_sqrt, exact zeros dropped at every
+//            scipy op, columns ascending, diagonal stored.
+//   GRF_LAP_NUMPY / _SAFE / _COMBINATORIAL / _NONE (dense input):
+//     efficient_graph_gp/graph_kernels/utils.py:21-26 and
+//     efficient_graph_gp/preprocessing/laplacian_np.py:13-34; deg = np.sum(W, 1)
+//     (numpy pairwise summation over the full dense row); the walk matrix is the
+//     CSR of the nonzeros in ascending column order (np.flatnonzero,
+//     random_walk_samplers/sampler.py:22-28).
+#include "grf_block.h"
+
+namespace grf {
+
+int32_t scan_counts_i32(int64_t n, const int32_t *cnt, int64_t *out, void *ws, size_t ws_bytes, hipStream_t st);
+size_t scan_ws_bytes(int64_t n);
+
+// numpy pairwise_sum_DOUBLE leaf (n <= 128)
+__device__ inline double pw_leaf(const double *a, int64_t n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int64_t i = 0; i < n; ++i) r += a[i];
+        return r;
+    }
+    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    int64_t i;
+    for (i = 8; i < n - (n % 8); i += 8) {
+        r0 += a[i + 0]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+        r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; ++i) res += a[i];
+    return res;
+}
+
+// numpy pairwise_sum_DOUBLE, recursion unrolled onto an explicit stack
+__device__ double np_pairwise(const double *a, int64_t n) {
+    if (n <= 128) return pw_leaf(a, n);
+    struct Frame { int64_t off, n; int state; double left; };
+    Frame st[64];
+    int sp = 0;
+    st[0] = {0, n, 0, 0.0};
+    double ret = 0.0;
+    while (sp >= 0) {
+        Frame &f = st[sp];
+        if (f.n <= 128) {
+            ret = pw_leaf(a + f.off, f.n);
+            --sp;
+            continue;
+        }
+        int64_t n2 = f.n / 2;
+        n2 -= n2 % 8;
+        if (f.state == 0) {
+            f.state = 1;
+            st[sp + 1] = {f.off, n2, 0, 0.0};
+            ++sp;
+        } else if (f.state == 1) {
+            f.left = ret;
+            f.state = 2;
+            st[sp + 1] = {f.off + n2, f.n - n2, 0, 0.0};
+            ++sp;
+        } else {
+            ret = f.left + ret;
+            --sp;
+        }
+    }
+    return ret;
+}
+
+// ------------------------------------------------------------------- scipy
+__global__ void lap_deg_kernel(int64_t n, const int64_t *ptr, const double *val, double *deg, double *dinv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t b = ptr[i], e = ptr[i + 1];
+    double d = e > b ? val[b] + np_pairwise(val + b + 1, e - b - 1) : 0.0;
+    deg[i] = d;
+    double v = 1.0 / sqrt(d);
+    dinv[i] = isinf(v) ? 0.0 : v;
+}
+
+// One row of D^-1/2 (D - A) D^-1/2 in scipy order.  EMIT=false counts.
+template <bool EMIT>
+__global__ void lap_row_kernel(int64_t n, const int64_t *ptr, const int32_t *idx, const double *val,
+                               const double *deg, const double *dinv, int32_t *cnt, const int64_t *l_ptr,
+                               int32_t *l_idx, double *l_val, int64_t l_cap) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double d = deg[i], di = dinv[i];
+    int64_t a = ptr[i];
+    const int64_t ae = ptr[i + 1];
+    bool diag_done = (d == 0.0);  // sp.diags drops a zero diagonal
+    int64_t out = EMIT ? l_ptr[i] : 0;
+    int32_t c = 0;
+    for (;;) {
+        int64_t col;
+        double v;
+        if (!diag_done && (a >= ae || idx[a] > i)) {
+            col = i; v = d; diag_done = true;
+        } else if (a < ae) {
+            col = idx[a];
+            if (!diag_done && col == i) { v = d - val[a]; diag_done = true; }
+            else v = 0.0 - val[a];
+            ++a;
+        } else {
+            break;
+        }
+        if (v == 0.0 || di == 0.0) continue;
+        double t = di * v;
+        if (t == 0.0) continue;
+        double dj = dinv[col];
+        if (dj == 0.0) continue;
+        double u = t * dj;
+        if (u == 0.0) continue;
+        if (EMIT) {
+            if (out < l_cap) { l_idx[out] = (int32_t)col; l_val[out] = u; }
+            ++out;
+        } else {
+            ++c;
+        }
+    }
+    if (!EMIT) cnt[i] = c;
+}
+
+// ------------------------------------------------------------------- dense
+__global__ void lapd_deg_kernel(int64_t n, const double *W, int32_t mode, double *deg, double *dinv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double d = np_pairwise(W + i * n, n);
+    deg[i] = d;
+    if (mode == GRF_LAP_NUMPY) dinv[i] = d > 0.0 ? 1.0 / sqrt(d) : 0.0;
+    else dinv[i] = 1.0 / sqrt(d > 0.0 ? d : 1.0);
+}
+
+__device__ inline double lapd_value(int32_t mode, int64_t i, int64_t j, double w, const double *deg,
+                                    const double *dinv) {
+    switch (mode) {
+        case GRF_LAP_COMBINATORIAL: return (i == j ? deg[i] : 0.0) - w;
+        case GRF_LAP_NONE: return w;
+        default: return (i == j ? 1.0 : 0.0) - (dinv[i] * w) * dinv[j];
+    }
+}
+
+// one wave per row; EMIT=false counts nonzeros, EMIT=true writes them in column order
+template <bool EMIT>
+__global__ __launch_bounds__(256) void lapd_row_kernel(int64_t n, const double *W, int32_t mode, const double *deg,
+                                                       const double *dinv, int32_t *cnt, const int64_t *l_ptr,
+                                                       int32_t *l_idx, double *l_val, int64_t l_cap) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const int lane = threadIdx.x & 63;
+    int64_t out = EMIT ? l_ptr[i] : 0;
+    int32_t c = 0;
+    for (int64_t j0 = 0; j0 < n; j0 += 64) {
+        const int64_t j = j0 + lane;
+        double v = 0.0;
+        bool nz = false;
+        if (j < n) {
+            v = lapd_value(mode, i, j, W[i * n + j], deg, dinv);
+            nz = (v != 0.0);
+        }
+        const uint64_t mask = __ballot(nz);
+        if (EMIT) {
+            if (nz) {
+                const int64_t pos = out + __popcll(mask & ((1ull << lane) - 1ull));
+                if (pos < l_cap) { l_idx[pos] = (int32_t)j; l_val[pos] = v; }
+            }
+            out += __popcll(mask);
+        } else {
+            c += __popcll(mask);
+        }
+    }
+    if (!EMIT && lane == 0) cnt[i] = c;
+}
+
+}  // namespace grf
+
+using namespace grf;
+
+extern "C" {
+#pragma GCC visibility push(default)
+
+size_t grf_laplacian_csr_workspace_bytes(int64_t n) {
+    const size_t cnt_bytes = ((size_t)(n > 0 ? n : 1) * sizeof(int32_t) + 255) & ~(size_t)255;
+    return cnt_bytes + scan_ws_bytes(n);
+}
+
+size_t grf_laplacian_dense_workspace_bytes(int64_t n) {
+    const size_t nn = (size_t)(n > 0 ? n : 1);
+    return ((nn * sizeof(double) + 255) & ~(size_t)255) + ((nn * sizeof(int32_t) + 255) & ~(size_t)255) +
+           scan_ws_bytes(n);
+}
+
+int32_t grf_laplacian_csr(int64_t n, const int64_t *a_ptr, const int32_t *a_idx, const double *a_val, int32_t mode,
+                          int64_t *l_ptr, int32_t *l_idx, double *l_val, int64_t l_cap, double *deg, double *dinv,
+                          void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && a_ptr && l_ptr && deg && dinv, GRF_EINVAL, "grf_laplacian_csr: bad arguments");
+    GRF_REQUIRE(mode == GRF_LAP_SCIPY, GRF_EUNSUPPORTED,
+                "grf_laplacian_csr: only GRF_LAP_SCIPY is defined for CSR input (got %d)", mode);
+    const size_t cnt_bytes = ((size_t)(n > 0 ? n : 1) * sizeof(int32_t) + 255) & ~(size_t)255;
+    GRF_REQUIRE(workspace_bytes >= cnt_bytes + scan_ws_bytes(n), GRF_EINVAL,
+                "grf_laplacian_csr: workspace too small (%zu < %zu)", workspace_bytes, cnt_bytes + scan_ws_bytes(n));
+    hipStream_t st = S(stream);
+    int32_t *cnt = (int32_t *)workspace;
+    if (n == 0) {
+        GRF_CHECK_HIP(hipMemsetAsync(l_ptr, 0, sizeof(int64_t), st));
+        return GRF_OK;
+    }
+    const unsigned g = (unsigned)cdiv<int64_t>(n, 256);
+    lap_deg_kernel<<<g, 256, 0, st>>>(n, a_ptr, a_val, deg, dinv);
+    GRF_CHECK_LAUNCH("lap_deg_kernel");
+    lap_row_kernel<false><<<g, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
+    GRF_CHECK_LAUNCH("lap_row_kernel<count>");
+    int32_t rc = scan_counts_i32(n, cnt, l_ptr, (char *)workspace + cnt_bytes, workspace_bytes - cnt_bytes, st);
+    if (rc != GRF_OK) return rc;
+    lap_row_kernel<true><<<g, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
+    GRF_CHECK_LAUNCH("lap_row_kernel<fill>");
+    return GRF_OK;
+}
+
+int32_t grf_laplacian_dense(int64_t n, const double *W, int32_t mode, int64_t *l_ptr, int32_t *l_idx, double *l_val,
+                            int64_t l_cap, double *deg, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && W && l_ptr && deg, GRF_EINVAL, "grf_laplacian_dense: bad arguments");
+    GRF_REQUIRE(mode == GRF_LAP_NUMPY || mode == GRF_LAP_NUMPY_SAFE || mode == GRF_LAP_COMBINATORIAL ||
+                    mode == GRF_LAP_NONE,
+                GRF_EINVAL, "grf_laplacian_dense: bad mode %d", mode);
+    const size_t nn = (size_t)(n > 0 ? n : 1);
+    const size_t dinv_bytes = (nn * sizeof(double) + 255) & ~(size_t)255;
+    const size_t cnt_bytes = (nn * sizeof(int32_t) + 255) & ~(size_t)255;
+    GRF_REQUIRE(workspace_bytes >= dinv_bytes + cnt_bytes + scan_ws_bytes(n), GRF_EINVAL,
+                "grf_laplacian_dense: workspace too small");
+    hipStream_t st = S(stream);
+    if (n == 0) {
+        GRF_CHECK_HIP(hipMemsetAsync(l_ptr, 0, sizeof(int64_t), st));
+        return GRF_OK;
+    }
+    double *dinv = (double *)workspace;
+    int32_t *cnt = (int32_t *)((char *)workspace + dinv_bytes);
+    void *scan_ws = (char *)workspace + dinv_bytes + cnt_bytes;
+    lapd_deg_kernel<<<(unsigned)cdiv<int64_t>(n, 128), 128, 0, st>>>(n, W, mode, deg, dinv);
+    GRF_CHECK_LAUNCH("lapd_deg_kernel");
+    const unsigned g = (unsigned)cdiv<int64_t>(n, 4);
+    lapd_row_kernel<false><<<g, 256, 0, st>>>(n, W, mode, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
+    GRF_CHECK_LAUNCH("lapd_row_kernel<count>");
+    int32_t rc = scan_counts_i32(n, cnt, l_ptr, scan_ws, workspace_bytes - dinv_bytes - cnt_bytes, st);
+    if (rc != GRF_OK) return rc;
+    lapd_row_kernel<true><<<g, 256, 0, st>>>(n, W, mode, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
+    GRF_CHECK_LAUNCH("lapd_row_kernel<fill>");
+    return GRF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,312 @@
+// grf_steps.hip -- visit slots -> per-step occupancy rows -> feature rows Phi.
+//
+// Reference behaviour replaced (paths under the reference checkout):
+//   step_accumulators[step][(start, cur)] += load, merged and normalised:
+//     efficient_graph_gp_sparse/random_walk_samplers_sparse/sparse_sampler.py:47,107-130
+//     efficient_graph_gp/random_walk_samplers/sampler.py:47,137-146,188-203
+//   Phi = sum_l f_l M_l (scipy CSR adds drop exact zeros):
+//     efficient_graph_gp_sparse/graph_kernels_sparse/fast_grf_kernel_general.py:47-52
+//
+// Bit-exactness: every (source, step, node) value is the left-to-right sum of
+// the loads in walk order starting from 0.0 (dict `+=`), then divided by m
+// (dense sampler) or multiplied by 1/m (scipy), and Phi entries are summed in
+// step order starting from 0.0 -- the orders the reference uses.  Sorting
+// (node, walk) keys in LDS gives those orders without atomics.
+#include "grf_block.h"
+
+namespace grf {
+
+__device__ inline double normalise(double acc, int32_t norm, int64_t m) {
+    return norm == GRF_NORM_DIV ? acc / (double)m : acc * (1.0 / (double)m);
+}
+
+// --------------------------------------------------------------- grf_steps
+// one workgroup per (source, step) group of m slots; P = next_pow2(m) keys in LDS
+__global__ __launch_bounds__(256) void steps_kernel(int64_t m, int32_t norm, int32_t P,
+                                                    const int32_t *__restrict__ slot_node,
+                                                    const double *__restrict__ slot_load,
+                                                    int32_t *__restrict__ step_cnt, int32_t *__restrict__ step_idx,
+                                                    double *__restrict__ step_val) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t key[];
+    int32_t *scratch = reinterpret_cast<int32_t *>(key + P);  // 17 ints after the keys
+    const int64_t g = blockIdx.x;
+    const int32_t *nd = slot_node + g * m;
+    const double *ld = slot_load + g * m;
+    for (int t = threadIdx.x; t < P; t += blockDim.x) {
+        uint64_t k = ~0ull;
+        if (t < m) {
+            const int32_t v = nd[t];
+            if (v >= 0) k = ((uint64_t)(uint32_t)v << 32) | (uint32_t)t;
+        }
+        key[t] = k;
+    }
+    __syncthreads();
+    block_bitonic_sort(key, P);
+    // contiguous chunk per thread
+    const int T = blockDim.x;
+    const int per = P >= T ? P / T : 1;
+    const int i0 = threadIdx.x * per;
+    int c = 0;
+    for (int i = i0; i < i0 + per && i < P; ++i) {
+        const uint64_t k = key[i];
+        if (k != ~0ull && (i == 0 || (key[i - 1] >> 32) != (k >> 32))) ++c;
+    }
+    int32_t total;
+    int32_t rank = block_exclusive_scan<int32_t>(c, scratch, &total);
+    for (int i = i0; i < i0 + per && i < P; ++i) {
+        const uint64_t k = key[i];
+        if (k == ~0ull || (i > 0 && (key[i - 1] >> 32) == (k >> 32))) continue;
+        double acc = 0.0;
+        int j = i;
+        do {
+            acc += ld[(uint32_t)key[j]];
+            ++j;
+        } while (j < P && (key[j] >> 32) == (k >> 32));
+        step_idx[g * m + rank] = (int32_t)(k >> 32);
+        step_val[g * m + rank] = normalise(acc, norm, m);
+        ++rank;
+    }
+    if (threadIdx.x == 0) step_cnt[g] = total;
+}
+
+// ------------------------------------------------------------------ grf_phi
+// one wave per source: L-way merge of the sorted step rows (L <= 64)
+__global__ __launch_bounds__(256) void phi_merge_kernel(int64_t n_src, int64_t m, int32_t L, int32_t Lf,
+                                                        const int32_t *__restrict__ step_cnt,
+                                                        const int32_t *__restrict__ step_idx,
+                                                        const double *__restrict__ step_val,
+                                                        const double *__restrict__ f, int64_t cap,
+                                                        int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
+                                                        double *__restrict__ phi_val, float *__restrict__ phi_val32) {
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= n_src) return;
+    const int lane = threadIdx.x & 63;
+    int64_t pos = 0, end = 0;
+    double fl = 0.0;
+    if (lane < Lf) {
+        pos = (s * L + lane) * m;
+        end = pos + step_cnt[s * L + lane];
+        fl = f[lane];
+    }
+    int32_t head = pos < end ? step_idx[pos] : INT32_MAX;
+    int64_t out = 0;
+    const int64_t obase = s * cap;
+    for (;;) {
+        int32_t mn = head;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mn = min(mn, __shfl_xor(mn, off, 64));
+        if (mn == INT32_MAX) break;
+        const bool match = (head == mn);
+        const double t = match ? fl * step_val[pos] : 0.0;
+        uint64_t mask = __ballot(match);
+        double acc = 0.0;
+        bool first = true;
+        while (mask) {
+            const int b = __ffsll((long long)mask) - 1;
+            mask &= mask - 1;
+            const double tb = __shfl(t, b, 64);
+            acc = first ? 0.0 + tb : acc + tb;
+            first = false;
+        }
+        if (acc != 0.0) {
+            if (lane == 0 && out < cap) {
+                phi_idx[obase + out] = mn;
+                phi_val[obase + out] = acc;
+                if (phi_val32) phi_val32[obase + out] = (float)acc;
+            }
+            ++out;
+        }
+        if (match) {
+            ++pos;
+            head = pos < end ? step_idx[pos] : INT32_MAX;
+        }
+    }
+    if (lane == 0) phi_cnt[s] = (int32_t)(out < cap ? out : cap);
+}
+
+// ------------------------------------------------------------ grf_phi_fused
+// one workgroup per source: sort (node, step, walk) of all m*L slots in LDS;
+// runs of (node, step) are the step entries, runs of node the Phi entries.
+__global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, int32_t norm, int32_t P, int32_t wbits,
+                                                        int32_t lbits, const int32_t *__restrict__ slot_node,
+                                                        const double *__restrict__ slot_load,
+                                                        const double *__restrict__ f, int32_t Lf, int64_t cap,
+                                                        int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
+                                                        double *__restrict__ phi_val, float *__restrict__ phi_val32) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    const int E = (int)(m * L);
+    uint64_t *key = smem;                               // [P]
+    double *ld = reinterpret_cast<double *>(smem + P);  // [E] loads by slot, later Phi values by position
+    double *mv = ld + E;                                // [P] step values at run heads
+    int32_t *scratch = reinterpret_cast<int32_t *>(mv + P);  // 17 ints
+    const int64_t s = blockIdx.x;
+    const int32_t *nd = slot_node + s * E;
+    const double *sl = slot_load + s * E;
+    const int sh = wbits + lbits;
+    const uint64_t wmask = (1ull << wbits) - 1ull, lmask = (1ull << lbits) - 1ull;
+    for (int t = threadIdx.x; t < P; t += blockDim.x) {
+        uint64_t k = ~0ull;
+        if (t < E) {
+            const int32_t v = nd[t];
+            if (v >= 0) {
+                const int l = t / (int)m, w = t - l * (int)m;
+                k = ((uint64_t)(uint32_t)v << sh) | ((uint64_t)l << wbits) | (uint64_t)w;
+                ld[t] = sl[t];
+            }
+        }
+        key[t] = k;
+    }
+    __syncthreads();
+    block_bitonic_sort(key, P);
+    // step values at (node, step) run heads, loads summed in walk order
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const uint64_t k = key[i];
+        if (k == ~0ull || (i > 0 && (key[i - 1] >> wbits) == (k >> wbits))) continue;
+        double acc = 0.0;
+        int j = i;
+        do {
+            const uint64_t kj = key[j];
+            acc += ld[((kj >> wbits) & lmask) * m + (kj & wmask)];
+            ++j;
+        } while (j < P && (key[j] >> wbits) == (k >> wbits));
+        mv[i] = normalise(acc, norm, m);
+    }
+    __syncthreads();
+    // Phi entries at node run heads; values parked in ld[i] (i < #valid <= E)
+    const int T = blockDim.x;
+    const int per = P >= T ? P / T : 1;
+    const int i0 = threadIdx.x * per;
+    int c = 0;
+    for (int i = i0; i < i0 + per && i < P; ++i) {
+        const uint64_t k = key[i];
+        if (k == ~0ull || (i > 0 && (key[i - 1] >> sh) == (k >> sh))) continue;
+        double acc = 0.0;
+        bool present = false;
+        int j = i;
+        do {
+            const uint64_t kj = key[j];
+            if (j == i || (key[j - 1] >> wbits) != (kj >> wbits)) {  // a step run head
+                const int l = (int)((kj >> wbits) & lmask);
+                if (l < Lf) {
+                    const double t = f[l] * mv[j];
+                    acc = present ? acc + t : 0.0 + t;
+                    present = true;
+                }
+            }
+            ++j;
+        } while (j < P && (key[j] >> sh) == (k >> sh));
+        if (present && acc != 0.0) {
+            ++c;
+        } else {
+            acc = 0.0;
+            present = false;
+        }
+        ld[i] = acc;  // 0.0 <=> not emitted
+    }
+    int32_t total;
+    int32_t rank = block_exclusive_scan<int32_t>(c, scratch, &total);
+    const int64_t obase = s * cap;
+    for (int i = i0; i < i0 + per && i < P; ++i) {
+        const uint64_t k = key[i];
+        if (k == ~0ull || (i > 0 && (key[i - 1] >> sh) == (k >> sh))) continue;
+        const double v = ld[i];
+        if (v == 0.0) continue;
+        if (rank < cap) {
+            phi_idx[obase + rank] = (int32_t)(k >> sh);
+            phi_val[obase + rank] = v;
+            if (phi_val32) phi_val32[obase + rank] = (float)v;
+        }
+        ++rank;
+    }
+    if (threadIdx.x == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
+}
+
+// ------------------------------------------------------- dense (N, N, L) out
+__global__ __launch_bounds__(256) void steps_densify_kernel(int64_t n_src, int64_t m, int32_t L, int64_t n_cols,
+                                                            const int32_t *__restrict__ step_cnt,
+                                                            const int32_t *__restrict__ step_idx,
+                                                            const double *__restrict__ step_val,
+                                                            double *__restrict__ out) {
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= n_src * L) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t s = g / L;
+    const int l = (int)(g - s * L);
+    for (int64_t r = lane; r < step_cnt[g]; r += 64)
+        out[(s * n_cols + step_idx[g * m + r]) * L + l] = step_val[g * m + r];
+}
+
+}  // namespace grf
+
+using namespace grf;
+
+extern "C" {
+#pragma GCC visibility push(default)
+
+int32_t grf_steps(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
+                  const double *slot_load, int32_t *step_cnt, int32_t *step_idx, double *step_val,
+                  grf_stream_t stream) {
+    GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && slot_node && slot_load && step_cnt && step_idx && step_val,
+                GRF_EINVAL, "grf_steps: bad arguments");
+    GRF_REQUIRE(norm == GRF_NORM_DIV || norm == GRF_NORM_MUL_RECIP, GRF_EINVAL, "grf_steps: bad norm");
+    GRF_REQUIRE(m <= 16384, GRF_EUNSUPPORTED, "grf_steps: walks_per_node > 16384 not supported by this build");
+    if (n_src == 0) return GRF_OK;
+    const int P = (int)next_pow2_u32((uint32_t)m);
+    const int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
+    const size_t lds = (size_t)P * sizeof(uint64_t) + 128;
+    steps_kernel<<<(unsigned)(n_src * L), T, lds, S(stream)>>>(m, norm, P, slot_node, slot_load, step_cnt, step_idx,
+                                                              step_val);
+    GRF_CHECK_LAUNCH("steps_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, const int32_t *step_idx,
+                const double *step_val, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
+                int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream) {
+    GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && step_cnt && step_idx && step_val && phi_cnt && phi_idx && phi_val,
+                GRF_EINVAL, "grf_phi: bad arguments");
+    GRF_REQUIRE(n_f >= 0 && (n_f == 0 || f), GRF_EINVAL, "grf_phi: bad modulator");
+    GRF_REQUIRE(L <= 64, GRF_EUNSUPPORTED, "grf_phi: max_walk_length > 64 not supported by this build");
+    GRF_REQUIRE(phi_cap >= 1, GRF_EINVAL, "grf_phi: phi_cap must be >= 1");
+    if (n_src == 0) return GRF_OK;
+    const int32_t Lf = n_f < L ? n_f : L;
+    phi_merge_kernel<<<(unsigned)cdiv<int64_t>(n_src, 4), 256, 0, S(stream)>>>(
+        n_src, m, L, Lf, step_cnt, step_idx, step_val, f, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
+    GRF_CHECK_LAUNCH("phi_merge_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
+                      const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
+                      int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream) {
+    GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && slot_node && slot_load && phi_cnt && phi_idx && phi_val,
+                GRF_EINVAL, "grf_phi_fused: bad arguments");
+    GRF_REQUIRE(norm == GRF_NORM_DIV || norm == GRF_NORM_MUL_RECIP, GRF_EINVAL, "grf_phi_fused: bad norm");
+    GRF_REQUIRE(n_f >= 0 && (n_f == 0 || f), GRF_EINVAL, "grf_phi_fused: bad modulator");
+    GRF_REQUIRE(m * (int64_t)L <= 4096, GRF_EUNSUPPORTED, "grf_phi_fused: needs walks_per_node * L <= 4096");
+    GRF_REQUIRE(phi_cap >= 1, GRF_EINVAL, "grf_phi_fused: phi_cap must be >= 1");
+    if (n_src == 0) return GRF_OK;
+    const int E = (int)(m * L);
+    const int P = (int)next_pow2_u32((uint32_t)E);
+    const int wbits = ceil_log2((uint64_t)m), lbits = ceil_log2((uint64_t)L) > 0 ? ceil_log2((uint64_t)L) : 1;
+    const size_t lds = (size_t)P * 8 + (size_t)E * 8 + (size_t)P * 8 + 128;
+    const int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
+    const int32_t Lf = n_f < L ? n_f : L;
+    phi_fused_kernel<<<(unsigned)n_src, T, lds, S(stream)>>>(m, L, norm, P, wbits, lbits, slot_node, slot_load, f, Lf,
+                                                             phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
+    GRF_CHECK_LAUNCH("phi_fused_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_steps_densify(int64_t n_src, int64_t m, int32_t L, int64_t n_cols, const int32_t *step_cnt,
+                          const int32_t *step_idx, const double *step_val, double *out, grf_stream_t stream) {
+    GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && n_cols >= 0 && step_cnt && step_idx && step_val && out,
+                GRF_EINVAL, "grf_steps_densify: bad arguments");
+    if (n_src == 0) return GRF_OK;
+    steps_densify_kernel<<<(unsigned)cdiv<int64_t>(n_src * L, 4), 256, 0, S(stream)>>>(n_src, m, L, n_cols, step_cnt,
+                                                                                      step_idx, step_val, out);
+    GRF_CHECK_LAUNCH("steps_densify_kernel");
+    return GRF_OK;
+}
+
+}  // extern "C"

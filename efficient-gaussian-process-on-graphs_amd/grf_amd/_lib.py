@@ -1,0 +1,117 @@
+"""ctypes binding of ``libgrf_amd.so`` (the C ABI declared in ``include/grf.h``).
+
+The shared library is built in-tree by ``csrc/Makefile`` (hipcc, gfx950).  If
+it is missing this module raises -- there is no CPU fallback anywhere in the
+product path.  ``torch`` is imported first so that the HIP runtime torch ships
+(SONAME ``libamdhip64.so.7``) is the one the library binds to: device
+pointers and streams are then shared between torch and the engine.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import torch  # noqa: F401  (load torch's HIP runtime before ours)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libgrf_amd.so")
+CSRC = os.path.join(os.path.dirname(_PKG), "csrc")
+
+GRF_OK, GRF_EINVAL, GRF_EHIP, GRF_ECAPACITY, GRF_EUNSUPPORTED = 0, -1, -2, -3, -4
+LAP_SCIPY, LAP_NUMPY, LAP_NUMPY_SAFE, LAP_COMBINATORIAL, LAP_NONE = 0, 1, 2, 3, 4
+RNG_PCG64, RNG_PHILOX = 0, 1
+LOAD_CUMULATIVE, LOAD_NONCUMULATIVE, LOAD_ABLATION = 0, 1, 2
+NORM_DIV, NORM_MUL_RECIP = 0, 1
+
+
+class GrfWalkParams(ctypes.Structure):
+    _fields_ = [
+        ("walks_per_node", ctypes.c_int64),
+        ("p_halt", ctypes.c_double),
+        ("max_walk_length", ctypes.c_int32),
+        ("load_rule", ctypes.c_int32),
+        ("rng", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("n_chunks", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+_i32, _i64, _u64, _dbl, _vp, _sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double,
+                                    ctypes.c_void_p, ctypes.c_size_t)
+
+# name -> (restype, argtypes); mirrors include/grf.h exactly
+SIGNATURES = {
+    "grf_last_error": (ctypes.c_char_p, []),
+    "grf_version": (_i32, []),
+    "grf_device_count": (_i32, []),
+    "grf_set_device": (_i32, [_i32]),
+    "grf_laplacian_csr": (_i32, [_i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "grf_laplacian_csr_workspace_bytes": (_sz, [_i64]),
+    "grf_laplacian_dense": (_i32, [_i64, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _sz, _vp]),
+    "grf_laplacian_dense_workspace_bytes": (_sz, [_i64]),
+    "grf_walk": (_i32, [_i64, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _vp, _vp, _vp]),
+    "grf_chunk_bounds": (_i64, [_i64, _i64, _i64]),
+    "grf_steps": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "grf_steps_densify": (_i32, [_i64, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "grf_phi": (_i32, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "grf_phi_fused": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
+    "grf_scan_workspace_bytes": (_sz, [_i64]),
+    "grf_compact_rows": (_i32, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "grf_transpose_banded": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "grf_transpose_workspace_bytes": (_sz, [_i64]),
+    "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+}
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libgrf_amd.so for gfx950 with hipcc (make -C csrc)."""
+    cmd = ["make", "-s", "-C", CSRC, f"-j{min(16, os.cpu_count() or 1)}"]
+    if force:
+        subprocess.run(["make", "-s", "-C", CSRC, "clean"], check=True)
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+def load():
+    """Load the engine library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"grf_amd: native library {LIB_PATH} is missing; build it with "
+            f"`make -C {CSRC}` (or __graft_entry__.build()).  There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class GrfError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    """Map a grf_status to the reference's exception types (SURVEY.md §8b Errors)."""
+    if rc == GRF_OK:
+        return
+    msg = f"{what}: {load().grf_last_error().decode(errors='replace')}"
+    if rc == GRF_EINVAL:
+        raise ValueError(msg)
+    if rc == GRF_EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise GrfError(msg)
+
+
+def exported_symbols() -> list[str]:
+    return sorted(SIGNATURES)

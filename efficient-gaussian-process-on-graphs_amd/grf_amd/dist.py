@@ -1,0 +1,95 @@
+"""Multi-GPU sharding of the GRF kernel matrix (one process per GPU, RCCL over xGMI).
+
+Walks are independent per source node, so rank r owns the contiguous source
+range ``shard_range(n, r, world)``: it runs the walks and builds its Phi rows
+locally (Philox is keyed by (seed, source, walk), so the result does not depend
+on the number of GPUs).  The one real exchange is Phi itself: K[i, :] needs
+every row of Phi, so the ranks all-gather their Phi rows (CSR; ~0.35-0.7 GB at
+N = 100k) and each computes its row block K[R_r, :] = Phi[R_r] Phi^T.  K stays
+row-sharded; no reduction over the 40 GB K is ever needed (an
+all-reduce of K would move ~70 GB per GPU through the xGMI ring).
+
+The reference has no distributed code; its only parallelism is a fork pool over
+source chunks (sparse_sampler.py:90-114), which this replaces.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous source range of ``rank`` (np.array_split boundaries)."""
+    base, extra = divmod(n, world)
+    b = rank * base + min(rank, extra)
+    return b, b + base + (1 if rank < extra else 0)
+
+
+def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, group=None):
+    """All-gather row-sharded CSR pieces (rank order) into the full CSR on every rank.
+
+    ``ptr`` is the local int64 row pointer (n_local + 1, starting at 0), ``idx``
+    int32 columns, ``val`` values.  Works with RCCL (device tensors) and gloo
+    (CPU tensors).  Returns (ptr, idx, val) of the concatenation.
+    """
+    world = dist.get_world_size(group)
+    dev = ptr.device
+    n_local = ptr.numel() - 1
+    nnz_local = int(ptr[-1].item()) if n_local >= 0 else 0
+    sizes = torch.tensor([n_local, nnz_local], dtype=torch.int64, device=dev)
+    all_sizes = [torch.empty_like(sizes) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    all_sizes = torch.stack(all_sizes).cpu()
+    n_max, nnz_max = int(all_sizes[:, 0].max()), int(all_sizes[:, 1].max())
+
+    counts = torch.zeros(n_max, dtype=torch.int64, device=dev)
+    counts[:n_local] = ptr[1:] - ptr[:-1]
+    idx_pad = torch.zeros(max(nnz_max, 1), dtype=idx.dtype, device=dev)
+    idx_pad[:nnz_local] = idx[:nnz_local]
+    val_pad = torch.zeros(max(nnz_max, 1), dtype=val.dtype, device=dev)
+    val_pad[:nnz_local] = val[:nnz_local]
+
+    g_counts = torch.empty((world, n_max), dtype=torch.int64, device=dev)
+    g_idx = torch.empty((world, max(nnz_max, 1)), dtype=idx.dtype, device=dev)
+    g_val = torch.empty((world, max(nnz_max, 1)), dtype=val.dtype, device=dev)
+    dist.all_gather_into_tensor(g_counts, counts, group=group)
+    dist.all_gather_into_tensor(g_idx, idx_pad, group=group)
+    dist.all_gather_into_tensor(g_val, val_pad, group=group)
+
+    parts_c, parts_i, parts_v = [], [], []
+    for r in range(world):
+        nr, zr = int(all_sizes[r, 0]), int(all_sizes[r, 1])
+        parts_c.append(g_counts[r, :nr])
+        parts_i.append(g_idx[r, :zr])
+        parts_v.append(g_val[r, :zr])
+    cnt = torch.cat(parts_c)
+    full_ptr = torch.zeros(cnt.numel() + 1, dtype=torch.int64, device=dev)
+    full_ptr[1:] = torch.cumsum(cnt, 0)
+    return full_ptr, torch.cat(parts_i), torch.cat(parts_v)
+
+
+def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length, *, seed=42, group=None,
+                          rng=None):
+    """This rank's row block of K = Phi Phi^T (float32, on the engine's device), and its row range."""
+    from . import _lib as C
+    from .engine import DeviceCSR
+
+    rng = C.RNG_PHILOX if rng is None else rng
+    if rng != C.RNG_PHILOX:
+        raise NotImplementedError("sharded walks use Philox (shard-invariant); PCG64 replay is single-GPU")
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    G = engine.laplacian(A)
+    n = G.n_rows
+    b, e = shard_range(n, rank, world)
+    slots = engine.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed, src_begin=b, src_end=e)
+    local = engine.compact(engine.features(slots, f), want64=False, want32=True)
+    if world > 1:
+        ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32, group)
+        phi = DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))
+    else:
+        phi = DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
+    tr = engine.transpose_banded(phi)
+    return engine.gram_sparse(phi, tr, b, e), (b, e)

@@ -1,0 +1,364 @@
+"""Device-resident GRF pipeline on one MI355X: thin Python over the C ABI.
+
+Every stage is one call into ``libgrf_amd.so`` on the current torch stream of
+the engine's device; buffers are torch tensors (device memory plumbing only).
+Nothing here computes on the host: the only host reads are sizes
+(``DeviceCSR.nnz``) needed to allocate an output exactly.
+
+Pipeline (re-designed for gfx950)::
+
+    A (CSR) --laplacian--> L (CSR) --walk--> visit slots [n][L][m]
+      --steps--> per-step rows (sampler API)   --phi--> Phi rows
+      --phi_fused (m*L <= 4096)-----------------------> Phi rows
+      --compact--> Phi CSR --transpose_banded--> Phi^T buckets --gram_sparse--> K (fp32)
+                           --densify--> dense Phi --gram_dense (MFMA)-----------> K (fp32)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from . import _lib as C
+
+DEFAULT_BAND_WIDTH = 4096  # transpose band = one wave's LDS window; a Gram tile spans 4 bands
+
+
+def _p(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+@dataclass
+class DeviceCSR:
+    """CSR matrix in device memory (int64 row pointers, int32 columns)."""
+
+    n_rows: int
+    n_cols: int
+    ptr: torch.Tensor
+    idx: torch.Tensor
+    val: Optional[torch.Tensor] = None    # float64
+    val32: Optional[torch.Tensor] = None  # float32
+    _nnz: Optional[int] = None
+
+    @property
+    def nnz(self) -> int:
+        if self._nnz is None:
+            self._nnz = int(self.ptr[-1].item())
+        return self._nnz
+
+    @classmethod
+    def from_scipy(cls, A, device) -> "DeviceCSR":
+        A = sp.csr_matrix(A)
+        if A.shape[0] > 0x7FFFFFFF or A.shape[1] > 0x7FFFFFFF:
+            raise ValueError("graphs with more than 2^31-1 nodes are not supported")
+        ptr = torch.from_numpy(np.asarray(A.indptr, dtype=np.int64)).to(device)
+        idx = torch.from_numpy(np.asarray(A.indices, dtype=np.int32)).to(device)
+        val = torch.from_numpy(np.asarray(A.data, dtype=np.float64)).to(device)
+        return cls(A.shape[0], A.shape[1], ptr, idx, val, None, int(A.nnz))
+
+    def to_scipy(self) -> sp.csr_matrix:
+        nnz = self.nnz
+        ptr = self.ptr.cpu().numpy()
+        idx = self.idx[:nnz].cpu().numpy()
+        val = (self.val if self.val is not None else self.val32)[:nnz].cpu().numpy()
+        if ptr[-1] <= np.iinfo(np.int32).max:
+            ptr = ptr.astype(np.int32)
+        return sp.csr_matrix((val, idx, ptr), shape=(self.n_rows, self.n_cols))
+
+
+@dataclass
+class Slots:
+    node: torch.Tensor  # int32 [n_src, L, m], -1 = no visit
+    load: torch.Tensor  # float64 [n_src, L, m]
+    src_begin: int
+    n: int              # nodes of the graph (columns)
+
+    @property
+    def n_src(self):
+        return self.node.shape[0]
+
+    @property
+    def L(self):
+        return self.node.shape[1]
+
+    @property
+    def m(self):
+        return self.node.shape[2]
+
+
+@dataclass
+class StepRows:
+    cnt: torch.Tensor  # int32 [n_src * L]
+    idx: torch.Tensor  # int32 [n_src * L * m]
+    val: torch.Tensor  # float64 [n_src * L * m]
+    n_src: int
+    L: int
+    m: int
+    n: int
+
+
+@dataclass
+class PaddedRows:
+    cnt: torch.Tensor             # int32 [n_rows]
+    idx: torch.Tensor             # int32 [n_rows * cap]
+    val: torch.Tensor             # float64 [n_rows * cap]
+    val32: Optional[torch.Tensor]  # float32 [n_rows * cap]
+    cap: int
+    n_cols: int
+
+    @property
+    def n_rows(self):
+        return self.cnt.shape[0]
+
+
+@dataclass
+class Banded:
+    t_ptr: torch.Tensor  # int64 [n_bands * n_cols + 1]
+    t_row: torch.Tensor  # int32 [nnz]
+    t_val: torch.Tensor  # float32 [nnz]
+    band_width: int
+    n_rows: int
+    n_cols: int
+
+
+class GRFEngine:
+    """All device work for one GPU.  ``device`` is a torch device (``cuda:N``)."""
+
+    def __init__(self, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("grf_amd needs a ROCm GPU (MI355X / gfx950); none is visible")
+        self.lib = C.load()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        C.check(self.lib.grf_set_device(self.device.index), "grf_set_device")
+
+    # ------------------------------------------------------------ utilities
+    @property
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _empty(self, n, dtype):
+        return torch.empty(int(max(n, 0)), dtype=dtype, device=self.device)
+
+    def _ws(self, nbytes: int) -> torch.Tensor:
+        return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+
+    def _set_device(self):
+        C.check(self.lib.grf_set_device(self.device.index), "grf_set_device")
+
+    def to_device(self, A) -> DeviceCSR:
+        return A if isinstance(A, DeviceCSR) else DeviceCSR.from_scipy(A, self.device)
+
+    # ----------------------------------------------------------- Laplacians
+    def laplacian(self, A) -> DeviceCSR:
+        """scipy-semantics normalised Laplacian (utils_sparse/graph_utils.py:5-30)."""
+        A = self.to_device(A)
+        if A.n_rows != A.n_cols:
+            raise ValueError("Adjacency matrix must be square.")
+        n = A.n_rows
+        cap = A.nnz + n
+        lp, li, lv = self._empty(n + 1, torch.int64), self._empty(cap, torch.int32), self._empty(cap, torch.float64)
+        deg, dinv = self._empty(n, torch.float64), self._empty(n, torch.float64)
+        ws = self._ws(self.lib.grf_laplacian_csr_workspace_bytes(n))
+        C.check(self.lib.grf_laplacian_csr(n, _p(A.ptr), _p(A.idx), _p(A.val), C.LAP_SCIPY, _p(lp), _p(li), _p(lv),
+                                           cap, _p(deg), _p(dinv), _p(ws), ws.numel(), self.stream),
+                "grf_laplacian_csr")
+        return DeviceCSR(n, n, lp, li, lv)
+
+    def walk_matrix_dense(self, W, mode: int) -> DeviceCSR:
+        """Dense-input walk matrix (numpy Laplacian variants or the matrix itself) as CSR."""
+        Wt = torch.as_tensor(np.ascontiguousarray(W, dtype=np.float64) if not torch.is_tensor(W) else W)
+        Wt = Wt.to(self.device, torch.float64).contiguous()
+        n = Wt.shape[0]
+        if Wt.dim() != 2 or Wt.shape[1] != n:
+            raise ValueError("Adjacency matrix must be square.")
+        cap = int(torch.count_nonzero(Wt).item()) + n
+        lp, li, lv = self._empty(n + 1, torch.int64), self._empty(cap, torch.int32), self._empty(cap, torch.float64)
+        deg = self._empty(n, torch.float64)
+        ws = self._ws(self.lib.grf_laplacian_dense_workspace_bytes(n))
+        C.check(self.lib.grf_laplacian_dense(n, _p(Wt), mode, _p(lp), _p(li), _p(lv), cap, _p(deg), _p(ws),
+                                             ws.numel(), self.stream), "grf_laplacian_dense")
+        return DeviceCSR(n, n, lp, li, lv)
+
+    # ---------------------------------------------------------------- walks
+    def walk(self, G: DeviceCSR, walks_per_node: int, p_halt: float, max_walk_length: int, *, rng: int = C.RNG_PHILOX,
+             seed: int = 42, n_chunks: int = 1, load_rule: int = C.LOAD_CUMULATIVE, src_begin: int = 0,
+             src_end: Optional[int] = None) -> Slots:
+        n = G.n_rows
+        src_end = n if src_end is None else src_end
+        m, L = int(walks_per_node), int(max_walk_length)
+        if m < 1 or L < 1:
+            raise ValueError("walks_per_node and max_walk_length must be >= 1")
+        ns = src_end - src_begin
+        node = torch.empty((ns, L, m), dtype=torch.int32, device=self.device)
+        load = torch.empty((ns, L, m), dtype=torch.float64, device=self.device)
+        prm = C.GrfWalkParams(m, float(p_halt), L, int(load_rule), int(rng), 0, int(n_chunks),
+                              int(seed) & 0xFFFFFFFFFFFFFFFF)
+        C.check(self.lib.grf_walk(n, _p(G.ptr), _p(G.idx), _p(G.val), ctypes.byref(prm), src_begin, src_end,
+                                  _p(node), _p(load), self.stream), "grf_walk")
+        return Slots(node, load, src_begin, n)
+
+    def chunk_bounds(self, n: int, n_chunks: int) -> list[int]:
+        return [int(self.lib.grf_chunk_bounds(n, n_chunks, c)) for c in range(n_chunks)] + [n]
+
+    # ----------------------------------------------------- steps / features
+    def steps(self, slots: Slots, norm: int = C.NORM_MUL_RECIP) -> StepRows:
+        ns, L, m = slots.n_src, slots.L, slots.m
+        cnt = self._empty(ns * L, torch.int32)
+        idx = self._empty(ns * L * m, torch.int32)
+        val = self._empty(ns * L * m, torch.float64)
+        C.check(self.lib.grf_steps(ns, m, L, norm, _p(slots.node), _p(slots.load), _p(cnt), _p(idx), _p(val),
+                                   self.stream), "grf_steps")
+        return StepRows(cnt, idx, val, ns, L, m, slots.n)
+
+    def _f(self, f) -> torch.Tensor:
+        return torch.as_tensor(np.asarray(f, dtype=np.float64).reshape(-1)).to(self.device)
+
+    def phi(self, st: StepRows, f, want32: bool = True) -> PaddedRows:
+        ft = self._f(f)
+        cap = max(1, min(st.m * st.L, st.n))
+        cnt = self._empty(st.n_src, torch.int32)
+        idx = self._empty(st.n_src * cap, torch.int32)
+        val = self._empty(st.n_src * cap, torch.float64)
+        v32 = self._empty(st.n_src * cap, torch.float32) if want32 else None
+        C.check(self.lib.grf_phi(st.n_src, st.m, st.L, _p(st.cnt), _p(st.idx), _p(st.val), _p(ft), ft.numel(), cap,
+                                 _p(cnt), _p(idx), _p(val), _p(v32), self.stream), "grf_phi")
+        return PaddedRows(cnt, idx, val, v32, cap, st.n)
+
+    def phi_fused(self, slots: Slots, f, norm: int = C.NORM_MUL_RECIP, want32: bool = True) -> PaddedRows:
+        ft = self._f(f)
+        ns, L, m = slots.n_src, slots.L, slots.m
+        cap = max(1, min(m * L, slots.n))
+        cnt = self._empty(ns, torch.int32)
+        idx = self._empty(ns * cap, torch.int32)
+        val = self._empty(ns * cap, torch.float64)
+        v32 = self._empty(ns * cap, torch.float32) if want32 else None
+        C.check(self.lib.grf_phi_fused(ns, m, L, norm, _p(slots.node), _p(slots.load), _p(ft), ft.numel(), cap,
+                                       _p(cnt), _p(idx), _p(val), _p(v32), self.stream), "grf_phi_fused")
+        return PaddedRows(cnt, idx, val, v32, cap, slots.n)
+
+    def features(self, slots: Slots, f, norm: int = C.NORM_MUL_RECIP) -> PaddedRows:
+        """Phi rows; the fused kernel when m*L fits LDS, else steps + merge (bit-identical)."""
+        if slots.m * slots.L <= 4096:
+            return self.phi_fused(slots, f, norm)
+        return self.phi(self.steps(slots, norm), f)
+
+    # ------------------------------------------------------ sparse utilities
+    def compact(self, rows: PaddedRows, want64: bool = True, want32: bool = True) -> DeviceCSR:
+        n = rows.n_rows
+        ptr = self._empty(n + 1, torch.int64)
+        ws = self._ws(self.lib.grf_scan_workspace_bytes(n))
+        C.check(self.lib.grf_scan_counts(n, _p(rows.cnt), _p(ptr), _p(ws), ws.numel(), self.stream),
+                "grf_scan_counts")
+        nnz = int(ptr[-1].item())
+        idx = self._empty(nnz, torch.int32)
+        v64 = self._empty(nnz, torch.float64) if want64 else None
+        v32 = self._empty(nnz, torch.float32) if (want32 and rows.val32 is not None) else None
+        C.check(self.lib.grf_compact_rows(n, rows.cap, _p(rows.cnt), _p(ptr), _p(rows.idx),
+                                          _p(rows.val if want64 else None),
+                                          _p(rows.val32 if v32 is not None else None), _p(idx), _p(v64),
+                                          _p(v32), self.stream), "grf_compact_rows")
+        return DeviceCSR(n, rows.n_cols, ptr, idx, v64, v32, nnz)
+
+    def step_matrices(self, st: StepRows) -> list[DeviceCSR]:
+        """Per-step CSR matrices (rows = the sources of this step block)."""
+        out = []
+        cnt2 = st.cnt.view(st.n_src, st.L)
+        for l in range(st.L):
+            rows = PaddedRows(cnt2[:, l].contiguous(), st.idx[l * st.m:], st.val[l * st.m:], None, st.L * st.m, st.n)
+            out.append(self.compact(rows, want64=True, want32=False))
+        return out
+
+    def steps_dense(self, st: StepRows, n_cols: Optional[int] = None) -> torch.Tensor:
+        n_cols = st.n if n_cols is None else n_cols
+        out = torch.zeros((st.n_src, n_cols, st.L), dtype=torch.float64, device=self.device)
+        C.check(self.lib.grf_steps_densify(st.n_src, st.m, st.L, n_cols, _p(st.cnt), _p(st.idx), _p(st.val), _p(out),
+                                           self.stream), "grf_steps_densify")
+        return out
+
+    def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH) -> Banded:
+        n_rows, n_cols = phi.n_rows, phi.n_cols
+        nb = -(-n_rows // band_width)
+        nbk = nb * n_cols
+        t_ptr = self._empty(nbk + 1, torch.int64)
+        t_row = self._empty(phi.nnz, torch.int32)
+        t_val = self._empty(phi.nnz, torch.float32)
+        ws = self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
+        C.check(self.lib.grf_transpose_banded(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
+                                              _p(t_ptr), _p(t_row), _p(t_val), _p(ws), ws.numel(), self.stream),
+                "grf_transpose_banded")
+        return Banded(t_ptr, t_row, t_val, band_width, n_rows, n_cols)
+
+    # ----------------------------------------------------------------- Gram
+    @staticmethod
+    def leading_dim(n: int) -> int:
+        return max(64, -(-n // 64) * 64)
+
+    def gram_sparse(self, phi: DeviceCSR, tr: Banded, row_begin: int = 0, row_end: Optional[int] = None,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """K[row_begin:row_end, :] (float32) with leading dimension padded to 64."""
+        n = tr.n_rows
+        row_end = n if row_end is None else row_end
+        ldk = self.leading_dim(n)
+        if out is None:
+            out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
+        C.check(self.lib.grf_gram_sparse(n, row_begin, row_end, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
+                                         tr.band_width, _p(tr.t_ptr), _p(tr.t_row), _p(tr.t_val), _p(out),
+                                         out.stride(0), self.stream), "grf_gram_sparse")
+        return out[:, :n]
+
+    def densify(self, phi: DeviceCSR) -> torch.Tensor:
+        lda = max(16, -(-phi.n_cols // 16) * 16)
+        out = torch.empty((phi.n_rows, lda), dtype=torch.float32, device=self.device)
+        C.check(self.lib.grf_densify(phi.n_rows, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(out), lda, self.stream),
+                "grf_densify")
+        return out
+
+    def gram_dense(self, dense_phi: torch.Tensor, k_dim: int) -> torch.Tensor:
+        n = dense_phi.shape[0]
+        ldk = self.leading_dim(n)
+        out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
+        C.check(self.lib.grf_gram_dense(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, self.stream),
+                "grf_gram_dense")
+        return out[:, :n]
+
+    def gram(self, phi: DeviceCSR, method: str = "auto") -> torch.Tensor:
+        """K = Phi Phi^T (float32).  'dense' = MFMA on densified Phi, 'sparse' = LDS Gustavson."""
+        if method == "auto":
+            n = phi.n_rows
+            # dense MFMA costs 2 n^3 flop at ~100 TF/s; sparse ~ (sum_k c_k^2) * 8 B at a few TB/s
+            method = "dense" if n <= 8192 else "sparse"
+        if method == "dense":
+            return self.gram_dense(self.densify(phi), phi.n_cols)
+        if method == "sparse":
+            return self.gram_sparse(phi, self.transpose_banded(phi))
+        raise ValueError(f"unknown gram method {method!r}")
+
+    # ------------------------------------------------------------- pipelines
+    def kernel_matrix(self, A, modulator_vector: Sequence[float], walks_per_node: int, p_halt: float,
+                      max_walk_length: int, *, rng: int = C.RNG_PHILOX, seed: int = 42, n_chunks: int = 1,
+                      laplacian: bool = True, method: str = "auto", norm: int = C.NORM_MUL_RECIP) -> torch.Tensor:
+        """Sparse-path K = Phi Phi^T (fast_grf_kernel_general.py:42-55), float32 on the device."""
+        G = self.laplacian(A) if laplacian else self.to_device(A)
+        slots = self.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed, n_chunks=n_chunks)
+        phi = self.compact(self.features(slots, modulator_vector, norm))
+        return self.gram(phi, method)
+
+
+_engines: dict = {}
+
+
+def get_engine(device=None) -> GRFEngine:
+    """Process-wide engine per device (GRF_AMD_DEVICE overrides the default)."""
+    if device is None:
+        device = os.environ.get("GRF_AMD_DEVICE")
+    key = str(device)
+    if key not in _engines:
+        _engines[key] = GRFEngine(device)
+    return _engines[key]

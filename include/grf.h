@@ -1,0 +1,198 @@
+/*
+ * grf.h -- C ABI of the MI355X (gfx950) Graph Random Features engine.
+ *
+ * Every compute entry point is asynchronous on the HIP stream it is given,
+ * takes DEVICE pointers (allocated by the caller, e.g. torch tensors on
+ * cuda:N), plain integer sizes and no C++ / torch types.  Return value:
+ * GRF_OK (0) or a negative grf_status; the message of the last failure on
+ * the calling thread is in grf_last_error().  No exception crosses the ABI.
+ * Buffers whose size depends on the data are bounded by documented caps
+ * (`*_cap` arguments) so that no entry point needs a host round trip.
+ *
+ * The reference has no FFI: its boundary is a set of Python functions
+ * (SURVEY.md §8b).  Each entry point below replaces the reference routine
+ * cited next to it (paths relative to the reference checkout).
+ */
+#ifndef GRF_H
+#define GRF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *grf_stream_t; /* hipStream_t; NULL = default stream */
+
+enum grf_status {
+    GRF_OK = 0,
+    GRF_EINVAL = -1,      /* bad argument (reference: ValueError / AssertionError) */
+    GRF_EHIP = -2,        /* HIP runtime / launch failure                           */
+    GRF_ECAPACITY = -3,   /* an output cap was too small                            */
+    GRF_EUNSUPPORTED = -4 /* size outside what this build handles                   */
+};
+
+/* Laplacian semantics */
+enum grf_laplacian_mode {
+    GRF_LAP_SCIPY = 0,         /* utils_sparse/graph_utils.py:5-30  (D^-1/2 (D-A) D^-1/2, scipy order) */
+    GRF_LAP_NUMPY = 1,         /* graph_kernels/utils.py:21-26      (I - D^-1/2 W D^-1/2, dinv=0 at deg<=0) */
+    GRF_LAP_NUMPY_SAFE = 2,    /* preprocessing/laplacian_np.py:13-20 (safe degrees)                   */
+    GRF_LAP_COMBINATORIAL = 3, /* preprocessing/laplacian_np.py:32-34 (D - W)                          */
+    GRF_LAP_NONE = 4           /* walk the matrix as given (RandomWalk(Graph(adj)))                    */
+};
+
+enum grf_rng {
+    GRF_RNG_PCG64 = 0, /* numpy PCG64 stream replay, one sequential stream per chunk (reference-exact) */
+    GRF_RNG_PHILOX = 1 /* Philox4x32-10 keyed (seed), counter (step, walk, source, block)          */
+};
+
+enum grf_load_rule {
+    GRF_LOAD_CUMULATIVE = 0,    /* load *= deg*w/(1-p)   sparse_sampler.py:54, sampler.py:58 */
+    GRF_LOAD_NONCUMULATIVE = 1, /* load  = deg*w/(1-p)   sampler.py:183                      */
+    GRF_LOAD_ABLATION = 2       /* load  = w             sampler.py:180-181                  */
+};
+
+enum grf_norm {
+    GRF_NORM_DIV = 0,      /* value / m       (sampler.py:201)                          */
+    GRF_NORM_MUL_RECIP = 1 /* value * (1/m)   (sparse_sampler.py:130 via scipy _mul_scalar) */
+};
+
+const char *grf_last_error(void);
+int32_t grf_version(void);
+/* number of HIP devices visible (0 if none); never fails */
+int32_t grf_device_count(void);
+/* select the device for subsequent calls on this host thread */
+int32_t grf_set_device(int32_t device);
+
+/* ------------------------------------------------------------------ Laplacian
+ * Replaces efficient_graph_gp_sparse/utils_sparse/graph_utils.py:5-30
+ * (get_normalized_laplacian, sparse) for mode GRF_LAP_SCIPY.
+ * In : A (n x n CSR, canonical: sorted, no duplicates): a_ptr[n+1] (int64),
+ *      a_idx[nnz] (int32), a_val[nnz] (float64).
+ * Out: l_ptr[n+1], l_idx[l_cap], l_val[l_cap] with l_cap >= nnz(A) + n;
+ *      deg[n], dinv[n] (float64, scratch + diagnostics).  Columns ascending. */
+int32_t grf_laplacian_csr(int64_t n, const int64_t *a_ptr, const int32_t *a_idx, const double *a_val, int32_t mode,
+                          int64_t *l_ptr, int32_t *l_idx, double *l_val, int64_t l_cap, double *deg, double *dinv,
+                          void *workspace, size_t workspace_bytes, grf_stream_t stream);
+
+size_t grf_laplacian_csr_workspace_bytes(int64_t n);
+
+/* Replaces efficient_graph_gp/graph_kernels/utils.py:6-28 and
+ * efficient_graph_gp/preprocessing/laplacian_np.py:3-35 followed by the
+ * neighbour scan np.flatnonzero(L[row]) of random_walk_samplers/sampler.py:22-28.
+ * In : W dense row-major n x n float64.  mode: NUMPY / NUMPY_SAFE / COMBINATORIAL / NONE.
+ * Out: the walk matrix as CSR of its nonzeros (ascending columns), l_cap >= nnz. */
+int32_t grf_laplacian_dense(int64_t n, const double *W, int32_t mode, int64_t *l_ptr, int32_t *l_idx, double *l_val,
+                            int64_t l_cap, double *deg, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+
+size_t grf_laplacian_dense_workspace_bytes(int64_t n);
+
+/* --------------------------------------------------------------------- walks
+ * Replaces the walk loops of
+ *   efficient_graph_gp_sparse/random_walk_samplers_sparse/sparse_sampler.py:26-56 and
+ *   efficient_graph_gp/random_walk_samplers/sampler.py:30-61,148-186.
+ * Walks on the CSR (g_ptr, g_idx, g_val).  Records visit slots
+ *   slot_node[(s - src_begin) * L * m + l * m + w] (int32, -1 = no visit),
+ *   slot_load[same]                                   (float64)
+ * for sources s in [src_begin, src_end).
+ * RNG GRF_RNG_PHILOX: key = seed (64 bit).  Any [src_begin, src_end).
+ * RNG GRF_RNG_PCG64 : chunks = np.array_split(arange(n), n_chunks); chunk c is one
+ *   numpy default_rng(seed + c) stream; [src_begin, src_end) must be a union of
+ *   whole chunks (use grf_chunk_bounds). */
+typedef struct grf_walk_params {
+    int64_t walks_per_node; /* m                     */
+    double p_halt;          /* p                     */
+    int32_t max_walk_length;/* L                     */
+    int32_t load_rule;      /* enum grf_load_rule    */
+    int32_t rng;            /* enum grf_rng          */
+    int32_t reserved;
+    int64_t n_chunks;       /* PCG64 only            */
+    uint64_t seed;          /* PCG64: chunk c seeded with seed + c; Philox: key */
+} grf_walk_params;
+
+int32_t grf_walk(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
+                 const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t *slot_node,
+                 double *slot_load, grf_stream_t stream);
+
+/* host helper: first source of chunk c (np.array_split boundaries) */
+int64_t grf_chunk_bounds(int64_t n, int64_t n_chunks, int64_t c);
+
+/* ------------------------------------------------------- per-step occupancy
+ * Replaces the accumulate/normalise part of sparse_sampler.py:36-47,107-130 and
+ * sampler.py:137-146,188-203: for every (source, step) the distinct visited nodes
+ * (ascending) with value = (sum of loads in walk order) normalised by `norm`.
+ * Out (padded rows, row capacity m): step_cnt[ns*L], step_idx[ns*L*m],
+ * step_val[ns*L*m] at row (s_local * L + l).  Explicit zeros are kept. */
+int32_t grf_steps(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
+                  const double *slot_load, int32_t *step_cnt, int32_t *step_idx, double *step_val,
+                  grf_stream_t stream);
+
+/* Dense (N, N, L) feature tensor of RandomWalk.get_random_walk_matrices
+ * (sampler.py:188-203): out[(s * n_cols + j) * L + l] = step value; out must be
+ * zero-filled by the caller. */
+int32_t grf_steps_densify(int64_t n_src, int64_t m, int32_t L, int64_t n_cols, const int32_t *step_cnt,
+                          const int32_t *step_idx, const double *step_val, double *out, grf_stream_t stream);
+
+/* ------------------------------------------------------------------------ Phi
+ * Replaces efficient_graph_gp_sparse/graph_kernels_sparse/fast_grf_kernel_general.py:47-52
+ * (Phi = sum_l f_l M_l, exact zeros dropped; steps l < min(n_f, L)).
+ * From padded step rows (grf_steps output).  Out: padded Phi rows with capacity
+ * phi_cap >= min(m * L, n): phi_cnt[ns], phi_idx[ns*phi_cap], phi_val[ns*phi_cap]
+ * (float64), and optionally phi_val32 (float32 copy, may be NULL). */
+int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, const int32_t *step_idx,
+                const double *step_val, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
+                int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream);
+
+/* Fused slots -> Phi (no step rows), same result bit-for-bit as grf_steps + grf_phi.
+ * Requires m * L <= 4096.  norm as in grf_steps. */
+int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
+                      const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
+                      int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream);
+
+/* --------------------------------------------------------- sparse utilities */
+/* exclusive scan of int32 counts -> int64 row pointers out[n+1] */
+int32_t grf_scan_counts(int64_t n, const int32_t *cnt, int64_t *out_ptr, void *workspace, size_t workspace_bytes,
+                        grf_stream_t stream);
+size_t grf_scan_workspace_bytes(int64_t n);
+/* padded rows (row r at r*cap, cnt[r] entries) -> compact CSR using out_ptr from grf_scan_counts.
+ * Any of the value arrays may be NULL. */
+int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const int64_t *out_ptr,
+                         const int32_t *in_idx, const double *in_val, const float *in_val32, int32_t *out_idx,
+                         double *out_val, float *out_val32, grf_stream_t stream);
+
+/* Banded transpose for the Gram kernel: entries (j, k, v) of Phi (CSR rows j)
+ * bucketed by (band = j / band_width, k):  bucket id = band * n_cols + k.
+ * t_ptr[n_bands * n_cols + 1], t_row[nnz] (int32 j), t_val[nnz] (float32).
+ * workspace >= grf_transpose_workspace_bytes(n_bands * n_cols). */
+int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
+                             const int32_t *idx, const float *val, int64_t *t_ptr, int32_t *t_row, float *t_val,
+                             void *workspace, size_t workspace_bytes, grf_stream_t stream);
+size_t grf_transpose_workspace_bytes(int64_t n_buckets);
+
+/* ---------------------------------------------------------------------- Gram
+ * Replaces `Phi @ Phi.T` of fast_grf_kernel_general.py:55 (sparse) and :39 (dense).
+ * Sparse path: K[r, :] for rows r in [row_begin, row_end) of Phi (compact CSR,
+ * float32 values) against the banded transpose of the FULL Phi.  K is
+ * float32, row-major with leading dimension ldk (>= n_cols of K = n_rows_total),
+ * K row (r - row_begin) is written.  band_width must equal the transpose's
+ * (multiple of 16, <= 8192); one workgroup computes 4 bands of one row with a
+ * fixed summation order, so K is bit-reproducible run to run and across row
+ * splits (multi-GPU). */
+int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
+                        const float *val, int64_t band_width, const int64_t *t_ptr, const int32_t *t_row,
+                        const float *t_val, float *K, int64_t ldk, grf_stream_t stream);
+
+/* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
+ * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */
+int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                       grf_stream_t stream);
+
+/* CSR (float32) -> dense float32 [n_rows x lda], zero filled. */
+int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,
+                    int64_t lda, grf_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRF_H */

@@ -1,0 +1,276 @@
+"""GPU parity: every HIP stage against the CPU oracle (and, through it, the reference).
+
+Tolerances
+  * Laplacian, walk slots, step rows, Phi (fp64): bit-exact.
+  * K = Phi Phi^T in float32 against the fp64 oracle: |dK_ij| <= 3e-5 * (|Phi| |Phi|^T)_ij
+    elementwise (fp32 rounding of Phi plus an fp32 sum of at most a few hundred
+    products), and relative Frobenius error <= 1e-6.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from golden_util import csr, same_csr
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from grf_amd.engine import GRFEngine
+    return GRFEngine("cuda:0")
+
+
+def er_graph(n, avg_deg, seed, weighted=False):
+    r = np.random.default_rng(seed)
+    m = int(n * avg_deg / 2)
+    u = r.integers(0, n, m)
+    v = r.integers(0, n, m)
+    keep = u != v
+    u, v = u[keep], v[keep]
+    w = r.uniform(0.2, 3.0, len(u)) if weighted else np.ones(len(u))
+    A = sp.coo_matrix((w, (u, v)), shape=(n, n)).tocsr()
+    A = (A + A.T).tocsr()
+    if not weighted:
+        A.data[:] = 1.0
+    A.sum_duplicates()
+    A.sort_indices()
+    return A
+
+
+def bit_equal(a, b):
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+def slots_equal(gpu, ora):
+    gn, gl = gpu.node.cpu().numpy(), gpu.load.cpu().numpy()
+    on, ol = ora
+    if not np.array_equal(gn, on):
+        return False
+    mask = on >= 0
+    return bit_equal(gl[mask], ol[mask])
+
+
+def gram_close(K, phi64, rows=None):
+    Kref = O.gram_rows(phi64, *(rows or (0, phi64.shape[0])))
+    absphi = abs(phi64)
+    bound = O.gram_rows(absphi, *(rows or (0, phi64.shape[0])))
+    err = np.abs(np.asarray(K, np.float64) - Kref)
+    ok_elem = bool(np.all(err <= 3e-5 * bound + 1e-30))
+    fro = np.linalg.norm(err) / max(np.linalg.norm(Kref), 1e-300)
+    return ok_elem and fro <= 1e-6, fro
+
+
+# ----------------------------------------------------------------- Laplacians
+def test_laplacian_sparse_golden(eng, golden):
+    d = golden("small_graphs")
+    for name in d["names"]:
+        A = d[f"{name}_A"]
+        L = eng.laplacian(sp.csr_matrix(A)).to_scipy()
+        assert same_csr(L, csr(d, f"{name}_Lsp", A.shape[0])), name
+
+
+def test_laplacian_sparse_random(eng):
+    for seed, weighted in [(0, False), (1, True), (2, True)]:
+        A = er_graph(3000, 12, seed, weighted)
+        A = A.tolil()
+        A[5, :] = 0
+        A[:, 5] = 0
+        A = A.tocsr()
+        A.eliminate_zeros()
+        ref, _ = O.laplacian_sparse(A)
+        got = eng.laplacian(A).to_scipy()
+        assert same_csr(got, ref), seed
+
+
+def test_laplacian_dense_modes(eng, golden):
+    d = golden("small_graphs")
+    for name in d["names"]:
+        A = d[f"{name}_A"]
+        for mode, key, ref_mode in ((1, "Ld", 0), (2, "Lnp", 1), (3, "Lcomb", 2)):
+            G = eng.walk_matrix_dense(A, mode).to_scipy()
+            ip, ix, dx = O.dense_to_walk_csr(d[f"{name}_{key}"])
+            assert np.array_equal(G.indptr, ip) and np.array_equal(G.indices, ix), (name, key)
+            assert bit_equal(G.data, dx), (name, key)
+    r = np.random.default_rng(3)
+    W = r.random((700, 700)) * (r.random((700, 700)) < 0.05)
+    W = W + W.T
+    for mode, ref_mode in ((1, 0), (2, 1), (3, 2)):
+        G = eng.walk_matrix_dense(W, mode).to_scipy()
+        ip, ix, dx = O.dense_to_walk_csr(O.laplacian_dense(W, ref_mode))
+        assert np.array_equal(G.indices, ix) and bit_equal(G.data, dx), mode
+
+
+# ---------------------------------------------------------------------- walks
+@pytest.mark.parametrize("rule", [0, 1, 2])
+def test_walk_philox_matches_oracle(eng, rule):
+    A = er_graph(2000, 10, 4)
+    Ls, _ = O.laplacian_sparse(A)
+    G = eng.laplacian(A)
+    ip, ix, dx = O._csr_arrays(Ls)
+    for m, p, L, seed in [(16, 0.1, 8, 7), (33, 0.3, 5, 2**40 + 3), (1, 0.0, 3, 0)]:
+        got = eng.walk(G, m, p, L, rng=1, seed=seed, load_rule=rule)
+        ref = O.walk_slots(ip, ix, dx, m, p, L, rng=O.RNG_PHILOX, load_rule=rule, seed=seed)
+        assert slots_equal(got, ref), (m, p, L, seed)
+
+
+def test_walk_philox_shard_invariant(eng):
+    A = er_graph(1500, 8, 5)
+    G = eng.laplacian(A)
+    full = eng.walk(G, 24, 0.15, 6, rng=1, seed=99)
+    a = eng.walk(G, 24, 0.15, 6, rng=1, seed=99, src_begin=0, src_end=700)
+    b = eng.walk(G, 24, 0.15, 6, rng=1, seed=99, src_begin=700, src_end=1500)
+    import torch
+    assert torch.equal(full.node, torch.cat([a.node, b.node]))
+    mask = full.node >= 0
+    assert torch.equal(full.load[mask], torch.cat([a.load, b.load])[mask])
+
+
+@pytest.mark.parametrize("n_chunks", [1, 3, 8, 64])
+def test_walk_pcg64_matches_oracle(eng, n_chunks):
+    A = er_graph(800, 9, 6, weighted=True)
+    Ls, _ = O.laplacian_sparse(A)
+    G = eng.laplacian(A)
+    ip, ix, dx = O._csr_arrays(Ls)
+    got = eng.walk(G, 20, 0.2, 6, rng=0, seed=42, n_chunks=n_chunks)
+    ref = O.walk_slots(ip, ix, dx, 20, 0.2, 6, rng=O.RNG_PCG64, n_chunks=n_chunks, seed=42)
+    assert slots_equal(got, ref)
+
+
+def test_pcg64_sampler_reproduces_reference_golden(eng, golden):
+    """GPU reference-stream mode gives the reference's step matrices bit-for-bit."""
+    d = golden("small_graphs")
+    for name in d["names"]:
+        n = d[f"{name}_A"].shape[0]
+        Ls = csr(d, f"{name}_Lsp", n)
+        p = 0.0 if name == "perm12" else 0.2
+        G = eng.to_device(Ls)
+        for nproc in (1, 3, 8):
+            for seed in (None, 7):
+                slots = eng.walk(G, 20, p, 4, rng=0, seed=(seed or 42), n_chunks=nproc)
+                mats = eng.step_matrices(eng.steps(slots, norm=1))
+                for l, M in enumerate(mats):
+                    assert same_csr(M.to_scipy(), csr(d, f"{name}_sp_n{nproc}_s{seed}_l{l}", n)), (name, nproc, l)
+
+
+def test_cora_m128_reference_digests(eng, golden):
+    from golden_util import digest
+    d = golden("cora")
+    n = len(d["A_indptr"]) - 1
+    G = eng.laplacian(csr(d, "A", n))
+    assert digest(G.to_scipy()) == str(d["L_digest"][0])
+    slots = eng.walk(G, 128, 0.1, 8, rng=0, seed=42, n_chunks=8)
+    mats = eng.step_matrices(eng.steps(slots, norm=1))
+    assert [digest(M.to_scipy()) for M in mats] == [str(x) for x in d["m128_digests"]]
+    f = np.array([(-1.0) ** l / (2.0 ** l * float(np.prod(np.arange(1, l + 1)))) for l in range(8)])
+    phi = eng.compact(eng.features(slots, f))
+    assert digest(phi.to_scipy()) == str(d["m128_phi_digest"][0])
+    K = eng.gram(phi, "sparse").cpu().numpy()
+    np.testing.assert_allclose(K[:16], d["m128_K_rows0_16"], rtol=3e-5, atol=1e-6)
+    np.testing.assert_allclose(np.diag(K), d["m128_K_diag"], rtol=3e-5)
+    Kd = eng.gram(phi, "dense").cpu().numpy()
+    np.testing.assert_allclose(Kd[:16], d["m128_K_rows0_16"], rtol=3e-5, atol=1e-6)
+
+
+# -------------------------------------------------------------- steps / Phi
+@pytest.mark.parametrize("m,L,p", [(16, 8, 0.1), (128, 8, 0.1), (50, 3, 0.1), (300, 4, 0.05), (7, 20, 0.02)])
+def test_steps_and_phi_bitexact(eng, m, L, p):
+    A = er_graph(600, 7, m + L)
+    Ls, _ = O.laplacian_sparse(A)
+    G = eng.laplacian(A)
+    slots = eng.walk(G, m, p, L, rng=1, seed=5)
+    node, load = slots.node.cpu().numpy(), slots.load.cpu().numpy()
+    load = np.where(node >= 0, load, 0.0)
+    f = np.random.default_rng(m).standard_normal(L + 1)
+    for norm in (0, 1):
+        ref_steps = O.reduce_steps(node, load, norm)
+        st = eng.steps(slots, norm)
+        mats = eng.step_matrices(st)
+        for l in range(L):
+            assert same_csr(mats[l].to_scipy(), ref_steps[l]), (norm, l)
+        ref_phi = O.phi_sparse(ref_steps, f[:L - 1])
+        got = eng.compact(eng.phi(st, f[:L - 1])).to_scipy()
+        assert same_csr(got, ref_phi), norm
+        if m * L <= 4096:
+            fused = eng.compact(eng.phi_fused(slots, f[:L - 1], norm)).to_scipy()
+            assert same_csr(fused, ref_phi), norm
+
+
+def test_steps_dense_tensor(eng):
+    A = er_graph(200, 6, 11)
+    G = eng.laplacian(A)
+    slots = eng.walk(G, 12, 0.2, 4, rng=1, seed=1)
+    st = eng.steps(slots, 0)
+    F = eng.steps_dense(st).cpu().numpy()
+    mats = [M.to_scipy().toarray() for M in eng.step_matrices(st)]
+    for l in range(4):
+        assert bit_equal(F[:, :, l], mats[l])
+
+
+# ----------------------------------------------------------------------- Gram
+@pytest.mark.parametrize("n,deg,m,L,bw", [(1000, 8, 32, 6, 64), (5000, 10, 64, 8, 256), (3000, 4, 16, 5, 4096), (777, 5, 8, 3, 16)])
+def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
+    A = er_graph(n, deg, n)
+    G = eng.laplacian(A)
+    slots = eng.walk(G, m, 0.1, L, rng=1, seed=3)
+    f = [(-1.0) ** l / 2 ** l for l in range(L)]
+    phi = eng.compact(eng.features(slots, f))
+    tr = eng.transpose_banded(phi, bw)
+    K = eng.gram_sparse(phi, tr).cpu().numpy()
+    ok, fro = gram_close(K, phi.to_scipy())
+    assert ok, fro
+    # row block, and a rerun: bit-identical (fixed summation order)
+    Kb = eng.gram_sparse(phi, tr, 17, 300).cpu().numpy()
+    assert np.array_equal(Kb, K[17:300])
+    assert np.array_equal(eng.gram_sparse(phi, eng.transpose_banded(phi, bw)).cpu().numpy(), K)
+
+
+@pytest.mark.parametrize("n", [1, 31, 128, 1000, 2708])
+def test_gram_dense_mfma_vs_oracle(eng, n):
+    A = er_graph(max(n, 2), 6, n + 1)[:n, :n]
+    G = eng.laplacian(A)
+    slots = eng.walk(G, 24, 0.15, 5, rng=1, seed=2)
+    phi = eng.compact(eng.features(slots, [1.0, -0.5, 0.25, -0.125, 0.0625]))
+    K = eng.gram(phi, "dense").cpu().numpy()
+    ok, fro = gram_close(K, phi.to_scipy())
+    assert ok, fro
+
+
+def test_gram_dense_asymmetric_layout(eng):
+    """A = I-style check with an asymmetric operand: catches row/col swaps in the MFMA C map."""
+    import torch
+    n = 160
+    Ad = np.zeros((n, 176), np.float32)
+    r = np.random.default_rng(0)
+    Ad[:, :150] = r.standard_normal((n, 150)).astype(np.float32)
+    At = torch.from_numpy(Ad).cuda()
+    K = eng.gram_dense(At, 150).cpu().numpy()
+    ref = Ad.astype(np.float64) @ Ad.astype(np.float64).T
+    np.testing.assert_allclose(K, ref, rtol=1e-5, atol=1e-4)
+
+
+def test_full_pipeline_c2_scale(eng):
+    """ER N=10k (C2-like) -- Philox walks vs oracle on a source sample, K rows vs oracle, symmetry."""
+    n = 10000
+    A = er_graph(n, 10, 2024)
+    G = eng.laplacian(A)
+    slots = eng.walk(G, 128, 0.1, 8, rng=1, seed=42)
+    Ls, _ = O.laplacian_sparse(A)
+    ip, ix, dx = O._csr_arrays(Ls)
+    ref = O.walk_slots(ip, ix, dx, 128, 0.1, 8, rng=O.RNG_PHILOX, seed=42, begin=0, end=n)
+    assert slots_equal(slots, ref)
+    f = [(-1.0) ** l / (2.0 ** l * float(np.prod(np.arange(1, l + 1)))) for l in range(8)]
+    phi = eng.compact(eng.features(slots, f))
+    node, load = ref
+    ref_phi = O.phi_sparse(O.reduce_steps(node, np.where(node >= 0, load, 0.0), 1), f)
+    assert same_csr(phi.to_scipy(), ref_phi)
+    K = eng.gram(phi, "sparse")
+    rows = np.r_[0:64, 5000:5064, n - 64:n]
+    ok, fro = gram_close(K[rows[:64]].cpu().numpy(), ref_phi, (0, 64))
+    assert ok, fro
+    Kc = K.cpu().numpy()
+    sub = Kc[:2000, :2000]
+    assert np.max(np.abs(sub - sub.T)) <= 1e-5 * np.max(np.abs(sub))
