@@ -118,17 +118,25 @@ __global__ __launch_bounds__(256) void tr_count_kernel(int64_t n_rows, int64_t n
 
 __global__ __launch_bounds__(256) void tr_fill_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, const int64_t *ptr,
                                                       const int32_t *idx, const float *val, const int64_t *t_ptr,
-                                                      int32_t *cursor, int32_t *t_row, float *t_val) {
+                                                      int32_t *cursor, uint16_t *t_col, float *t_val,
+                                                      unsigned int *maxabs_bits) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n_rows) return;
     const int lane = threadIdx.x & 63;
-    const int64_t band_off = (row / bw) * n_cols;
+    const int64_t band = row / bw, band_off = band * n_cols;
+    const uint16_t jr = (uint16_t)(row - band * bw);
+    float mx = 0.f;
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) {
         int64_t b = band_off + idx[e];
         int64_t pos = t_ptr[b] + atomicAdd(&cursor[b], 1);
-        t_row[pos] = (int32_t)row;
+        t_col[pos] = jr;
         t_val[pos] = val[e];
+        mx = fmaxf(mx, fabsf(val[e]));
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    // non-negative floats order like their bit patterns
+    if (lane == 0 && mx > 0.f) atomicMax(maxabs_bits, __float_as_uint(mx));
 }
 
 }  // namespace grf
@@ -166,10 +174,12 @@ size_t grf_transpose_workspace_bytes(int64_t n_buckets) {
 }
 
 int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                             const int32_t *idx, const float *val, int64_t *t_ptr, int32_t *t_row, float *t_val,
-                             void *workspace, size_t workspace_bytes, grf_stream_t stream) {
-    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && ptr && idx && val && t_ptr && t_row && t_val,
+                             const int32_t *idx, const float *val, int64_t *t_ptr, uint16_t *t_col, float *t_val,
+                             float *t_maxabs, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && ptr && idx && val && t_ptr && t_col && t_val &&
+                    t_maxabs,
                 GRF_EINVAL, "grf_transpose_banded: bad arguments");
+    GRF_REQUIRE(band_width <= 65536, GRF_EUNSUPPORTED, "grf_transpose_banded: band_width must be <= 65536");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
     GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,
                 "grf_transpose_banded: workspace too small (%zu < %zu)", workspace_bytes,
@@ -179,6 +189,7 @@ int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width,
     size_t a = ((size_t)nbk * sizeof(int32_t) + 255) & ~(size_t)255;
     void *scan_ws = (char *)workspace + a;
     GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));
+    GRF_CHECK_HIP(hipMemsetAsync(t_maxabs, 0, sizeof(float), st));
     if (n_rows > 0) {
         tr_count_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, st>>>(n_rows, n_cols, band_width, ptr, idx,
                                                                           cnt);
@@ -189,7 +200,8 @@ int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width,
     GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));
     if (n_rows > 0) {
         tr_fill_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, st>>>(n_rows, n_cols, band_width, ptr, idx, val,
-                                                                         t_ptr, cnt, t_row, t_val);
+                                                                         t_ptr, cnt, t_col, t_val,
+                                                                         reinterpret_cast<unsigned int *>(t_maxabs));
         GRF_CHECK_LAUNCH("tr_fill_kernel");
     }
     return GRF_OK;

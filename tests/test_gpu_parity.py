@@ -2,9 +2,12 @@
 
 Tolerances
   * Laplacian, walk slots, step rows, Phi (fp64): bit-exact.
-  * K = Phi Phi^T in float32 against the fp64 oracle: |dK_ij| <= 3e-5 * (|Phi| |Phi|^T)_ij
-    elementwise (fp32 rounding of Phi plus an fp32 sum of at most a few hundred
-    products), and relative Frobenius error <= 1e-6.
+  * K = Phi Phi^T in float32 against the fp64 oracle, elementwise
+      |dK_ij| <= 3e-5 (|Phi| |Phi|^T)_ij + 1e-12 max_k|Phi_ik| max|Phi|
+    (fp32 rounding of Phi's entries, fp32 output rounding, and the sparse kernel's
+    int64 fixed-point resolution of 2^-50 per term), and relative Frobenius error <= 1e-6.  The sparse Gram kernel is
+    much tighter than that (fp32 rounding of Phi's entries, then an exact
+    fixed-point sum rounded once), the MFMA dense Gram is an fp32 FMA chain.
 """
 import numpy as np
 import pytest
@@ -55,11 +58,15 @@ def slots_equal(gpu, ora):
 
 
 def gram_close(K, phi64, rows=None):
-    Kref = O.gram_rows(phi64, *(rows or (0, phi64.shape[0])))
+    r0, r1 = rows or (0, phi64.shape[0])
+    Kref = O.gram_rows(phi64, r0, r1)
     absphi = abs(phi64)
-    bound = O.gram_rows(absphi, *(rows or (0, phi64.shape[0])))
+    bound = O.gram_rows(absphi, r0, r1)
+    # fixed-point resolution of the sparse Gram kernel: 2^-50 max_k|Phi_ik| max|Phi| per term
+    rowmax = np.asarray(absphi[r0:r1].max(axis=1).todense()).ravel()
+    fx = 1e-12 * rowmax[:, None] * absphi.max()
     err = np.abs(np.asarray(K, np.float64) - Kref)
-    ok_elem = bool(np.all(err <= 3e-5 * bound + 1e-30))
+    ok_elem = bool(np.all(err <= 3e-5 * bound + fx + 1e-30))
     fro = np.linalg.norm(err) / max(np.linalg.norm(Kref), 1e-300)
     return ok_elem and fro <= 1e-6, fro
 
@@ -211,7 +218,7 @@ def test_steps_dense_tensor(eng):
 
 
 # ----------------------------------------------------------------------- Gram
-@pytest.mark.parametrize("n,deg,m,L,bw", [(1000, 8, 32, 6, 64), (5000, 10, 64, 8, 256), (3000, 4, 16, 5, 4096), (777, 5, 8, 3, 16)])
+@pytest.mark.parametrize("n,deg,m,L,bw", [(1000, 8, 32, 6, 64), (5000, 10, 64, 8, 256), (3000, 4, 16, 5, 8192), (777, 5, 8, 3, 128), (20000, 10, 32, 6, 4096)])
 def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
     A = er_graph(n, deg, n)
     G = eng.laplacian(A)
