@@ -4,9 +4,10 @@
 //   efficient_graph_gp_sparse/graph_kernels_sparse/fast_grf_kernel_general.py:55 (scipy SpGEMM)
 //   efficient_graph_gp/graph_kernels/fast_grf_kernel_general.py:39 (dense BLAS)
 //
-// Sparse path (Gustavson, output-stationary in LDS): one workgroup owns the
-// tile K[row, j0 : j0 + W] (W = one band of the banded transpose, 8192 columns =
-// 64 KB of int64 accumulator, 2 workgroups per CU).  For every nonzero
+// Sparse path (Gustavson, output-stationary in LDS): one wave owns the
+// tile K[row, j0 : j0 + W] (W = one band of the banded transpose, ~1k columns =
+// 8 KB of int64 accumulator; bands pinned to XCDs so each band's Phi^T slice
+// stays in that XCD's L2).  For every nonzero
 // Phi[row, k] it streams bucket (band, k) -- the entries Phi[j, k] with j in the
 // band, stored as (uint16 j - j0, float32 value) -- and adds the exact product
 // Phi[row,k]*Phi[j,k] in int64 fixed point with ds_add_u64.  Measured on gfx950
@@ -18,15 +19,15 @@
 //
 // Dense path: LDS-tiled fp32 MFMA (v_mfma_f32_32x32x2f32, exact f32 FMA chain),
 // 128x128 tile per 256-thread workgroup, 2x2 waves of 64x64.
+#include <stdlib.h>
+
 #include "grf_block.h"
 
 namespace grf {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGramThreads = 256;  // 4 waves share one tile
-constexpr int kChunk = 1024;       // stream positions covered by one marker chunk
-constexpr int kGramUnroll = 4;     // windows of 64 tuples in flight per wave
+constexpr int kChunk = 1024;  // stream positions covered by one marker chunk
 
 // inclusive max-scan over the 64 lanes with DPP (VALU only, no LDS traffic)
 __device__ inline int wave_incl_max(int v) {
@@ -45,47 +46,121 @@ __device__ inline long long fx_round(double x) {
     return (long long)(__double_as_longlong(x + magic) - __double_as_longlong(magic));
 }
 
-// One workgroup = one tile K[row, j0 : j0 + W] (W = a band of the banded
-// transpose).  Accumulation is exact int64 fixed point with a per-row power-of-two
-// scale S = 2^(50 - ceil(log2(sum_k |Phi[row,k]| * max|Phi|))), so every partial sum
-// stays below 2^51: the result is the exactly rounded fixed-point sum, independent of
-// the order of the adds (ds_add_u64) and therefore of scheduling, GPU count, row split.
-// The 4 waves pull batches of 64 nonzeros of the row from an LDS counter; each batch's
-// buckets are flattened into one lane-dense stream whose bucket index per position is
-// recovered from bucket-start markers (one u8 LDS read) and a DPP max-scan.
-// Grid is band-major so the Phi^T slice in use stays resident in the Infinity Cache.
-__global__ __launch_bounds__(kGramThreads, 2) void gram_sparse_kernel(
-    int64_t n_total, int64_t row_begin, int64_t n_rows, int64_t W, const int64_t *__restrict__ ptr,
+// Per-wave state of one flattened batch stream (see gram_sparse_kernel).
+struct GramStream {
+    const unsigned char *mark;  // bucket-start markers of the current chunk (LDS)
+    const int64_t *tbase;       // per bucket: pair index - stream position (LDS)
+    const double *ascale;       // per bucket: Phi[row,k] * S (LDS)
+    const uint4 *t_pair;        // Phi^T record pairs (global)
+    unsigned long long *acc;    // tile accumulator (LDS)
+};
+
+// NW windows of 64 pairs starting at stream position w0 (chunk base c0, chunk end cend).
+// TAIL: positions >= cend are masked (they fetch pair 0 and add exactly 0).
+template <int NW, bool TAIL>
+__device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, int32_t c0, int32_t cend, int lane,
+                                             int &carry) {
+    int m[NW];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+        const int32_t p = w0 + u * 64 + lane;
+        m[u] = (!TAIL || p < cend) ? (int)g.mark[p - c0] : 255;
+    }
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+        int v = m[u] == 255 ? -1 : m[u];
+        if (lane == 0) v = max(v, carry);
+        v = wave_incl_max(v);
+        carry = __builtin_amdgcn_readlane(v, 63);
+        m[u] = v < 0 ? 0 : v;
+    }
+    int64_t pos[NW];
+    double sc[NW];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+        pos[u] = g.tbase[m[u]] + (w0 + u * 64 + lane);
+        sc[u] = g.ascale[m[u]];
+    }
+    if (TAIL) {
+#pragma unroll
+        for (int u = 0; u < NW; ++u) {
+            const bool ok = w0 + u * 64 + lane < cend;
+            pos[u] = ok ? pos[u] : 0;  // pair 0 always exists when the stream is non-empty
+            sc[u] = ok ? sc[u] : 0.0;
+        }
+    }
+    // phase order pinned: all descriptor reads, then all gathers in flight, then the adds
+    __builtin_amdgcn_sched_barrier(0);
+    uint4 rec[NW];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) rec[u] = g.t_pair[pos[u]];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+        const long long q0 = fx_round(sc[u] * (double)__uint_as_float(rec[u].y));
+        const long long q1 = fx_round(sc[u] * (double)__uint_as_float(rec[u].w));
+        __hip_atomic_fetch_add(&g.acc[rec[u].x], (unsigned long long)q0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&g.acc[rec[u].z], (unsigned long long)q1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// One workgroup of kWaves waves = one tile K[row, j0 : j0 + W] (W = a band of the
+// banded transpose).  Accumulation is exact int64 fixed point with a per-row
+// power-of-two scale S chosen so that every term |Phi[row,k] Phi[j,k]| S < 2^51 and
+// the sum of all terms < 2^62: each exact fp64 product is rounded once to an integer
+// and the integer sum does not depend on the order of the adds (ds_add_u64) -- nor on
+// scheduling, GPU count or row split.  Resolution 1/S <= 2^-50 max_k|Phi[row,k]| max|Phi|.
+// Phi^T buckets hold (col, value) records padded to pairs; the waves pull batches of
+// 128 nonzeros of the row from an LDS counter and flatten each batch's buckets into
+// one stream of record PAIRS (one 16-byte load fetches two records: the texture-address
+// path, not bandwidth, bounds short scattered segments).  The bucket of each pair comes
+// from bucket-start markers (one u8 LDS read) and a DPP max-scan.
+// Optional placement (speed only, kXcd): blocks b and b+8 are dealt to the same XCD, so
+// block b % 8 = x works on bands x, x+8, ...: each XCD's L2 holds one band's slice.
+template <int kWaves, int kGramUnroll, bool kXcd>
+__global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
+    int64_t n_total, int64_t row_begin, int64_t n_rows, int64_t W, int64_t nb, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const int64_t *__restrict__ t_ptr,
-    const uint16_t *__restrict__ t_col, const float *__restrict__ t_val, const float *__restrict__ maxabs,
-    float *__restrict__ K, int64_t ldk) {
+    const uint4 *__restrict__ t_pair, const float *__restrict__ maxabs, float *__restrict__ K, int64_t ldk) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    unsigned char *mark_all = reinterpret_cast<unsigned char *>(acc + W);       // [4][kChunk]
-    int64_t *tb_all = reinterpret_cast<int64_t *>(mark_all + 4 * kChunk);       // [4][64]
-    double *as_all = reinterpret_cast<double *>(tb_all + 4 * 64);              // [4][64]
-    double *red = as_all + 4 * 64;                                             // [8]
-    int *next_batch = reinterpret_cast<int *>(red + 8);                        // [1]
-    unsigned char *mark = mark_all + wave * kChunk;
-    int64_t *tbase = tb_all + wave * 64;
-    double *ascale = as_all + wave * 64;
+    unsigned char *mark = reinterpret_cast<unsigned char *>(acc + W) + wave * kChunk;      // [kWaves][kChunk]
+    int64_t *tbase = reinterpret_cast<int64_t *>(reinterpret_cast<unsigned char *>(acc + W) + kWaves * kChunk) +
+                     wave * 128;                                                          // [kWaves][128]
+    double *ascale = reinterpret_cast<double *>(reinterpret_cast<int64_t *>(reinterpret_cast<unsigned char *>(
+                         acc + W) + kWaves * kChunk) + kWaves * 128) + wave * 128;         // [kWaves][128]
+    double *red = reinterpret_cast<double *>(reinterpret_cast<int64_t *>(reinterpret_cast<unsigned char *>(
+                      acc + W) + kWaves * kChunk) + 2 * kWaves * 128);                    // [2 * kWaves]
+    int *next_batch = reinterpret_cast<int *>(red + 2 * kWaves);
 
     const int64_t bid = blockIdx.x;
-    const int64_t band = bid / n_rows, r = bid - band * n_rows, row = row_begin + r;
+    int64_t band, r;
+    if (kXcd) {
+        const int64_t xcd = bid & 7, s = bid >> 3;
+        const int64_t phase = s / n_rows;
+        r = s - phase * n_rows;
+        band = xcd + 8 * phase;
+        if (band >= nb) return;  // uniform over the workgroup
+    } else {
+        band = bid / n_rows;
+        r = bid - band * n_rows;
+    }
+    const int64_t row = row_begin + r;
     const int64_t j0 = band * W;
     const int64_t wlen = (n_total - j0) < W ? (n_total - j0) : W;
     const int64_t e0 = ptr[row], e1 = ptr[row + 1];
 
-    // zero the accumulator, sum |Phi[row, :]| for the scale
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     u64x2 *acc2 = reinterpret_cast<u64x2 *>(acc);
     const u64x2 z2 = {0ull, 0ull};
-    for (int64_t i = tid; i < (wlen + 1) / 2; i += kGramThreads) acc2[i] = z2;
+    for (int64_t i = tid; i < (wlen + 1) / 2; i += 64 * kWaves) acc2[i] = z2;
     // scale: every term |Phi[row,k] Phi[j,k]| S < 2^51 (exact magic-number rounding) and
     // the sum of all |terms| S < 2^62 (no int64 overflow)
     double sa = 0.0;
     float ma = 0.f;
-    for (int64_t e = e0 + tid; e < e1; e += kGramThreads) {
+    for (int64_t e = e0 + tid; e < e1; e += 64 * kWaves) {
         const float a = fabsf(val[e]);
         sa += (double)a;
         ma = fmaxf(ma, a);
@@ -93,90 +168,84 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_sparse_kernel(
     sa = wave_sum<double>(sa);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) ma = fmaxf(ma, __shfl_xor(ma, off, 64));
-    if (lane == 0) { red[wave] = sa; red[4 + wave] = (double)ma; }
-    if (tid == 0) *next_batch = 0;
-    __syncthreads();
+    if (kWaves > 1) {
+        if (lane == 0) { red[wave] = sa; red[kWaves + wave] = (double)ma; }
+        if (tid == 0) *next_batch = 0;
+        __syncthreads();
+        sa = 0.0;
+        double mm = 0.0;
+        for (int w = 0; w < kWaves; ++w) { sa += red[w]; mm = fmax(mm, red[kWaves + w]); }
+        ma = (float)mm;
+    }
     const double mx = (double)maxabs[0];
-    const double B = (red[0] + red[1] + red[2] + red[3]) * mx;
-    const double T = fmax(fmax(red[4], red[5]), fmax(red[6], red[7])) * mx;
+    const double B = sa * mx, T = (double)ma * mx;
     const int eB = B > 0.0 ? ilogb(B) + 1 : 0;  // B < 2^eB
     const int eT = T > 0.0 ? ilogb(T) + 1 : 0;  // every term < 2^eT
     const int sh = min(51 - eT, 62 - eB);
     const double S = ldexp(1.0, sh), inv_S = ldexp(1.0, -sh);
 
+    const GramStream gs{mark, tbase, ascale, t_pair, acc};
     const int64_t boff = band * n_total;
-    for (;;) {
-        int bi = 0;
-        if (lane == 0) bi = atomicAdd(next_batch, 1);
-        bi = __builtin_amdgcn_readfirstlane(bi);
-        const int64_t g0 = e0 + (int64_t)bi * 64;
-        if (g0 >= e1) break;
-        const int64_t e = g0 + lane;
-        int32_t cnt = 0;
-        int64_t t0 = 0;
-        double as = 0.0;
-        if (e < e1) {
-            const int32_t k = idx[e];
-            as = (double)val[e] * S;
-            t0 = t_ptr[boff + k];
-            cnt = (int32_t)(t_ptr[boff + k + 1] - t0);
+    for (int it = 0;; ++it) {
+        int bi = it;
+        if (kWaves > 1) {
+            if (lane == 0) bi = atomicAdd(next_batch, 1);
+            bi = __builtin_amdgcn_readfirstlane(bi);
         }
-        const int32_t incl = wave_inclusive_scan<int32_t>(cnt);
-        const int32_t excl = incl - cnt;
-        const int32_t total = __shfl(incl, 63, 64);
-        tbase[lane] = t0 - excl;
-        ascale[lane] = as;
+        const int64_t g0 = e0 + (int64_t)bi * 128;
+        if (g0 >= e1) break;
+        int32_t cnt[2], excl[2];
+        int64_t t0[2];
+        double as[2];
+        int32_t k[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t e = g0 + h * 64 + lane;
+            k[h] = e < e1 ? idx[e] : -1;
+            as[h] = e < e1 ? (double)val[e] * S : 0.0;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            t0[h] = k[h] >= 0 ? t_ptr[boff + k[h]] : 0;
+            cnt[h] = k[h] >= 0 ? (int32_t)((t_ptr[boff + k[h] + 1] - t0[h]) >> 1) : 0;  // pairs
+        }
+        const int32_t inc0 = wave_inclusive_scan<int32_t>(cnt[0]);
+        const int32_t tot0 = __shfl(inc0, 63, 64);
+        const int32_t inc1 = wave_inclusive_scan<int32_t>(cnt[1]) + tot0;
+        const int32_t total = __shfl(inc1, 63, 64);
+        excl[0] = inc0 - cnt[0];
+        excl[1] = inc1 - cnt[1];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            tbase[h * 64 + lane] = (t0[h] >> 1) - excl[h];  // pair index = tbase + stream position
+            ascale[h * 64 + lane] = as[h];
+        }
         int carry = -1;
         for (int32_t c0 = 0; c0 < total; c0 += kChunk) {
-            reinterpret_cast<uint4 *>(mark)[lane] = make_uint4(~0u, ~0u, ~0u, ~0u);  // 64 x 16 B = kChunk
-            if (cnt > 0 && excl >= c0 && excl < c0 + kChunk) mark[excl - c0] = (unsigned char)lane;
+#pragma unroll
+            for (int i = 0; i < kChunk / 1024; ++i)
+                reinterpret_cast<uint4 *>(mark)[i * 64 + lane] = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (cnt[h] > 0 && excl[h] >= c0 && excl[h] < c0 + kChunk)
+                    mark[excl[h] - c0] = (unsigned char)(h * 64 + lane);
             __builtin_amdgcn_wave_barrier();
             const int32_t cend = (total - c0) < kChunk ? total : c0 + kChunk;
-            for (int32_t w0 = c0; w0 < cend; w0 += 64 * kGramUnroll) {
-                int bk[kGramUnroll];
-#pragma unroll
-                for (int u = 0; u < kGramUnroll; ++u) {
-                    const int32_t p = w0 + u * 64 + lane;
-                    int m = p < cend ? (int)mark[p - c0] : 255;
-                    m = m == 255 ? -1 : m;
-                    if (lane == 0) m = max(m, carry);
-                    m = wave_incl_max(m);
-                    carry = __builtin_amdgcn_readlane(m, 63);
-                    bk[u] = m;
-                }
-                int64_t pos[kGramUnroll];
-                double sc[kGramUnroll];
-#pragma unroll
-                for (int u = 0; u < kGramUnroll; ++u) {
-                    const int32_t p = w0 + u * 64 + lane;
-                    const bool ok = p < cend;
-                    const int b = bk[u] < 0 ? 0 : bk[u];
-                    pos[u] = ok ? tbase[b] + p : 0;  // tuple 0 always exists when total > 0
-                    sc[u] = ok ? ascale[b] : 0.0;
-                }
-                uint32_t jj[kGramUnroll];
-                float v[kGramUnroll];
-#pragma unroll
-                for (int u = 0; u < kGramUnroll; ++u) jj[u] = t_col[pos[u]];
-#pragma unroll
-                for (int u = 0; u < kGramUnroll; ++u) v[u] = t_val[pos[u]];
-#pragma unroll
-                for (int u = 0; u < kGramUnroll; ++u) {
-                    const long long q = fx_round(sc[u] * (double)v[u]);  // exact product, one rounding
-                    __hip_atomic_fetch_add(&acc[jj[u]], (unsigned long long)q, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
+            int32_t w0 = c0;
+            for (; w0 + 64 * kGramUnroll <= cend; w0 += 64 * kGramUnroll)
+                gram_windows<kGramUnroll, false>(gs, w0, c0, cend, lane, carry);
+            for (; w0 < cend; w0 += 64) gram_windows<1, true>(gs, w0, c0, cend, lane, carry);
             __builtin_amdgcn_wave_barrier();
         }
     }
-    __syncthreads();
+    if (kWaves > 1) __syncthreads();
+    else __builtin_amdgcn_wave_barrier();
 
     float *krow = K + r * ldk + j0;
     if ((ldk & 3) == 0 && (j0 & 3) == 0) {
         const int64_t n4 = wlen / 4;
         f32x4 *k4 = reinterpret_cast<f32x4 *>(krow);
-        for (int64_t i = tid; i < n4; i += kGramThreads) {
+        for (int64_t i = tid; i < n4; i += 64 * kWaves) {
             const u64x2 a = acc2[2 * i], b = acc2[2 * i + 1];
             f32x4 o;
             o[0] = (float)((double)(long long)a[0] * inv_S);
@@ -185,10 +254,10 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_sparse_kernel(
             o[3] = (float)((double)(long long)b[1] * inv_S);
             __builtin_nontemporal_store(o, &k4[i]);
         }
-        for (int64_t i = n4 * 4 + tid; i < wlen; i += kGramThreads)
+        for (int64_t i = n4 * 4 + tid; i < wlen; i += 64 * kWaves)
             krow[i] = (float)((double)(long long)acc[i] * inv_S);
     } else {
-        for (int64_t i = tid; i < wlen; i += kGramThreads) krow[i] = (float)((double)(long long)acc[i] * inv_S);
+        for (int64_t i = tid; i < wlen; i += 64 * kWaves) krow[i] = (float)((double)(long long)acc[i] * inv_S);
     }
 }
 
@@ -268,22 +337,46 @@ extern "C" {
 #pragma GCC visibility push(default)
 
 int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
-                        const float *val, int64_t band_width, const int64_t *t_ptr, const uint16_t *t_col,
-                        const float *t_val, const float *t_maxabs, float *K, int64_t ldk, grf_stream_t stream) {
+                        const float *val, int64_t band_width, const int64_t *t_ptr, const uint32_t *t_rec,
+                        const float *t_maxabs, float *K, int64_t ldk, grf_stream_t stream) {
     GRF_REQUIRE(n_total >= 0 && 0 <= row_begin && row_begin <= row_end && row_end <= n_total && ptr && t_ptr && K &&
-                    t_maxabs,
+                    t_maxabs && t_rec,
                 GRF_EINVAL, "grf_gram_sparse: bad arguments");
+    GRF_REQUIRE(((uintptr_t)t_rec & 15) == 0, GRF_EINVAL, "grf_gram_sparse: t_rec must be 16-byte aligned");
     GRF_REQUIRE(ldk >= n_total, GRF_EINVAL, "grf_gram_sparse: ldk < n");
-    GRF_REQUIRE(band_width >= 64 && band_width % 64 == 0 && band_width <= 8192, GRF_EUNSUPPORTED,
-                "grf_gram_sparse: band_width must be a multiple of 64 in [64, 8192]");
+    GRF_REQUIRE(band_width >= 16 && band_width % 16 == 0 && band_width <= 8192, GRF_EUNSUPPORTED,
+                "grf_gram_sparse: band_width must be a multiple of 16 in [16, 8192]");
     const int64_t rows = row_end - row_begin;
     if (rows == 0 || n_total == 0) return GRF_OK;
     const int64_t nb = cdiv<int64_t>(n_total, band_width);
-    const int64_t tiles = rows * nb;
-    GRF_REQUIRE(tiles < (1ll << 31), GRF_EUNSUPPORTED, "grf_gram_sparse: too many tiles; split the row range");
-    const size_t lds = (size_t)band_width * 8 + 4 * kChunk + 4 * 64 * 8 + 4 * 64 * 8 + 8 * 8 + 16;
-    gram_sparse_kernel<<<(unsigned)tiles, kGramThreads, lds, S(stream)>>>(
-        n_total, row_begin, rows, band_width, ptr, idx, val, t_ptr, t_col, t_val, t_maxabs, K, ldk);
+    // tuning knobs (defaults = measured best on MI355X): waves per tile, unroll, XCD pinning
+    static const int knobs = [] {
+        const char *e = getenv("GRF_GRAM_UNROLL"), *x = getenv("GRF_GRAM_XCD"), *w = getenv("GRF_GRAM_WAVES");
+        const int u = e ? atoi(e) : 4, ww = w ? atoi(w) : 4;
+        return ((u == 2 || u == 4 || u == 8) ? u : 4) + (x && atoi(x) ? 100 : 0) + (ww == 1 ? 1000 : 0);
+    }();
+    const bool xcd = (knobs / 100) % 10 == 1;
+    const int unroll = knobs % 100, waves = knobs >= 1000 ? 1 : 4;
+    const int64_t tiles = xcd ? 8 * cdiv<int64_t>(nb, 8) * rows : nb * rows;
+    GRF_REQUIRE(tiles < (1ll << 32), GRF_EUNSUPPORTED, "grf_gram_sparse: too many tiles; split the row range");
+    const size_t lds = (size_t)band_width * 8 + waves * (kChunk + 128 * 8 + 128 * 8) + 2 * waves * 8 + 16;
+    const uint4 *t_pair = reinterpret_cast<const uint4 *>(t_rec);
+#define GRF_GRAM_LAUNCH(WV, U, X)                                                                                 \
+    gram_sparse_kernel<WV, U, X><<<(unsigned)tiles, 64 * WV, lds, S(stream)>>>(                                   \
+        n_total, row_begin, rows, band_width, nb, ptr, idx, val, t_ptr, t_pair, t_maxabs, K, ldk)
+#define GRF_GRAM_U(WV, X)                                                                                         \
+    switch (unroll) {                                                                                             \
+        case 2: GRF_GRAM_LAUNCH(WV, 2, X); break;                                                                 \
+        case 8: GRF_GRAM_LAUNCH(WV, 8, X); break;                                                                 \
+        default: GRF_GRAM_LAUNCH(WV, 4, X); break;                                                                \
+    }
+    if (waves == 1) {
+        if (xcd) { GRF_GRAM_U(1, true) } else { GRF_GRAM_U(1, false) }
+    } else {
+        if (xcd) { GRF_GRAM_U(4, true) } else { GRF_GRAM_U(4, false) }
+    }
+#undef GRF_GRAM_U
+#undef GRF_GRAM_LAUNCH
     GRF_CHECK_LAUNCH("gram_sparse_kernel");
     return GRF_OK;
 }

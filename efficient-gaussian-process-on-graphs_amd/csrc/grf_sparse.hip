@@ -116,27 +116,36 @@ __global__ __launch_bounds__(256) void tr_count_kernel(int64_t n_rows, int64_t n
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) atomicAdd(&cnt[band_off + idx[e]], 1);
 }
 
+__global__ void tr_pad_counts_kernel(int64_t n, int32_t *cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) cnt[i] += cnt[i] & 1;  // every bucket holds an even number of records
+}
+
 __global__ __launch_bounds__(256) void tr_fill_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, const int64_t *ptr,
                                                       const int32_t *idx, const float *val, const int64_t *t_ptr,
-                                                      int32_t *cursor, uint16_t *t_col, float *t_val,
-                                                      unsigned int *maxabs_bits) {
+                                                      int32_t *cursor, uint2 *t_rec, unsigned int *maxabs_bits) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n_rows) return;
     const int lane = threadIdx.x & 63;
     const int64_t band = row / bw, band_off = band * n_cols;
-    const uint16_t jr = (uint16_t)(row - band * bw);
+    const uint32_t jr = (uint32_t)(row - band * bw);
     float mx = 0.f;
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) {
-        int64_t b = band_off + idx[e];
-        int64_t pos = t_ptr[b] + atomicAdd(&cursor[b], 1);
-        t_col[pos] = jr;
-        t_val[pos] = val[e];
+        const int64_t b = band_off + idx[e];
+        const int64_t pos = t_ptr[b] + atomicAdd(&cursor[b], 1);
+        t_rec[pos] = make_uint2(jr, __float_as_uint(val[e]));
         mx = fmaxf(mx, fabsf(val[e]));
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
     // non-negative floats order like their bit patterns
     if (lane == 0 && mx > 0.f) atomicMax(maxabs_bits, __float_as_uint(mx));
+}
+
+// odd buckets get a (col 0, +0.0) pad record: adds exactly 0 in the Gram kernel
+__global__ void tr_pad_fill_kernel(int64_t n, const int64_t *t_ptr, const int32_t *cursor, uint2 *t_rec) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < n && (cursor[b] & 1)) t_rec[t_ptr[b] + cursor[b]] = make_uint2(0u, 0u);
 }
 
 }  // namespace grf
@@ -174,12 +183,11 @@ size_t grf_transpose_workspace_bytes(int64_t n_buckets) {
 }
 
 int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                             const int32_t *idx, const float *val, int64_t *t_ptr, uint16_t *t_col, float *t_val,
-                             float *t_maxabs, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
-    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && ptr && idx && val && t_ptr && t_col && t_val &&
-                    t_maxabs,
+                             const int32_t *idx, const float *val, int64_t *t_ptr, uint32_t *t_rec, float *t_maxabs,
+                             void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && ptr && idx && val && t_ptr && t_rec && t_maxabs,
                 GRF_EINVAL, "grf_transpose_banded: bad arguments");
-    GRF_REQUIRE(band_width <= 65536, GRF_EUNSUPPORTED, "grf_transpose_banded: band_width must be <= 65536");
+    GRF_REQUIRE(((uintptr_t)t_rec & 15) == 0, GRF_EINVAL, "grf_transpose_banded: t_rec must be 16-byte aligned");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
     GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,
                 "grf_transpose_banded: workspace too small (%zu < %zu)", workspace_bytes,
@@ -195,15 +203,20 @@ int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width,
                                                                           cnt);
         GRF_CHECK_LAUNCH("tr_count_kernel");
     }
+    tr_pad_counts_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, cnt);
+    GRF_CHECK_LAUNCH("tr_pad_counts_kernel");
     int32_t rc = scan_counts_i32(nbk, cnt, t_ptr, scan_ws, workspace_bytes - a, st);
     if (rc != GRF_OK) return rc;
     GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));
     if (n_rows > 0) {
-        tr_fill_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, st>>>(n_rows, n_cols, band_width, ptr, idx, val,
-                                                                         t_ptr, cnt, t_col, t_val,
-                                                                         reinterpret_cast<unsigned int *>(t_maxabs));
+        tr_fill_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, st>>>(
+            n_rows, n_cols, band_width, ptr, idx, val, t_ptr, cnt, reinterpret_cast<uint2 *>(t_rec),
+            reinterpret_cast<unsigned int *>(t_maxabs));
         GRF_CHECK_LAUNCH("tr_fill_kernel");
     }
+    tr_pad_fill_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, t_ptr, cnt,
+                                                                          reinterpret_cast<uint2 *>(t_rec));
+    GRF_CHECK_LAUNCH("tr_pad_fill_kernel");
     return GRF_OK;
 }
 

@@ -119,8 +119,7 @@ class PaddedRows:
 @dataclass
 class Banded:
     t_ptr: torch.Tensor  # int64 [n_bands * n_cols + 1]
-    t_col: torch.Tensor  # uint16 [nnz]  (j - band * band_width)
-    t_val: torch.Tensor  # float32 [nnz]
+    t_rec: torch.Tensor  # int32 [2 * cap]: (j - band * band_width, float32 bits) records, padded to pairs
     t_maxabs: torch.Tensor  # float32 [1], max |Phi|
     band_width: int
     n_rows: int
@@ -288,14 +287,13 @@ class GRFEngine:
         nb = -(-n_rows // band_width)
         nbk = nb * n_cols
         t_ptr = self._empty(nbk + 1, torch.int64)
-        t_col = self._empty(phi.nnz, torch.uint16)
-        t_val = self._empty(phi.nnz, torch.float32)
+        t_rec = self._empty(2 * (phi.nnz + nbk) + 4, torch.int32)  # torch allocations are 256-B aligned
         t_max = self._empty(1, torch.float32)
         ws = self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
         C.check(self.lib.grf_transpose_banded(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
-                                              _p(t_ptr), _p(t_col), _p(t_val), _p(t_max), _p(ws), ws.numel(),
-                                              self.stream), "grf_transpose_banded")
-        return Banded(t_ptr, t_col, t_val, t_max, band_width, n_rows, n_cols)
+                                              _p(t_ptr), _p(t_rec), _p(t_max), _p(ws), ws.numel(), self.stream),
+                "grf_transpose_banded")
+        return Banded(t_ptr, t_rec, t_max, band_width, n_rows, n_cols)
 
     # ----------------------------------------------------------------- Gram
     @staticmethod
@@ -311,7 +309,7 @@ class GRFEngine:
         if out is None:
             out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_gram_sparse(n, row_begin, row_end, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
-                                         tr.band_width, _p(tr.t_ptr), _p(tr.t_col), _p(tr.t_val), _p(tr.t_maxabs), _p(out),
+                                         tr.band_width, _p(tr.t_ptr), _p(tr.t_rec), _p(tr.t_maxabs), _p(out),
                                          out.stride(0), self.stream), "grf_gram_sparse")
         return out[:, :n]
 

@@ -163,28 +163,30 @@ int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const 
 
 /* Banded transpose for the Gram kernel: entries (j, k, v) of Phi (CSR rows j)
  * bucketed by (band = j / band_width, k):  bucket id = band * n_cols + k.
- * t_ptr[n_bands * n_cols + 1], t_col[nnz] (uint16 j - band * band_width),
- * t_val[nnz] (float32); band_width <= 65536.  t_maxabs[1] receives max |Phi|
+ * Records are (uint32 j - band * band_width, float32 bits of v) pairs of words;
+ * every bucket is padded to an even number of records with (0, +0.0).
+ * t_ptr[n_bands * n_cols + 1] (record offsets, all even), t_rec[2 * cap] with
+ * cap >= nnz + n_bands * n_cols (16-byte aligned).  t_maxabs[1] receives max |Phi|
  * (the fixed-point scale bound of the Gram kernel).
  * workspace >= grf_transpose_workspace_bytes(n_bands * n_cols). */
 int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                             const int32_t *idx, const float *val, int64_t *t_ptr, uint16_t *t_col, float *t_val,
-                             float *t_maxabs, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+                             const int32_t *idx, const float *val, int64_t *t_ptr, uint32_t *t_rec, float *t_maxabs,
+                             void *workspace, size_t workspace_bytes, grf_stream_t stream);
 size_t grf_transpose_workspace_bytes(int64_t n_buckets);
 
 /* ---------------------------------------------------------------------- Gram
  * Replaces `Phi @ Phi.T` of fast_grf_kernel_general.py:55 (sparse) and :39 (dense).
  * Sparse path: K[r, :] for rows r in [row_begin, row_end) of Phi (compact CSR,
  * float32 values) against the banded transpose of the FULL Phi (band_width equal
- * to the transpose's, multiple of 64, <= 8192; t_maxabs from the transpose).
+ * to the transpose's, multiple of 16, <= 8192; t_rec / t_maxabs from the transpose).
  * K is float32, row-major with leading dimension ldk (>= n_total); K row
  * (r - row_begin) is written.  Each K entry is the fp32 rounding of the exact
  * int64 fixed-point sum of the exact products Phi[r,k]*Phi[j,k] (per-row
  * power-of-two scale), so K does not depend on summation order: it is
  * bit-reproducible run to run, across row splits and GPU counts. */
 int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
-                        const float *val, int64_t band_width, const int64_t *t_ptr, const uint16_t *t_col,
-                        const float *t_val, const float *t_maxabs, float *K, int64_t ldk, grf_stream_t stream);
+                        const float *val, int64_t band_width, const int64_t *t_ptr, const uint32_t *t_rec,
+                        const float *t_maxabs, float *K, int64_t ldk, grf_stream_t stream);
 
 /* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
  * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */
