@@ -51,12 +51,15 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
     val_pad = torch.zeros(max(nnz_max, 1), dtype=val.dtype, device=dev)
     val_pad[:nnz_local] = val[:nnz_local]
 
-    g_counts = torch.empty((world, n_max), dtype=torch.int64, device=dev)
-    g_idx = torch.empty((world, max(nnz_max, 1)), dtype=idx.dtype, device=dev)
-    g_val = torch.empty((world, max(nnz_max, 1)), dtype=val.dtype, device=dev)
+    # flat outputs (gloo requires world * numel; RCCL accepts either)
+    z = max(nnz_max, 1)
+    g_counts = torch.empty(world * n_max, dtype=torch.int64, device=dev)
+    g_idx = torch.empty(world * z, dtype=idx.dtype, device=dev)
+    g_val = torch.empty(world * z, dtype=val.dtype, device=dev)
     dist.all_gather_into_tensor(g_counts, counts, group=group)
     dist.all_gather_into_tensor(g_idx, idx_pad, group=group)
     dist.all_gather_into_tensor(g_val, val_pad, group=group)
+    g_counts, g_idx, g_val = g_counts.view(world, n_max), g_idx.view(world, z), g_val.view(world, z)
 
     parts_c, parts_i, parts_v = [], [], []
     for r in range(world):

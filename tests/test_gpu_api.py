@@ -1,0 +1,196 @@
+"""The reference's public API, re-pointed at the MI355X engine (GPU).
+
+Mirrors the reference's own tests (tests/test_grf_dense.py, tests/test_grf_sparse.py)
+and checks every entry point against golden vectors made by the reference.
+Step matrices / Laplacians: bit-exact.  K (float32 on the GPU vs float64
+reference): |dK| <= 3e-5 (|Phi||Phi|^T) + 1e-12 scale, checked here as
+rtol=3e-5 against the reference values.
+"""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from golden_util import csr, same_csr
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------ the reference's own 4 tests
+def test_random_walk_shapes(toy_cycle_adj):
+    from efficient_graph_gp.random_walk_samplers.sampler import Graph, RandomWalk
+    graph = Graph(toy_cycle_adj)
+    rw = RandomWalk(graph, seed=0)
+    mats = rw.get_random_walk_matrices(num_walks=5, p_halt=0.2, max_walk_length=3, n_processes=1)
+    assert mats.shape == (4, 4, 3)
+    assert np.allclose(np.diag(mats[:, :, 0]), 1.0, atol=1e-6)
+
+
+def test_fast_general_grf_kernel_psd(toy_cycle_adj):
+    from efficient_graph_gp.graph_kernels.fast_grf_kernel_general import fast_general_grf_kernel
+    k = fast_general_grf_kernel(adj_matrix=toy_cycle_adj, modulator_vector=np.array([1.0, 0.5, 0.25]),
+                                walks_per_node=10, p_halt=0.2, max_walk_length=3)
+    assert np.allclose(k, k.T, atol=1e-8)
+    assert np.linalg.eigvalsh(k).min() >= -1e-8
+
+
+def test_sparse_random_walk_shapes(toy_cycle_csr):
+    from efficient_graph_gp_sparse.random_walk_samplers_sparse.sparse_sampler import SparseRandomWalk
+    rw = SparseRandomWalk(toy_cycle_csr, seed=0)
+    mats = rw.get_random_walk_matrices(num_walks=5, p_halt=0.2, max_walk_length=3, n_processes=1)
+    assert len(mats) == 3 and all(m.shape == (4, 4) for m in mats)
+    assert np.allclose(mats[0].diagonal(), 1.0, atol=1e-6)
+
+
+def test_fast_general_grf_kernel_sparse_psd(toy_cycle_csr):
+    from efficient_graph_gp_sparse.graph_kernels_sparse.fast_grf_kernel_general import fast_general_grf_kernel
+    k = fast_general_grf_kernel(adj_matrix=toy_cycle_csr, modulator_vector=np.array([1.0, 0.5, 0.25]),
+                                walks_per_node=10, p_halt=0.2, max_walk_length=3)
+    kd = k.toarray()
+    assert np.allclose(kd, kd.T, atol=1e-8)
+    assert np.linalg.eigvalsh(kd).min() >= -1e-8
+
+
+# ------------------------------------------------------------ golden vectors
+def test_entry_points_match_reference(golden):
+    from efficient_graph_gp.graph_kernels.fast_grf_kernel_diffusion import fast_diffusion_grf_kernel
+    from efficient_graph_gp.graph_kernels.fast_grf_kernel_general import fast_general_grf_kernel as dense_k
+    from efficient_graph_gp_sparse.graph_kernels_sparse.fast_grf_kernel_general import fast_general_grf_kernel as sk
+    d = golden("entry_points")
+    g = golden("small_graphs")
+    nproc = int(d["cpu_count"][0])  # the host the vectors were made on
+    f = [1.0, 0.5, 0.25]
+    K = dense_k(g["readme_A"], f, walks_per_node=50, p_halt=0.1, max_walk_length=3, n_processes=nproc)
+    np.testing.assert_allclose(K, d["readme_dense_K"], rtol=3e-5, atol=1e-6)
+    assert abs(K[0, 0] - 2.1806250000000005) < 1e-4  # README quickstart value quoted in SURVEY.md
+    K = fast_diffusion_grf_kernel(g["readme_A"], walks_per_node=50, p_halt=0.1, max_walk_length=3, beta=1.0,
+                                  n_processes=nproc)
+    np.testing.assert_allclose(K, d["readme_dense_diff_K"], rtol=3e-5, atol=1e-6)
+    for name, ff, m, p, L in [("readme", f, 50, 0.1, 3), ("cycle4", f, 10, 0.2, 3),
+                              ("er40", [1.0, -0.4, 0.3, 0.1, -0.05], 32, 0.15, 5)]:
+        K = sk(sp.csr_matrix(g[f"{name}_A"]), ff, walks_per_node=m, p_halt=p, max_walk_length=L, n_processes=nproc)
+        ref = d[f"{name}_sparse_K"]
+        np.testing.assert_allclose(K.toarray(), ref, rtol=3e-5, atol=1e-6 * np.abs(ref).max())
+    with pytest.raises(ValueError):
+        dense_k(g["readme_A"], [1.0, 0.5], walks_per_node=5, max_walk_length=3)
+
+
+def test_samplers_match_reference_bitwise(golden):
+    from efficient_graph_gp.random_walk_samplers.sampler import Graph, RandomWalk
+    from efficient_graph_gp_sparse.random_walk_samplers_sparse.sparse_sampler import SparseRandomWalk
+    d = golden("small_graphs")
+    for name in d["names"]:
+        n = d[f"{name}_A"].shape[0]
+        p = 0.0 if name == "perm12" else 0.2
+        Ls = csr(d, f"{name}_Lsp", n)
+        for nproc in (1, 3, 8):
+            for seed in (None, 7):
+                mats = SparseRandomWalk(Ls, seed=seed).get_random_walk_matrices(20, p, 4, n_processes=nproc)
+                for l, M in enumerate(mats):
+                    assert same_csr(M, csr(d, f"{name}_sp_n{nproc}_s{seed}_l{l}", n)), (name, nproc, seed, l)
+        mats = SparseRandomWalk(sp.csr_matrix(d[f"{name}_A"]), seed=0).get_random_walk_matrices(15, 0.3, 3,
+                                                                                               n_processes=2)
+        for l, M in enumerate(mats):
+            assert same_csr(M, csr(d, f"{name}_spA_l{l}", n)), (name, l)
+        Ld = d[f"{name}_Ld"]
+        for seed in (0, 5):
+            F = RandomWalk(Graph(Ld), seed=seed).get_random_walk_matrices(12, p, 4, n_processes=1)
+            assert np.array_equal(F, d[f"{name}_dseq_s{seed}"]), (name, seed)
+        F = RandomWalk(Graph(Ld), seed=0).get_random_walk_matrices(12, p, 4, n_processes=1, ablation=True)
+        assert np.array_equal(F, d[f"{name}_dabl_s0"]), name
+        for nproc in (2, 3):
+            key = f"{name}_dpar_n{nproc}"
+            if key in d:
+                F = RandomWalk(Graph(Ld), seed=None).get_random_walk_matrices(12, p, 4, n_processes=nproc)
+                assert np.array_equal(F, d[key]), (name, nproc)
+
+
+def test_laplacian_mirrors_bitwise(golden):
+    from efficient_graph_gp.graph_kernels.utils import get_normalized_laplacian as lap_d
+    from efficient_graph_gp.preprocessing.laplacian_np import get_laplacian, get_normalized_laplacian as lap_np
+    from efficient_graph_gp_sparse.utils_sparse.graph_utils import get_normalized_laplacian as lap_sp
+    d = golden("small_graphs")
+    for name in d["names"]:
+        A = d[f"{name}_A"]
+        assert same_csr(lap_sp(sp.csr_matrix(A)), csr(d, f"{name}_Lsp", A.shape[0])), name
+        assert np.array_equal(lap_d(A), d[f"{name}_Ld"]), name
+        assert np.array_equal(lap_np(A), d[f"{name}_Lnp"]), name
+        assert np.array_equal(get_laplacian(A), d[f"{name}_Lcomb"]), name
+
+
+# ---------------------------------------------------------- GPyTorch surface
+def _phi_dense(steps, f):
+    return sum(fl * M.toarray() for fl, M in zip(f, steps))
+
+
+def test_graph_preprocessor_and_sparse_kernels(golden, tmp_path):
+    from efficient_graph_gp_sparse.gptorch_kernels_sparse import SparseDiffusionKernel, SparseGRFKernel
+    from efficient_graph_gp_sparse.preprocessor import GraphPreprocessor
+    d = golden("small_graphs")
+    A = sp.csr_matrix(d["er40_A"])
+    with pytest.raises(ValueError):
+        GraphPreprocessor(sp.csr_matrix(np.ones((3, 4))))
+    with pytest.raises(ValueError):
+        GraphPreprocessor.from_scipy_csr(A.tocoo())
+    cache = str(tmp_path / "steps.npz")
+    pre = GraphPreprocessor(A, walks_per_node=20, p_halt=0.2, max_walk_length=4, random_walk_seed=7,
+                            cache_filename=cache, n_processes=3)
+    ops = pre.preprocess_graph(save_to_disk=True)
+    assert len(ops) == 4 and all(op.sparse_csr_tensor.device.type == "cuda" for op in ops)
+    for l, M in enumerate(pre.step_matrices_scipy):
+        assert same_csr(M, csr(d, f"er40_sp_n3_s7_l{l}", 40)), l
+    again = GraphPreprocessor(A, walks_per_node=20, p_halt=0.2, max_walk_length=4, random_walk_seed=7,
+                              cache_filename=cache, load_from_disk=True)
+    for M1, M2 in zip(again.step_matrices_scipy, pre.step_matrices_scipy):
+        assert same_csr(M1, M2)
+    with pytest.raises(FileNotFoundError):
+        GraphPreprocessor(A, cache_filename=str(tmp_path / "missing.npz"), load_from_disk=True)
+
+    kern = SparseGRFKernel(4, ops).cuda()
+    x = torch.tensor([0, 3, 5], device="cuda")
+    f = kern.modulator_vector.detach().cpu().numpy().astype(np.float64)
+    Phi = _phi_dense(pre.step_matrices_scipy, f)
+    np.testing.assert_allclose(kern(x, x).detach().cpu().numpy(), Phi[[0, 3, 5]] @ Phi[[0, 3, 5]].T,
+                               rtol=2e-5, atol=1e-6)
+    assert SparseDiffusionKernel(4, ops).cuda()().shape == (40, 40)
+
+
+def test_gpflow_style_kernels():
+    from efficient_graph_gp.gpflow_kernels import GraphDiffusionFastGRFKernel, GraphGeneralFastGRFKernel
+    r = np.random.default_rng(8)
+    U = np.triu((r.random((30, 30)) < 0.2).astype(float), 1)
+    A = U + U.T
+    with pytest.raises(AssertionError):
+        GraphGeneralFastGRFKernel(np.ones((3, 4)))
+    with pytest.raises(ValueError):
+        GraphGeneralFastGRFKernel(A, max_walk_length=4, modulator_vector=[1.0, 2.0])
+    k = GraphGeneralFastGRFKernel(A, walks_per_node=16, p_halt=0.2, max_walk_length=4)
+    np.random.seed(42)
+    np.testing.assert_array_equal(k.modulator_vector, np.random.randn(4))
+    Phi = k.feature_matrices @ k.modulator_vector
+    X = np.array([[0], [4], [29]])
+    np.testing.assert_allclose(k.K(X), (Phi @ Phi.T)[np.ix_([0, 4, 29], [0, 4, 29])], rtol=3e-5, atol=1e-6)
+    np.testing.assert_allclose(k.K_diag(X), np.diag(Phi @ Phi.T)[[0, 4, 29]], rtol=3e-5, atol=1e-6)
+    kd = GraphDiffusionFastGRFKernel(A, walks_per_node=16, p_halt=0.2, max_walk_length=4, beta=2.0, sigma_f=1.5)
+    fm = np.array([(-2.0) ** l / (2 ** l * np.prod(np.arange(1, l + 1))) for l in range(4)])
+    Phi = kd.feature_matrices @ fm
+    np.testing.assert_allclose(kd.K(np.arange(30)), 2.25 * Phi @ Phi.T, rtol=3e-5, atol=1e-6)
+
+
+def test_philox_mode_through_api_matches_oracle():
+    from efficient_graph_gp_sparse.random_walk_samplers_sparse.sparse_sampler import SparseRandomWalk
+    from oracle import oracle as O
+    U = sp.random(500, 500, density=0.02, random_state=3, format="csr")
+    A = ((U + U.T) > 0).astype(np.float64).tocsr()
+    A.setdiag(0)
+    A.eliminate_zeros()
+    A.sort_indices()
+    L, _ = O.laplacian_sparse(A)
+    mats = SparseRandomWalk(L, seed=11, rng="philox").get_random_walk_matrices(24, 0.15, 5)
+    ip, ix, dx = O._csr_arrays(L)
+    node, load = O.walk_slots(ip, ix, dx, 24, 0.15, 5, rng=O.RNG_PHILOX, seed=11)
+    ref = O.reduce_steps(node, load, O.NORM_MUL_RECIP)
+    for a, b in zip(mats, ref):
+        assert same_csr(a, b)

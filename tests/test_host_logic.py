@@ -1,0 +1,157 @@
+"""CPU-only: host-side logic of the engine (no GPU calls)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def test_shard_range_partitions():
+    from grf_amd.dist import shard_range
+    for n in (0, 1, 7, 100, 100_000):
+        for w in (1, 2, 3, 8):
+            rs = [shard_range(n, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+            sizes = [e - b for b, e in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_chunk_bounds_match_numpy_array_split():
+    from grf_amd import _lib
+    from oracle import oracle as O
+    lib = _lib.load()
+    for n, c in [(10, 3), (100, 8), (5, 8), (1, 1), (100_000, 192)]:
+        ours = [lib.grf_chunk_bounds(n, c, i) for i in range(c)] + [n]
+        ref = [int(a[0]) if len(a) else None for a in np.array_split(np.arange(n), c)]
+        assert list(O.chunk_bounds(n, c)) == ours
+        assert [x for x in ref if x is not None] == [ours[i] for i in range(c) if ours[i] < ours[i + 1]]
+
+
+def test_rng_mode_resolution(monkeypatch):
+    from grf_amd import api
+    monkeypatch.delenv("GRF_AMD_RNG", raising=False)
+    assert api.resolve_rng(None) == "reference"
+    monkeypatch.setenv("GRF_AMD_RNG", "philox")
+    assert api.resolve_rng(None) == "philox"
+    with pytest.raises(ValueError):
+        api.resolve_rng("mt19937")
+    assert api.resolve_processes(None) == os.cpu_count()
+    with pytest.raises(ValueError):
+        api.resolve_processes(0)
+
+
+def test_product_path_fails_loudly_without_gpu():
+    """No CPU fallback: the engine refuses to run when no GPU is visible."""
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from grf_amd.engine import GRFEngine
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        GRFEngine()
+    from efficient_graph_gp_sparse.graph_kernels_sparse.fast_grf_kernel_general import fast_general_grf_kernel
+    import scipy.sparse as sp
+    with pytest.raises(RuntimeError):
+        fast_general_grf_kernel(sp.eye(4, format="csr"), [1.0, 0.5], walks_per_node=2, max_walk_length=2)
+
+
+def test_mirror_packages_import():
+    import efficient_graph_gp.gpflow_kernels as gk
+    import efficient_graph_gp.graph_kernels as g
+    import efficient_graph_gp_sparse.gptorch_kernels_sparse as tk
+    import efficient_graph_gp_sparse.preprocessor as pp
+    assert callable(g.fast_diffusion_grf_kernel) and callable(gk.GraphGeneralFastGRFKernel)
+    assert tk.SparseGRFKernel and pp.GraphPreprocessor
+    with pytest.raises(NotImplementedError):
+        g.diffusion_kernel(np.eye(2))
+
+
+def test_step_cache_roundtrip_without_pickle(tmp_path):
+    import scipy.sparse as sp
+    from efficient_graph_gp_sparse.preprocessor.graph_preprocessor import GraphPreprocessor
+    mats = [sp.random(30, 30, density=0.1, random_state=i, format="csr") for i in range(3)]
+    fn = str(tmp_path / "c" / "steps.npz")
+    GraphPreprocessor.save_step_matrices(mats, fn)
+    back = GraphPreprocessor.load_step_matrices(fn)
+    for a, b in zip(mats, back):
+        assert (a != b).nnz == 0
+    with pytest.raises(ValueError):
+        GraphPreprocessor.load_step_matrices(str(tmp_path / "x.pkl"))
+
+
+# ------------------------------------------------------------- 2-rank gloo
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import scipy.sparse as sp
+        from grf_amd.dist import allgather_csr_rows, shard_range
+        n = 57
+        full = sp.random(n, n, density=0.2, random_state=5, format="csr")
+        full.sort_indices()
+        b, e = shard_range(n, rank, world)
+        part = full[b:e]
+        ptr = torch.from_numpy(part.indptr.astype(np.int64))
+        idx = torch.from_numpy(part.indices.astype(np.int32))
+        val = torch.from_numpy(part.data.astype(np.float32))
+        gptr, gidx, gval = allgather_csr_rows(ptr, idx, val)
+        ok = (np.array_equal(gptr.numpy(), full.indptr) and np.array_equal(gidx.numpy(), full.indices)
+              and np.array_equal(gval.numpy(), full.data.astype(np.float32)))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allgather_csr_rows_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(r, True) for r in range(world)]
+
+
+def test_gptorch_kernels_on_golden_steps(golden):
+    """Differentiable Phi / K of the GPyTorch wrappers (torch ops) on reference step matrices."""
+    from golden_util import csr
+    from efficient_graph_gp_sparse.gptorch_kernels_sparse import SparseDiffusionKernel, SparseGRFKernel
+    from efficient_graph_gp_sparse.preprocessor import GraphPreprocessor
+    from efficient_graph_gp_sparse.utils_sparse.sparse_lo import SparseLinearOperator
+    d = golden("small_graphs")
+    steps = [csr(d, f"er40_sp_n3_s7_l{l}", 40) for l in range(4)]
+    ops = [SparseLinearOperator(GraphPreprocessor.from_scipy_csr(M)) for M in steps]
+    torch.manual_seed(0)
+    kern = SparseGRFKernel(4, ops)
+    f = kern.modulator_vector.detach().numpy().astype(np.float64)
+    dense = [M.toarray() for M in steps]
+    Phi = sum(fl * M for fl, M in zip(f, dense))
+    i1, i2 = [0, 3, 5, 17, 39, 3], [1, 3, 20]
+    x1, x2 = torch.tensor(i1), torch.tensor(i2)
+    np.testing.assert_allclose(kern(x1, x2).detach().numpy(), Phi[i1] @ Phi[i2].T, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(kern(x1, x1, diag=True).detach().numpy(), np.einsum("ij,ij->i", Phi[i1], Phi[i1]),
+                               rtol=1e-5, atol=1e-6)
+    kern(x1, x2).sum().backward()
+    gref = [np.sum(dense[l][i1] @ Phi[i2].T + Phi[i1] @ dense[l][i2].T) for l in range(4)]
+    np.testing.assert_allclose(kern.raw_modulator_vector.grad.numpy(), gref, rtol=1e-4, atol=1e-5)
+    dk = SparseDiffusionKernel(4, ops)
+    fm = dk.modulator_vector.detach().numpy().astype(np.float64)
+    beta = float(np.log1p(np.exp(1.0)))
+    ref = [beta * (-beta) ** l / (2 ** l * np.prod(np.arange(1, l + 1))) for l in range(4)]
+    np.testing.assert_allclose(fm, ref, rtol=1e-6)
+    Phi = sum(fl * M for fl, M in zip(fm, dense))
+    np.testing.assert_allclose(dk().detach().numpy(), Phi @ Phi.T, rtol=1e-5, atol=1e-6)
