@@ -64,3 +64,10 @@ __device__ inline int32_t uniform32(int32_t v) { return __builtin_amdgcn_readfir
             return code;                                                                 \
         }                                                                                \
     } while (0)
+
+// The dispatcher takes at most 2^32 - 1 work-items per launch (gridDim.x * blockDim.x):
+// a larger grid is silently truncated on gfx950, so every variable-size launch checks it.
+#define GRF_REQUIRE_GRID(blocks, threads, name)                                          \
+    GRF_REQUIRE((int64_t)(blocks) * (int64_t)(threads) < (1ll << 32), GRF_EUNSUPPORTED,  \
+                "%s: %lld work-items exceed one launch (2^32); split the input", name,   \
+                (long long)((int64_t)(blocks) * (int64_t)(threads)))

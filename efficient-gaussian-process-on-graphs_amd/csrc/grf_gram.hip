@@ -27,18 +27,7 @@ namespace grf {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kChunk = 1024;  // stream positions covered by one marker chunk
-
-// inclusive max-scan over the 64 lanes with DPP (VALU only, no LDS traffic)
-__device__ inline int wave_incl_max(int v) {
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-    return v;
-}
+constexpr int kChunk = 1024;  // stream positions covered by one bucket-id chunk
 
 // |x| < 2^51 -> round-to-nearest int64 with one f64 add and one integer subtract
 __device__ inline long long fx_round(double x) {
@@ -48,166 +37,148 @@ __device__ inline long long fx_round(double x) {
 
 // Per-wave state of one flattened batch stream (see gram_sparse_kernel).
 struct GramStream {
-    const unsigned char *mark;  // bucket-start markers of the current chunk (LDS)
-    const int64_t *tbase;       // per bucket: pair index - stream position (LDS)
-    const double *ascale;       // per bucket: Phi[row,k] * S (LDS)
-    const uint4 *t_pair;        // Phi^T record pairs (global)
+    const unsigned char *bid;   // bucket of every stream position of the current chunk (LDS)
+    const int32_t *tbase;       // per bucket: byte offset of its first pair (from the band's
+                                // first line) - 12 * stream position (LDS)
+    const float *aval;          // per bucket: Phi[row,k] (LDS)
+    const unsigned char *rec;   // the band's record pairs, 12 bytes each (global)
     unsigned long long *acc;    // tile accumulator (LDS)
+    double S;                   // the row's fixed-point scale 2^sh
+};
+
+// one 12-byte record pair: {u16 col0 | u16 col1 << 16, f32 v0, f32 v1}
+struct __attribute__((aligned(4))) RecPair {
+    uint32_t cols;
+    float v0, v1;
 };
 
 // NW windows of 64 pairs starting at stream position w0 (chunk base c0, chunk end cend).
-// TAIL: positions >= cend are masked (they fetch pair 0 and add exactly 0).
+// TAIL: positions >= cend are masked: they read pair 0 of the band and add exactly 0 to
+// distinct entries.
 template <int NW, bool TAIL>
-__device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, int32_t c0, int32_t cend, int lane,
-                                             int &carry) {
+__device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, int32_t c0, int32_t cend, int lane) {
     int m[NW];
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
         const int32_t p = w0 + u * 64 + lane;
-        m[u] = (!TAIL || p < cend) ? (int)g.mark[p - c0] : 255;
+        m[u] = (!TAIL || p < cend) ? (int)g.bid[p - c0] : 0;
     }
-#pragma unroll
-    for (int u = 0; u < NW; ++u) {
-        int v = m[u] == 255 ? -1 : m[u];
-        if (lane == 0) v = max(v, carry);
-        v = wave_incl_max(v);
-        carry = __builtin_amdgcn_readlane(v, 63);
-        m[u] = v < 0 ? 0 : v;
-    }
-    int64_t pos[NW];
+    int32_t pos[NW];
     double sc[NW];
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
-        pos[u] = g.tbase[m[u]] + (w0 + u * 64 + lane);
-        sc[u] = g.ascale[m[u]];
+        pos[u] = g.tbase[m[u]] + 12 * (w0 + u * 64 + lane);
+        sc[u] = (double)g.aval[m[u]] * g.S;  // exact: a power-of-two scaling of an f32
     }
     if (TAIL) {
 #pragma unroll
         for (int u = 0; u < NW; ++u) {
             const bool ok = w0 + u * 64 + lane < cend;
-            pos[u] = ok ? pos[u] : 0;  // pair 0 always exists when the stream is non-empty
+            pos[u] = ok ? pos[u] : 0;  // the band's first pair: valid and finite
             sc[u] = ok ? sc[u] : 0.0;
         }
     }
     // phase order pinned: all descriptor reads, then all gathers in flight, then the adds
     __builtin_amdgcn_sched_barrier(0);
-    uint4 rec[NW];
+    RecPair rec[NW];
 #pragma unroll
-    for (int u = 0; u < NW; ++u) rec[u] = g.t_pair[pos[u]];
+    for (int u = 0; u < NW; ++u) rec[u] = *reinterpret_cast<const RecPair *>(g.rec + pos[u]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
-        const long long q0 = fx_round(sc[u] * (double)__uint_as_float(rec[u].y));
-        const long long q1 = fx_round(sc[u] * (double)__uint_as_float(rec[u].w));
-        __hip_atomic_fetch_add(&g.acc[rec[u].x], (unsigned long long)q0, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(&g.acc[rec[u].z], (unsigned long long)q1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        const long long q0 = fx_round(sc[u] * (double)rec[u].v0);
+        const long long q1 = fx_round(sc[u] * (double)rec[u].v1);
+        uint32_t c0 = rec[u].cols & 0xffffu, c1 = rec[u].cols >> 16;
+        if (TAIL) {
+            const bool ok = w0 + u * 64 + lane < cend;
+            c0 = ok ? c0 : (uint32_t)(lane & 15);
+            c1 = ok ? c1 : (uint32_t)(lane & 15);
+        }
+        __hip_atomic_fetch_add(&g.acc[c0], (unsigned long long)q0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&g.acc[c1], (unsigned long long)q1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
+// int64 fixed point (scale 2^sh) -> float: two exact-width converts, one fma, one ldexp
+// (|error| <= 1.5 ulp of the result; deterministic)
+__device__ inline float fx_to_float(unsigned long long a, int sh) {
+    const float hi = (float)(int)(a >> 32), lo = (float)(unsigned)(a & 0xffffffffull);
+    return ldexpf(fmaf(hi, 4294967296.0f, lo), -sh);
+}
+
+// LDS bytes of one gram_sparse_kernel workgroup (W int64 counters + per-wave stream state):
+// at W = 4096 and 4 waves exactly 40 KiB, i.e. four workgroups per CU.
+constexpr size_t gram_lds_bytes(int64_t W, int waves) {
+    return (size_t)W * 8 + (size_t)waves * (kChunk + 128 * 4 + 128 * 4);
+}
+
 // One workgroup of kWaves waves = one tile K[row, j0 : j0 + W] (W = a band of the
-// banded transpose).  Accumulation is exact int64 fixed point with a per-row
-// power-of-two scale S chosen so that every term |Phi[row,k] Phi[j,k]| S < 2^51 and
-// the sum of all terms < 2^62: each exact fp64 product is rounded once to an integer
-// and the integer sum does not depend on the order of the adds (ds_add_u64) -- nor on
-// scheduling, GPU count or row split.  Resolution 1/S <= 2^-50 max_k|Phi[row,k]| max|Phi|.
-// Phi^T buckets hold (col, value) records padded to pairs; the waves pull batches of
-// 128 nonzeros of the row from an LDS counter and flatten each batch's buckets into
-// one stream of record PAIRS (one 16-byte load fetches two records: the texture-address
-// path, not bandwidth, bounds short scattered segments).  The bucket of each pair comes
-// from bucket-start markers (one u8 LDS read) and a DPP max-scan.
+// banded transpose).  Accumulation is exact int64 fixed point with the per-row
+// power-of-two scale S = 2^rowshift[row] (from the transpose) chosen so that every term
+// |Phi[row,k] Phi[j,k]| S < 2^51 and the sum of all terms < 2^62: each exact fp64 product
+// is rounded once to an integer and the integer sum does not depend on the order of the
+// adds (ds_add_u64) -- nor on scheduling, GPU count or row split.
+// Phi^T buckets hold 12-byte record pairs starting on 128-byte lines; wave w takes the
+// batches w, w + kWaves, ... of 128 nonzeros of the row and flattens each batch's buckets
+// into one stream of PAIRS.  The bucket of each pair comes from a per-position u8 bucket
+// id that the lanes fill for their own buckets (one LDS read); the gathers of kGramUnroll
+// windows of 64 pairs are in flight together.
 // Optional placement (speed only, kXcd): blocks b and b+8 are dealt to the same XCD, so
 // block b % 8 = x works on bands x, x+8, ...: each XCD's L2 holds one band's slice.
 template <int kWaves, int kGramUnroll, bool kXcd>
 __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, int64_t n_rows, int64_t W, int64_t nb, const int64_t *__restrict__ ptr,
-    const int32_t *__restrict__ idx, const float *__restrict__ val, const int64_t *__restrict__ t_ptr,
-    const uint4 *__restrict__ t_pair, const float *__restrict__ maxabs, float *__restrict__ K, int64_t ldk) {
+    const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
+    const unsigned char *__restrict__ t_rec, const int32_t *__restrict__ rowshift, float *__restrict__ K,
+    int64_t ldk) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    unsigned char *mark = reinterpret_cast<unsigned char *>(acc + W) + wave * kChunk;      // [kWaves][kChunk]
-    int64_t *tbase = reinterpret_cast<int64_t *>(reinterpret_cast<unsigned char *>(acc + W) + kWaves * kChunk) +
-                     wave * 128;                                                          // [kWaves][128]
-    double *ascale = reinterpret_cast<double *>(reinterpret_cast<int64_t *>(reinterpret_cast<unsigned char *>(
-                         acc + W) + kWaves * kChunk) + kWaves * 128) + wave * 128;         // [kWaves][128]
-    double *red = reinterpret_cast<double *>(reinterpret_cast<int64_t *>(reinterpret_cast<unsigned char *>(
-                      acc + W) + kWaves * kChunk) + 2 * kWaves * 128);                    // [2 * kWaves]
-    int *next_batch = reinterpret_cast<int *>(red + 2 * kWaves);
+    unsigned char *st = reinterpret_cast<unsigned char *>(acc + W) + wave * (kChunk + 128 * 8);
+    unsigned char *bidv = st;                                        // [kChunk]
+    int32_t *tbase = reinterpret_cast<int32_t *>(st + kChunk);       // [128]
+    float *aval = reinterpret_cast<float *>(st + kChunk + 128 * 4);  // [128]
 
-    const int64_t bid = blockIdx.x;
+    const int64_t blk = blockIdx.x;
     int64_t band, r;
     if (kXcd) {
-        const int64_t xcd = bid & 7, s = bid >> 3;
+        const int64_t xcd = blk & 7, s = blk >> 3;
         const int64_t phase = s / n_rows;
         r = s - phase * n_rows;
         band = xcd + 8 * phase;
         if (band >= nb) return;  // uniform over the workgroup
     } else {
-        band = bid / n_rows;
-        r = bid - band * n_rows;
+        band = blk / n_rows;
+        r = blk - band * n_rows;
     }
     const int64_t row = row_begin + r;
     const int64_t j0 = band * W;
     const int64_t wlen = (n_total - j0) < W ? (n_total - j0) : W;
     const int64_t e0 = ptr[row], e1 = ptr[row + 1];
+    const int64_t boff = band * n_total;
+    const int sh = rowshift[row];
+    // the band's records, addressed by 32-bit offsets from its first line
+    const unsigned char *brec = t_rec + (int64_t)t_desc[boff].x * 128;
 
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     u64x2 *acc2 = reinterpret_cast<u64x2 *>(acc);
     const u64x2 z2 = {0ull, 0ull};
     for (int64_t i = tid; i < (wlen + 1) / 2; i += 64 * kWaves) acc2[i] = z2;
-    // scale: every term |Phi[row,k] Phi[j,k]| S < 2^51 (exact magic-number rounding) and
-    // the sum of all |terms| S < 2^62 (no int64 overflow)
-    double sa = 0.0;
-    float ma = 0.f;
-    for (int64_t e = e0 + tid; e < e1; e += 64 * kWaves) {
-        const float a = fabsf(val[e]);
-        sa += (double)a;
-        ma = fmaxf(ma, a);
-    }
-    sa = wave_sum<double>(sa);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) ma = fmaxf(ma, __shfl_xor(ma, off, 64));
-    if (kWaves > 1) {
-        if (lane == 0) { red[wave] = sa; red[kWaves + wave] = (double)ma; }
-        if (tid == 0) *next_batch = 0;
-        __syncthreads();
-        sa = 0.0;
-        double mm = 0.0;
-        for (int w = 0; w < kWaves; ++w) { sa += red[w]; mm = fmax(mm, red[kWaves + w]); }
-        ma = (float)mm;
-    }
-    const double mx = (double)maxabs[0];
-    const double B = sa * mx, T = (double)ma * mx;
-    const int eB = B > 0.0 ? ilogb(B) + 1 : 0;  // B < 2^eB
-    const int eT = T > 0.0 ? ilogb(T) + 1 : 0;  // every term < 2^eT
-    const int sh = min(51 - eT, 62 - eB);
-    const double S = ldexp(1.0, sh), inv_S = ldexp(1.0, -sh);
+    if (kWaves > 1) __syncthreads();
+    else __builtin_amdgcn_wave_barrier();
 
-    const GramStream gs{mark, tbase, ascale, t_pair, acc};
-    const int64_t boff = band * n_total;
-    for (int it = 0;; ++it) {
-        int bi = it;
-        if (kWaves > 1) {
-            if (lane == 0) bi = atomicAdd(next_batch, 1);
-            bi = __builtin_amdgcn_readfirstlane(bi);
-        }
-        const int64_t g0 = e0 + (int64_t)bi * 128;
-        if (g0 >= e1) break;
-        int32_t cnt[2], excl[2];
-        int64_t t0[2];
-        double as[2];
-        int32_t k[2];
+    const GramStream gs{bidv, tbase, aval, brec, acc, ldexp(1.0, sh)};
+    const int32_t line0 = (int32_t)t_desc[boff].x;
+    for (int64_t g0 = e0 + (int64_t)wave * 128; g0 < e1; g0 += 128 * kWaves) {
+        int32_t cnt[2], excl[2], t0[2];
+        float av[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int64_t e = g0 + h * 64 + lane;
-            k[h] = e < e1 ? idx[e] : -1;
-            as[h] = e < e1 ? (double)val[e] * S : 0.0;
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            t0[h] = k[h] >= 0 ? t_ptr[boff + k[h]] : 0;
-            cnt[h] = k[h] >= 0 ? (int32_t)((t_ptr[boff + k[h] + 1] - t0[h]) >> 1) : 0;  // pairs
+            const int32_t k = e < e1 ? idx[e] : -1;
+            av[h] = e < e1 ? val[e] : 0.f;
+            const uint2 d = k >= 0 ? t_desc[boff + k] : make_uint2((uint32_t)line0, 0u);
+            t0[h] = ((int32_t)d.x - line0) * 128;  // bucket byte offset within the band
+            cnt[h] = (int32_t)d.y;                 // pairs
         }
         const int32_t inc0 = wave_inclusive_scan<int32_t>(cnt[0]);
         const int32_t tot0 = __shfl(inc0, 63, 64);
@@ -217,24 +188,23 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
         excl[1] = inc1 - cnt[1];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            tbase[h * 64 + lane] = (t0[h] >> 1) - excl[h];  // pair index = tbase + stream position
-            ascale[h * 64 + lane] = as[h];
+            tbase[h * 64 + lane] = t0[h] - 12 * excl[h];  // byte offset = tbase + 12 * position
+            aval[h * 64 + lane] = av[h];
         }
-        int carry = -1;
         for (int32_t c0 = 0; c0 < total; c0 += kChunk) {
-#pragma unroll
-            for (int i = 0; i < kChunk / 1024; ++i)
-                reinterpret_cast<uint4 *>(mark)[i * 64 + lane] = make_uint4(~0u, ~0u, ~0u, ~0u);
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (cnt[h] > 0 && excl[h] >= c0 && excl[h] < c0 + kChunk)
-                    mark[excl[h] - c0] = (unsigned char)(h * 64 + lane);
-            __builtin_amdgcn_wave_barrier();
             const int32_t cend = (total - c0) < kChunk ? total : c0 + kChunk;
+            // every stream position of the chunk gets its bucket id (lanes fill their own ranges)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int32_t lo = excl[h] > c0 ? excl[h] : c0;
+                const int32_t hi = (excl[h] + cnt[h]) < cend ? (excl[h] + cnt[h]) : cend;
+                for (int32_t p = lo; p < hi; ++p) bidv[p - c0] = (unsigned char)(h * 64 + lane);
+            }
+            __builtin_amdgcn_wave_barrier();
             int32_t w0 = c0;
             for (; w0 + 64 * kGramUnroll <= cend; w0 += 64 * kGramUnroll)
-                gram_windows<kGramUnroll, false>(gs, w0, c0, cend, lane, carry);
-            for (; w0 < cend; w0 += 64) gram_windows<1, true>(gs, w0, c0, cend, lane, carry);
+                gram_windows<kGramUnroll, false>(gs, w0, c0, cend, lane);
+            if (w0 < cend) gram_windows<kGramUnroll, true>(gs, w0, c0, cend, lane);  // masked last group
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -248,16 +218,15 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
         for (int64_t i = tid; i < n4; i += 64 * kWaves) {
             const u64x2 a = acc2[2 * i], b = acc2[2 * i + 1];
             f32x4 o;
-            o[0] = (float)((double)(long long)a[0] * inv_S);
-            o[1] = (float)((double)(long long)a[1] * inv_S);
-            o[2] = (float)((double)(long long)b[0] * inv_S);
-            o[3] = (float)((double)(long long)b[1] * inv_S);
+            o[0] = fx_to_float(a[0], sh);
+            o[1] = fx_to_float(a[1], sh);
+            o[2] = fx_to_float(b[0], sh);
+            o[3] = fx_to_float(b[1], sh);
             __builtin_nontemporal_store(o, &k4[i]);
         }
-        for (int64_t i = n4 * 4 + tid; i < wlen; i += 64 * kWaves)
-            krow[i] = (float)((double)(long long)acc[i] * inv_S);
+        for (int64_t i = n4 * 4 + tid; i < wlen; i += 64 * kWaves) krow[i] = fx_to_float(acc[i], sh);
     } else {
-        for (int64_t i = tid; i < wlen; i += 64 * kWaves) krow[i] = (float)((double)(long long)acc[i] * inv_S);
+        for (int64_t i = tid; i < wlen; i += 64 * kWaves) krow[i] = fx_to_float(acc[i], sh);
     }
 }
 
@@ -337,12 +306,12 @@ extern "C" {
 #pragma GCC visibility push(default)
 
 int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
-                        const float *val, int64_t band_width, const int64_t *t_ptr, const uint32_t *t_rec,
-                        const float *t_maxabs, float *K, int64_t ldk, grf_stream_t stream) {
-    GRF_REQUIRE(n_total >= 0 && 0 <= row_begin && row_begin <= row_end && row_end <= n_total && ptr && t_ptr && K &&
-                    t_maxabs && t_rec,
+                        const float *val, int64_t band_width, const uint32_t *t_desc, const void *t_rec,
+                        const int32_t *t_rowshift, float *K, int64_t ldk, grf_stream_t stream) {
+    GRF_REQUIRE(n_total >= 0 && 0 <= row_begin && row_begin <= row_end && row_end <= n_total && ptr && t_desc && K &&
+                    t_rowshift && t_rec,
                 GRF_EINVAL, "grf_gram_sparse: bad arguments");
-    GRF_REQUIRE(((uintptr_t)t_rec & 15) == 0, GRF_EINVAL, "grf_gram_sparse: t_rec must be 16-byte aligned");
+    GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_gram_sparse: t_rec must be 128-byte aligned");
     GRF_REQUIRE(ldk >= n_total, GRF_EINVAL, "grf_gram_sparse: ldk < n");
     GRF_REQUIRE(band_width >= 16 && band_width % 16 == 0 && band_width <= 8192, GRF_EUNSUPPORTED,
                 "grf_gram_sparse: band_width must be a multiple of 16 in [16, 8192]");
@@ -352,32 +321,40 @@ int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, con
     // tuning knobs (defaults = measured best on MI355X): waves per tile, unroll, XCD pinning
     static const int knobs = [] {
         const char *e = getenv("GRF_GRAM_UNROLL"), *x = getenv("GRF_GRAM_XCD"), *w = getenv("GRF_GRAM_WAVES");
-        const int u = e ? atoi(e) : 4, ww = w ? atoi(w) : 4;
-        return ((u == 2 || u == 4 || u == 8) ? u : 4) + (x && atoi(x) ? 100 : 0) + (ww == 1 ? 1000 : 0);
+        const int u = e ? atoi(e) : 8, ww = w ? atoi(w) : 4;
+        return ((u == 4 || u == 8 || u == 16) ? u : 8) + (x && atoi(x) ? 100 : 0) + (ww == 1 ? 1000 : 0);
     }();
     const bool xcd = (knobs / 100) % 10 == 1;
     const int unroll = knobs % 100, waves = knobs >= 1000 ? 1 : 4;
-    const int64_t tiles = xcd ? 8 * cdiv<int64_t>(nb, 8) * rows : nb * rows;
-    GRF_REQUIRE(tiles < (1ll << 32), GRF_EUNSUPPORTED, "grf_gram_sparse: too many tiles; split the row range");
-    const size_t lds = (size_t)band_width * 8 + waves * (kChunk + 128 * 8 + 128 * 8) + 2 * waves * 8 + 16;
-    const uint4 *t_pair = reinterpret_cast<const uint4 *>(t_rec);
+    const int64_t per_row = xcd ? 8 * cdiv<int64_t>(nb, 8) : nb;
+    const size_t lds = gram_lds_bytes(band_width, waves);
+    const uint2 *desc = reinterpret_cast<const uint2 *>(t_desc);
+    const unsigned char *rec = reinterpret_cast<const unsigned char *>(t_rec);
+    // one launch covers at most 2^32 - 1 work-items: split the row range
+    const int64_t max_rows = ((1ll << 32) - 1) / (per_row * 64 * waves);
+    GRF_REQUIRE(max_rows >= 1, GRF_EUNSUPPORTED, "grf_gram_sparse: too many bands for one row");
+    for (int64_t r0 = 0; r0 < rows; r0 += max_rows) {
+        const int64_t rr = (rows - r0) < max_rows ? (rows - r0) : max_rows;
+        const int64_t tiles = per_row * rr;
+        float *Kr = K + r0 * ldk;
 #define GRF_GRAM_LAUNCH(WV, U, X)                                                                                 \
     gram_sparse_kernel<WV, U, X><<<(unsigned)tiles, 64 * WV, lds, S(stream)>>>(                                   \
-        n_total, row_begin, rows, band_width, nb, ptr, idx, val, t_ptr, t_pair, t_maxabs, K, ldk)
+        n_total, row_begin + r0, rr, band_width, nb, ptr, idx, val, desc, rec, t_rowshift, Kr, ldk)
 #define GRF_GRAM_U(WV, X)                                                                                         \
     switch (unroll) {                                                                                             \
-        case 2: GRF_GRAM_LAUNCH(WV, 2, X); break;                                                                 \
-        case 8: GRF_GRAM_LAUNCH(WV, 8, X); break;                                                                 \
-        default: GRF_GRAM_LAUNCH(WV, 4, X); break;                                                                \
+        case 4: GRF_GRAM_LAUNCH(WV, 4, X); break;                                                                 \
+        case 16: GRF_GRAM_LAUNCH(WV, 16, X); break;                                                               \
+        default: GRF_GRAM_LAUNCH(WV, 8, X); break;                                                                \
     }
-    if (waves == 1) {
-        if (xcd) { GRF_GRAM_U(1, true) } else { GRF_GRAM_U(1, false) }
-    } else {
-        if (xcd) { GRF_GRAM_U(4, true) } else { GRF_GRAM_U(4, false) }
-    }
+        if (waves == 1) {
+            if (xcd) { GRF_GRAM_U(1, true) } else { GRF_GRAM_U(1, false) }
+        } else {
+            if (xcd) { GRF_GRAM_U(4, true) } else { GRF_GRAM_U(4, false) }
+        }
 #undef GRF_GRAM_U
 #undef GRF_GRAM_LAUNCH
-    GRF_CHECK_LAUNCH("gram_sparse_kernel");
+        GRF_CHECK_LAUNCH("gram_sparse_kernel");
+    }
     return GRF_OK;
 }
 
@@ -402,6 +379,7 @@ int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, cons
     GRF_REQUIRE(n_rows >= 0 && ptr && out && lda >= 0, GRF_EINVAL, "grf_densify: bad arguments");
     if (n_rows == 0) return GRF_OK;
     GRF_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)n_rows * (size_t)lda * sizeof(float), S(stream)));
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "densify_kernel");
     densify_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, S(stream)>>>(n_rows, ptr, idx, val, out, lda);
     GRF_CHECK_LAUNCH("densify_kernel");
     return GRF_OK;

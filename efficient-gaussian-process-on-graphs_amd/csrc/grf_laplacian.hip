@@ -211,12 +211,15 @@ int32_t grf_laplacian_csr(int64_t n, const int64_t *a_ptr, const int32_t *a_idx,
         return GRF_OK;
     }
     const unsigned g = (unsigned)cdiv<int64_t>(n, 256);
+    GRF_REQUIRE_GRID(g, 256, "lap_deg_kernel");
     lap_deg_kernel<<<g, 256, 0, st>>>(n, a_ptr, a_val, deg, dinv);
     GRF_CHECK_LAUNCH("lap_deg_kernel");
+    GRF_REQUIRE_GRID(g, 256, "lap_row_kernel");
     lap_row_kernel<false><<<g, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
     GRF_CHECK_LAUNCH("lap_row_kernel<count>");
     int32_t rc = scan_counts_i32(n, cnt, l_ptr, (char *)workspace + cnt_bytes, workspace_bytes - cnt_bytes, st);
     if (rc != GRF_OK) return rc;
+    GRF_REQUIRE_GRID(g, 256, "lap_row_kernel");
     lap_row_kernel<true><<<g, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
     GRF_CHECK_LAUNCH("lap_row_kernel<fill>");
     return GRF_OK;
@@ -241,13 +244,16 @@ int32_t grf_laplacian_dense(int64_t n, const double *W, int32_t mode, int64_t *l
     double *dinv = (double *)workspace;
     int32_t *cnt = (int32_t *)((char *)workspace + dinv_bytes);
     void *scan_ws = (char *)workspace + dinv_bytes + cnt_bytes;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n, 128), 128, "lapd_deg_kernel");
     lapd_deg_kernel<<<(unsigned)cdiv<int64_t>(n, 128), 128, 0, st>>>(n, W, mode, deg, dinv);
     GRF_CHECK_LAUNCH("lapd_deg_kernel");
     const unsigned g = (unsigned)cdiv<int64_t>(n, 4);
+    GRF_REQUIRE_GRID(g, 256, "lapd_row_kernel");
     lapd_row_kernel<false><<<g, 256, 0, st>>>(n, W, mode, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
     GRF_CHECK_LAUNCH("lapd_row_kernel<count>");
     int32_t rc = scan_counts_i32(n, cnt, l_ptr, scan_ws, workspace_bytes - dinv_bytes - cnt_bytes, st);
     if (rc != GRF_OK) return rc;
+    GRF_REQUIRE_GRID(g, 256, "lapd_row_kernel");
     lapd_row_kernel<true><<<g, 256, 0, st>>>(n, W, mode, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
     GRF_CHECK_LAUNCH("lapd_row_kernel<fill>");
     return GRF_OK;

@@ -63,15 +63,18 @@ static int32_t scan_exclusive(int64_t n, const TIn *in, int64_t *out, int64_t *w
         return GRF_OK;
     }
     if (nb == 1) {
+        GRF_REQUIRE_GRID(1, kScanThreads, "scan_apply_kernel");
         scan_apply_kernel<TIn><<<1, kScanThreads, 0, st>>>(n, in, nullptr, out);
         GRF_CHECK_LAUNCH("scan_apply_kernel");
         return GRF_OK;
     }
     int64_t *part = ws, *part_ex = ws + nb, *rest = ws + nb + nb + 1;
+    GRF_REQUIRE_GRID(nb, kScanThreads, "scan_reduce_kernel");
     scan_reduce_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part);
     GRF_CHECK_LAUNCH("scan_reduce_kernel");
     int32_t rc = scan_exclusive<int64_t>(nb, part, part_ex, rest, st);
     if (rc != GRF_OK) return rc;
+    GRF_REQUIRE_GRID(nb, kScanThreads, "scan_apply_kernel");
     scan_apply_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part_ex, out);
     GRF_CHECK_LAUNCH("scan_apply_kernel");
     return GRF_OK;
@@ -107,6 +110,12 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(int64_t n_rows, int64
 }
 
 // ------------------------------------------------------------ banded transpose
+// Bucket b = band * n_cols + k holds the entries Phi[j, k], j in the band, as PAIRS of
+// records packed in 12 bytes: {u16 j0 - band start, u16 j1 - band start, f32 v0, f32 v1}.
+// Every bucket starts on a 128-byte line (the Gram kernel reads a bucket as one short
+// segment; aligned, a segment of <= 10 pairs is one line instead of two).
+constexpr int kPairBytes = 12, kLineBytes = 128;
+
 __global__ __launch_bounds__(256) void tr_count_kernel(int64_t n_rows, int64_t n_cols, int64_t bw,
                                                        const int64_t *ptr, const int32_t *idx, int32_t *cnt) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -116,36 +125,67 @@ __global__ __launch_bounds__(256) void tr_count_kernel(int64_t n_rows, int64_t n
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) atomicAdd(&cnt[band_off + idx[e]], 1);
 }
 
-__global__ void tr_pad_counts_kernel(int64_t n, int32_t *cnt) {
+__global__ void tr_lines_kernel(int64_t n, const int32_t *cnt, int32_t *lines) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) cnt[i] += cnt[i] & 1;  // every bucket holds an even number of records
+    if (i < n) lines[i] = (kPairBytes * ((cnt[i] + 1) >> 1) + kLineBytes - 1) / kLineBytes;
+}
+
+__global__ void tr_desc_kernel(int64_t n, const int32_t *cnt, const int64_t *line_off, uint2 *desc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) desc[i] = make_uint2((uint32_t)line_off[i], (uint32_t)((cnt[i] + 1) >> 1));
+    if (i == n) desc[n] = make_uint2((uint32_t)line_off[n], (uint32_t)(line_off[n] >> 32));
 }
 
 __global__ __launch_bounds__(256) void tr_fill_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, const int64_t *ptr,
-                                                      const int32_t *idx, const float *val, const int64_t *t_ptr,
-                                                      int32_t *cursor, uint2 *t_rec, unsigned int *maxabs_bits) {
+                                                      const int32_t *idx, const float *val, const uint2 *desc,
+                                                      int32_t *cursor, unsigned char *t_rec,
+                                                      unsigned int *maxabs_bits, float *row_max, double *row_sum) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n_rows) return;
     const int lane = threadIdx.x & 63;
     const int64_t band = row / bw, band_off = band * n_cols;
-    const uint32_t jr = (uint32_t)(row - band * bw);
+    const uint16_t jr = (uint16_t)(row - band * bw);
     float mx = 0.f;
+    double sm = 0.0;
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) {
         const int64_t b = band_off + idx[e];
-        const int64_t pos = t_ptr[b] + atomicAdd(&cursor[b], 1);
-        t_rec[pos] = make_uint2(jr, __float_as_uint(val[e]));
+        const int32_t s = atomicAdd(&cursor[b], 1);
+        unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (s >> 1);
+        reinterpret_cast<uint16_t *>(pair)[s & 1] = jr;
+        reinterpret_cast<float *>(pair + 4)[s & 1] = val[e];
         mx = fmaxf(mx, fabsf(val[e]));
+        sm += (double)fabsf(val[e]);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    sm = wave_sum<double>(sm);
+    if (lane == 0) { row_max[row] = mx; row_sum[row] = sm; }
     // non-negative floats order like their bit patterns
     if (lane == 0 && mx > 0.f) atomicMax(maxabs_bits, __float_as_uint(mx));
 }
 
-// odd buckets get a (col 0, +0.0) pad record: adds exactly 0 in the Gram kernel
-__global__ void tr_pad_fill_kernel(int64_t n, const int64_t *t_ptr, const int32_t *cursor, uint2 *t_rec) {
+// Gram fixed-point shift of every row r: the largest power of two S = 2^sh with every
+// term |Phi[r,k] Phi[j,k]| S <= T S < 2^51 (exact magic-number rounding) and the sum of all
+// |terms| S <= B S < 2^62 (no int64 overflow); T = max_k |Phi[r,k]| max|Phi|, B = sum_k |Phi[r,k]| max|Phi|.
+__global__ void tr_rowshift_kernel(int64_t n_rows, const float *row_max, const double *row_sum,
+                                   const float *maxabs, int32_t *shift) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    const double mx = (double)maxabs[0];
+    const double B = row_sum[r] * mx * (1.0 + 1e-12), T = (double)row_max[r] * mx;
+    const int eB = B > 0.0 ? ilogb(B) + 1 : 0;  // B < 2^eB
+    const int eT = T > 0.0 ? ilogb(T) + 1 : 0;  // every term < 2^eT
+    shift[r] = min(51 - eT, 62 - eB);
+}
+
+// odd buckets: the second record of the last pair is (col 0, +0.0) -- adds exactly 0
+__global__ void tr_pad_fill_kernel(int64_t n, const uint2 *desc, const int32_t *cursor, unsigned char *t_rec) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < n && (cursor[b] & 1)) t_rec[t_ptr[b] + cursor[b]] = make_uint2(0u, 0u);
+    if (b < n && (cursor[b] & 1)) {
+        unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (cursor[b] >> 1);
+        reinterpret_cast<uint16_t *>(pair)[1] = 0;
+        reinterpret_cast<float *>(pair + 4)[1] = 0.f;
+    }
 }
 
 }  // namespace grf
@@ -171,51 +211,86 @@ int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const 
     GRF_REQUIRE(!out_val || in_val, GRF_EINVAL, "grf_compact_rows: out_val needs in_val");
     GRF_REQUIRE(!out_val32 || in_val32, GRF_EINVAL, "grf_compact_rows: out_val32 needs in_val32");
     if (n_rows == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "compact_rows_kernel");
     compact_rows_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, S(stream)>>>(
         n_rows, cap, cnt, out_ptr, in_idx, in_val, in_val32, out_idx, out_val, out_val32);
     GRF_CHECK_LAUNCH("compact_rows_kernel");
     return GRF_OK;
 }
 
+static size_t tr_align(size_t x) { return (x + 255) & ~(size_t)255; }
+
 size_t grf_transpose_workspace_bytes(int64_t n_buckets) {
-    size_t a = ((size_t)n_buckets * sizeof(int32_t) + 255) & ~(size_t)255;
-    return a + scan_ws_bytes(n_buckets);
+    return 2 * tr_align((size_t)n_buckets * sizeof(int32_t)) + tr_align((size_t)(n_buckets + 1) * sizeof(int64_t)) +
+           scan_ws_bytes(n_buckets);
 }
 
-int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                             const int32_t *idx, const float *val, int64_t *t_ptr, uint32_t *t_rec, float *t_maxabs,
-                             void *workspace, size_t workspace_bytes, grf_stream_t stream) {
-    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && ptr && idx && val && t_ptr && t_rec && t_maxabs,
-                GRF_EINVAL, "grf_transpose_banded: bad arguments");
-    GRF_REQUIRE(((uintptr_t)t_rec & 15) == 0, GRF_EINVAL, "grf_transpose_banded: t_rec must be 16-byte aligned");
+int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
+                                  const int32_t *idx, uint32_t *t_desc, void *workspace, size_t workspace_bytes,
+                                  grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 65536 && ptr && idx && t_desc,
+                GRF_EINVAL, "grf_transpose_banded_plan: bad arguments");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
     GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,
-                "grf_transpose_banded: workspace too small (%zu < %zu)", workspace_bytes,
+                "grf_transpose_banded_plan: workspace too small (%zu < %zu)", workspace_bytes,
                 grf_transpose_workspace_bytes(nbk));
     hipStream_t st = S(stream);
-    int32_t *cnt = (int32_t *)workspace;
-    size_t a = ((size_t)nbk * sizeof(int32_t) + 255) & ~(size_t)255;
-    void *scan_ws = (char *)workspace + a;
+    char *w = (char *)workspace;
+    int32_t *cnt = (int32_t *)w;
+    int32_t *lines = (int32_t *)(w + tr_align((size_t)nbk * 4));
+    int64_t *line_off = (int64_t *)(w + 2 * tr_align((size_t)nbk * 4));
+    void *scan_ws = w + 2 * tr_align((size_t)nbk * 4) + tr_align((size_t)(nbk + 1) * 8);
     GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));
-    GRF_CHECK_HIP(hipMemsetAsync(t_maxabs, 0, sizeof(float), st));
     if (n_rows > 0) {
+        GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "tr_count_kernel");
         tr_count_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, st>>>(n_rows, n_cols, band_width, ptr, idx,
                                                                           cnt);
         GRF_CHECK_LAUNCH("tr_count_kernel");
     }
-    tr_pad_counts_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, cnt);
-    GRF_CHECK_LAUNCH("tr_pad_counts_kernel");
-    int32_t rc = scan_counts_i32(nbk, cnt, t_ptr, scan_ws, workspace_bytes - a, st);
+    GRF_REQUIRE_GRID(cdiv<int64_t>(nbk, 256), 256, "tr_lines_kernel");
+    tr_lines_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, cnt, lines);
+    GRF_CHECK_LAUNCH("tr_lines_kernel");
+    int32_t rc = scan_counts_i32(nbk, lines, line_off, scan_ws, scan_ws_bytes(nbk), st);
     if (rc != GRF_OK) return rc;
-    GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));
+    GRF_REQUIRE_GRID(cdiv<int64_t>(nbk + 1, 256), 256, "tr_desc_kernel");
+    tr_desc_kernel<<<(unsigned)cdiv<int64_t>(nbk + 1, 256), 256, 0, st>>>(nbk, cnt, line_off,
+                                                                         reinterpret_cast<uint2 *>(t_desc));
+    GRF_CHECK_LAUNCH("tr_desc_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
+                                  const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
+                                  int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift, void *workspace,
+                                  size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 65536 && ptr && idx && val && t_desc &&
+                    t_rec && t_maxabs && t_rowshift && t_rec_bytes >= 0,
+                GRF_EINVAL, "grf_transpose_banded_fill: bad arguments");
+    GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_transpose_banded_fill: t_rec must be 128-byte aligned");
+    const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
+    GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,
+                "grf_transpose_banded_fill: workspace too small");
+    hipStream_t st = S(stream);
+    char *w = (char *)workspace;
+    int32_t *cursor = (int32_t *)w;
+    float *row_max = (float *)(w + tr_align((size_t)nbk * 4));                                // n_rows <= nbk
+    double *row_sum = (double *)(w + 2 * tr_align((size_t)nbk * 4));                         // n_rows <= nbk + 1
+    const uint2 *desc = reinterpret_cast<const uint2 *>(t_desc);
+    GRF_CHECK_HIP(hipMemsetAsync(cursor, 0, (size_t)nbk * sizeof(int32_t), st));
+    GRF_CHECK_HIP(hipMemsetAsync(t_maxabs, 0, sizeof(float), st));
     if (n_rows > 0) {
+        GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "tr_fill_kernel");
         tr_fill_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, st>>>(
-            n_rows, n_cols, band_width, ptr, idx, val, t_ptr, cnt, reinterpret_cast<uint2 *>(t_rec),
-            reinterpret_cast<unsigned int *>(t_maxabs));
+            n_rows, n_cols, band_width, ptr, idx, val, desc, cursor, (unsigned char *)t_rec,
+            reinterpret_cast<unsigned int *>(t_maxabs), row_max, row_sum);
         GRF_CHECK_LAUNCH("tr_fill_kernel");
+        GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 256), 256, "tr_rowshift_kernel");
+        tr_rowshift_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 256), 256, 0, st>>>(n_rows, row_max, row_sum, t_maxabs,
+                                                                                t_rowshift);
+        GRF_CHECK_LAUNCH("tr_rowshift_kernel");
     }
-    tr_pad_fill_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, t_ptr, cnt,
-                                                                          reinterpret_cast<uint2 *>(t_rec));
+    GRF_REQUIRE_GRID(cdiv<int64_t>(nbk, 256), 256, "tr_pad_fill_kernel");
+    tr_pad_fill_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, desc, cursor, (unsigned char *)t_rec);
     GRF_CHECK_LAUNCH("tr_pad_fill_kernel");
     return GRF_OK;
 }

@@ -254,6 +254,7 @@ int32_t grf_steps(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32
     const int P = (int)next_pow2_u32((uint32_t)m);
     const int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
     const size_t lds = (size_t)P * sizeof(uint64_t) + 128;
+    GRF_REQUIRE_GRID((n_src * L), T, "steps_kernel");
     steps_kernel<<<(unsigned)(n_src * L), T, lds, S(stream)>>>(m, norm, P, slot_node, slot_load, step_cnt, step_idx,
                                                               step_val);
     GRF_CHECK_LAUNCH("steps_kernel");
@@ -270,6 +271,7 @@ int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, co
     GRF_REQUIRE(phi_cap >= 1, GRF_EINVAL, "grf_phi: phi_cap must be >= 1");
     if (n_src == 0) return GRF_OK;
     const int32_t Lf = n_f < L ? n_f : L;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_src, 4), 256, "phi_merge_kernel");
     phi_merge_kernel<<<(unsigned)cdiv<int64_t>(n_src, 4), 256, 0, S(stream)>>>(
         n_src, m, L, Lf, step_cnt, step_idx, step_val, f, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
     GRF_CHECK_LAUNCH("phi_merge_kernel");
@@ -292,6 +294,7 @@ int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const i
     const size_t lds = (size_t)P * 8 + (size_t)E * 8 + (size_t)P * 8 + 128;
     const int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
     const int32_t Lf = n_f < L ? n_f : L;
+    GRF_REQUIRE_GRID(n_src, T, "phi_fused_kernel");
     phi_fused_kernel<<<(unsigned)n_src, T, lds, S(stream)>>>(m, L, norm, P, wbits, lbits, slot_node, slot_load, f, Lf,
                                                              phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
     GRF_CHECK_LAUNCH("phi_fused_kernel");
@@ -303,6 +306,7 @@ int32_t grf_steps_densify(int64_t n_src, int64_t m, int32_t L, int64_t n_cols, c
     GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && n_cols >= 0 && step_cnt && step_idx && step_val && out,
                 GRF_EINVAL, "grf_steps_densify: bad arguments");
     if (n_src == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_src * L, 4), 256, "steps_densify_kernel");
     steps_densify_kernel<<<(unsigned)cdiv<int64_t>(n_src * L, 4), 256, 0, S(stream)>>>(n_src, m, L, n_cols, step_cnt,
                                                                                       step_idx, step_val, out);
     GRF_CHECK_LAUNCH("steps_densify_kernel");

@@ -238,6 +238,7 @@ extern "C" __attribute__((visibility("default"))) int32_t grf_walk(int64_t n, co
     if (n_src == 0) return GRF_OK;
     if (P.rng == GRF_RNG_PHILOX) {
         const int64_t total = n_src * P.walks_per_node;
+        GRF_REQUIRE_GRID(cdiv<int64_t>(total, 256), 256, "walk_philox_kernel");
         walk_philox_kernel<<<(unsigned)cdiv<int64_t>(total, 256), 256, 0, st>>>(
             g_ptr, g_idx, g_val, P.walks_per_node, P.p_halt, P.max_walk_length, P.load_rule, (uint32_t)P.seed,
             (uint32_t)(P.seed >> 32), src_begin, n_src, slot_node, slot_load);
@@ -264,6 +265,7 @@ extern "C" __attribute__((visibility("default"))) int32_t grf_walk(int64_t n, co
     // empty chunks (n_chunks > n) have first(c) == first(c+1); cover [cb, ce) plus trailing empties is harmless
     const int64_t nch = ce - cb;
     if (nch <= 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(nch, 64), 64, "walk_pcg64_kernel");
     walk_pcg64_kernel<<<(unsigned)cdiv<int64_t>(nch, 64), 64, 0, st>>>(
         n, g_ptr, g_idx, g_val, P.walks_per_node, P.p_halt, P.max_walk_length, P.load_rule, P.n_chunks, P.seed, cb,
         ce, src_begin, slot_node, slot_load);

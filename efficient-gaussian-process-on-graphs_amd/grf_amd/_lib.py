@@ -60,7 +60,8 @@ SIGNATURES = {
     "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_scan_workspace_bytes": (_sz, [_i64]),
     "grf_compact_rows": (_i32, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "grf_transpose_banded": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "grf_transpose_banded_plan": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "grf_transpose_banded_fill": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_transpose_workspace_bytes": (_sz, [_i64]),
     "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),

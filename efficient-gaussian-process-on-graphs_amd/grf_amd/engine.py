@@ -118,9 +118,10 @@ class PaddedRows:
 
 @dataclass
 class Banded:
-    t_ptr: torch.Tensor  # int64 [n_bands * n_cols + 1]
-    t_rec: torch.Tensor  # int32 [2 * cap]: (j - band * band_width, float32 bits) records, padded to pairs
+    t_desc: torch.Tensor  # int32 [2 * (n_bands * n_cols + 1)]: per bucket {first 128-B line, pairs}
+    t_rec: torch.Tensor   # uint8 [lines * 128]: 12-byte record pairs {u16 j0 | u16 j1, f32 v0, f32 v1}
     t_maxabs: torch.Tensor  # float32 [1], max |Phi|
+    t_rowshift: torch.Tensor  # int32 [n_rows], Gram fixed-point scale exponent per row
     band_width: int
     n_rows: int
     n_cols: int
@@ -286,14 +287,26 @@ class GRFEngine:
         n_rows, n_cols = phi.n_rows, phi.n_cols
         nb = -(-n_rows // band_width)
         nbk = nb * n_cols
-        t_ptr = self._empty(nbk + 1, torch.int64)
-        t_rec = self._empty(2 * (phi.nnz + nbk) + 4, torch.int32)  # torch allocations are 256-B aligned
+        t_desc = self._empty(2 * (nbk + 1), torch.int32)
         t_max = self._empty(1, torch.float32)
+        t_shift = self._empty(max(n_rows, 1), torch.int32)
         ws = self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
-        C.check(self.lib.grf_transpose_banded(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
-                                              _p(t_ptr), _p(t_rec), _p(t_max), _p(ws), ws.numel(), self.stream),
-                "grf_transpose_banded")
-        return Banded(t_ptr, t_rec, t_max, band_width, n_rows, n_cols)
+        C.check(self.lib.grf_transpose_banded_plan(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(t_desc),
+                                                   _p(ws), ws.numel(), self.stream), "grf_transpose_banded_plan")
+        # band starts (first line of bucket (band, 0)) and the total: the Gram kernel addresses a
+        # band's records with 32-bit byte offsets
+        starts = torch.cat([t_desc[0:2 * nbk:2 * n_cols], t_desc[2 * nbk:2 * nbk + 1]]).cpu().numpy()
+        starts = starts.view(np.uint32).astype(np.int64)
+        tail = t_desc[2 * nbk:].cpu().numpy().view(np.uint32).astype(np.int64)
+        lines = int(tail[0] + (tail[1] << 32))
+        starts[-1] = lines
+        if nb and int(np.diff(starts).max(initial=0)) * 128 >= 2 ** 31:
+            raise NotImplementedError("a transpose band holds >= 2 GiB of records; use a smaller band_width")
+        t_rec = self._empty(max(lines, 1) * 128, torch.uint8)  # torch allocations are 256-B aligned
+        C.check(self.lib.grf_transpose_banded_fill(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx),
+                                                   _p(phi.val32), _p(t_desc), _p(t_rec), t_rec.numel(), _p(t_max),
+                                                   _p(t_shift), _p(ws), ws.numel(), self.stream), "grf_transpose_banded_fill")
+        return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols)
 
     # ----------------------------------------------------------------- Gram
     @staticmethod
@@ -309,7 +322,7 @@ class GRFEngine:
         if out is None:
             out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_gram_sparse(n, row_begin, row_end, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
-                                         tr.band_width, _p(tr.t_ptr), _p(tr.t_rec), _p(tr.t_maxabs), _p(out),
+                                         tr.band_width, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out),
                                          out.stride(0), self.stream), "grf_gram_sparse")
         return out[:, :n]
 

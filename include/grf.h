@@ -162,31 +162,39 @@ int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const 
                          double *out_val, float *out_val32, grf_stream_t stream);
 
 /* Banded transpose for the Gram kernel: entries (j, k, v) of Phi (CSR rows j)
- * bucketed by (band = j / band_width, k):  bucket id = band * n_cols + k.
- * Records are (uint32 j - band * band_width, float32 bits of v) pairs of words;
- * every bucket is padded to an even number of records with (0, +0.0).
- * t_ptr[n_bands * n_cols + 1] (record offsets, all even), t_rec[2 * cap] with
- * cap >= nnz + n_bands * n_cols (16-byte aligned).  t_maxabs[1] receives max |Phi|
- * (the fixed-point scale bound of the Gram kernel).
- * workspace >= grf_transpose_workspace_bytes(n_bands * n_cols). */
-int32_t grf_transpose_banded(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                             const int32_t *idx, const float *val, int64_t *t_ptr, uint32_t *t_rec, float *t_maxabs,
-                             void *workspace, size_t workspace_bytes, grf_stream_t stream);
+ * bucketed by (band = j / band_width, k):  bucket id b = band * n_cols + k.
+ * A bucket is a run of 12-byte record PAIRS {u16 j0 - band start, u16 j1 - band start
+ * (low / high half of one word), f32 v0, f32 v1}, starting on a 128-byte line; an odd
+ * bucket ends with the pad record (0, +0.0).  Two calls:
+ *   plan: t_desc[2 * (n_bands * n_cols + 1)] = per bucket {first line, pairs}; the last
+ *         entry holds the total line count (lo, hi words).
+ *   fill: t_rec (>= total lines * 128 bytes, 128-byte aligned), t_maxabs[1] = max |Phi| and
+ *         t_rowshift[n_rows]: the Gram kernel's per-row fixed-point scale 2^shift (every term
+ *         < 2^51, the row's sum of |terms| < 2^62).
+ * workspace >= grf_transpose_workspace_bytes(n_bands * n_cols), shared by both calls.
+ * band_width <= 65536. */
+int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
+                                  const int32_t *idx, uint32_t *t_desc, void *workspace, size_t workspace_bytes,
+                                  grf_stream_t stream);
+int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
+                                  const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
+                                  int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift, void *workspace,
+                                  size_t workspace_bytes, grf_stream_t stream);
 size_t grf_transpose_workspace_bytes(int64_t n_buckets);
 
 /* ---------------------------------------------------------------------- Gram
  * Replaces `Phi @ Phi.T` of fast_grf_kernel_general.py:55 (sparse) and :39 (dense).
  * Sparse path: K[r, :] for rows r in [row_begin, row_end) of Phi (compact CSR,
  * float32 values) against the banded transpose of the FULL Phi (band_width equal
- * to the transpose's, multiple of 16, <= 8192; t_rec / t_maxabs from the transpose).
+ * to the transpose's, multiple of 16, <= 8192; t_desc / t_rec / t_rowshift from the transpose).
  * K is float32, row-major with leading dimension ldk (>= n_total); K row
  * (r - row_begin) is written.  Each K entry is the fp32 rounding of the exact
  * int64 fixed-point sum of the exact products Phi[r,k]*Phi[j,k] (per-row
  * power-of-two scale), so K does not depend on summation order: it is
  * bit-reproducible run to run, across row splits and GPU counts. */
 int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
-                        const float *val, int64_t band_width, const int64_t *t_ptr, const uint32_t *t_rec,
-                        const float *t_maxabs, float *K, int64_t ldk, grf_stream_t stream);
+                        const float *val, int64_t band_width, const uint32_t *t_desc, const void *t_rec,
+                        const int32_t *t_rowshift, float *K, int64_t ldk, grf_stream_t stream);
 
 /* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
  * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */

@@ -235,6 +235,21 @@ def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
     assert np.array_equal(eng.gram_sparse(phi, eng.transpose_banded(phi, bw)).cpu().numpy(), K)
 
 
+def test_gram_sparse_split_launch_and_band_invariance(eng):
+    """Tiles x threads > 2^32 (W = 16 at n = 20000) must be split into several launches, and the
+    int64 fixed-point K is independent of the band width -- bit for bit."""
+    n = 20000
+    A = er_graph(n, 6, 99)
+    G = eng.laplacian(A)
+    slots = eng.walk(G, 4, 0.3, 3, rng=1, seed=5)
+    phi = eng.compact(eng.features(slots, [1.0, -0.5, 0.25]))
+    K_wide = eng.gram_sparse(phi, eng.transpose_banded(phi, 4096)).cpu().numpy()
+    K_narrow = eng.gram_sparse(phi, eng.transpose_banded(phi, 16)).cpu().numpy()
+    assert np.array_equal(K_wide, K_narrow)
+    ok, fro = gram_close(K_wide[:16], phi.to_scipy(), (0, 16))
+    assert ok, fro
+
+
 @pytest.mark.parametrize("n", [1, 31, 128, 1000, 2708])
 def test_gram_dense_mfma_vs_oracle(eng, n):
     A = er_graph(max(n, 2), 6, n + 1)[:n, :n]

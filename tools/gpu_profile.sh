@@ -1,0 +1,16 @@
+#!/bin/bash
+# Bench + kernel-trace stats + PMC passes for the headline config (writes gpurun_out/<tag>/).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+TAG=${1:-prof}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail $O/bench.err; exit 1; }
+echo bench ok; cat $O/bench.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
+    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/trace.log 2>&1 || { echo trace failed; tail $O/trace.log; exit 1; }
+echo trace ok
+$R/tools/pmc_passes.sh $O/pmc $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline || exit 1
+python3 $R/tools/pmc_summary.py $O/pmc > $O/pmc_summary.json && echo pmc ok
