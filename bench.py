@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--p-halt", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=2048)
+    ap.add_argument("--no-sym", action="store_true", help="single GPU: compute every K tile (no symmetric mode)")
     args = ap.parse_args()
 
     import torch
@@ -144,7 +145,10 @@ def main():
         tr = eng.transpose_banded(phi)
         if record:
             ev[0].record()
-        eng.gram_sparse(phi, tr, b, e, out=K)
+        if world == 1 and not args.no_sym:
+            eng.gram_sparse_sym(phi, tr, out=K)  # upper band tiles + mirror
+        else:
+            eng.gram_sparse(phi, tr, b, e, out=K)
         if record:
             ev[1].record()
             ev[1].synchronize()
@@ -177,8 +181,8 @@ def main():
         gram_avg = float(np.mean(gram_ms))
 
     ms_per_step = 1000.0 * t / args.steps
-    # algorithmic bytes of one gram_sparse launch: write this rank's K rows once, read
-    # its Phi rows (col int32 + val fp32) and every Phi^T entry at least once
+    # algorithmic bytes of the K assembly (gram_sparse_kernel [+ gram_mirror_kernel]): write this
+    # rank's K rows once, read its Phi rows (col int32 + val fp32) and every Phi^T entry once
     rows = e - b
     alg_bytes = 4.0 * rows * n + 8.0 * local_nnz + 8.0 * nnz_phi[0]
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
@@ -202,7 +206,8 @@ def main():
                    "parallelism": f"source-sharded x{world}, Phi all-gather, K row blocks"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "gram_sparse_kernel", "kernel_ms": gram_avg, "algorithmic_bytes": alg_bytes},
+                     "kernel": ("gram_sparse_kernel+gram_mirror_kernel" if world == 1 and not args.no_sym
+                                else "gram_sparse_kernel"), "kernel_ms": gram_avg, "algorithmic_bytes": alg_bytes},
         "nnz_phi": nnz_phi[0],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -19,7 +19,10 @@
 //
 // Dense path: LDS-tiled fp32 MFMA (v_mfma_f32_32x32x2f32, exact f32 FMA chain),
 // 128x128 tile per 256-thread workgroup, 2x2 waves of 64x64.
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <algorithm>
 
 #include "grf_block.h"
 
@@ -27,7 +30,8 @@ namespace grf {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kChunk = 1024;  // stream positions covered by one bucket-id chunk
+constexpr int kChunk = 1008;  // stream positions covered by one bucket-id chunk
+constexpr int kWaveState = 1024 + 128 * 4 + 128 * 4;  // per wave: ids [kChunk], spare 16 B, tbase, aval
 
 // |x| < 2^51 -> round-to-nearest int64 with one f64 add and one integer subtract
 __device__ inline long long fx_round(double x) {
@@ -109,65 +113,85 @@ __device__ inline float fx_to_float(unsigned long long a, int sh) {
 // LDS bytes of one gram_sparse_kernel workgroup (W int64 counters + per-wave stream state):
 // at W = 4096 and 4 waves exactly 40 KiB, i.e. four workgroups per CU.
 constexpr size_t gram_lds_bytes(int64_t W, int waves) {
-    return (size_t)W * 8 + (size_t)waves * (kChunk + 128 * 4 + 128 * 4);
+    return (size_t)W * 8 + (size_t)waves * kWaveState;
 }
 
-// One workgroup of kWaves waves = one tile K[row, j0 : j0 + W] (W = a band of the
-// banded transpose).  Accumulation is exact int64 fixed point with the per-row
-// power-of-two scale S = 2^rowshift[row] (from the transpose) chosen so that every term
-// |Phi[row,k] Phi[j,k]| S < 2^51 and the sum of all terms < 2^62: each exact fp64 product
-// is rounded once to an integer and the integer sum does not depend on the order of the
-// adds (ds_add_u64) -- nor on scheduling, GPU count or row split.
+// Tiles of one Gram call in band-major order: band J holds count(J) tiles, the local rows
+// 0 .. count(J)-1 (full mode: all rows; symmetric mode, whole K: the rows of bands <= J).
+struct GramTiles {
+    int64_t rows, W, nb;
+    bool sym;
+    __host__ __device__ int64_t count(int64_t J) const {
+        if (!sym) return rows;
+        const int64_t c = (J + 1) * W;
+        return c < rows ? c : rows;
+    }
+    // tiles before band J
+    __host__ __device__ int64_t before(int64_t J) const {
+        if (!sym) return J * rows;
+        const int64_t full = (rows + W - 1) / W - 1;  // bands J < full hold (J + 1) W rows
+        return J <= full ? W * J * (J + 1) / 2 : W * full * (full + 1) / 2 + (J - full) * rows;
+    }
+    __host__ __device__ int64_t total() const { return before(nb); }
+    // band and local row of tile t
+    __device__ void locate(int64_t t, int64_t &J, int64_t &r) const {
+        if (!sym) {
+            J = t / rows;
+        } else {
+            J = (int64_t)((sqrt(8.0 * (double)(t / W) + 1.0) - 1.0) * 0.5);
+            if (J > nb - 1) J = nb - 1;
+            while (J > 0 && before(J) > t) --J;
+            while (J < nb - 1 && before(J + 1) <= t) ++J;
+        }
+        r = t - before(J);
+    }
+};
+
+// One workgroup of kWaves waves = one tile K[row, j0 : j0 + W] (W = a band of the banded
+// transpose), accumulated in LDS in exact int64 fixed point with the per-row power-of-two
+// scale S = 2^rowshift[row] (from the transpose) such that every term |Phi[row,k] Phi[j,k]| S
+// < 2^51 and the sum of all terms < 2^62: each exact fp64 product is rounded once to an
+// integer and the integer sum does not depend on the order of the adds (ds_add_u64) -- nor
+// on scheduling, GPU count, row split or band width.
 // Phi^T buckets hold 12-byte record pairs starting on 128-byte lines; wave w takes the
 // batches w, w + kWaves, ... of 128 nonzeros of the row and flattens each batch's buckets
 // into one stream of PAIRS.  The bucket of each pair comes from a per-position u8 bucket
 // id that the lanes fill for their own buckets (one LDS read); the gathers of kGramUnroll
-// windows of 64 pairs are in flight together.
-// Optional placement (speed only, kXcd): blocks b and b+8 are dealt to the same XCD, so
-// block b % 8 = x works on bands x, x+8, ...: each XCD's L2 holds one band's slice.
-template <int kWaves, int kGramUnroll, bool kXcd>
+// windows of 64 pairs are in flight together.  Tiles are dispatched band-major, so the
+// tiles in flight share one band's records (L2 / Infinity Cache).
+template <int kWaves, int kGramUnroll>
 __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
-    int64_t n_total, int64_t row_begin, int64_t n_rows, int64_t W, int64_t nb, const int64_t *__restrict__ ptr,
+    int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
     const unsigned char *__restrict__ t_rec, const int32_t *__restrict__ rowshift, float *__restrict__ K,
     int64_t ldk) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    unsigned char *st = reinterpret_cast<unsigned char *>(acc + W) + wave * (kChunk + 128 * 8);
-    unsigned char *bidv = st;                                        // [kChunk]
-    int32_t *tbase = reinterpret_cast<int32_t *>(st + kChunk);       // [128]
-    float *aval = reinterpret_cast<float *>(st + kChunk + 128 * 4);  // [128]
+    const int64_t W = tl.W;
+    unsigned char *st = reinterpret_cast<unsigned char *>(acc + W) + wave * kWaveState;
+    unsigned char *bidv = st;                                      // [kChunk]
+    int32_t *tbase = reinterpret_cast<int32_t *>(st + 1024);       // [128]
+    float *aval = reinterpret_cast<float *>(st + 1024 + 128 * 4);  // [128]
 
-    const int64_t blk = blockIdx.x;
-    int64_t band, r;
-    if (kXcd) {
-        const int64_t xcd = blk & 7, s = blk >> 3;
-        const int64_t phase = s / n_rows;
-        r = s - phase * n_rows;
-        band = xcd + 8 * phase;
-        if (band >= nb) return;  // uniform over the workgroup
-    } else {
-        band = blk / n_rows;
-        r = blk - band * n_rows;
-    }
+    int64_t J, r;
+    tl.locate(t_begin + (int64_t)blockIdx.x, J, r);
     const int64_t row = row_begin + r;
-    const int64_t j0 = band * W;
+    const int64_t j0 = J * W;
     const int64_t wlen = (n_total - j0) < W ? (n_total - j0) : W;
     const int64_t e0 = ptr[row], e1 = ptr[row + 1];
-    const int64_t boff = band * n_total;
+    const int64_t boff = J * n_total;
     const int sh = rowshift[row];
-    // the band's records, addressed by 32-bit offsets from its first line
-    const unsigned char *brec = t_rec + (int64_t)t_desc[boff].x * 128;
+    const int32_t line0 = (int32_t)t_desc[boff].x;
+    const unsigned char *brec = t_rec + (int64_t)line0 * 128;  // the band's records
 
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     u64x2 *acc2 = reinterpret_cast<u64x2 *>(acc);
     const u64x2 z2 = {0ull, 0ull};
-    for (int64_t i = tid; i < (wlen + 1) / 2; i += 64 * kWaves) acc2[i] = z2;
+    for (int64_t i = tid; i < W / 2; i += 64 * kWaves) acc2[i] = z2;
     if (kWaves > 1) __syncthreads();
     else __builtin_amdgcn_wave_barrier();
 
     const GramStream gs{bidv, tbase, aval, brec, acc, ldexp(1.0, sh)};
-    const int32_t line0 = (int32_t)t_desc[boff].x;
     for (int64_t g0 = e0 + (int64_t)wave * 128; g0 < e1; g0 += 128 * kWaves) {
         int32_t cnt[2], excl[2], t0[2];
         float av[2];
@@ -211,6 +235,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     if (kWaves > 1) __syncthreads();
     else __builtin_amdgcn_wave_barrier();
 
+    // write the tile once (non-temporal: K is write-once)
     float *krow = K + r * ldk + j0;
     if ((ldk & 3) == 0 && (j0 & 3) == 0) {
         const int64_t n4 = wlen / 4;
@@ -227,6 +252,31 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
         for (int64_t i = n4 * 4 + tid; i < wlen; i += 64 * kWaves) krow[i] = fx_to_float(acc[i], sh);
     } else {
         for (int64_t i = tid; i < wlen; i += 64 * kWaves) krow[i] = fx_to_float(acc[i], sh);
+    }
+}
+
+// Symmetric completion: K[j, i] = K[i, j] for every j > i (the Gram launch in symmetric
+// mode wrote the tiles K[i, band >= band(i)], which cover the upper triangle; the lower
+// parts of the diagonal band tiles are overwritten, so K is exactly symmetric).  One
+// workgroup moves a 64 x 64 block through LDS: coalesced 256-byte row reads and writes.
+__global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, float *__restrict__ K, int64_t ldk) {
+    __shared__ float tile[64][65];
+    const int64_t bi = blockIdx.y, bj = blockIdx.x;  // source block K[bi*64.., bj*64..]
+    const int64_t i0 = bi * 64, j0 = bj * 64;
+    if (bj < bi || j0 >= n) return;  // upper-triangle blocks only
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int y = ty + 4 * q;
+        const int64_t i = i0 + y, j = j0 + tx;
+        tile[y][tx] = (i < n && j < n) ? K[i * ldk + j] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int y = ty + 4 * q;
+        const int64_t j = j0 + y, i = i0 + tx;
+        if (i < n && j < n && j > i) __builtin_nontemporal_store(tile[tx][y], &K[j * ldk + i]);
     }
 }
 
@@ -305,56 +355,80 @@ using namespace grf;
 extern "C" {
 #pragma GCC visibility push(default)
 
-int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
-                        const float *val, int64_t band_width, const uint32_t *t_desc, const void *t_rec,
-                        const int32_t *t_rowshift, float *K, int64_t ldk, grf_stream_t stream) {
+size_t grf_gram_workspace_bytes(void) { return 256; }
+
+static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t rows, bool sym, const int64_t *ptr,
+                                  const int32_t *idx, const float *val, int64_t band_width, const uint32_t *t_desc,
+                                  const void *t_rec, const int32_t *t_rowshift, float *K, int64_t ldk,
+                                  hipStream_t st) {
+    const int64_t nb = cdiv<int64_t>(n_total, band_width);
+    const GramTiles tl{rows, band_width, nb, sym};
+    const int64_t n_tiles = tl.total();
+    if (n_tiles == 0) return GRF_OK;
+    // tuning knob (default = measured best on MI355X): gathers in flight per wave
+    static const int unroll = [] {
+        const char *e = getenv("GRF_GRAM_UNROLL");
+        const int u = e ? atoi(e) : 8;
+        return (u == 4 || u == 8 || u == 16) ? u : 8;
+    }();
+    const size_t lds = gram_lds_bytes(band_width, 4);
+    // one launch covers at most 2^32 - 1 work-items: split the tile range
+    const int64_t max_tiles = ((1ll << 32) - 1) / 256;
+    for (int64_t t0 = 0; t0 < n_tiles; t0 += max_tiles) {
+        const int64_t nt = (n_tiles - t0) < max_tiles ? (n_tiles - t0) : max_tiles;
+#define GRF_GRAM_LAUNCH(U)                                                                                        \
+    gram_sparse_kernel<4, U><<<(unsigned)nt, 256, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx, val,           \
+                                                            reinterpret_cast<const uint2 *>(t_desc),              \
+                                                            reinterpret_cast<const unsigned char *>(t_rec),       \
+                                                            t_rowshift, K, ldk)
+        switch (unroll) {
+            case 4: GRF_GRAM_LAUNCH(4); break;
+            case 16: GRF_GRAM_LAUNCH(16); break;
+            default: GRF_GRAM_LAUNCH(8); break;
+        }
+#undef GRF_GRAM_LAUNCH
+        GRF_CHECK_LAUNCH("gram_sparse_kernel");
+    }
+    return GRF_OK;
+}
+
+static int32_t gram_sparse_check(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                                 int64_t band_width, const uint32_t *t_desc, const void *t_rec,
+                                 const int32_t *t_rowshift, float *K, int64_t ldk) {
     GRF_REQUIRE(n_total >= 0 && 0 <= row_begin && row_begin <= row_end && row_end <= n_total && ptr && t_desc && K &&
                     t_rowshift && t_rec,
                 GRF_EINVAL, "grf_gram_sparse: bad arguments");
     GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_gram_sparse: t_rec must be 128-byte aligned");
     GRF_REQUIRE(ldk >= n_total, GRF_EINVAL, "grf_gram_sparse: ldk < n");
-    GRF_REQUIRE(band_width >= 16 && band_width % 16 == 0 && band_width <= 8192, GRF_EUNSUPPORTED,
-                "grf_gram_sparse: band_width must be a multiple of 16 in [16, 8192]");
-    const int64_t rows = row_end - row_begin;
-    if (rows == 0 || n_total == 0) return GRF_OK;
-    const int64_t nb = cdiv<int64_t>(n_total, band_width);
-    // tuning knobs (defaults = measured best on MI355X): waves per tile, unroll, XCD pinning
-    static const int knobs = [] {
-        const char *e = getenv("GRF_GRAM_UNROLL"), *x = getenv("GRF_GRAM_XCD"), *w = getenv("GRF_GRAM_WAVES");
-        const int u = e ? atoi(e) : 8, ww = w ? atoi(w) : 4;
-        return ((u == 4 || u == 8 || u == 16) ? u : 8) + (x && atoi(x) ? 100 : 0) + (ww == 1 ? 1000 : 0);
-    }();
-    const bool xcd = (knobs / 100) % 10 == 1;
-    const int unroll = knobs % 100, waves = knobs >= 1000 ? 1 : 4;
-    const int64_t per_row = xcd ? 8 * cdiv<int64_t>(nb, 8) : nb;
-    const size_t lds = gram_lds_bytes(band_width, waves);
-    const uint2 *desc = reinterpret_cast<const uint2 *>(t_desc);
-    const unsigned char *rec = reinterpret_cast<const unsigned char *>(t_rec);
-    // one launch covers at most 2^32 - 1 work-items: split the row range
-    const int64_t max_rows = ((1ll << 32) - 1) / (per_row * 64 * waves);
-    GRF_REQUIRE(max_rows >= 1, GRF_EUNSUPPORTED, "grf_gram_sparse: too many bands for one row");
-    for (int64_t r0 = 0; r0 < rows; r0 += max_rows) {
-        const int64_t rr = (rows - r0) < max_rows ? (rows - r0) : max_rows;
-        const int64_t tiles = per_row * rr;
-        float *Kr = K + r0 * ldk;
-#define GRF_GRAM_LAUNCH(WV, U, X)                                                                                 \
-    gram_sparse_kernel<WV, U, X><<<(unsigned)tiles, 64 * WV, lds, S(stream)>>>(                                   \
-        n_total, row_begin + r0, rr, band_width, nb, ptr, idx, val, desc, rec, t_rowshift, Kr, ldk)
-#define GRF_GRAM_U(WV, X)                                                                                         \
-    switch (unroll) {                                                                                             \
-        case 4: GRF_GRAM_LAUNCH(WV, 4, X); break;                                                                 \
-        case 16: GRF_GRAM_LAUNCH(WV, 16, X); break;                                                               \
-        default: GRF_GRAM_LAUNCH(WV, 8, X); break;                                                                \
-    }
-        if (waves == 1) {
-            if (xcd) { GRF_GRAM_U(1, true) } else { GRF_GRAM_U(1, false) }
-        } else {
-            if (xcd) { GRF_GRAM_U(4, true) } else { GRF_GRAM_U(4, false) }
-        }
-#undef GRF_GRAM_U
-#undef GRF_GRAM_LAUNCH
-        GRF_CHECK_LAUNCH("gram_sparse_kernel");
-    }
+    GRF_REQUIRE(band_width >= 64 && band_width % 64 == 0 && band_width <= 8192, GRF_EUNSUPPORTED,
+                "grf_gram_sparse: band_width must be a multiple of 64 in [64, 8192]");
+    return GRF_OK;
+}
+
+int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
+                        const float *val, int64_t band_width, const uint32_t *t_desc, const void *t_rec,
+                        const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
+                        grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, t_desc, t_rec, t_rowshift, K, ldk);
+    if (rc != GRF_OK) return rc;
+    if (row_end == row_begin || n_total == 0) return GRF_OK;
+    return gram_sparse_launch(n_total, row_begin, row_end - row_begin, false, ptr, idx, val, band_width, t_desc, t_rec,
+                              t_rowshift, K, ldk, S(stream));
+}
+
+int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                            int64_t band_width, const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift,
+                            float *K, int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, t_desc, t_rec, t_rowshift, K, ldk);
+    if (rc != GRF_OK) return rc;
+    if (n_total == 0) return GRF_OK;
+    rc = gram_sparse_launch(n_total, 0, n_total, true, ptr, idx, val, band_width, t_desc, t_rec, t_rowshift, K, ldk,
+                            S(stream));
+    if (rc != GRF_OK) return rc;
+    const int64_t nt = cdiv<int64_t>(n_total, 64);
+    GRF_REQUIRE(nt < 65536, GRF_EUNSUPPORTED, "grf_gram_sparse_sym: n too large for the mirror grid");
+    gram_mirror_kernel<<<dim3((unsigned)nt, (unsigned)nt), 256, 0, S(stream)>>>(n_total, K, ldk);
+    GRF_CHECK_LAUNCH("gram_mirror_kernel");
     return GRF_OK;
 }
 

@@ -63,7 +63,9 @@ SIGNATURES = {
     "grf_transpose_banded_plan": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_transpose_banded_fill": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_transpose_workspace_bytes": (_sz, [_i64]),
-    "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
+    "grf_gram_workspace_bytes": (_sz, []),
+    "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
 }

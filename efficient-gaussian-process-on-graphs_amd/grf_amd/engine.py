@@ -138,6 +138,8 @@ class GRFEngine:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         C.check(self.lib.grf_set_device(self.device.index), "grf_set_device")
+        # the Gram kernels' tile work counter (calls on this engine's stream are ordered)
+        self._gram_ws = self._ws(self.lib.grf_gram_workspace_bytes())
 
     # ------------------------------------------------------------ utilities
     @property
@@ -323,7 +325,20 @@ class GRFEngine:
             out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_gram_sparse(n, row_begin, row_end, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
                                          tr.band_width, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out),
-                                         out.stride(0), self.stream), "grf_gram_sparse")
+                                         out.stride(0), _p(self._gram_ws), self._gram_ws.numel(), self.stream),
+                "grf_gram_sparse")
+        return out[:, :n]
+
+    def gram_sparse_sym(self, phi: DeviceCSR, tr: Banded, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Whole K (float32) on this device from the upper band tiles plus a mirror pass."""
+        n = tr.n_rows
+        ldk = self.leading_dim(n)
+        if out is None:
+            out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
+        C.check(self.lib.grf_gram_sparse_sym(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
+                                             _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out), out.stride(0),
+                                             _p(self._gram_ws), self._gram_ws.numel(), self.stream),
+                "grf_gram_sparse_sym")
         return out[:, :n]
 
     def densify(self, phi: DeviceCSR) -> torch.Tensor:
@@ -350,6 +365,8 @@ class GRFEngine:
         if method == "dense":
             return self.gram_dense(self.densify(phi), phi.n_cols)
         if method == "sparse":
+            return self.gram_sparse_sym(phi, self.transpose_banded(phi))
+        if method == "sparse-rows":
             return self.gram_sparse(phi, self.transpose_banded(phi))
         raise ValueError(f"unknown gram method {method!r}")
 

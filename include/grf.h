@@ -186,7 +186,7 @@ size_t grf_transpose_workspace_bytes(int64_t n_buckets);
  * Replaces `Phi @ Phi.T` of fast_grf_kernel_general.py:55 (sparse) and :39 (dense).
  * Sparse path: K[r, :] for rows r in [row_begin, row_end) of Phi (compact CSR,
  * float32 values) against the banded transpose of the FULL Phi (band_width equal
- * to the transpose's, multiple of 16, <= 8192; t_desc / t_rec / t_rowshift from the transpose).
+ * to the transpose's, multiple of 64, <= 8192; t_desc / t_rec / t_rowshift from the transpose).
  * K is float32, row-major with leading dimension ldk (>= n_total); K row
  * (r - row_begin) is written.  Each K entry is the fp32 rounding of the exact
  * int64 fixed-point sum of the exact products Phi[r,k]*Phi[j,k] (per-row
@@ -194,7 +194,20 @@ size_t grf_transpose_workspace_bytes(int64_t n_buckets);
  * bit-reproducible run to run, across row splits and GPU counts. */
 int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
                         const float *val, int64_t band_width, const uint32_t *t_desc, const void *t_rec,
-                        const int32_t *t_rowshift, float *K, int64_t ldk, grf_stream_t stream);
+                        const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
+                        grf_stream_t stream);
+/* device workspace of one grf_gram_sparse / grf_gram_sparse_sym call (reserved for a tile
+ * work counter; this build does not touch it and accepts NULL) */
+size_t grf_gram_workspace_bytes(void);
+
+/* Whole K = Phi Phi^T on one device using its symmetry: the Gram kernel computes the tiles
+ * K[i, band >= band(i)] (about half the work) and a mirror pass copies K[j, i] = K[i, j]
+ * for band(j) > band(i).  Same arguments and per-entry values as grf_gram_sparse with
+ * row_begin = 0, row_end = n_total, except that the mirrored entries carry the
+ * fixed-point rounding of row i (K is exactly symmetric).  band_width multiple of 64. */
+int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                            int64_t band_width, const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift,
+                            float *K, int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
 
 /* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
  * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */

@@ -63,8 +63,9 @@ def gram_close(K, phi64, rows=None):
     absphi = abs(phi64)
     bound = O.gram_rows(absphi, r0, r1)
     # fixed-point resolution of the sparse Gram kernel: 2^-50 max_k|Phi_ik| max|Phi| per term
-    rowmax = np.asarray(absphi[r0:r1].max(axis=1).todense()).ravel()
-    fx = 1e-12 * rowmax[:, None] * absphi.max()
+    rowmax = np.asarray(absphi.max(axis=1).todense()).ravel()
+    # (a mirrored entry K[j, i] of the symmetric mode carries row i's resolution)
+    fx = 1e-12 * np.maximum(rowmax[r0:r1, None], rowmax[None, :]) * absphi.max()
     err = np.abs(np.asarray(K, np.float64) - Kref)
     ok_elem = bool(np.all(err <= 3e-5 * bound + fx + 1e-30))
     fro = np.linalg.norm(err) / max(np.linalg.norm(Kref), 1e-300)
@@ -218,7 +219,7 @@ def test_steps_dense_tensor(eng):
 
 
 # ----------------------------------------------------------------------- Gram
-@pytest.mark.parametrize("n,deg,m,L,bw", [(1000, 8, 32, 6, 64), (5000, 10, 64, 8, 256), (3000, 4, 16, 5, 8192), (777, 5, 8, 3, 128), (20000, 10, 32, 6, 4096)])
+@pytest.mark.parametrize("n,deg,m,L,bw", [(1000, 8, 32, 6, 64), (5000, 10, 64, 8, 256), (3000, 4, 16, 5, 8192), (777, 5, 8, 3, 128), (20000, 10, 32, 6, 4096), (4100, 6, 16, 4, 1024)])
 def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
     A = er_graph(n, deg, n)
     G = eng.laplacian(A)
@@ -233,18 +234,25 @@ def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
     Kb = eng.gram_sparse(phi, tr, 17, 300).cpu().numpy()
     assert np.array_equal(Kb, K[17:300])
     assert np.array_equal(eng.gram_sparse(phi, eng.transpose_banded(phi, bw)).cpu().numpy(), K)
+    # symmetric mode: the upper triangle is the same bits; the lower triangle is its mirror
+    Ks = eng.gram_sparse_sym(phi, tr).cpu().numpy()
+    assert np.array_equal(Ks, Ks.T)
+    upper = np.triu(np.ones((n, n), bool))
+    assert np.array_equal(Ks[upper], K[upper])
+    ok, fro = gram_close(Ks, phi.to_scipy())
+    assert ok, fro
 
 
-def test_gram_sparse_split_launch_and_band_invariance(eng):
-    """Tiles x threads > 2^32 (W = 16 at n = 20000) must be split into several launches, and the
-    int64 fixed-point K is independent of the band width -- bit for bit."""
+def test_gram_sparse_band_invariance(eng):
+    """The int64 fixed-point K is independent of the band width (many small tiles vs few wide
+    ones, 313 bands at W = 64) -- bit for bit."""
     n = 20000
     A = er_graph(n, 6, 99)
     G = eng.laplacian(A)
     slots = eng.walk(G, 4, 0.3, 3, rng=1, seed=5)
     phi = eng.compact(eng.features(slots, [1.0, -0.5, 0.25]))
     K_wide = eng.gram_sparse(phi, eng.transpose_banded(phi, 4096)).cpu().numpy()
-    K_narrow = eng.gram_sparse(phi, eng.transpose_banded(phi, 16)).cpu().numpy()
+    K_narrow = eng.gram_sparse(phi, eng.transpose_banded(phi, 64)).cpu().numpy()
     assert np.array_equal(K_wide, K_narrow)
     ok, fro = gram_close(K_wide[:16], phi.to_scipy(), (0, 16))
     assert ok, fro
