@@ -258,25 +258,52 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
 // Symmetric completion: K[j, i] = K[i, j] for every j > i (the Gram launch in symmetric
 // mode wrote the tiles K[i, band >= band(i)], which cover the upper triangle; the lower
 // parts of the diagonal band tiles are overwritten, so K is exactly symmetric).  One
-// workgroup moves a 64 x 64 block through LDS: coalesced 256-byte row reads and writes.
-__global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, float *__restrict__ K, int64_t ldk) {
+// workgroup per upper-triangle 64 x 64 block (triangular grid: no idle workgroups) moves
+// it through LDS with 16-byte loads and 16-byte non-temporal stores.
+__global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, int64_t nt, float *__restrict__ K, int64_t ldk) {
     __shared__ float tile[64][65];
-    const int64_t bi = blockIdx.y, bj = blockIdx.x;  // source block K[bi*64.., bj*64..]
+    // block b -> (bi, bj), bj >= bi, row-major over the upper triangle of the nt x nt grid
+    const int64_t b = blockIdx.x;
+    int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
+    auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };  // first block of block-row i
+    if (bi < 0) bi = 0;
+    if (bi > nt - 1) bi = nt - 1;
+    while (bi > 0 && first(bi) > b) --bi;
+    while (bi < nt - 1 && first(bi + 1) <= b) ++bi;
+    const int64_t bj = bi + (b - first(bi));
     const int64_t i0 = bi * 64, j0 = bj * 64;
-    if (bj < bi || j0 >= n) return;  // upper-triangle blocks only
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int t = threadIdx.x;
+    const bool full = i0 + 64 <= n && j0 + 64 <= n && (ldk & 3) == 0;
+    // load K[i0 + y, j0 .. j0 + 63]: 16 float4 per row, 4 rows per pass
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int y = ty + 4 * q;
-        const int64_t i = i0 + y, j = j0 + tx;
-        tile[y][tx] = (i < n && j < n) ? K[i * ldk + j] : 0.f;
+    for (int q = 0; q < 4; ++q) {
+        const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
+        const int64_t i = i0 + y;
+        if (full) {
+            const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(K + i * ldk + j0 + x));
+            tile[y][x] = v[0]; tile[y][x + 1] = v[1]; tile[y][x + 2] = v[2]; tile[y][x + 3] = v[3];
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) tile[y][x + c] = (i < n && j0 + x + c < n) ? K[i * ldk + j0 + x + c] : 0.f;
+        }
     }
     __syncthreads();
+    // store K[j0 + y, i0 .. i0 + 63] = column y of the tile (strictly below the diagonal)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int y = ty + 4 * q;
-        const int64_t j = j0 + y, i = i0 + tx;
-        if (i < n && j < n && j > i) __builtin_nontemporal_store(tile[tx][y], &K[j * ldk + i]);
+    for (int q = 0; q < 4; ++q) {
+        const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
+        const int64_t j = j0 + y;
+        if (full && bi != bj) {
+            f32x4 v;
+            v[0] = tile[x][y]; v[1] = tile[x + 1][y]; v[2] = tile[x + 2][y]; v[3] = tile[x + 3][y];
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(K + j * ldk + i0 + x));
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int64_t i = i0 + x + c;
+                if (j < n && i < n && j > i) K[j * ldk + i] = tile[x + c][y];
+            }
+        }
     }
 }
 
@@ -425,9 +452,9 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
     rc = gram_sparse_launch(n_total, 0, n_total, true, ptr, idx, val, band_width, t_desc, t_rec, t_rowshift, K, ldk,
                             S(stream));
     if (rc != GRF_OK) return rc;
-    const int64_t nt = cdiv<int64_t>(n_total, 64);
-    GRF_REQUIRE(nt < 65536, GRF_EUNSUPPORTED, "grf_gram_sparse_sym: n too large for the mirror grid");
-    gram_mirror_kernel<<<dim3((unsigned)nt, (unsigned)nt), 256, 0, S(stream)>>>(n_total, K, ldk);
+    const int64_t nt = cdiv<int64_t>(n_total, 64), blocks = nt * (nt + 1) / 2;
+    GRF_REQUIRE_GRID(blocks, 256, "gram_mirror_kernel");
+    gram_mirror_kernel<<<(unsigned)blocks, 256, 0, S(stream)>>>(n_total, nt, K, ldk);
     GRF_CHECK_LAUNCH("gram_mirror_kernel");
     return GRF_OK;
 }
