@@ -30,13 +30,66 @@ namespace grf {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kChunk = 1008;  // stream positions covered by one bucket-id chunk
+constexpr int kChunk = 1024;  // stream positions covered by one bucket-id chunk (16 per lane)
 constexpr int kWaveState = 1024 + 128 * 4 + 128 * 4;  // per wave: ids [kChunk], spare 16 B, tbase, aval
 
 // |x| < 2^51 -> round-to-nearest int64 with one f64 add and one integer subtract
 __device__ inline long long fx_round(double x) {
     const double magic = 6755399441055744.0;  // 1.5 * 2^52
     return (long long)(__double_as_longlong(x + magic) - __double_as_longlong(magic));
+}
+
+
+// inclusive max-scan of non-negative ints over the 64 lanes (DPP row shifts + row broadcasts)
+__device__ inline int wave_incl_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+}
+
+// Bucket ids of a chunk of 1024 stream positions from bucket-start markers: bid[p] holds
+// (bucket + 1) at the first position of every non-empty bucket and 0 elsewhere; since the
+// ids increase along the stream, the id of a position is the running maximum.  Lane l owns
+// positions 16 l .. 16 l + 15 (one 16-byte LDS read and write); carry = the id running at
+// the chunk start (0 for the first chunk).  Returns the id running at the chunk end.
+__device__ inline int gram_propagate_ids(unsigned char *bid, int carry, int lane) {
+    uint4 x = reinterpret_cast<uint4 *>(bid)[lane];
+    uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    // in-lane running max over the 16 bytes (from 0), and the lane's maximum
+    int run = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            run = max(run, (int)((w[i] >> (8 * b)) & 0xffu));
+            o |= (uint32_t)run << (8 * b);
+        }
+        w[i] = o;
+    }
+    // ids running into this lane: the maximum over the previous lanes and the carry
+    int before = __builtin_amdgcn_update_dpp(0, wave_incl_max(run), 0x138, 0xf, 0xf, false);  // wave_shr:1
+    before = max(before, carry);
+    const uint32_t rep = (uint32_t)before * 0x01010101u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        // bytewise max(w, before): the bytes of w are non-decreasing, so only a leading run
+        // of bytes below `before` changes
+        uint32_t o = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t v = (w[i] >> (8 * b)) & 0xffu;
+            o |= (v > (uint32_t)before ? v : (uint32_t)before) << (8 * b);
+        }
+        w[i] = o;
+    }
+    (void)rep;
+    reinterpret_cast<uint4 *>(bid)[lane] = make_uint4(w[0], w[1], w[2], w[3]);
+    return __builtin_amdgcn_readlane(max(run, before), 63);
 }
 
 // Per-wave state of one flattened batch stream (see gram_sparse_kernel).
@@ -65,7 +118,7 @@ __device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, in
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
         const int32_t p = w0 + u * 64 + lane;
-        m[u] = (!TAIL || p < cend) ? (int)g.bid[p - c0] : 0;
+        m[u] = (!TAIL || p < cend) ? (int)g.bid[p - c0] - 1 : 0;
     }
     int32_t pos[NW];
     double sc[NW];
@@ -156,7 +209,7 @@ struct GramTiles {
 // Phi^T buckets hold 12-byte record pairs starting on 128-byte lines; wave w takes the
 // batches w, w + kWaves, ... of 128 nonzeros of the row and flattens each batch's buckets
 // into one stream of PAIRS.  The bucket of each pair comes from a per-position u8 bucket
-// id that the lanes fill for their own buckets (one LDS read); the gathers of kGramUnroll
+// id (bucket-start markers propagated by a running maximum, one LDS read); the gathers of kGramUnroll
 // windows of 64 pairs are in flight together.  Tiles are dispatched band-major, so the
 // tiles in flight share one band's records (L2 / Infinity Cache).
 template <int kWaves, int kGramUnroll>
@@ -215,15 +268,18 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             tbase[h * 64 + lane] = t0[h] - 12 * excl[h];  // byte offset = tbase + 12 * position
             aval[h * 64 + lane] = av[h];
         }
+        int carry = 0;
         for (int32_t c0 = 0; c0 < total; c0 += kChunk) {
             const int32_t cend = (total - c0) < kChunk ? total : c0 + kChunk;
-            // every stream position of the chunk gets its bucket id (lanes fill their own ranges)
+            // bucket ids of the chunk: clear, mark every non-empty bucket's first position, propagate
+            reinterpret_cast<uint4 *>(bidv)[lane] = make_uint4(0u, 0u, 0u, 0u);
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int32_t lo = excl[h] > c0 ? excl[h] : c0;
-                const int32_t hi = (excl[h] + cnt[h]) < cend ? (excl[h] + cnt[h]) : cend;
-                for (int32_t p = lo; p < hi; ++p) bidv[p - c0] = (unsigned char)(h * 64 + lane);
-            }
+            for (int h = 0; h < 2; ++h)
+                if (cnt[h] > 0 && excl[h] >= c0 && excl[h] < cend)
+                    bidv[excl[h] - c0] = (unsigned char)(h * 64 + lane + 1);
+            __builtin_amdgcn_wave_barrier();
+            carry = gram_propagate_ids(bidv, carry, lane);
             __builtin_amdgcn_wave_barrier();
             int32_t w0 = c0;
             for (; w0 + 64 * kGramUnroll <= cend; w0 += 64 * kGramUnroll)
