@@ -134,9 +134,8 @@ def main():
 
     def step(record: bool):
         G = eng.laplacian(A_dev)
-        slots = eng.walk(G, m, p, L, rng=C.RNG_PHILOX, seed=42, src_begin=b, src_end=e)
-        local = eng.compact(eng.features(slots, f), want64=False, want32=True)
-        del slots
+        # Philox walks of this rank's sources straight to Phi rows (one kernel, no slot round trip)
+        local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e), want64=False, want32=True)
         if world > 1:
             ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32)
             phi = DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))

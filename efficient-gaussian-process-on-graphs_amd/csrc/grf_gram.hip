@@ -31,7 +31,8 @@ namespace grf {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kChunk = 1024;  // stream positions covered by one bucket-id chunk (16 per lane)
-constexpr int kWaveState = 1024 + 128 * 4 + 128 * 4;  // per wave: ids [kChunk], spare 16 B, tbase, aval
+// per wave: ids [kChunk], then tbase and aval for a batch of 64 * halves nonzeros
+constexpr int wave_state_bytes(int halves) { return kChunk + halves * 64 * 8; }
 
 // |x| < 2^51 -> round-to-nearest int64 with one f64 add and one integer subtract
 __device__ inline long long fx_round(double x) {
@@ -165,8 +166,8 @@ __device__ inline float fx_to_float(unsigned long long a, int sh) {
 
 // LDS bytes of one gram_sparse_kernel workgroup (W int64 counters + per-wave stream state):
 // at W = 4096 and 4 waves exactly 40 KiB, i.e. four workgroups per CU.
-constexpr size_t gram_lds_bytes(int64_t W, int waves) {
-    return (size_t)W * 8 + (size_t)waves * kWaveState;
+constexpr size_t gram_lds_bytes(int64_t W, int waves, int halves) {
+    return (size_t)W * 8 + (size_t)waves * wave_state_bytes(halves);
 }
 
 // Tiles of one Gram call in band-major order: band J holds count(J) tiles, the local rows
@@ -212,7 +213,7 @@ struct GramTiles {
 // id (bucket-start markers propagated by a running maximum, one LDS read); the gathers of kGramUnroll
 // windows of 64 pairs are in flight together.  Tiles are dispatched band-major, so the
 // tiles in flight share one band's records (L2 / Infinity Cache).
-template <int kWaves, int kGramUnroll>
+template <int kWaves, int kHalves, int kGramUnroll>
 __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
@@ -221,10 +222,11 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t W = tl.W;
-    unsigned char *st = reinterpret_cast<unsigned char *>(acc + W) + wave * kWaveState;
-    unsigned char *bidv = st;                                      // [kChunk]
-    int32_t *tbase = reinterpret_cast<int32_t *>(st + 1024);       // [128]
-    float *aval = reinterpret_cast<float *>(st + 1024 + 128 * 4);  // [128]
+    constexpr int kB = 64 * kHalves;  // nonzeros per wave batch
+    unsigned char *st = reinterpret_cast<unsigned char *>(acc + W) + wave * wave_state_bytes(kHalves);
+    unsigned char *bidv = st;                                          // [kChunk]
+    int32_t *tbase = reinterpret_cast<int32_t *>(st + kChunk);         // [kB]
+    float *aval = reinterpret_cast<float *>(st + kChunk + kB * 4);     // [kB]
 
     int64_t J, r;
     tl.locate(t_begin + (int64_t)blockIdx.x, J, r);
@@ -245,11 +247,11 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     else __builtin_amdgcn_wave_barrier();
 
     const GramStream gs{bidv, tbase, aval, brec, acc, ldexp(1.0, sh)};
-    for (int64_t g0 = e0 + (int64_t)wave * 128; g0 < e1; g0 += 128 * kWaves) {
-        int32_t cnt[2], excl[2], t0[2];
-        float av[2];
+    for (int64_t g0 = e0 + (int64_t)wave * kB; g0 < e1; g0 += kB * kWaves) {
+        int32_t cnt[kHalves], excl[kHalves], t0[kHalves];
+        float av[kHalves];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < kHalves; ++h) {
             const int64_t e = g0 + h * 64 + lane;
             const int32_t k = e < e1 ? idx[e] : -1;
             av[h] = e < e1 ? val[e] : 0.f;
@@ -257,14 +259,15 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             t0[h] = ((int32_t)d.x - line0) * 128;  // bucket byte offset within the band
             cnt[h] = (int32_t)d.y;                 // pairs
         }
-        const int32_t inc0 = wave_inclusive_scan<int32_t>(cnt[0]);
-        const int32_t tot0 = __shfl(inc0, 63, 64);
-        const int32_t inc1 = wave_inclusive_scan<int32_t>(cnt[1]) + tot0;
-        const int32_t total = __shfl(inc1, 63, 64);
-        excl[0] = inc0 - cnt[0];
-        excl[1] = inc1 - cnt[1];
+        int32_t total = 0;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < kHalves; ++h) {
+            const int32_t inc = wave_inclusive_scan<int32_t>(cnt[h]) + total;
+            excl[h] = inc - cnt[h];
+            total = __shfl(inc, 63, 64);
+        }
+#pragma unroll
+        for (int h = 0; h < kHalves; ++h) {
             tbase[h * 64 + lane] = t0[h] - 12 * excl[h];  // byte offset = tbase + 12 * position
             aval[h * 64 + lane] = av[h];
         }
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             reinterpret_cast<uint4 *>(bidv)[lane] = make_uint4(0u, 0u, 0u, 0u);
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < kHalves; ++h)
                 if (cnt[h] > 0 && excl[h] >= c0 && excl[h] < cend)
                     bidv[excl[h] - c0] = (unsigned char)(h * 64 + lane + 1);
             __builtin_amdgcn_wave_barrier();
@@ -448,26 +451,30 @@ static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t ro
     const GramTiles tl{rows, band_width, nb, sym};
     const int64_t n_tiles = tl.total();
     if (n_tiles == 0) return GRF_OK;
-    // tuning knob (default = measured best on MI355X): gathers in flight per wave
-    static const int unroll = [] {
-        const char *e = getenv("GRF_GRAM_UNROLL");
-        const int u = e ? atoi(e) : 8;
-        return (u == 4 || u == 8 || u == 16) ? u : 8;
+    // tuning knobs (defaults = measured best on MI355X): gathers in flight per wave, waves per tile
+    static const int knobs = [] {
+        const char *e = getenv("GRF_GRAM_UNROLL"), *w = getenv("GRF_GRAM_WAVES");
+        const int u = e ? atoi(e) : 8, ww = w ? atoi(w) : 4;
+        return ((u == 4 || u == 8 || u == 16) ? u : 8) * 10 + (ww == 8 ? 8 : 4);
     }();
-    const size_t lds = gram_lds_bytes(band_width, 4);
+    const int unroll = knobs / 10, waves = knobs % 10, halves = waves == 8 ? 1 : 2;
+    const size_t lds = gram_lds_bytes(band_width, waves, halves);
     // one launch covers at most 2^32 - 1 work-items: split the tile range
-    const int64_t max_tiles = ((1ll << 32) - 1) / 256;
+    const int64_t max_tiles = ((1ll << 32) - 1) / (64 * waves);
     for (int64_t t0 = 0; t0 < n_tiles; t0 += max_tiles) {
         const int64_t nt = (n_tiles - t0) < max_tiles ? (n_tiles - t0) : max_tiles;
-#define GRF_GRAM_LAUNCH(U)                                                                                        \
-    gram_sparse_kernel<4, U><<<(unsigned)nt, 256, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx, val,           \
-                                                            reinterpret_cast<const uint2 *>(t_desc),              \
-                                                            reinterpret_cast<const unsigned char *>(t_rec),       \
-                                                            t_rowshift, K, ldk)
-        switch (unroll) {
-            case 4: GRF_GRAM_LAUNCH(4); break;
-            case 16: GRF_GRAM_LAUNCH(16); break;
-            default: GRF_GRAM_LAUNCH(8); break;
+#define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
+    gram_sparse_kernel<WV, H, U><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx, val,   \
+                                                                     reinterpret_cast<const uint2 *>(t_desc),     \
+                                                                     reinterpret_cast<const unsigned char *>(t_rec), \
+                                                                     t_rowshift, K, ldk)
+        if (waves == 8) {
+            if (unroll == 4) GRF_GRAM_LAUNCH(8, 1, 4);
+            else GRF_GRAM_LAUNCH(8, 1, 8);
+        } else {
+            if (unroll == 4) GRF_GRAM_LAUNCH(4, 2, 4);
+            else if (unroll == 16) GRF_GRAM_LAUNCH(4, 2, 16);
+            else GRF_GRAM_LAUNCH(4, 2, 8);
         }
 #undef GRF_GRAM_LAUNCH
         GRF_CHECK_LAUNCH("gram_sparse_kernel");

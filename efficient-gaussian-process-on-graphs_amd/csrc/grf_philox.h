@@ -1,0 +1,82 @@
+// grf_philox.h -- the Philox4x32-10 random walk shared by the walk kernel and the fused
+// walk -> Phi kernel (one definition, so both produce the same visits bit for bit).
+#pragma once
+#include "grf_common.h"
+
+namespace grf {
+
+// ------------------------------------------------------------------ Philox
+__device__ inline void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                                     uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    o0 = c0; o1 = c1; o2 = c2; o3 = c3;
+}
+
+// Lemire rejection tail (probability < deg / 2^32): words continue with x3 of
+// block 0, then blocks 1, 2, ... of the same (step, walk, source) counter.
+__device__ __noinline__ uint64_t philox_lemire_retry(uint32_t d, uint32_t thr, uint32_t x3, uint32_t l, uint32_t w,
+                                                     uint32_t s, uint32_t k0, uint32_t k1) {
+    uint64_t mm = (uint64_t)x3 * d;
+    if ((uint32_t)mm >= thr) return mm;
+    for (uint32_t blk = 1;; ++blk) {
+        uint32_t y[4];
+        philox4x32_10(l, w, s, blk, k0, k1, y[0], y[1], y[2], y[3]);
+        for (int i = 0; i < 4; ++i) {
+            mm = (uint64_t)y[i] * d;
+            if ((uint32_t)mm >= thr) return mm;
+        }
+    }
+}
+
+__device__ inline double load_update(int rule, double load, int64_t deg, double w, double p) {
+    const double f = ((double)deg * w) / (1.0 - p);
+    if (rule == GRF_LOAD_CUMULATIVE) return load * f;
+    if (rule == GRF_LOAD_NONCUMULATIVE) return f;
+    return w;
+}
+
+// One Philox walk (source s, walk w) of at most L recorded visits: visit(l, node, load) is
+// called for the recorded steps l = 0, 1, ...; returns the number of recorded visits.
+// Per step: record (current node, load); stop at a zero-degree node or with probability
+// p_halt (53-bit double from words x0, x1 < p); otherwise move to neighbour Lemire(x2, deg)
+// and update the load by the importance weight deg * w / (1 - p).
+template <typename Visit>
+__device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const int32_t *__restrict__ g_idx,
+                                      const double *__restrict__ g_val, int64_t s, uint32_t w, double p, int32_t L,
+                                      int32_t rule, uint32_t k0, uint32_t k1, Visit visit) {
+    int64_t cur = s;
+    double load = 1.0;
+    int32_t l = 0;
+    for (; l < L; ++l) {
+        visit(l, (int32_t)cur, load);
+        const int64_t rs = g_ptr[cur], deg = g_ptr[cur + 1] - rs;
+        if (deg == 0) return l + 1;
+        uint32_t x0, x1, x2, x3;
+        philox4x32_10((uint32_t)l, w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
+        const double h = (double)((((uint64_t)x0 << 32) | x1) >> 11) * (1.0 / 9007199254740992.0);
+        if (h < p) return l + 1;
+        const uint32_t d = (uint32_t)deg;
+        uint32_t k = 0;
+        if (d > 1) {
+            uint64_t mm = (uint64_t)x2 * d;
+            if ((uint32_t)mm < d) {
+                const uint32_t thr = (0u - d) % d;
+                if ((uint32_t)mm < thr) mm = philox_lemire_retry(d, thr, x3, (uint32_t)l, w, (uint32_t)s, k0, k1);
+            }
+            k = (uint32_t)(mm >> 32);
+        }
+        const double wt = g_val[rs + k];
+        load = load_update(rule, load, deg, wt, p);
+        cur = g_idx[rs + k];
+    }
+    return L;
+}
+
+}  // namespace grf

@@ -12,7 +12,10 @@
 // (dense sampler) or multiplied by 1/m (scipy), and Phi entries are summed in
 // step order starting from 0.0 -- the orders the reference uses.  Sorting
 // (node, walk) keys in LDS gives those orders without atomics.
+#include <algorithm>
+
 #include "grf_block.h"
+#include "grf_philox.h"
 
 namespace grf {
 
@@ -125,100 +128,158 @@ __global__ __launch_bounds__(256) void phi_merge_kernel(int64_t n_src, int64_t m
 }
 
 // ------------------------------------------------------------ grf_phi_fused
-// one workgroup per source: sort (node, step, walk) of all m*L slots in LDS;
-// runs of (node, step) are the step entries, runs of node the Phi entries.
+// One workgroup per source: the (node, step, walk) keys of all m*L visit slots are sorted
+// in LDS; runs of (node, step) are the step entries (loads summed in walk order), runs of
+// node the Phi entries (f_l * step value summed in step order).  The slots come from HBM
+// (kWalk = false, grf_phi_fused) or from the source's own Philox walks run by the
+// workgroup (kWalk = true, grf_walk_phi: no slot round trip through HBM).
+constexpr int kPhiMaxPer = 16;  // sorted positions per thread (P <= 4096, 256 threads)
+
+template <bool kWalk>
 __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, int32_t norm, int32_t P, int32_t wbits,
                                                         int32_t lbits, const int32_t *__restrict__ slot_node,
                                                         const double *__restrict__ slot_load,
+                                                        const int64_t *__restrict__ g_ptr,
+                                                        const int32_t *__restrict__ g_idx,
+                                                        const double *__restrict__ g_val, double p_halt, int32_t rule,
+                                                        uint32_t k0, uint32_t k1, int64_t src_begin,
                                                         const double *__restrict__ f, int32_t Lf, int64_t cap,
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
                                                         double *__restrict__ phi_val, float *__restrict__ phi_val32) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    const int E = (int)(m * L);
-    uint64_t *key = smem;                               // [P]
-    double *ld = reinterpret_cast<double *>(smem + P);  // [E] loads by slot, later Phi values by position
-    double *mv = ld + E;                                // [P] step values at run heads
-    int32_t *scratch = reinterpret_cast<int32_t *>(mv + P);  // 17 ints
+    const int E = (int)(m * L), T = (int)blockDim.x, tid = (int)threadIdx.x;
+    uint64_t *key = smem;                               // [P]  sorted keys, later compacted step keys
+    double *ld = reinterpret_cast<double *>(smem + P);  // [E]  loads by slot, later compacted step values
+    double *mv = ld + E;                                // [P]  step values at (node, step) run heads
+    int32_t *scratch = reinterpret_cast<int32_t *>(mv + P);  // block-scan scratch (<= 17 ints)
     const int64_t s = blockIdx.x;
-    const int32_t *nd = slot_node + s * E;
-    const double *sl = slot_load + s * E;
     const int sh = wbits + lbits;
     const uint64_t wmask = (1ull << wbits) - 1ull, lmask = (1ull << lbits) - 1ull;
-    for (int t = threadIdx.x; t < P; t += blockDim.x) {
-        uint64_t k = ~0ull;
-        if (t < E) {
-            const int32_t v = nd[t];
-            if (v >= 0) {
-                const int l = t / (int)m, w = t - l * (int)m;
-                k = ((uint64_t)(uint32_t)v << sh) | ((uint64_t)l << wbits) | (uint64_t)w;
-                ld[t] = sl[t];
+    auto make_key = [&](int32_t node, int l, int64_t w) {
+        return ((uint64_t)(uint32_t)node << sh) | ((uint64_t)l << wbits) | (uint64_t)w;
+    };
+
+    // ---- slots -> keys
+    if (kWalk) {
+        for (int t = tid; t < P; t += T) key[t] = ~0ull;
+        __syncthreads();
+        const int64_t src = src_begin + s;
+        for (int64_t w = tid; w < m; w += T)
+            philox_walk(g_ptr, g_idx, g_val, src, (uint32_t)w, p_halt, L, rule, k0, k1,
+                        [&](int32_t l, int32_t node, double load) {
+                            key[l * m + w] = make_key(node, l, w);
+                            ld[l * m + w] = load;
+                        });
+    } else {
+        const int32_t *nd = slot_node + s * E;
+        const double *sl = slot_load + s * E;
+        for (int t = tid; t < P; t += T) {
+            uint64_t k = ~0ull;
+            if (t < E) {
+                const int32_t v = nd[t];
+                if (v >= 0) {
+                    const int l = t / (int)m;
+                    k = make_key(v, l, t - l * (int)m);
+                    ld[t] = sl[t];
+                }
             }
+            key[t] = k;
         }
-        key[t] = k;
     }
     __syncthreads();
     block_bitonic_sort(key, P);
-    // step values at (node, step) run heads, loads summed in walk order
-    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+
+    // ---- step values at (node, step) run heads: loads in walk order from 0.0 (the run is
+    //      read 8 keys / loads per LDS round trip; the source's step-0 run is m long)
+    for (int i = tid; i < P; i += T) {
         const uint64_t k = key[i];
         if (k == ~0ull || (i > 0 && (key[i - 1] >> wbits) == (k >> wbits))) continue;
+        const uint64_t hk = k >> wbits;
         double acc = 0.0;
-        int j = i;
-        do {
-            const uint64_t kj = key[j];
-            acc += ld[((kj >> wbits) & lmask) * m + (kj & wmask)];
-            ++j;
-        } while (j < P && (key[j] >> wbits) == (k >> wbits));
+        for (int j = i;; j += 8) {
+            uint64_t kk[8];
+            double lv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) kk[q] = j + q < P ? key[j + q] : ~0ull;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                lv[q] = (kk[q] >> wbits) == hk ? ld[((kk[q] >> wbits) & lmask) * m + (kk[q] & wmask)] : 0.0;
+            bool more = true;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if ((kk[q] >> wbits) == hk) acc += lv[q];  // keys are sorted: the run is contiguous
+                else more = false;
+            }
+            if (!more) break;
+        }
         mv[i] = normalise(acc, norm, m);
     }
     __syncthreads();
-    // Phi entries at node run heads; values parked in ld[i] (i < #valid <= E)
-    const int T = blockDim.x;
-    const int per = P >= T ? P / T : 1;
-    const int i0 = threadIdx.x * per;
+
+    // ---- compact the step heads (sorted order): key -> key[rank], value -> ld[rank]
+    const int per = P / T;  // <= kPhiMaxPer
+    const int i0 = tid * per;
+    uint64_t hk_[kPhiMaxPer];
+    double hv_[kPhiMaxPer];
     int c = 0;
-    for (int i = i0; i < i0 + per && i < P; ++i) {
+#pragma unroll
+    for (int q = 0; q < kPhiMaxPer; ++q) {
+        if (q >= per) break;
+        const int i = i0 + q;
         const uint64_t k = key[i];
-        if (k == ~0ull || (i > 0 && (key[i - 1] >> sh) == (k >> sh))) continue;
+        const bool head = k != ~0ull && (i == 0 || (key[i - 1] >> wbits) != (k >> wbits));
+        if (head) {
+            hk_[c] = k;
+            hv_[c] = mv[i];
+            ++c;
+        }
+    }
+    int32_t n_heads;
+    const int32_t rank0 = block_exclusive_scan<int32_t>(c, scratch, &n_heads);  // (barriers: reads done)
+#pragma unroll
+    for (int q = 0; q < kPhiMaxPer; ++q) {
+        if (q >= c) break;
+        key[rank0 + q] = hk_[q];
+        ld[rank0 + q] = hv_[q];
+    }
+    __syncthreads();
+
+    // ---- Phi entries at node run heads of the compacted list: f_l * value in step order
+    const int per2 = (n_heads + T - 1) / T;
+    const int q0 = tid * per2;
+    int emit = 0;
+    double pv_[kPhiMaxPer];
+    int32_t pn_[kPhiMaxPer];
+    for (int q = q0; q < q0 + per2 && q < n_heads; ++q) {
+        const uint64_t k = key[q];
+        if (q > 0 && (key[q - 1] >> sh) == (k >> sh)) continue;
         double acc = 0.0;
         bool present = false;
-        int j = i;
-        do {
-            const uint64_t kj = key[j];
-            if (j == i || (key[j - 1] >> wbits) != (kj >> wbits)) {  // a step run head
-                const int l = (int)((kj >> wbits) & lmask);
-                if (l < Lf) {
-                    const double t = f[l] * mv[j];
-                    acc = present ? acc + t : 0.0 + t;
-                    present = true;
-                }
+        for (int j = q; j < n_heads && (key[j] >> sh) == (k >> sh); ++j) {
+            const int l = (int)((key[j] >> wbits) & lmask);
+            if (l < Lf) {
+                const double t = f[l] * ld[j];
+                acc = present ? acc + t : 0.0 + t;
+                present = true;
             }
-            ++j;
-        } while (j < P && (key[j] >> sh) == (k >> sh));
-        if (present && acc != 0.0) {
-            ++c;
-        } else {
-            acc = 0.0;
-            present = false;
         }
-        ld[i] = acc;  // 0.0 <=> not emitted
+        if (present && acc != 0.0) {
+            pv_[emit] = acc;
+            pn_[emit] = (int32_t)(k >> sh);
+            ++emit;
+        }
     }
     int32_t total;
-    int32_t rank = block_exclusive_scan<int32_t>(c, scratch, &total);
+    int32_t rank = block_exclusive_scan<int32_t>(emit, scratch, &total);
     const int64_t obase = s * cap;
-    for (int i = i0; i < i0 + per && i < P; ++i) {
-        const uint64_t k = key[i];
-        if (k == ~0ull || (i > 0 && (key[i - 1] >> sh) == (k >> sh))) continue;
-        const double v = ld[i];
-        if (v == 0.0) continue;
+    for (int q = 0; q < emit; ++q, ++rank) {
         if (rank < cap) {
-            phi_idx[obase + rank] = (int32_t)(k >> sh);
-            phi_val[obase + rank] = v;
-            if (phi_val32) phi_val32[obase + rank] = (float)v;
+            phi_idx[obase + rank] = pn_[q];
+            phi_val[obase + rank] = pv_[q];
+            if (phi_val32) phi_val32[obase + rank] = (float)pv_[q];
         }
-        ++rank;
     }
-    if (threadIdx.x == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
+    if (tid == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
 }
 
 // ------------------------------------------------------- dense (N, N, L) out
@@ -278,27 +339,64 @@ int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, co
     return GRF_OK;
 }
 
-int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
-                      const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
-                      int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream) {
-    GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && slot_node && slot_load && phi_cnt && phi_idx && phi_val,
-                GRF_EINVAL, "grf_phi_fused: bad arguments");
+static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, int32_t norm,
+                                const int32_t *slot_node, const double *slot_load, const int64_t *g_ptr,
+                                const int32_t *g_idx, const double *g_val, double p_halt, int32_t rule, uint64_t seed,
+                                int64_t src_begin, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
+                                int32_t *phi_idx, double *phi_val, float *phi_val32, hipStream_t st) {
     GRF_REQUIRE(norm == GRF_NORM_DIV || norm == GRF_NORM_MUL_RECIP, GRF_EINVAL, "grf_phi_fused: bad norm");
     GRF_REQUIRE(n_f >= 0 && (n_f == 0 || f), GRF_EINVAL, "grf_phi_fused: bad modulator");
     GRF_REQUIRE(m * (int64_t)L <= 4096, GRF_EUNSUPPORTED, "grf_phi_fused: needs walks_per_node * L <= 4096");
     GRF_REQUIRE(phi_cap >= 1, GRF_EINVAL, "grf_phi_fused: phi_cap must be >= 1");
     if (n_src == 0) return GRF_OK;
     const int E = (int)(m * L);
-    const int P = (int)next_pow2_u32((uint32_t)E);
+    const int P = std::max(64, (int)next_pow2_u32((uint32_t)E));
     const int wbits = ceil_log2((uint64_t)m), lbits = ceil_log2((uint64_t)L) > 0 ? ceil_log2((uint64_t)L) : 1;
+    GRF_REQUIRE(wbits + lbits <= 32, GRF_EUNSUPPORTED, "grf_phi_fused: key overflow");
     const size_t lds = (size_t)P * 8 + (size_t)E * 8 + (size_t)P * 8 + 128;
     const int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
+    GRF_REQUIRE(P / T <= kPhiMaxPer, GRF_EUNSUPPORTED, "grf_phi_fused: too many positions per thread");
     const int32_t Lf = n_f < L ? n_f : L;
     GRF_REQUIRE_GRID(n_src, T, "phi_fused_kernel");
-    phi_fused_kernel<<<(unsigned)n_src, T, lds, S(stream)>>>(m, L, norm, P, wbits, lbits, slot_node, slot_load, f, Lf,
-                                                             phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
+    if (walk)
+        phi_fused_kernel<true><<<(unsigned)n_src, T, lds, st>>>(
+            m, L, norm, P, wbits, lbits, nullptr, nullptr, g_ptr, g_idx, g_val, p_halt, rule, (uint32_t)seed,
+            (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
+    else
+        phi_fused_kernel<false><<<(unsigned)n_src, T, lds, st>>>(
+            m, L, norm, P, wbits, lbits, slot_node, slot_load, nullptr, nullptr, nullptr, 0.0, 0, 0u, 0u, 0, f, Lf,
+            phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
     GRF_CHECK_LAUNCH("phi_fused_kernel");
     return GRF_OK;
+}
+
+int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
+                      const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
+                      int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream) {
+    GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && slot_node && slot_load && phi_cnt && phi_idx && phi_val,
+                GRF_EINVAL, "grf_phi_fused: bad arguments");
+    return phi_fused_launch(false, n_src, m, L, norm, slot_node, slot_load, nullptr, nullptr, nullptr, 0.0, 0, 0, 0, f,
+                            n_f, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, S(stream));
+}
+
+int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
+                     const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
+                     int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
+                     float *phi_val32, grf_stream_t stream) {
+    GRF_REQUIRE(params != nullptr, GRF_EINVAL, "grf_walk_phi: params is NULL");
+    const grf_walk_params P = *params;
+    GRF_REQUIRE(n >= 0 && g_ptr && phi_cnt && phi_idx && phi_val, GRF_EINVAL, "grf_walk_phi: bad arguments");
+    GRF_REQUIRE(P.rng == GRF_RNG_PHILOX, GRF_EUNSUPPORTED, "grf_walk_phi: Philox walks only (use grf_walk for PCG64)");
+    GRF_REQUIRE(P.walks_per_node >= 1 && P.walks_per_node <= 0x7fffffff, GRF_EINVAL,
+                "grf_walk_phi: walks_per_node must be in [1, 2^31)");
+    GRF_REQUIRE(P.max_walk_length >= 1, GRF_EINVAL, "grf_walk_phi: max_walk_length must be >= 1");
+    GRF_REQUIRE(P.p_halt >= 0.0 && P.p_halt < 1.0, GRF_EINVAL, "grf_walk_phi: p_halt must be in [0, 1)");
+    GRF_REQUIRE(P.load_rule >= 0 && P.load_rule <= 2, GRF_EINVAL, "grf_walk_phi: bad load_rule %d", P.load_rule);
+    GRF_REQUIRE(0 <= src_begin && src_begin <= src_end && src_end <= n, GRF_EINVAL, "grf_walk_phi: bad source range");
+    GRF_REQUIRE(n <= 0x7fffffffLL, GRF_EUNSUPPORTED, "grf_walk_phi: n must fit int32 node ids");
+    return phi_fused_launch(true, src_end - src_begin, P.walks_per_node, P.max_walk_length, norm, nullptr, nullptr,
+                            g_ptr, g_idx, g_val, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, phi_cnt,
+                            phi_idx, phi_val, phi_val32, S(stream));
 }
 
 int32_t grf_steps_densify(int64_t n_src, int64_t m, int32_t L, int64_t n_cols, const int32_t *step_cnt,

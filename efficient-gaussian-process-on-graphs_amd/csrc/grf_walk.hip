@@ -15,46 +15,9 @@
 //     as the reference consumes it (random() for the halt, integers(deg) through
 //     the buffered 32-bit Lemire path, no draw for deg == 1).  Reference-exact,
 //     sequential within a chunk (the reference's own parallel granularity).
-#include "grf_common.h"
+#include "grf_philox.h"
 
 namespace grf {
-
-// ------------------------------------------------------------------ Philox
-__device__ inline void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
-                                     uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-    o0 = c0; o1 = c1; o2 = c2; o3 = c3;
-}
-
-// Lemire rejection tail (probability < deg / 2^32): words continue with x3 of
-// block 0, then blocks 1, 2, ... of the same (step, walk, source) counter.
-__device__ __noinline__ uint64_t philox_lemire_retry(uint32_t d, uint32_t thr, uint32_t x3, uint32_t l, uint32_t w,
-                                                     uint32_t s, uint32_t k0, uint32_t k1) {
-    uint64_t mm = (uint64_t)x3 * d;
-    if ((uint32_t)mm >= thr) return mm;
-    for (uint32_t blk = 1;; ++blk) {
-        uint32_t y[4];
-        philox4x32_10(l, w, s, blk, k0, k1, y[0], y[1], y[2], y[3]);
-        for (int i = 0; i < 4; ++i) {
-            mm = (uint64_t)y[i] * d;
-            if ((uint32_t)mm >= thr) return mm;
-        }
-    }
-}
-
-__device__ inline double load_update(int rule, double load, int64_t deg, double w, double p) {
-    const double f = ((double)deg * w) / (1.0 - p);
-    if (rule == GRF_LOAD_CUMULATIVE) return load * f;
-    if (rule == GRF_LOAD_NONCUMULATIVE) return f;
-    return w;
-}
 
 __global__ __launch_bounds__(256) void walk_philox_kernel(const int64_t *__restrict__ g_ptr,
                                                           const int32_t *__restrict__ g_idx,
@@ -68,33 +31,12 @@ __global__ __launch_bounds__(256) void walk_philox_kernel(const int64_t *__restr
     const int64_t sl = gid / m, w = gid - sl * m, s = src_begin + sl;
     int32_t *nd = slot_node + sl * L * m + w;
     double *ld = slot_load + sl * L * m + w;
-    int64_t cur = s;
-    double load = 1.0;
-    int32_t l = 0;
-    for (; l < L; ++l) {
-        nd[(int64_t)l * m] = (int32_t)cur;
-        ld[(int64_t)l * m] = load;
-        const int64_t rs = g_ptr[cur], deg = g_ptr[cur + 1] - rs;
-        if (deg == 0) { ++l; break; }
-        uint32_t x0, x1, x2, x3;
-        philox4x32_10((uint32_t)l, (uint32_t)w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
-        const double h = (double)((((uint64_t)x0 << 32) | x1) >> 11) * (1.0 / 9007199254740992.0);
-        if (h < p) { ++l; break; }
-        const uint32_t d = (uint32_t)deg;
-        uint32_t k = 0;
-        if (d > 1) {
-            uint64_t mm = (uint64_t)x2 * d;
-            if ((uint32_t)mm < d) {
-                const uint32_t thr = (0u - d) % d;
-                if ((uint32_t)mm < thr) mm = philox_lemire_retry(d, thr, x3, (uint32_t)l, (uint32_t)w, (uint32_t)s, k0, k1);
-            }
-            k = (uint32_t)(mm >> 32);
-        }
-        const double wt = g_val[rs + k];
-        load = load_update(rule, load, deg, wt, p);
-        cur = g_idx[rs + k];
-    }
-    for (; l < L; ++l) nd[(int64_t)l * m] = -1;
+    const int32_t n_vis = philox_walk(g_ptr, g_idx, g_val, s, (uint32_t)w, p, L, rule, k0, k1,
+                                      [&](int32_t l, int32_t node, double load) {
+                                          nd[(int64_t)l * m] = node;
+                                          ld[(int64_t)l * m] = load;
+                                      });
+    for (int32_t l = n_vis; l < L; ++l) nd[(int64_t)l * m] = -1;
 }
 
 // ------------------------------------------------------------------- PCG64

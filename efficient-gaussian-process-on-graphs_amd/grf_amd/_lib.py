@@ -56,6 +56,8 @@ SIGNATURES = {
     "grf_steps": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "grf_steps_densify": (_i32, [_i64, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_phi": (_i32, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "grf_walk_phi": (_i32, [_i64, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32, _i64,
+                             _vp, _vp, _vp, _vp, _vp]),
     "grf_phi_fused": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_scan_workspace_bytes": (_sz, [_i64]),

@@ -87,8 +87,12 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
     G = engine.laplacian(A)
     n = G.n_rows
     b, e = shard_range(n, rank, world)
-    slots = engine.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed, src_begin=b, src_end=e)
-    local = engine.compact(engine.features(slots, f), want64=False, want32=True)
+    if walks_per_node * max_walk_length <= 4096:
+        rows = engine.walk_phi(G, walks_per_node, p_halt, max_walk_length, f, seed=seed, src_begin=b, src_end=e)
+    else:
+        rows = engine.features(engine.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed,
+                                           src_begin=b, src_end=e), f)
+    local = engine.compact(rows, want64=False, want32=True)
     if world > 1:
         ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32, group)
         phi = DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))

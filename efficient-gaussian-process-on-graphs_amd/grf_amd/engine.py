@@ -246,6 +246,28 @@ class GRFEngine:
                                        _p(cnt), _p(idx), _p(val), _p(v32), self.stream), "grf_phi_fused")
         return PaddedRows(cnt, idx, val, v32, cap, slots.n)
 
+    def walk_phi(self, G: DeviceCSR, walks_per_node: int, p_halt: float, max_walk_length: int, f, *,
+                 seed: int = 42, load_rule: int = C.LOAD_CUMULATIVE, norm: int = C.NORM_MUL_RECIP,
+                 src_begin: int = 0, src_end: Optional[int] = None, want32: bool = True) -> PaddedRows:
+        """Philox walks straight to Phi rows (one kernel; identical to walk + features)."""
+        n = G.n_rows
+        src_end = n if src_end is None else src_end
+        m, L = int(walks_per_node), int(max_walk_length)
+        if m < 1 or L < 1:
+            raise ValueError("walks_per_node and max_walk_length must be >= 1")
+        ft = self._f(f)
+        ns = src_end - src_begin
+        cap = max(1, min(m * L, n))
+        cnt = self._empty(ns, torch.int32)
+        idx = self._empty(ns * cap, torch.int32)
+        val = self._empty(ns * cap, torch.float64)
+        v32 = self._empty(ns * cap, torch.float32) if want32 else None
+        prm = C.GrfWalkParams(m, float(p_halt), L, int(load_rule), C.RNG_PHILOX, 0, 1, int(seed) & 0xFFFFFFFFFFFFFFFF)
+        C.check(self.lib.grf_walk_phi(n, _p(G.ptr), _p(G.idx), _p(G.val), ctypes.byref(prm), src_begin, src_end,
+                                      norm, _p(ft), ft.numel(), cap, _p(cnt), _p(idx), _p(val), _p(v32), self.stream),
+                "grf_walk_phi")
+        return PaddedRows(cnt, idx, val, v32, cap, n)
+
     def features(self, slots: Slots, f, norm: int = C.NORM_MUL_RECIP) -> PaddedRows:
         """Phi rows; the fused kernel when m*L fits LDS, else steps + merge (bit-identical)."""
         if slots.m * slots.L <= 4096:

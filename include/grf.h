@@ -146,6 +146,13 @@ int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, co
 
 /* Fused slots -> Phi (no step rows), same result bit-for-bit as grf_steps + grf_phi.
  * Requires m * L <= 4096.  norm as in grf_steps. */
+/* Philox walks of the sources [src_begin, src_end) straight to Phi rows in one kernel (the
+ * visit slots never touch HBM): bit-identical to grf_walk (params->rng = GRF_RNG_PHILOX)
+ * followed by grf_phi_fused.  Requires m * L <= 4096. */
+int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
+                     const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
+                     int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
+                     float *phi_val32, grf_stream_t stream);
 int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
                       const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
                       int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream);

@@ -304,3 +304,22 @@ def test_full_pipeline_c2_scale(eng):
     Kc = K.cpu().numpy()
     sub = Kc[:2000, :2000]
     assert np.max(np.abs(sub - sub.T)) <= 1e-5 * np.max(np.abs(sub))
+
+
+@pytest.mark.parametrize("n,deg,m,L,p,rule", [(3000, 8, 128, 8, 0.1, 0), (500, 3, 16, 5, 0.3, 1), (800, 12, 64, 3, 0.0, 2),
+                                             (300, 4, 7, 6, 0.2, 0), (2000, 10, 256, 16, 0.05, 0)])
+def test_walk_phi_fused_bitexact(eng, n, deg, m, L, p, rule):
+    """grf_walk_phi == grf_walk (Philox) + grf_phi_fused, bit for bit, on a graph with isolated nodes."""
+    A = er_graph(n, deg, n + m)
+    A = A.tolil()
+    A[5, :] = 0
+    A[:, 5] = 0
+    A = A.tocsr()
+    A.eliminate_zeros()
+    G = eng.laplacian(A)
+    f = [(-0.7) ** l for l in range(L - 1)]  # shorter than L: truncated like the sparse reference
+    for src in [(0, n), (17, 211)]:
+        slots = eng.walk(G, m, p, L, rng=1, seed=9, load_rule=rule, src_begin=src[0], src_end=src[1])
+        ref = eng.compact(eng.phi_fused(slots, f)).to_scipy()
+        got = eng.compact(eng.walk_phi(G, m, p, L, f, seed=9, load_rule=rule, src_begin=src[0], src_end=src[1]))
+        assert same_csr(got.to_scipy(), ref), src
