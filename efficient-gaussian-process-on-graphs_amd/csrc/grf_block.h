@@ -48,6 +48,26 @@ __device__ inline T block_exclusive_scan(T v, T *scratch, T *total) {
     return res;
 }
 
+// Exclusive scan over the whole workgroup with ONE barrier (blockDim.x multiple of 64,
+// <= 1024): every wave publishes its total and every thread adds the totals of the waves
+// before it.  `scratch` holds blockDim.x/64 elements of T and must not be reused by the
+// caller before another barrier.
+template <typename T>
+__device__ inline T block_exclusive_scan_fast(T v, T *scratch, T *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const T inc = wave_inclusive_scan(v);
+    if (lane == 63) scratch[wid] = inc;
+    __syncthreads();
+    T before = 0, all = 0;
+    for (int w = 0; w < nw; ++w) {
+        const T t = scratch[w];
+        before += w < wid ? t : (T)0;
+        all += t;
+    }
+    *total = all;
+    return before + inc - v;
+}
+
 // In-LDS bitonic sort (ascending) of P = power-of-two 64-bit keys by the whole
 // workgroup.  Caller must __syncthreads() before (keys written) and after.
 __device__ inline void block_bitonic_sort(uint64_t *key, int P) {

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void phi_merge_kernel(int64_t n_src, int64_t m
 // workgroup (kWalk = true, grf_walk_phi: no slot round trip through HBM).
 constexpr int kPhiMaxPer = 16;  // sorted positions per thread (P <= 4096, 256 threads)
 
-template <bool kWalk>
+template <bool kWalk, int kPer>  // kPer = P / blockDim.x sorted positions per thread
 __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, int32_t norm, int32_t P, int32_t wbits,
                                                         int32_t lbits, const int32_t *__restrict__ slot_node,
                                                         const double *__restrict__ slot_load,
@@ -151,7 +151,8 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     uint64_t *key = smem;                               // [P]  sorted keys, later compacted step keys
     double *ld = reinterpret_cast<double *>(smem + P);  // [E]  loads by slot, later compacted step values
     double *mv = ld + E;                                // [P]  step values at (node, step) run heads
-    int32_t *scratch = reinterpret_cast<int32_t *>(mv + P);  // block-scan scratch (<= 17 ints)
+    double *fl = mv + P;                                // [64] the modulator
+    int32_t *scratch = reinterpret_cast<int32_t *>(fl + 64);  // block-scan scratch (2 x 16 ints)
     const int64_t s = blockIdx.x;
     const int sh = wbits + lbits;
     const uint64_t wmask = (1ull << wbits) - 1ull, lmask = (1ull << lbits) - 1ull;
@@ -159,6 +160,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         return ((uint64_t)(uint32_t)node << sh) | ((uint64_t)l << wbits) | (uint64_t)w;
     };
 
+    for (int l = tid; l < Lf; l += T) fl[l] = f[l];
     // ---- slots -> keys
     if (kWalk) {
         for (int t = tid; t < P; t += T) key[t] = ~0ull;
@@ -195,88 +197,102 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         const uint64_t k = key[i];
         if (k == ~0ull || (i > 0 && (key[i - 1] >> wbits) == (k >> wbits))) continue;
         const uint64_t hk = k >> wbits;
-        double acc = 0.0;
-        for (int j = i;; j += 8) {
-            uint64_t kk[8];
-            double lv[8];
+        const uint64_t k1 = i + 1 < P ? key[i + 1] : ~0ull;
+        double acc = 0.0 + ld[((k >> wbits) & lmask) * m + (k & wmask)];
+        if ((k1 >> wbits) == hk) {  // a run of more than one visit: 8 keys / loads per round trip
+            acc += ld[((k1 >> wbits) & lmask) * m + (k1 & wmask)];
+            for (int j = i + 2;; j += 8) {
+                uint64_t kk[8];
+                double lv[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) kk[q] = j + q < P ? key[j + q] : ~0ull;
+                for (int q = 0; q < 8; ++q) kk[q] = j + q < P ? key[j + q] : ~0ull;
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                lv[q] = (kk[q] >> wbits) == hk ? ld[((kk[q] >> wbits) & lmask) * m + (kk[q] & wmask)] : 0.0;
-            bool more = true;
+                for (int q = 0; q < 8; ++q)
+                    lv[q] = (kk[q] >> wbits) == hk ? ld[((kk[q] >> wbits) & lmask) * m + (kk[q] & wmask)] : 0.0;
+                bool more = true;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if ((kk[q] >> wbits) == hk) acc += lv[q];  // keys are sorted: the run is contiguous
-                else more = false;
+                for (int q = 0; q < 8; ++q) {
+                    if ((kk[q] >> wbits) == hk) acc += lv[q];  // keys are sorted: the run is contiguous
+                    else more = false;
+                }
+                if (!more) break;
             }
-            if (!more) break;
         }
         mv[i] = normalise(acc, norm, m);
     }
     __syncthreads();
 
     // ---- compact the step heads (sorted order): key -> key[rank], value -> ld[rank]
-    const int per = P / T;  // <= kPhiMaxPer
-    const int i0 = tid * per;
-    uint64_t hk_[kPhiMaxPer];
-    double hv_[kPhiMaxPer];
+    const int i0 = tid * kPer;
+    uint64_t hk_[kPer];
+    double hv_[kPer];
     int c = 0;
 #pragma unroll
-    for (int q = 0; q < kPhiMaxPer; ++q) {
-        if (q >= per) break;
+    for (int q = 0; q < kPer; ++q) {
         const int i = i0 + q;
         const uint64_t k = key[i];
         const bool head = k != ~0ull && (i == 0 || (key[i - 1] >> wbits) != (k >> wbits));
         if (head) {
-            hk_[c] = k;
-            hv_[c] = mv[i];
+#pragma unroll
+            for (int e = 0; e < kPer; ++e)  // static register indexing
+                if (e == c) {
+                    hk_[e] = k;
+                    hv_[e] = mv[i];
+                }
             ++c;
         }
     }
     int32_t n_heads;
-    const int32_t rank0 = block_exclusive_scan<int32_t>(c, scratch, &n_heads);  // (barriers: reads done)
+    const int32_t rank0 = block_exclusive_scan_fast<int32_t>(c, scratch, &n_heads);  // (barrier: reads done)
 #pragma unroll
-    for (int q = 0; q < kPhiMaxPer; ++q) {
-        if (q >= c) break;
-        key[rank0 + q] = hk_[q];
-        ld[rank0 + q] = hv_[q];
+    for (int q = 0; q < kPer; ++q) {
+        if (q < c) {
+            key[rank0 + q] = hk_[q];
+            ld[rank0 + q] = hv_[q];
+        }
     }
     __syncthreads();
 
     // ---- Phi entries at node run heads of the compacted list: f_l * value in step order
-    const int per2 = (n_heads + T - 1) / T;
+    const int per2 = (n_heads + T - 1) / T;  // <= kPer
     const int q0 = tid * per2;
     int emit = 0;
-    double pv_[kPhiMaxPer];
-    int32_t pn_[kPhiMaxPer];
-    for (int q = q0; q < q0 + per2 && q < n_heads; ++q) {
+    double pv_[kPer];
+    int32_t pn_[kPer];
+    for (int qq = 0; qq < per2; ++qq) {
+        const int q = q0 + qq;
+        if (q >= n_heads) break;
         const uint64_t k = key[q];
-        if (q > 0 && (key[q - 1] >> sh) == (k >> sh)) continue;
+        if (q > 0 && (key[q - 1] >> sh) == (k >> sh)) continue;  // not a node head
         double acc = 0.0;
         bool present = false;
         for (int j = q; j < n_heads && (key[j] >> sh) == (k >> sh); ++j) {
             const int l = (int)((key[j] >> wbits) & lmask);
             if (l < Lf) {
-                const double t = f[l] * ld[j];
+                const double t = fl[l] * ld[j];
                 acc = present ? acc + t : 0.0 + t;
                 present = true;
             }
         }
         if (present && acc != 0.0) {
-            pv_[emit] = acc;
-            pn_[emit] = (int32_t)(k >> sh);
+#pragma unroll
+            for (int e = 0; e < kPer; ++e)  // static register indexing: pv_[emit] without a dynamic index
+                if (e == emit) {
+                    pv_[e] = acc;
+                    pn_[e] = (int32_t)(k >> sh);
+                }
             ++emit;
         }
     }
     int32_t total;
-    int32_t rank = block_exclusive_scan<int32_t>(emit, scratch, &total);
+    int32_t rank = block_exclusive_scan_fast<int32_t>(emit, scratch + 16, &total);
     const int64_t obase = s * cap;
-    for (int q = 0; q < emit; ++q, ++rank) {
-        if (rank < cap) {
-            phi_idx[obase + rank] = pn_[q];
-            phi_val[obase + rank] = pv_[q];
-            if (phi_val32) phi_val32[obase + rank] = (float)pv_[q];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        if (q < emit && rank + q < cap) {
+            phi_idx[obase + rank + q] = pn_[q];
+            phi_val[obase + rank + q] = pv_[q];
+            if (phi_val32) phi_val32[obase + rank + q] = (float)pv_[q];
         }
     }
     if (tid == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
@@ -353,19 +369,27 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     const int P = std::max(64, (int)next_pow2_u32((uint32_t)E));
     const int wbits = ceil_log2((uint64_t)m), lbits = ceil_log2((uint64_t)L) > 0 ? ceil_log2((uint64_t)L) : 1;
     GRF_REQUIRE(wbits + lbits <= 32, GRF_EUNSUPPORTED, "grf_phi_fused: key overflow");
-    const size_t lds = (size_t)P * 8 + (size_t)E * 8 + (size_t)P * 8 + 128;
+    const size_t lds = (size_t)P * 8 + (size_t)E * 8 + (size_t)P * 8 + 64 * 8 + 128;
     const int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
+    GRF_REQUIRE(n_f <= 64 || L <= 64, GRF_EUNSUPPORTED, "grf_phi_fused: max_walk_length > 64");
     GRF_REQUIRE(P / T <= kPhiMaxPer, GRF_EUNSUPPORTED, "grf_phi_fused: too many positions per thread");
     const int32_t Lf = n_f < L ? n_f : L;
     GRF_REQUIRE_GRID(n_src, T, "phi_fused_kernel");
-    if (walk)
-        phi_fused_kernel<true><<<(unsigned)n_src, T, lds, st>>>(
-            m, L, norm, P, wbits, lbits, nullptr, nullptr, g_ptr, g_idx, g_val, p_halt, rule, (uint32_t)seed,
-            (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
-    else
-        phi_fused_kernel<false><<<(unsigned)n_src, T, lds, st>>>(
-            m, L, norm, P, wbits, lbits, slot_node, slot_load, nullptr, nullptr, nullptr, 0.0, 0, 0u, 0u, 0, f, Lf,
-            phi_cap, phi_cnt, phi_idx, phi_val, phi_val32);
+#define GRF_PHI_LAUNCH(W, K)                                                                                      \
+    phi_fused_kernel<W, K><<<(unsigned)n_src, T, lds, st>>>(                                                      \
+        m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val, p_halt, rule, (uint32_t)seed,    \
+        (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32)
+#define GRF_PHI_PER(W)                                                                                            \
+    switch (P / T) {                                                                                              \
+        case 1: GRF_PHI_LAUNCH(W, 1); break;                                                                      \
+        case 2: GRF_PHI_LAUNCH(W, 2); break;                                                                      \
+        case 4: GRF_PHI_LAUNCH(W, 4); break;                                                                      \
+        case 8: GRF_PHI_LAUNCH(W, 8); break;                                                                      \
+        default: GRF_PHI_LAUNCH(W, 16); break;                                                                    \
+    }
+    if (walk) { GRF_PHI_PER(true) } else { GRF_PHI_PER(false) }
+#undef GRF_PHI_PER
+#undef GRF_PHI_LAUNCH
     GRF_CHECK_LAUNCH("phi_fused_kernel");
     return GRF_OK;
 }
