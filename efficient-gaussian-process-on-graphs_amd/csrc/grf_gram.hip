@@ -35,9 +35,12 @@ constexpr int kChunk = 1024;  // stream positions covered by one bucket-id chunk
 constexpr int wave_state_bytes(int halves) { return kChunk + halves * 64 * 8; }
 
 // |x| < 2^51 -> round-to-nearest int64 with one f64 add and one integer subtract
+// (the magic number's low word is 0: only the high word is corrected)
 __device__ inline long long fx_round(double x) {
     const double magic = 6755399441055744.0;  // 1.5 * 2^52
-    return (long long)(__double_as_longlong(x + magic) - __double_as_longlong(magic));
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x + magic);
+    const uint32_t hi = (uint32_t)(b >> 32) - 0x43380000u, lo = (uint32_t)b;
+    return (long long)(((unsigned long long)hi << 32) | lo);
 }
 
 
@@ -99,8 +102,8 @@ struct GramStream {
     const int32_t *tbase;       // per bucket: byte offset of its first pair (from the band's
                                 // first line) - 12 * stream position (LDS)
     const float *aval;          // per bucket: Phi[row,k] (LDS)
-    const unsigned char *rec;   // the band's record pairs, 12 bytes each (global)
-    unsigned long long *acc;    // tile accumulator (LDS)
+    __amdgpu_buffer_rsrc_t rec; // the band's record pairs, 12 bytes each (global, 32-bit offsets)
+    unsigned char *acc;         // tile accumulator (LDS), addressed by byte offset
     double S;                   // the row's fixed-point scale 2^sh
 };
 
@@ -140,7 +143,12 @@ __device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, in
     __builtin_amdgcn_sched_barrier(0);
     RecPair rec[NW];
 #pragma unroll
-    for (int u = 0; u < NW; ++u) rec[u] = *reinterpret_cast<const RecPair *>(g.rec + pos[u]);
+    for (int u = 0; u < NW; ++u) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(g.rec, (uint32_t)pos[u], 0, 0);
+        rec[u].cols = v[0];
+        rec[u].v0 = __uint_as_float(v[1]);
+        rec[u].v1 = __uint_as_float(v[2]);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
@@ -149,11 +157,13 @@ __device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, in
         uint32_t c0 = rec[u].cols & 0xffffu, c1 = rec[u].cols >> 16;
         if (TAIL) {
             const bool ok = w0 + u * 64 + lane < cend;
-            c0 = ok ? c0 : (uint32_t)(lane & 15);
-            c1 = ok ? c1 : (uint32_t)(lane & 15);
+            c0 = ok ? c0 : (uint32_t)(lane & 15) * 8u;
+            c1 = ok ? c1 : (uint32_t)(lane & 15) * 8u;
         }
-        __hip_atomic_fetch_add(&g.acc[c0], (unsigned long long)q0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(&g.acc[c1], (unsigned long long)q1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(g.acc + c0), (unsigned long long)q0,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(g.acc + c1), (unsigned long long)q1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -246,7 +256,10 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     if (kWaves > 1) __syncthreads();
     else __builtin_amdgcn_wave_barrier();
 
-    const GramStream gs{bidv, tbase, aval, brec, acc, ldexp(1.0, sh)};
+    const GramStream gs{bidv, tbase, aval,
+                        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char *>(brec), (short)0, 0x7fffffff,
+                                                          0x00020000),
+                        reinterpret_cast<unsigned char *>(acc), ldexp(1.0, sh)};
     for (int64_t g0 = e0 + (int64_t)wave * kB; g0 < e1; g0 += kB * kWaves) {
         int32_t cnt[kHalves], excl[kHalves], t0[kHalves];
         float av[kHalves];

@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(int64_t n_rows, int64
 
 // ------------------------------------------------------------ banded transpose
 // Bucket b = band * n_cols + k holds the entries Phi[j, k], j in the band, as PAIRS of
-// records packed in 12 bytes: {u16 j0 - band start, u16 j1 - band start, f32 v0, f32 v1}.
+// records packed in 12 bytes: {u16 8 (j0 - band start), u16 8 (j1 - band start), f32 v0, f32 v1}
+// (the row is stored as the byte offset of its int64 counter in the Gram tile).
 // Every bucket starts on a 128-byte line (the Gram kernel reads a bucket as one short
 // segment; aligned, a segment of <= 10 pairs is one line instead of two).
 constexpr int kPairBytes = 12, kLineBytes = 128;
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(256) void tr_fill_kernel(int64_t n_rows, int64_t n_
         const int64_t b = band_off + idx[e];
         const int32_t s = atomicAdd(&cursor[b], 1);
         unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (s >> 1);
-        reinterpret_cast<uint16_t *>(pair)[s & 1] = jr;
+        reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(jr * 8u);  // byte offset of the int64 counter
         reinterpret_cast<float *>(pair + 4)[s & 1] = val[e];
         mx = fmaxf(mx, fabsf(val[e]));
         sm += (double)fabsf(val[e]);
@@ -228,7 +229,7 @@ size_t grf_transpose_workspace_bytes(int64_t n_buckets) {
 int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
                                   const int32_t *idx, uint32_t *t_desc, void *workspace, size_t workspace_bytes,
                                   grf_stream_t stream) {
-    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 65536 && ptr && idx && t_desc,
+    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && t_desc,
                 GRF_EINVAL, "grf_transpose_banded_plan: bad arguments");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
     GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,
@@ -263,7 +264,7 @@ int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_w
                                   const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
                                   int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift, void *workspace,
                                   size_t workspace_bytes, grf_stream_t stream) {
-    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 65536 && ptr && idx && val && t_desc &&
+    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && val && t_desc &&
                     t_rec && t_maxabs && t_rowshift && t_rec_bytes >= 0,
                 GRF_EINVAL, "grf_transpose_banded_fill: bad arguments");
     GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_transpose_banded_fill: t_rec must be 128-byte aligned");

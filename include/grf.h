@@ -170,7 +170,7 @@ int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const 
 
 /* Banded transpose for the Gram kernel: entries (j, k, v) of Phi (CSR rows j)
  * bucketed by (band = j / band_width, k):  bucket id b = band * n_cols + k.
- * A bucket is a run of 12-byte record PAIRS {u16 j0 - band start, u16 j1 - band start
+ * A bucket is a run of 12-byte record PAIRS {u16 8 (j0 - band start), u16 8 (j1 - band start)
  * (low / high half of one word), f32 v0, f32 v1}, starting on a 128-byte line; an odd
  * bucket ends with the pad record (0, +0.0).  Two calls:
  *   plan: t_desc[2 * (n_bands * n_cols + 1)] = per bucket {first line, pairs}; the last
@@ -179,7 +179,7 @@ int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const 
  *         t_rowshift[n_rows]: the Gram kernel's per-row fixed-point scale 2^shift (every term
  *         < 2^51, the row's sum of |terms| < 2^62).
  * workspace >= grf_transpose_workspace_bytes(n_bands * n_cols), shared by both calls.
- * band_width <= 65536. */
+ * band_width <= 8192. */
 int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
                                   const int32_t *idx, uint32_t *t_desc, void *workspace, size_t workspace_bytes,
                                   grf_stream_t stream);
