@@ -30,6 +30,26 @@ for _p in (ROOT, os.path.join(ROOT, "efficient-gaussian-process-on-graphs_amd"))
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# rocprofv3 PMC summary of this workload (tools/gpu_profile.sh -> tools/pmc_summary.py), committed
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+DEFAULT_WORKLOAD = (100_000, 1_000_000, 128, 8, 0.1)
+
+
+def pmc_traffic(kernels):
+    """HBM bytes per launch of the named kernels from the committed PMC summary
+    (2 * FETCH_SIZE + WRITE_SIZE KiB, the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md)."""
+    import json as _json
+    try:
+        d = _json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None
+    total = 0.0
+    for k in kernels:
+        hits = [v for name, v in d.items() if name.split("<")[0].replace("void ", "") == k]
+        if not hits or "hbm_bytes_per_launch" not in hits[0]:
+            return None
+        total += hits[0]["hbm_bytes_per_launch"]
+    return total
 
 
 def er_graph_exact_edges(n: int, n_edges: int, seed: int = 0) -> sp.csr_matrix:
@@ -185,6 +205,11 @@ def main():
     rows = e - b
     alg_bytes = 4.0 * rows * n + 8.0 * local_nnz + 8.0 * nnz_phi[0]
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
+    sym = world == 1 and not args.no_sym
+    kernels = ["grf::gram_sparse_kernel", "grf::gram_mirror_kernel"] if sym else ["grf::gram_sparse_kernel"]
+    traffic = None
+    if (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and world == 1:
+        traffic = pmc_traffic(kernels)
     out = {
         "metric": "GRF kernel-matrices/sec (N=100k graph, m=128 walks; + achieved HBM GB/s of the Gram kernel)",
         "value": args.steps / t,
@@ -204,9 +229,12 @@ def main():
                    "n_nodes": n, "n_edges": args.edges, "walks_per_node": m, "max_walk_length": L,
                    "parallelism": f"source-sharded x{world}, Phi all-gather, K row blocks"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": ("gram_sparse_kernel+gram_mirror_kernel" if world == 1 and not args.no_sym
-                                else "gram_sparse_kernel"), "kernel_ms": gram_avg, "algorithmic_bytes": alg_bytes},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": ("rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of the same kernels on this workload, "
+                                        "profiles/r01_pmc_summary.json (2*FETCH_SIZE + WRITE_SIZE; bytes per launch)")
+                     if traffic is not None else None,
+                     "kernel": "+".join(k.split("::")[1] for k in kernels), "kernel_ms": gram_avg,
+                     "algorithmic_bytes": alg_bytes},
         "nnz_phi": nnz_phi[0],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
