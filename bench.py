@@ -130,7 +130,7 @@ def main():
 
     from grf_amd import _lib as C
     from grf_amd.dist import allgather_csr_rows, shard_range
-    from grf_amd.engine import DeviceCSR, GRFEngine
+    from grf_amd.engine import DEFAULT_BAND_WIDTH, DeviceCSR, GRFEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -154,14 +154,18 @@ def main():
 
     def step(record: bool):
         G = eng.laplacian(A_dev)
-        # Philox walks of this rank's sources straight to Phi rows (one kernel, no slot round trip)
-        local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e), want64=False, want32=True)
+        # Philox walks of this rank's sources straight to Phi rows (one kernel, no slot round trip);
+        # on one GPU the same kernel counts the banded transpose's buckets
+        tws = eng.transpose_workspace(n, n) if world == 1 else None
+        local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
+                                         band_width=DEFAULT_BAND_WIDTH if tws is not None else 0),
+                            want64=False, want32=True)
         if world > 1:
             ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32)
             phi = DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))
         else:
             phi = DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
-        tr = eng.transpose_banded(phi)
+        tr = eng.transpose_banded(phi, counted_ws=tws)
         if record:
             ev[0].record()
         if world == 1 and not args.no_sym:

@@ -227,8 +227,8 @@ size_t grf_transpose_workspace_bytes(int64_t n_buckets) {
 }
 
 int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                                  const int32_t *idx, uint32_t *t_desc, void *workspace, size_t workspace_bytes,
-                                  grf_stream_t stream) {
+                                  const int32_t *idx, uint32_t *t_desc, int32_t counted, void *workspace,
+                                  size_t workspace_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && t_desc,
                 GRF_EINVAL, "grf_transpose_banded_plan: bad arguments");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
@@ -241,8 +241,8 @@ int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_w
     int32_t *lines = (int32_t *)(w + tr_align((size_t)nbk * 4));
     int64_t *line_off = (int64_t *)(w + 2 * tr_align((size_t)nbk * 4));
     void *scan_ws = w + 2 * tr_align((size_t)nbk * 4) + tr_align((size_t)(nbk + 1) * 8);
-    GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));
-    if (n_rows > 0) {
+    if (!counted) GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));
+    if (n_rows > 0 && !counted) {
         GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "tr_count_kernel");
         tr_count_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, st>>>(n_rows, n_cols, band_width, ptr, idx,
                                                                           cnt);

@@ -145,7 +145,9 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         uint32_t k0, uint32_t k1, int64_t src_begin,
                                                         const double *__restrict__ f, int32_t Lf, int64_t cap,
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
-                                                        double *__restrict__ phi_val, float *__restrict__ phi_val32) {
+                                                        double *__restrict__ phi_val, float *__restrict__ phi_val32,
+                                                        int32_t *__restrict__ t_count, int64_t band_width,
+                                                        int64_t n_cols) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int E = (int)(m * L), T = (int)blockDim.x, tid = (int)threadIdx.x;
     uint64_t *key = smem;                               // [P]  sorted keys, later compacted step keys
@@ -293,6 +295,8 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
             phi_idx[obase + rank + q] = pn_[q];
             phi_val[obase + rank + q] = pv_[q];
             if (phi_val32) phi_val32[obase + rank + q] = (float)pv_[q];
+            // the banded transpose's bucket counts of this row's entries (grf_transpose_banded_plan)
+            if (t_count) atomicAdd(&t_count[((src_begin + s) / band_width) * n_cols + pn_[q]], 1);
         }
     }
     if (tid == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
@@ -359,7 +363,8 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
                                 const int32_t *slot_node, const double *slot_load, const int64_t *g_ptr,
                                 const int32_t *g_idx, const double *g_val, double p_halt, int32_t rule, uint64_t seed,
                                 int64_t src_begin, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
-                                int32_t *phi_idx, double *phi_val, float *phi_val32, hipStream_t st) {
+                                int32_t *phi_idx, double *phi_val, float *phi_val32, int32_t *t_count,
+                                int64_t band_width, int64_t n_cols, hipStream_t st) {
     GRF_REQUIRE(norm == GRF_NORM_DIV || norm == GRF_NORM_MUL_RECIP, GRF_EINVAL, "grf_phi_fused: bad norm");
     GRF_REQUIRE(n_f >= 0 && (n_f == 0 || f), GRF_EINVAL, "grf_phi_fused: bad modulator");
     GRF_REQUIRE(m * (int64_t)L <= 4096, GRF_EUNSUPPORTED, "grf_phi_fused: needs walks_per_node * L <= 4096");
@@ -378,7 +383,8 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
     phi_fused_kernel<W, K><<<(unsigned)n_src, T, lds, st>>>(                                                      \
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val, p_halt, rule, (uint32_t)seed,    \
-        (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32)
+        (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
+        n_cols)
 #define GRF_PHI_PER(W)                                                                                            \
     switch (P / T) {                                                                                              \
         case 1: GRF_PHI_LAUNCH(W, 1); break;                                                                      \
@@ -400,13 +406,13 @@ int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const i
     GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && slot_node && slot_load && phi_cnt && phi_idx && phi_val,
                 GRF_EINVAL, "grf_phi_fused: bad arguments");
     return phi_fused_launch(false, n_src, m, L, norm, slot_node, slot_load, nullptr, nullptr, nullptr, 0.0, 0, 0, 0, f,
-                            n_f, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, S(stream));
+                            n_f, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, nullptr, 1, 0, S(stream));
 }
 
 int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
                      const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
                      int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
-                     float *phi_val32, grf_stream_t stream) {
+                     float *phi_val32, int32_t *t_count, int64_t band_width, grf_stream_t stream) {
     GRF_REQUIRE(params != nullptr, GRF_EINVAL, "grf_walk_phi: params is NULL");
     const grf_walk_params P = *params;
     GRF_REQUIRE(n >= 0 && g_ptr && phi_cnt && phi_idx && phi_val, GRF_EINVAL, "grf_walk_phi: bad arguments");
@@ -418,9 +424,12 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
     GRF_REQUIRE(P.load_rule >= 0 && P.load_rule <= 2, GRF_EINVAL, "grf_walk_phi: bad load_rule %d", P.load_rule);
     GRF_REQUIRE(0 <= src_begin && src_begin <= src_end && src_end <= n, GRF_EINVAL, "grf_walk_phi: bad source range");
     GRF_REQUIRE(n <= 0x7fffffffLL, GRF_EUNSUPPORTED, "grf_walk_phi: n must fit int32 node ids");
+    GRF_REQUIRE(!t_count || (band_width >= 1 &&
+                             phi_cap >= std::min<int64_t>(P.walks_per_node * (int64_t)P.max_walk_length, n)),
+                GRF_EINVAL, "grf_walk_phi: counting needs band_width >= 1 and phi_cap that never truncates a row");
     return phi_fused_launch(true, src_end - src_begin, P.walks_per_node, P.max_walk_length, norm, nullptr, nullptr,
                             g_ptr, g_idx, g_val, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, phi_cnt,
-                            phi_idx, phi_val, phi_val32, S(stream));
+                            phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream));
 }
 
 int32_t grf_steps_densify(int64_t n_src, int64_t m, int32_t L, int64_t n_cols, const int32_t *step_cnt,

@@ -248,8 +248,12 @@ class GRFEngine:
 
     def walk_phi(self, G: DeviceCSR, walks_per_node: int, p_halt: float, max_walk_length: int, f, *,
                  seed: int = 42, load_rule: int = C.LOAD_CUMULATIVE, norm: int = C.NORM_MUL_RECIP,
-                 src_begin: int = 0, src_end: Optional[int] = None, want32: bool = True) -> PaddedRows:
-        """Philox walks straight to Phi rows (one kernel; identical to walk + features)."""
+                 src_begin: int = 0, src_end: Optional[int] = None, want32: bool = True,
+                 count_ws: Optional[torch.Tensor] = None, band_width: int = 0) -> PaddedRows:
+        """Philox walks straight to Phi rows (one kernel; identical to walk + features).
+
+        count_ws: a zeroed transpose workspace (``transpose_workspace``) in which the kernel also
+        counts the banded transpose's buckets, for ``transpose_banded(..., counted_ws=...)``."""
         n = G.n_rows
         src_end = n if src_end is None else src_end
         m, L = int(walks_per_node), int(max_walk_length)
@@ -264,8 +268,8 @@ class GRFEngine:
         v32 = self._empty(ns * cap, torch.float32) if want32 else None
         prm = C.GrfWalkParams(m, float(p_halt), L, int(load_rule), C.RNG_PHILOX, 0, 1, int(seed) & 0xFFFFFFFFFFFFFFFF)
         C.check(self.lib.grf_walk_phi(n, _p(G.ptr), _p(G.idx), _p(G.val), ctypes.byref(prm), src_begin, src_end,
-                                      norm, _p(ft), ft.numel(), cap, _p(cnt), _p(idx), _p(val), _p(v32), self.stream),
-                "grf_walk_phi")
+                                      norm, _p(ft), ft.numel(), cap, _p(cnt), _p(idx), _p(val), _p(v32),
+                                      _p(count_ws), int(band_width), self.stream), "grf_walk_phi")
         return PaddedRows(cnt, idx, val, v32, cap, n)
 
     def features(self, slots: Slots, f, norm: int = C.NORM_MUL_RECIP) -> PaddedRows:
@@ -307,16 +311,26 @@ class GRFEngine:
                                            self.stream), "grf_steps_densify")
         return out
 
-    def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH) -> Banded:
+    def transpose_workspace(self, n_rows: int, n_cols: int, band_width: int = DEFAULT_BAND_WIDTH) -> torch.Tensor:
+        """Zeroed workspace of ``transpose_banded`` (its first n_bands * n_cols int32 are bucket counts)."""
+        nbk = -(-n_rows // band_width) * n_cols
+        ws = self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
+        ws.zero_()
+        return ws
+
+    def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH,
+                         counted_ws: Optional[torch.Tensor] = None) -> Banded:
+        """Banded transpose of Phi.  counted_ws: workspace whose bucket counts ``walk_phi`` filled."""
         n_rows, n_cols = phi.n_rows, phi.n_cols
         nb = -(-n_rows // band_width)
         nbk = nb * n_cols
         t_desc = self._empty(2 * (nbk + 1), torch.int32)
         t_max = self._empty(1, torch.float32)
         t_shift = self._empty(max(n_rows, 1), torch.int32)
-        ws = self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
+        ws = counted_ws if counted_ws is not None else self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
         C.check(self.lib.grf_transpose_banded_plan(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(t_desc),
-                                                   _p(ws), ws.numel(), self.stream), "grf_transpose_banded_plan")
+                                                   int(counted_ws is not None), _p(ws), ws.numel(), self.stream),
+                "grf_transpose_banded_plan")
         # band starts (first line of bucket (band, 0)) and the total: the Gram kernel addresses a
         # band's records with 32-bit byte offsets
         starts = torch.cat([t_desc[0:2 * nbk:2 * n_cols], t_desc[2 * nbk:2 * nbk + 1]]).cpu().numpy()

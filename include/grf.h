@@ -148,11 +148,14 @@ int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, co
  * Requires m * L <= 4096.  norm as in grf_steps. */
 /* Philox walks of the sources [src_begin, src_end) straight to Phi rows in one kernel (the
  * visit slots never touch HBM): bit-identical to grf_walk (params->rng = GRF_RNG_PHILOX)
- * followed by grf_phi_fused.  Requires m * L <= 4096. */
+ * followed by grf_phi_fused.  Requires m * L <= 4096.
+ * Optional (t_count != NULL): also count the banded transpose's buckets of the rows written,
+ * t_count[(row / band_width) * n + col] += 1 -- pass the transpose workspace (zeroed) and then
+ * grf_transpose_banded_plan(..., counted = 1, ...); phi_cap must not truncate rows. */
 int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
                      const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
                      int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
-                     float *phi_val32, grf_stream_t stream);
+                     float *phi_val32, int32_t *t_count, int64_t band_width, grf_stream_t stream);
 int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
                       const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
                       int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream);
@@ -174,15 +177,16 @@ int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const 
  * (low / high half of one word), f32 v0, f32 v1}, starting on a 128-byte line; an odd
  * bucket ends with the pad record (0, +0.0).  Two calls:
  *   plan: t_desc[2 * (n_bands * n_cols + 1)] = per bucket {first line, pairs}; the last
- *         entry holds the total line count (lo, hi words).
+ *         entry holds the total line count (lo, hi words).  counted = 1: the bucket counts
+ *         are already in the workspace (from grf_walk_phi over all rows), skip counting.
  *   fill: t_rec (>= total lines * 128 bytes, 128-byte aligned), t_maxabs[1] = max |Phi| and
  *         t_rowshift[n_rows]: the Gram kernel's per-row fixed-point scale 2^shift (every term
  *         < 2^51, the row's sum of |terms| < 2^62).
  * workspace >= grf_transpose_workspace_bytes(n_bands * n_cols), shared by both calls.
  * band_width <= 8192. */
 int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                                  const int32_t *idx, uint32_t *t_desc, void *workspace, size_t workspace_bytes,
-                                  grf_stream_t stream);
+                                  const int32_t *idx, uint32_t *t_desc, int32_t counted, void *workspace,
+                                  size_t workspace_bytes, grf_stream_t stream);
 int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
                                   const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
                                   int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift, void *workspace,

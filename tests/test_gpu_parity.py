@@ -323,3 +323,10 @@ def test_walk_phi_fused_bitexact(eng, n, deg, m, L, p, rule):
         ref = eng.compact(eng.phi_fused(slots, f)).to_scipy()
         got = eng.compact(eng.walk_phi(G, m, p, L, f, seed=9, load_rule=rule, src_begin=src[0], src_end=src[1]))
         assert same_csr(got.to_scipy(), ref), src
+    # bucket counts from the walk kernel == the transpose's own counting (same K, bit for bit)
+    bw = 256
+    ws = eng.transpose_workspace(n, n, bw)
+    phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=9, load_rule=rule, count_ws=ws, band_width=bw))
+    K1 = eng.gram_sparse(phi, eng.transpose_banded(phi, bw, counted_ws=ws)).cpu().numpy()
+    K2 = eng.gram_sparse(phi, eng.transpose_banded(phi, bw)).cpu().numpy()
+    assert np.array_equal(K1, K2)
