@@ -528,9 +528,15 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
     rc = gram_sparse_launch(n_total, 0, n_total, true, ptr, idx, val, band_width, t_desc, t_rec, t_rowshift, K, ldk,
                             S(stream));
     if (rc != GRF_OK) return rc;
-    const int64_t nt = cdiv<int64_t>(n_total, 64), blocks = nt * (nt + 1) / 2;
+    return grf_gram_mirror(n_total, K, ldk, stream);
+}
+
+int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && K && ldk >= n, GRF_EINVAL, "grf_gram_mirror: bad arguments");
+    if (n == 0) return GRF_OK;
+    const int64_t nt = cdiv<int64_t>(n, 64), blocks = nt * (nt + 1) / 2;
     GRF_REQUIRE_GRID(blocks, 256, "gram_mirror_kernel");
-    gram_mirror_kernel<<<(unsigned)blocks, 256, 0, S(stream)>>>(n_total, nt, K, ldk);
+    gram_mirror_kernel<<<(unsigned)blocks, 256, 0, S(stream)>>>(n, nt, K, ldk);
     GRF_CHECK_LAUNCH("gram_mirror_kernel");
     return GRF_OK;
 }

@@ -220,6 +220,9 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
                             int64_t band_width, const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift,
                             float *K, int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
 
+/* The mirror pass of grf_gram_sparse_sym alone: K[j, i] = K[i, j] for every j > i. */
+int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, grf_stream_t stream);
+
 /* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
  * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */
 int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
