@@ -43,6 +43,17 @@ __device__ inline long long fx_round(double x) {
     return (long long)(((unsigned long long)hi << 32) | lo);
 }
 
+// round(a * v) for |a * v| < 2^51 in ONE fp64 operation: fma(a, v, 1.5 * 2^52) rounds the
+// exact product plus the magic number once, i.e. to the nearest integer (ties to even), which
+// is exactly fx_round(a * v) whenever a * v itself is exact in fp64 (a product of two f32
+// scaled by a power of two is)
+__device__ inline long long fx_fma_round(double a, double v) {
+    const double magic = 6755399441055744.0;  // 1.5 * 2^52
+    const unsigned long long b = (unsigned long long)__double_as_longlong(__builtin_fma(a, v, magic));
+    const uint32_t hi = (uint32_t)(b >> 32) - 0x43380000u, lo = (uint32_t)b;
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
 
 // inclusive max-scan of non-negative ints over the 64 lanes (DPP row shifts + row broadcasts)
 __device__ inline int wave_incl_max(int v) {
@@ -152,8 +163,8 @@ __device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, in
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
-        const long long q0 = fx_round(sc[u] * (double)rec[u].v0);
-        const long long q1 = fx_round(sc[u] * (double)rec[u].v1);
+        const long long q0 = fx_fma_round(sc[u], (double)rec[u].v0);
+        const long long q1 = fx_fma_round(sc[u], (double)rec[u].v1);
         uint32_t c0 = rec[u].cols & 0xffffu, c1 = rec[u].cols >> 16;
         if (TAIL) {
             const bool ok = w0 + u * 64 + lane < cend;
