@@ -123,13 +123,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=2048)
     ap.add_argument("--no-sym", action="store_true", help="single GPU: compute every K tile (no symmetric mode)")
+    ap.add_argument("--mode", choices=["rows", "allreduce"], default="rows",
+                    help="rows: K row blocks after a Phi all-gather (default); allreduce: the north star's literal "
+                         "option -- per-rank partial K over an inner-dimension slice + bucketed RCCL all-reduce, "
+                         "K replicated on every rank (SURVEY.md §8e)")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
     from grf_amd import _lib as C
-    from grf_amd.dist import allgather_csr_rows, shard_range
+    from grf_amd.dist import allgather_csr_rows, allreduce_buckets, shard_range
     from grf_amd.engine import DEFAULT_BAND_WIDTH, DeviceCSR, GRFEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,7 +151,9 @@ def main():
     A_dev = DeviceCSR.from_scipy(A, dev)
     b, e = shard_range(n, rank, world)
     ldk = eng.leading_dim(n)
-    K = torch.empty((e - b, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
+    allreduce = args.mode == "allreduce"
+    k_rows = n if allreduce else e - b
+    K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     gram_ms = []
     nnz_phi = [0]
@@ -168,7 +174,9 @@ def main():
         tr = eng.transpose_banded(phi, counted_ws=tws)
         if record:
             ev[0].record()
-        if world == 1 and not args.no_sym:
+        if allreduce:
+            eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
+        elif world == 1 and not args.no_sym:
             eng.gram_sparse_sym(phi, tr, out=K)  # upper band tiles + mirror
         else:
             eng.gram_sparse(phi, tr, b, e, out=K)
@@ -176,6 +184,8 @@ def main():
             ev[1].record()
             ev[1].synchronize()
             gram_ms.append(ev[0].elapsed_time(ev[1]))
+        if allreduce:
+            allreduce_buckets(K[:, :n])
         nnz_phi[0] = phi.nnz
         local_nnz = local.nnz
         return local_nnz
@@ -208,11 +218,13 @@ def main():
     # rank's K rows once, read its Phi rows (col int32 + val fp32) and every Phi^T entry once
     rows = e - b
     alg_bytes = 4.0 * rows * n + 8.0 * local_nnz + 8.0 * nnz_phi[0]
+    if allreduce:  # every K entry written; all of Phi scanned, the slice's share of Phi^T read
+        alg_bytes = 4.0 * n * n + 8.0 * nnz_phi[0] + 8.0 * nnz_phi[0] * rows / n
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
-    sym = world == 1 and not args.no_sym
+    sym = world == 1 and not args.no_sym and not allreduce
     kernels = ["grf::gram_sparse_kernel", "grf::gram_mirror_kernel"] if sym else ["grf::gram_sparse_kernel"]
     traffic = None
-    if (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and world == 1:
+    if (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and world == 1 and not allreduce:
         traffic = pmc_traffic(kernels)
     out = {
         "metric": "GRF kernel-matrices/sec (N=100k graph, m=128 walks; + achieved HBM GB/s of the Gram kernel)",
@@ -231,7 +243,9 @@ def main():
                                f"max_walk_length={L}, p_halt={p}, diffusion modulator beta=1, Philox seed 42, "
                                f"dense fp32 K resident in HBM",
                    "n_nodes": n, "n_edges": args.edges, "walks_per_node": m, "max_walk_length": L,
-                   "parallelism": f"source-sharded x{world}, Phi all-gather, K row blocks"},
+                   "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
+                                   f"RCCL all-reduce (K replicated)") if allreduce else
+                                  f"source-sharded x{world}, Phi all-gather, K row blocks"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": ("rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of the same kernels on this workload, "

@@ -196,6 +196,7 @@ constexpr size_t gram_lds_bytes(int64_t W, int waves, int halves) {
 struct GramTiles {
     int64_t rows, W, nb;
     bool sym;
+    int32_t k_begin, k_end;  // only the nonzeros Phi[i, k] with k in [k_begin, k_end) contribute
     __host__ __device__ int64_t count(int64_t J) const {
         if (!sym) return rows;
         const int64_t c = (J + 1) * W;
@@ -277,8 +278,9 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
 #pragma unroll
         for (int h = 0; h < kHalves; ++h) {
             const int64_t e = g0 + h * 64 + lane;
-            const int32_t k = e < e1 ? idx[e] : -1;
-            av[h] = e < e1 ? val[e] : 0.f;
+            int32_t k = e < e1 ? idx[e] : -1;
+            if (k < tl.k_begin || k >= tl.k_end) k = -1;  // (k-slice mode)
+            av[h] = k >= 0 ? val[e] : 0.f;
             const uint2 d = k >= 0 ? t_desc[boff + k] : make_uint2((uint32_t)line0, 0u);
             t0[h] = ((int32_t)d.x - line0) * 128;  // bucket byte offset within the band
             cnt[h] = (int32_t)d.y;                 // pairs
@@ -467,12 +469,13 @@ extern "C" {
 
 size_t grf_gram_workspace_bytes(void) { return 256; }
 
-static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t rows, bool sym, const int64_t *ptr,
+static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t rows, bool sym, int64_t k_begin,
+                                  int64_t k_end, const int64_t *ptr,
                                   const int32_t *idx, const float *val, int64_t band_width, const uint32_t *t_desc,
                                   const void *t_rec, const int32_t *t_rowshift, float *K, int64_t ldk,
                                   hipStream_t st) {
     const int64_t nb = cdiv<int64_t>(n_total, band_width);
-    const GramTiles tl{rows, band_width, nb, sym};
+    const GramTiles tl{rows, band_width, nb, sym, (int32_t)k_begin, (int32_t)k_end};
     const int64_t n_tiles = tl.total();
     if (n_tiles == 0) return GRF_OK;
     // tuning knobs (defaults = measured best on MI355X): gathers in flight per wave, waves per tile
@@ -526,7 +529,8 @@ int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, con
     int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, t_desc, t_rec, t_rowshift, K, ldk);
     if (rc != GRF_OK) return rc;
     if (row_end == row_begin || n_total == 0) return GRF_OK;
-    return gram_sparse_launch(n_total, row_begin, row_end - row_begin, false, ptr, idx, val, band_width, t_desc, t_rec,
+    return gram_sparse_launch(n_total, row_begin, row_end - row_begin, false, 0, n_total, ptr, idx, val, band_width,
+                              t_desc, t_rec,
                               t_rowshift, K, ldk, S(stream));
 }
 
@@ -536,10 +540,26 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
     int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, t_desc, t_rec, t_rowshift, K, ldk);
     if (rc != GRF_OK) return rc;
     if (n_total == 0) return GRF_OK;
-    rc = gram_sparse_launch(n_total, 0, n_total, true, ptr, idx, val, band_width, t_desc, t_rec, t_rowshift, K, ldk,
+    rc = gram_sparse_launch(n_total, 0, n_total, true, 0, n_total, ptr, idx, val, band_width, t_desc, t_rec,
+                            t_rowshift, K, ldk,
                             S(stream));
     if (rc != GRF_OK) return rc;
     return grf_gram_mirror(n_total, K, ldk, stream);
+}
+
+int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,
+                               const int64_t *ptr, const int32_t *idx, const float *val, int64_t band_width,
+                               const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
+                               int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, t_desc, t_rec, t_rowshift, K, ldk);
+    if (rc != GRF_OK) return rc;
+    GRF_REQUIRE(0 <= k_begin && k_begin <= k_end && k_end <= n_total, GRF_EINVAL,
+                "grf_gram_sparse_kslice: bad column slice [%lld, %lld)", (long long)k_begin, (long long)k_end);
+    if (row_end == row_begin || n_total == 0) return GRF_OK;
+    (void)workspace;
+    (void)workspace_bytes;
+    return gram_sparse_launch(n_total, row_begin, row_end - row_begin, false, k_begin, k_end, ptr, idx, val,
+                              band_width, t_desc, t_rec, t_rowshift, K, ldk, S(stream));
 }
 
 int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, grf_stream_t stream) {

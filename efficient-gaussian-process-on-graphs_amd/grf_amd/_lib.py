@@ -69,6 +69,8 @@ SIGNATURES = {
     "grf_gram_workspace_bytes": (_sz, []),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _vp]),
+    "grf_gram_sparse_kslice": (_i32, [_i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64,
+                                      _vp, _sz, _vp]),
     "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
 }

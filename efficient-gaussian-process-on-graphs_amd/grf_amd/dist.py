@@ -9,6 +9,12 @@ N = 100k) and each computes its row block K[R_r, :] = Phi[R_r] Phi^T.  K stays
 row-sharded; no reduction over the 40 GB K is ever needed (an
 all-reduce of K would move ~70 GB per GPU through the xGMI ring).
 
+``mode="allreduce"`` is the north star's literal alternative, kept as an option
+so both can be measured: after the same Phi all-gather, rank r computes the
+partial Gram over its slice of the inner dimension, K_r = sum over k in C_r of
+Phi[:, k] Phi[:, k]^T (all n rows), and the ranks sum the K_r with an all-reduce
+in fixed-size buckets.  Every rank ends with the whole K (replicated).
+
 The reference has no distributed code; its only parallelism is a fork pool over
 source chunks (sparse_sampler.py:90-114), which this replaces.
 """
@@ -73,9 +79,27 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
     return full_ptr, torch.cat(parts_i), torch.cat(parts_v)
 
 
+def allreduce_buckets(t: torch.Tensor, bucket_bytes: int = 1 << 30, group=None) -> torch.Tensor:
+    """In-place sum of a (possibly row-padded, row-strided) 2-D tensor over the ranks, one
+    contiguous row bucket of at most ``bucket_bytes`` per collective (bounds RCCL's staging)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return t
+    rows_per = max(1, bucket_bytes // max(1, t.stride(0) * t.element_size()))
+    base = t.as_strided((t.shape[0], t.stride(0)), (t.stride(0), 1)) if t.dim() == 2 else t.view(-1, 1)
+    for r0 in range(0, base.shape[0], rows_per):
+        dist.all_reduce(base[r0:r0 + rows_per], group=group)
+    return t
+
+
 def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length, *, seed=42, group=None,
-                          rng=None):
-    """This rank's row block of K = Phi Phi^T (float32, on the engine's device), and its row range."""
+                          rng=None, mode: str = "rows"):
+    """This rank's row block of K = Phi Phi^T (float32, on the engine's device), and its row range.
+
+    ``mode="allreduce"``: every rank returns the whole K (row range (0, n)), assembled as the
+    all-reduced sum of per-rank partial Grams over inner-dimension slices."""
+    if mode not in ("rows", "allreduce"):
+        raise ValueError(f"mode must be 'rows' or 'allreduce', got {mode!r}")
     from . import _lib as C
     from .engine import DeviceCSR
 
@@ -99,4 +123,8 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
     else:
         phi = DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
     tr = engine.transpose_banded(phi)
+    if mode == "allreduce":
+        K = engine.gram_sparse_kslice(phi, tr, b, e)
+        allreduce_buckets(K, group=group)
+        return K, (0, n)
     return engine.gram_sparse(phi, tr, b, e), (b, e)

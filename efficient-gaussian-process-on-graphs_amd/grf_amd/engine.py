@@ -365,6 +365,20 @@ class GRFEngine:
                 "grf_gram_sparse")
         return out[:, :n]
 
+    def gram_sparse_kslice(self, phi: DeviceCSR, tr: Banded, k_begin: int, k_end: int, row_begin: int = 0,
+                           row_end: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Partial K[row_begin:row_end, :] over the inner-dimension slice [k_begin, k_end) (float32)."""
+        n = tr.n_rows
+        row_end = n if row_end is None else row_end
+        ldk = self.leading_dim(n)
+        if out is None:
+            out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
+        C.check(self.lib.grf_gram_sparse_kslice(n, row_begin, row_end, k_begin, k_end, _p(phi.ptr), _p(phi.idx),
+                                                _p(phi.val32), tr.band_width, _p(tr.t_desc), _p(tr.t_rec),
+                                                _p(tr.t_rowshift), _p(out), out.stride(0), _p(self._gram_ws),
+                                                self._gram_ws.numel(), self.stream), "grf_gram_sparse_kslice")
+        return out[:, :n]
+
     def gram_sparse_sym(self, phi: DeviceCSR, tr: Banded, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Whole K (float32) on this device from the upper band tiles plus a mirror pass."""
         n = tr.n_rows

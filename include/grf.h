@@ -220,6 +220,14 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
                             int64_t band_width, const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift,
                             float *K, int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
 
+/* Partial Gram over a slice of the inner dimension: K[r, :] = sum over k in [k_begin, k_end)
+ * of Phi[r, k] Phi[:, k] (same fixed-point rule as grf_gram_sparse).  The partial Grams of
+ * disjoint slices sum to K -- the "partial K + all-reduce" multi-GPU option. */
+int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,
+                               const int64_t *ptr, const int32_t *idx, const float *val, int64_t band_width,
+                               const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
+                               int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+
 /* The mirror pass of grf_gram_sparse_sym alone: K[j, i] = K[i, j] for every j > i. */
 int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, grf_stream_t stream);
 

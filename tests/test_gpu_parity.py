@@ -258,6 +258,38 @@ def test_gram_sparse_band_invariance(eng):
     assert ok, fro
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_gram_kslice_partials_sum_to_K(eng, world):
+    """The all-reduce option: partial Grams over disjoint inner-dimension slices
+    are each exact against the oracle's column-restricted Gram and sum to K (fp32 sum of fp32
+    partials: within the fp32 tolerance of gram_close)."""
+    from grf_amd.dist import shard_range
+    n = 3000
+    A = er_graph(n, 8, 11)
+    G = eng.laplacian(A)
+    phi = eng.compact(eng.features(eng.walk(G, 16, 0.2, 4, rng=1, seed=9), [1.0, -0.5, 0.25, -0.125]))
+    tr = eng.transpose_banded(phi, 1024)
+    phi64 = phi.to_scipy()
+    Ksum = np.zeros((n, n), np.float64)
+    for r in range(world):
+        kb, ke = shard_range(n, r, world)
+        Kr = eng.gram_sparse_kslice(phi, tr, kb, ke).cpu().numpy()
+        mask = np.zeros(n)
+        mask[kb:ke] = 1.0
+        sub = (phi64 @ sp.diags(mask)).tocsr()
+        ok, fro = gram_close(Kr, sub)
+        assert ok, (r, fro)
+        Ksum += Kr
+    ok, fro = gram_close(Ksum, phi64)
+    assert ok, fro
+    if world == 1:
+        assert np.array_equal(Ksum.astype(np.float32), eng.gram_sparse(phi, tr).cpu().numpy())
+    # a row block of a slice is the same bits as those rows of the whole slice
+    kb, ke = shard_range(n, 0, world)
+    assert np.array_equal(eng.gram_sparse_kslice(phi, tr, kb, ke, 100, 400).cpu().numpy(),
+                          eng.gram_sparse_kslice(phi, tr, kb, ke).cpu().numpy()[100:400])
+
+
 @pytest.mark.parametrize("n", [1, 31, 128, 1000, 2708])
 def test_gram_dense_mfma_vs_oracle(eng, n):
     A = er_graph(max(n, 2), 6, n + 1)[:n, :n]

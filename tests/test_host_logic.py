@@ -112,6 +112,40 @@ def _gather_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _allreduce_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from grf_amd.dist import allreduce_buckets
+        n, ld = 37, 40
+        parts = [torch.from_numpy(np.random.default_rng(r).random((n, ld), dtype=np.float32)) for r in range(world)]
+        buf = parts[rank].clone()
+        view = buf[:, :n]                       # row-padded like the engine's K (leading dim > n)
+        allreduce_buckets(view, bucket_bytes=3 * ld * 4)   # several buckets, last one ragged
+        want = sum(p[:, :n] for p in parts)
+        q.put((rank, bool(torch.allclose(view, want, rtol=0, atol=1e-6))))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    return sorted(res)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allreduce_buckets_gloo(world):
+    assert _spawn(_allreduce_worker, world) == [(r, True) for r in range(world)]
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_allgather_csr_rows_gloo(world):
     ctx = mp.get_context("spawn")
