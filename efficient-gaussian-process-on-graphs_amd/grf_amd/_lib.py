@@ -69,6 +69,15 @@ SIGNATURES = {
     "grf_gram_workspace_bytes": (_sz, []),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _vp]),
+    "grf_csr_transpose_workspace_bytes": (_sz, [_i64, _i64]),
+    "grf_csr_transpose": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "grf_spmm_csr": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
+    "grf_spmm_csr_f64": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
+    "grf_cg_gram_solve_f64": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _dbl, _vp, _i64, _i32, _dbl,
+                                     _i32, _vp, _i64, _vp, _sz, _vp, _vp, _vp]),
+    "grf_cg_workspace_bytes": (_sz, [_i64, _i64, _i32]),
+    "grf_cg_gram_solve": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _dbl, _vp, _i64, _i32, _dbl, _i32,
+                                 _vp, _i64, _vp, _sz, _vp, _vp, _vp]),
     "grf_gram_sparse_kslice": (_i32, [_i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64,
                                       _vp, _sz, _vp]),
     "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),

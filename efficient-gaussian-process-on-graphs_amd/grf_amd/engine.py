@@ -420,6 +420,102 @@ class GRFEngine:
             return self.gram_sparse(phi, self.transpose_banded(phi))
         raise ValueError(f"unknown gram method {method!r}")
 
+    # ------------------------------------- K.v and CG (models/sparse_grf_model.py:21-45)
+    def _row_map(self, rows) -> Optional[torch.Tensor]:
+        if rows is None:
+            return None
+        return torch.as_tensor(rows, device=self.device).to(torch.int32).flatten().contiguous()
+
+    def csr_transpose(self, phi: DeviceCSR, rows=None) -> DeviceCSR:
+        """(Phi[rows])^T as CSR (n_cols x len(rows), float32); column lists in ascending row order."""
+        rmap = self._row_map(rows)
+        n_sel = phi.n_rows if rmap is None else rmap.numel()
+        if rmap is None:
+            nnz = phi.nnz
+        else:
+            rl = rmap.long()
+            nnz = int((phi.ptr[rl + 1] - phi.ptr[rl]).sum().item()) if n_sel else 0
+        t_ptr = self._empty(phi.n_cols + 1, torch.int64)
+        t_idx = self._empty(nnz, torch.int32)
+        t_val = self._empty(nnz, torch.float32)
+        ws = self._ws(self.lib.grf_csr_transpose_workspace_bytes(n_sel, phi.n_cols))
+        C.check(self.lib.grf_csr_transpose(n_sel, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(rmap), phi.n_cols,
+                                           _p(t_ptr), _p(t_idx), _p(t_val), _p(ws), ws.numel(), self.stream),
+                "grf_csr_transpose")
+        return DeviceCSR(phi.n_cols, n_sel, t_ptr, t_idx, None, t_val, nnz)
+
+    def spmm(self, A: DeviceCSR, X: torch.Tensor, rows=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Y = A[rows] X (X float32 or float64, n_cols x S with unit column stride; Y the same type)."""
+        if X.dtype not in (torch.float32, torch.float64) or X.dim() != 2 or X.stride(1) != 1 \
+                or X.shape[0] != A.n_cols:
+            raise ValueError("spmm: X must be a float32/float64 (n_cols x S) row-major matrix")
+        rmap = self._row_map(rows)
+        n_out = A.n_rows if rmap is None else rmap.numel()
+        S = X.shape[1]
+        if out is None:
+            out = torch.empty((n_out, S), dtype=X.dtype, device=self.device)
+        fn = self.lib.grf_spmm_csr if X.dtype == torch.float32 else self.lib.grf_spmm_csr_f64
+        C.check(fn(n_out, _p(A.ptr), _p(A.idx), _p(A.val32), _p(rmap), _p(X), X.stride(0), S, _p(out),
+                   out.stride(0), self.stream), "grf_spmm_csr")
+        return out
+
+    def gram_matvec(self, phi: DeviceCSR, V: torch.Tensor, rows=None, cols=None, phi_t: Optional[DeviceCSR] = None,
+                    noise: float = 0.0) -> torch.Tensor:
+        """K[rows, cols] V = Phi[rows] (Phi[cols]^T V) (+ noise V when rows == cols), K never formed."""
+        phi_t = self.csr_transpose(phi, cols) if phi_t is None else phi_t
+        Y = self.spmm(phi, self.spmm(phi_t, V), rows)
+        if noise:
+            Y.add_(V, alpha=float(noise))
+        return Y
+
+    def cg_solve(self, phi: DeviceCSR, B: torch.Tensor, noise: float, rows=None, phi_t: Optional[DeviceCSR] = None,
+                 tolerance: float = 1.0, max_iter: int = 1000, return_residuals: bool = False):
+        """linear_cg on (Phi[rows] Phi[rows]^T + noise I) X = B for the columns of B (n x S, S <= 256).
+
+        B float64 runs the recurrence in fp64, float32 in the reference's fp32.  Returns
+        (X, iterations) [+ the final residual norms of the normalised columns].  tolerance / max_iter default to gpytorch's settings.cg_tolerance (1)
+        and settings.max_cg_iterations (1000)."""
+        rmap = self._row_map(rows)
+        n_sys = phi.n_rows if rmap is None else rmap.numel()
+        if B.dtype not in (torch.float32, torch.float64) or B.dim() != 2 or B.stride(1) != 1 \
+                or B.shape[0] != n_sys:
+            raise ValueError("cg_solve: B must be a float32/float64 (n_rows x S) row-major matrix")
+        phi_t = self.csr_transpose(phi, rmap) if phi_t is None else phi_t
+        S = B.shape[1]
+        X = torch.empty((n_sys, S), dtype=B.dtype, device=self.device)
+        ws = self._ws(self.lib.grf_cg_workspace_bytes(n_sys, phi.n_cols, S))
+        iters = ctypes.c_int32(0)
+        resid = np.zeros(S, np.float64)
+        fn = self.lib.grf_cg_gram_solve if B.dtype == torch.float32 else self.lib.grf_cg_gram_solve_f64
+        C.check(fn(n_sys, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(rmap), phi.n_cols, _p(phi_t.ptr),
+                   _p(phi_t.idx), _p(phi_t.val32), float(noise), _p(B), B.stride(0), S, float(tolerance),
+                   int(max_iter), _p(X), X.stride(0), _p(ws), ws.numel(), ctypes.byref(iters),
+                   resid.ctypes.data_as(ctypes.c_void_p), self.stream), "grf_cg_gram_solve")
+        if return_residuals:
+            return X, int(iters.value), resid
+        return X, int(iters.value)
+
+    def pathwise_predict(self, phi: DeviceCSR, train_idx, test_idx, y_train: torch.Tensor, noise: float,
+                         eps1: torch.Tensor, eps2: torch.Tensor, tolerance: float = 1.0, max_iter: int = 1000,
+                         dtype: torch.dtype = torch.float64):
+        """SparseGraphGP.predict (models/sparse_grf_model.py:21-45) given its random draws.
+
+        eps1: (S x n_nodes) prior weights, eps2: (S x n_train) noise draws (already scaled by
+        the noise std).  dtype: float64 (default) or the reference's float32 for every dense
+        block and the CG recurrence.  Returns (S x n_test) posterior samples (dtype) and the
+        CG iteration count."""
+        tr = self._row_map(train_idx)
+        te = self._row_map(test_idx)
+        E = eps1.to(self.device, dtype).t().contiguous()                      # n_nodes x S
+        f_train = self.spmm(phi, E, tr)                                        # (eps1 @ phi_train.T)^T
+        f_test = self.spmm(phi, E, te)
+        y = y_train.to(self.device, dtype).flatten()
+        B = y[:, None] - (f_train + eps2.to(self.device, dtype).t())          # b_batch^T
+        phi_t = self.csr_transpose(phi, tr)
+        V, iters = self.cg_solve(phi, B.contiguous(), noise, tr, phi_t, tolerance, max_iter)
+        out = f_test + self.spmm(phi, self.spmm(phi_t, V), te)                # + K_test_train v
+        return out.t(), iters
+
     # ------------------------------------------------------------- pipelines
     def kernel_matrix(self, A, modulator_vector: Sequence[float], walks_per_node: int, p_halt: float,
                       max_walk_length: int, *, rng: int = C.RNG_PHILOX, seed: int = 42, n_chunks: int = 1,

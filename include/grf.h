@@ -240,6 +240,58 @@ int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, fl
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,
                     int64_t lda, grf_stream_t stream);
 
+/* ------------------------------------------- K.v and the pathwise-conditioning CG
+ * The step after the path: SparseGraphGP.predict
+ * (efficient_graph_gp_sparse/models/sparse_grf_model.py:21-45) and the linear_cg it
+ * calls (line 43; linear_operator 0.5 via gpytorch==1.11).  K = Phi Phi^T is never
+ * formed: K_rows,cols V = Phi[rows] (Phi[cols]^T V).  Dense blocks are float32
+ * row-major [rows x ld] with the S right-hand sides / samples as columns.
+ * `row_map` (int32, optional) selects rows of Phi; NULL = rows 0..n-1. */
+
+/* (Phi[row_map])^T as CSR: t_ptr[n_cols + 1] (int64), t_idx / t_val [nnz of the selected
+ * rows]; t_idx are positions in row_map; every column lists them in ascending order. */
+int32_t grf_csr_transpose(int64_t n_sel, const int64_t *ptr, const int32_t *idx, const float *val,
+                          const int32_t *row_map, int64_t n_cols, int64_t *t_ptr, int32_t *t_idx, float *t_val,
+                          void *workspace, size_t workspace_bytes, grf_stream_t stream);
+size_t grf_csr_transpose_workspace_bytes(int64_t n_sel, int64_t n_cols);
+
+/* Y[r, :] = sum_e val[e] X[idx[e], :] over row row_map[r] (fp32, fixed summation order):
+ * phi_test @ v, eps1 @ phi_train.T (sparse_grf_model.py:39-40, 45). */
+int32_t grf_spmm_csr(int64_t n_out, const int64_t *ptr, const int32_t *idx, const float *val, const int32_t *row_map,
+                     const float *X, int64_t ldx, int32_t n_rhs, float *Y, int64_t ldy, grf_stream_t stream);
+/* the same with fp64 dense blocks and accumulation (A's fp32 values widened) */
+int32_t grf_spmm_csr_f64(int64_t n_out, const int64_t *ptr, const int32_t *idx, const float *val,
+                         const int32_t *row_map, const double *X, int64_t ldx, int32_t n_rhs, double *Y, int64_t ldy,
+                         grf_stream_t stream);
+
+/* linear_cg(A._matmul, rhs, tolerance) with A = Phi_t Phi_t^T + noise I, Phi_t = Phi[row_map]
+ * (n_sys rows; t_* its transpose from grf_csr_transpose): sparse_grf_model.py:34, 43.
+ * rhs / x: [n_sys x ld] fp32, n_rhs in [1, 256] columns solved together.  Same rule as
+ * linear_cg: per-column normalisation, eps = stop_updating_after = 1e-10, stop after
+ * iteration k >= min(10, max_iter - 1) once the mean residual norm < tolerance.
+ * *iters_out (host pointer, may be NULL) receives the iterations run and resid_out (host,
+ * n_rhs doubles, may be NULL) the final residual norms of the normalised systems (the
+ * quantities the stopping rule averages); the call returns when they are (it polls a
+ * device flag, so it synchronises the stream).
+ * grf_cg_gram_solve keeps the reference's fp32 vectors and scalars; the _f64 variant
+ * runs the same recurrence in fp64 (Phi's fp32 values widened).  linear_cg's
+ * trajectory is sensitive to rounding once CG loses orthogonality (K + s2 I with
+ * condition ~1e4 reaches the cg_tolerance after 24 iterations in fp64, 36 in fp32; in
+ * fp64 a 1e-15 relative change of the rhs already moves the 11-iteration result by ~1e-3),
+ * so the fp64 solve is the one that tracks the algorithm itself. */
+int32_t grf_cg_gram_solve(int64_t n_sys, const int64_t *ptr, const int32_t *idx, const float *val,
+                          const int32_t *row_map, int64_t n_cols, const int64_t *t_ptr, const int32_t *t_idx,
+                          const float *t_val, double noise, const float *rhs, int64_t ld_rhs, int32_t n_rhs,
+                          double tolerance, int32_t max_iter, float *x, int64_t ldx, void *workspace,
+                          size_t workspace_bytes, int32_t *iters_out, double *resid_out, grf_stream_t stream);
+int32_t grf_cg_gram_solve_f64(int64_t n_sys, const int64_t *ptr, const int32_t *idx, const float *val,
+                              const int32_t *row_map, int64_t n_cols, const int64_t *t_ptr, const int32_t *t_idx,
+                              const float *t_val, double noise, const double *rhs, int64_t ld_rhs, int32_t n_rhs,
+                              double tolerance, int32_t max_iter, double *x, int64_t ldx, void *workspace,
+                              size_t workspace_bytes, int32_t *iters_out, double *resid_out, grf_stream_t stream);
+/* (covers both precisions) */
+size_t grf_cg_workspace_bytes(int64_t n_sys, int64_t n_cols, int32_t n_rhs);
+
 #ifdef __cplusplus
 }
 #endif
