@@ -90,19 +90,34 @@ static int64_t tr_chunks(int64_t n_sel, int64_t n_cols) {
 // SG lanes per column group; the 64/SG groups take the nonzeros j = g, g + G, ...
 // of each 64-batch and are summed by a fixed xor tree.  T = type of the dense blocks and
 // of the accumulation (float: the reference's precision; double: A's fp32 values widened).
+//
+// Column tiles: a gathered X row comes from the Infinity Cache at ~8.6 TB/s chip-wide but
+// from the XCD's L2 at ~17 TB/s (MI355X_MICROARCH.md, "Indexed rows").  With `seg` the
+// launch covers only the entries whose column lies in tile `tile` (X rows
+// [tile * tw, (tile + 1) * tw), a slice that fits every XCD's L2): row r's entries of that
+// tile are the contiguous range [seg[tile][r], seg[tile + 1][r]) of its (column-sorted) CSR
+// row.  Tiles run as successive launches; `accumulate` adds to the Y of the tiles before.
 template <int SG, typename T>
 __global__ __launch_bounds__(256) void spmm_kernel(int64_t n_out, const int64_t *ptr, const int32_t *idx,
                                                    const float *val, const int32_t *row_map, const T *X,
                                                    int64_t ldx, int32_t S, T *Y, int64_t ldy, const T *Z,
-                                                   int64_t ldz, T zc, const int32_t *done) {
+                                                   int64_t ldz, T zc, const int32_t *done, const int64_t *seg,
+                                                   int32_t tile, int32_t accumulate) {
     if (done && __builtin_nontemporal_load(done)) return;
     constexpr int G = 64 / SG;
     const int lane = threadIdx.x & 63;
     const int g = lane / SG, cl = lane % SG;
     const int64_t n_waves = (int64_t)gridDim.x * 4;
     for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n_out; r += n_waves) {
-        const int64_t row = uniform(row_map ? (int64_t)row_map[r] : r);
-        const int64_t e0 = uniform(ptr[row]), e1 = uniform(ptr[row + 1]);
+        int64_t e0, e1;
+        if (seg) {
+            e0 = uniform(seg[(int64_t)tile * n_out + r]);
+            e1 = uniform(seg[(int64_t)(tile + 1) * n_out + r]);
+        } else {
+            const int64_t row = uniform(row_map ? (int64_t)row_map[r] : r);
+            e0 = uniform(ptr[row]);
+            e1 = uniform(ptr[row + 1]);
+        }
         for (int c0 = 0; c0 < S; c0 += SG) {
             const int c = c0 + cl;
             const bool cok = c < S;
@@ -110,8 +125,8 @@ __global__ __launch_bounds__(256) void spmm_kernel(int64_t n_out, const int64_t 
             T acc = T(0);
             for (int64_t eb = e0; eb < e1; eb += 64) {
                 const int64_t e = eb + lane;
-                const int32_t k_l = e < e1 ? idx[e] : 0;
-                const float v_l = e < e1 ? val[e] : 0.f;
+                const int32_t k_l = e < e1 ? __builtin_nontemporal_load(&idx[e]) : 0;
+                const float v_l = e < e1 ? __builtin_nontemporal_load(&val[e]) : 0.f;
                 const int cnt = (int)min<int64_t>(64, e1 - eb);
                 if constexpr (SG == 64) {
                     int j = 0;
@@ -160,6 +175,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(int64_t n_out, const int64_t 
             for (int off = SG; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
             if (g == 0 && cok) {
                 T y = acc;
+                if (accumulate) y = Y[r * ldy + c] + y;
                 if (Z) y += zc * Z[r * ldz + c];
                 Y[r * ldy + c] = y;
             }
@@ -170,23 +186,85 @@ __global__ __launch_bounds__(256) void spmm_kernel(int64_t n_out, const int64_t 
 template <int SG, typename T>
 static int32_t spmm_launch(int64_t n_out, const int64_t *ptr, const int32_t *idx, const float *val,
                            const int32_t *row_map, const T *X, int64_t ldx, int32_t S, T *Y, int64_t ldy,
-                           const T *Z, int64_t ldz, T zc, const int32_t *done, hipStream_t st) {
+                           const T *Z, int64_t ldz, T zc, const int32_t *done, const int64_t *seg,
+                           int32_t n_tiles, hipStream_t st) {
     const int64_t blocks = std::min<int64_t>(cdiv<int64_t>(n_out, 4), 1 << 16);
-    spmm_kernel<SG, T><<<(unsigned)blocks, 256, 0, st>>>(n_out, ptr, idx, val, row_map, X, ldx, S, Y, ldy, Z, ldz, zc,
-                                                      done);
-    GRF_CHECK_LAUNCH("spmm_kernel");
+    if (!seg) {
+        spmm_kernel<SG, T><<<(unsigned)blocks, 256, 0, st>>>(n_out, ptr, idx, val, row_map, X, ldx, S, Y, ldy, Z,
+                                                             ldz, zc, done, nullptr, 0, 0);
+        GRF_CHECK_LAUNCH("spmm_kernel");
+        return GRF_OK;
+    }
+    for (int32_t t = 0; t < n_tiles; ++t) {
+        const bool last = t == n_tiles - 1;
+        spmm_kernel<SG, T><<<(unsigned)blocks, 256, 0, st>>>(n_out, ptr, idx, val, row_map, X, ldx, S, Y, ldy,
+                                                             last ? Z : nullptr, ldz, zc, done, seg, t, t > 0);
+        GRF_CHECK_LAUNCH("spmm_kernel");
+    }
     return GRF_OK;
 }
 
 template <typename T>
 static int32_t spmm_dispatch(int64_t n_out, const int64_t *ptr, const int32_t *idx, const float *val,
                              const int32_t *row_map, const T *X, int64_t ldx, int32_t S, T *Y, int64_t ldy,
-                             const T *Z, int64_t ldz, T zc, const int32_t *done, hipStream_t st) {
+                             const T *Z, int64_t ldz, T zc, const int32_t *done, hipStream_t st,
+                             const int64_t *seg = nullptr, int32_t n_tiles = 1) {
     if (n_out == 0 || S == 0) return GRF_OK;
-    if (S >= 48) return spmm_launch<64, T>(n_out, ptr, idx, val, row_map, X, ldx, S, Y, ldy, Z, ldz, zc, done, st);
-    if (S >= 12) return spmm_launch<16, T>(n_out, ptr, idx, val, row_map, X, ldx, S, Y, ldy, Z, ldz, zc, done, st);
-    if (S >= 3) return spmm_launch<4, T>(n_out, ptr, idx, val, row_map, X, ldx, S, Y, ldy, Z, ldz, zc, done, st);
-    return spmm_launch<1, T>(n_out, ptr, idx, val, row_map, X, ldx, S, Y, ldy, Z, ldz, zc, done, st);
+    if (n_tiles <= 1) seg = nullptr;
+#define GRF_SPMM(SGV) spmm_launch<SGV, T>(n_out, ptr, idx, val, row_map, X, ldx, S, Y, ldy, Z, ldz, zc, done, seg, n_tiles, st)
+    if (S >= 48) return GRF_SPMM(64);
+    if (S >= 12) return GRF_SPMM(16);
+    if (S >= 3) return GRF_SPMM(4);
+    return GRF_SPMM(1);
+#undef GRF_SPMM
+}
+
+// ---- column-tile plan: seg[t * n_out + r] = first entry of row r with column >= t * tw
+// (t = 0..n_tiles; seg[n_tiles][r] = row end).  One wave per output row, no atomics.
+__global__ __launch_bounds__(256) void spmm_plan_kernel(int64_t n_out, const int64_t *ptr, const int32_t *idx,
+                                                        const int32_t *row_map, int32_t tw, int32_t n_tiles,
+                                                        int64_t *seg) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n_out) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = row_map ? (int64_t)row_map[r] : r;
+    const int64_t s = ptr[row], e = ptr[row + 1];
+    for (int64_t i = s + lane; i < e; i += 64) {
+        const int32_t tc = idx[i] / tw;
+        const int32_t tp = i > s ? idx[i - 1] / tw : -1;
+        for (int32_t t = tp + 1; t <= tc; ++t) seg[(int64_t)t * n_out + r] = i;
+    }
+    const int32_t last = e > s ? idx[e - 1] / tw : -1;
+    for (int32_t t = last + 1 + lane; t <= n_tiles; t += 64) seg[(int64_t)t * n_out + r] = e;
+}
+
+static int64_t spmm_tile_bytes() {
+    static int64_t v = [] {
+        const char *e = getenv("GRF_SPMM_TILE_BYTES");
+        return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)(8 << 20);
+    }();
+    return v;
+}
+
+// tile width (X rows per tile) for S columns of elem bytes: a power of two, 0 = untiled.
+// Budget 8 MiB -> X tiles of <= 4 MiB (one XCD L2).  Measured at C4 (CG iteration, S = 64):
+// fp32 1.63 ms untiled -> 1.36 ms; fp64 3.39 -> 2.25 ms (2 MiB tiles: 1.45 / 2.18 ms;
+// 1 MiB: 1.72 / 2.82 ms -- per-tile overheads; 8 MiB: 1.51 / 2.89 ms -- spills past L2).
+static int32_t spmm_tile_rows(int64_t n_in, int32_t S, size_t elem) {
+    const int64_t tb = spmm_tile_bytes();
+    if (tb <= 0) return 0;
+    int64_t tw = 64;
+    while (tw * 2 * S * (int64_t)elem <= tb) tw *= 2;
+    return tw >= n_in ? 0 : (int32_t)tw;
+}
+
+static int32_t spmm_plan(int64_t n_out, const int64_t *ptr, const int32_t *idx, const int32_t *row_map, int32_t tw,
+                         int32_t n_tiles, int64_t *seg, hipStream_t st) {
+    if (n_out == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_out, 4), 256, "spmm_plan_kernel");
+    spmm_plan_kernel<<<(unsigned)cdiv<int64_t>(n_out, 4), 256, 0, st>>>(n_out, ptr, idx, row_map, tw, n_tiles, seg);
+    GRF_CHECK_LAUNCH("spmm_plan_kernel");
+    return GRF_OK;
 }
 
 // --------------------------------------------------------------------- CG
@@ -362,21 +440,28 @@ __global__ __launch_bounds__(256) void cg_out_kernel(int64_t n, int32_t S, const
 }
 
 struct CgLayout {
-    size_t R, P, Y, X, W, part, dbl, i32, total;
+    size_t R, P, Y, X, W, part, dbl, i32, seg1, seg2, total;
+    int32_t tw1, nt1, tw2, nt2;  // column tiles of Phi_t^T (over the n_sys rows of P) and Phi_t (over W)
 };
 
-static CgLayout cg_layout(int64_t n_sys, int64_t n_cols, int32_t S) {
+static CgLayout cg_layout(int64_t n_sys, int64_t n_cols, int32_t S, size_t elem) {
     CgLayout l{};
     size_t o = 0;
-    const size_t vec = al256((size_t)n_sys * S * sizeof(double));  // (sized for the fp64 solve)
+    const size_t vec = al256((size_t)n_sys * S * elem);
     l.R = o; o += vec;
     l.P = o; o += vec;
     l.Y = o; o += vec;
     l.X = o; o += vec;
-    l.W = o; o += al256((size_t)n_cols * S * sizeof(double));
+    l.W = o; o += al256((size_t)n_cols * S * elem);
     l.part = o; o += al256((size_t)kRedBlocks * S * sizeof(double));
     l.dbl = o; o += al256((size_t)5 * S * sizeof(double));
     l.i32 = o; o += al256((size_t)(2 * S + 8) * sizeof(int32_t));
+    l.tw1 = spmm_tile_rows(n_sys, S, elem);
+    l.nt1 = l.tw1 ? (int32_t)cdiv<int64_t>(n_sys, l.tw1) : 1;
+    l.tw2 = spmm_tile_rows(n_cols, S, elem);
+    l.nt2 = l.tw2 ? (int32_t)cdiv<int64_t>(n_cols, l.tw2) : 1;
+    l.seg1 = o; o += l.tw1 ? al256((size_t)(l.nt1 + 1) * n_cols * sizeof(int64_t)) : 0;
+    l.seg2 = o; o += l.tw2 ? al256((size_t)(l.nt2 + 1) * n_sys * sizeof(int64_t)) : 0;
     l.total = o;
     return l;
 }
@@ -391,7 +476,7 @@ static int32_t cg_solve_impl(int64_t n_sys, const int64_t *ptr, const int32_t *i
     GRF_REQUIRE(n_rhs >= 1 && n_rhs <= kMaxRhs, GRF_EUNSUPPORTED, "grf_cg_gram_solve: n_rhs must be in [1, %d]",
                 kMaxRhs);
     GRF_REQUIRE(ld_rhs >= n_rhs && ldx >= n_rhs && max_iter >= 0, GRF_EINVAL, "grf_cg_gram_solve: bad strides");
-    const CgLayout l = cg_layout(n_sys, n_cols, n_rhs);
+    const CgLayout l = cg_layout(n_sys, n_cols, n_rhs, sizeof(T));
     GRF_REQUIRE(workspace && workspace_bytes >= l.total, GRF_EINVAL, "grf_cg_gram_solve: workspace too small (%zu < %zu)",
                 workspace_bytes, l.total);
     hipStream_t sm = S(stream);
@@ -412,7 +497,11 @@ static int32_t cg_solve_impl(int64_t n_sys, const int64_t *ptr, const int32_t *i
     GRF_REQUIRE_GRID(cdiv<int64_t>(nel, 256), 256, "cg_dir_kernel");
     const unsigned eb = (unsigned)cdiv<int64_t>(nel, 256);
     const int32_t k_check = std::min(10, max_iter - 1);
+    int32_t rc0;
 
+    int64_t *seg1 = l.tw1 ? (int64_t *)(w + l.seg1) : nullptr, *seg2 = l.tw2 ? (int64_t *)(w + l.seg2) : nullptr;
+    if (seg1 && (rc0 = spmm_plan(n_cols, t_ptr, t_idx, nullptr, l.tw1, l.nt1, seg1, sm)) != GRF_OK) return rc0;
+    if (seg2 && (rc0 = spmm_plan(n_sys, ptr, idx, row_map, l.tw2, l.nt2, seg2, sm)) != GRF_OK) return rc0;
     cg_reduce_kernel<kFinNorm, T><<<rb, 256, 0, sm>>>(n_sys, Sn, R, P, Y, X, rhs, ld_rhs, st, k_check, tolerance);
     GRF_CHECK_LAUNCH("cg_reduce_kernel<norm>");
     cg_reduce_kernel<kFinInit, T><<<rb, 256, 0, sm>>>(n_sys, Sn, R, P, Y, X, rhs, ld_rhs, st, k_check, tolerance);
@@ -426,9 +515,11 @@ static int32_t cg_solve_impl(int64_t n_sys, const int64_t *ptr, const int32_t *i
     int32_t rc = GRF_OK;
     for (int32_t k = 0; k < max_iter && rc == GRF_OK; ++k) {
         // mvms = (K + s2 I) p = Phi_t (Phi_t^T p) + s2 p
-        rc = spmm_dispatch<T>(n_cols, t_ptr, t_idx, t_val, nullptr, P, Sn, Sn, W, Sn, nullptr, 0, T(0), st.done, sm);
+        rc = spmm_dispatch<T>(n_cols, t_ptr, t_idx, t_val, nullptr, P, Sn, Sn, W, Sn, nullptr, 0, T(0), st.done, sm,
+                              seg1, l.nt1);
         if (rc != GRF_OK) break;
-        rc = spmm_dispatch<T>(n_sys, ptr, idx, val, row_map, W, Sn, Sn, Y, Sn, P, Sn, (T)noise, st.done, sm);
+        rc = spmm_dispatch<T>(n_sys, ptr, idx, val, row_map, W, Sn, Sn, Y, Sn, P, Sn, (T)noise, st.done, sm, seg2,
+                              l.nt2);
         if (rc != GRF_OK) break;
         cg_reduce_kernel<kFinAlpha, T><<<rb, 256, 0, sm>>>(n_sys, Sn, R, P, Y, X, rhs, ld_rhs, st, k_check, tolerance);
         cg_reduce_kernel<kFinUpdate, T><<<rb, 256, 0, sm>>>(n_sys, Sn, R, P, Y, X, rhs, ld_rhs, st, k_check, tolerance);
@@ -545,7 +636,8 @@ int32_t grf_spmm_csr_f64(int64_t n_out, const int64_t *ptr, const int32_t *idx, 
 }
 
 size_t grf_cg_workspace_bytes(int64_t n_sys, int64_t n_cols, int32_t n_rhs) {
-    return cg_layout(n_sys, n_cols, n_rhs).total;
+    return std::max(cg_layout(n_sys, n_cols, n_rhs, sizeof(float)).total,
+                    cg_layout(n_sys, n_cols, n_rhs, sizeof(double)).total);
 }
 
 int32_t grf_cg_gram_solve(int64_t n_sys, const int64_t *ptr, const int32_t *idx, const float *val,
