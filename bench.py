@@ -110,6 +110,148 @@ def cpu_baseline(A, f, m, p, L, budget_rows: int, n_threads: int):
     }
 
 
+def cpu_baseline_predict(phi_csr, tr, te, y, noise, S, iters):
+    """SparseGraphGP.predict restated on the host (oracle/cg.py, scipy sparse, fp64, 1 thread):
+    setup + 1 and + 2 CG iterations timed, extrapolated to the GPU's iteration count."""
+    from oracle import cg as OCG
+
+    r = np.random.default_rng(1)
+    e1 = r.standard_normal((S, phi_csr.shape[0]))
+    e2 = np.sqrt(noise) * r.standard_normal((S, len(tr)))
+    t = []
+    for mi in (1, 2):
+        t0 = time.perf_counter()
+        OCG.pathwise_predict(phi_csr, tr, te, y, noise, e1, e2, max_iter=mi)
+        t.append(time.perf_counter() - t0)
+    per_iter = max(t[1] - t[0], 1e-9)
+    setup = max(t[0] - per_iter, 0.0)
+    t_full = setup + iters * per_iter
+    return {
+        "value": 1.0 / t_full,
+        "unit": "posterior-sample-batches/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"oracle/cg.py pathwise_predict (scipy sparse, fp64, 1 thread) at the same size: setup "
+                   f"{setup:.2f} s + {iters} CG iterations x {per_iter:.2f} s (timed at max_iter 1 and 2, "
+                   f"extrapolated)"),
+    }
+
+
+def main_predict(args):
+    """Pathwise-conditioning posterior samples (models/sparse_grf_model.py:21-45) at C4 scale:
+    Phi of the headline workload resident in HBM, 60/20 % train/test split (the reference's
+    scaling experiment, run_scaling_experiment.py splits=[0.6, 0.2, 0.2]), n_samples = 64.
+    One step = eps draws + Phi_train^T CSR + priors + linear_cg (cg_tolerance 1) + K_test,train V.
+    Multi-GPU: independent sample batches per rank (weak scaling, no collective)."""
+    import torch
+
+    from grf_amd.engine import DeviceCSR, GRFEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    eng = GRFEngine(f"cuda:{local_rank}")
+    n, m, L, p, S = args.n, args.walks, args.length, args.p_halt, args.samples
+    A = er_graph_exact_edges(n, args.edges, seed=0)
+    f = diffusion_modulator(L, 1.0)
+    G = eng.laplacian(DeviceCSR.from_scipy(A, eng.device))
+    phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42), want64=False)
+    perm = np.random.default_rng(0).permutation(n)
+    n_tr, n_te = int(0.6 * n), int(0.2 * n)
+    tr = torch.from_numpy(perm[:n_tr]).to(eng.device)
+    te = torch.from_numpy(perm[n_tr:n_tr + n_te]).to(eng.device)
+    y = torch.randn(n_tr, device=eng.device, generator=torch.Generator(eng.device).manual_seed(5))
+    noise = 0.01  # (the scaling experiment's noise_std 0.1)
+    dtype = torch.float64 if args.cg_dtype == "f64" else torch.float32
+    gen = torch.Generator(eng.device).manual_seed(1000 + rank)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    cg_ms, its = [], [0]
+
+    def step(record):
+        e1 = torch.randn(S, n, device=eng.device, generator=gen)
+        e2 = noise ** 0.5 * torch.randn(S, n_tr, device=eng.device, generator=gen)
+        E = e1.to(dtype).t().contiguous()
+        f_train = eng.spmm(phi, E, tr)
+        f_test = eng.spmm(phi, E, te)
+        B = (y.to(dtype)[:, None] - (f_train + e2.to(dtype).t())).contiguous()
+        phi_t = eng.csr_transpose(phi, tr)
+        if record:
+            ev[0].record()
+        V, it = eng.cg_solve(phi, B, noise, tr, phi_t)
+        if record:
+            ev[1].record()
+            ev[1].synchronize()
+            cg_ms.append(ev[0].elapsed_time(ev[1]))
+        its[0] = it
+        return f_test + eng.spmm(phi, eng.spmm(phi_t, V), te)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    nnz_tr = int((phi.ptr[tr + 1] - phi.ptr[tr]).sum().item())
+    elem = 8 if dtype == torch.float64 else 4
+    per_it_ms = float(np.mean(cg_ms)) / max(its[0], 1)
+    # one CG iteration = Phi_t^T P (n x S out) + Phi_t W (n_tr x S out): CSR entries (col + val)
+    # streamed twice, the dense inputs read once and outputs written once; gathers re-read rows
+    alg = 2 * 8.0 * nnz_tr + elem * S * (n_tr + n + n + 3 * n_tr)
+    gathers = 2.0 * nnz_tr * S * elem
+    out = {
+        "metric": "GRF pathwise-conditioning posterior sample batches/s (SparseGraphGP.predict, N=100k, 64 samples)",
+        "value": world * args.steps / t,
+        "unit": "posterior-sample-batches/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * t / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": ("fp64" if elem == 8 else "fp32") + " CG vectors, fp32 Phi",
+        "data": "synthetic Erdos-Renyi graph (seed 0), random targets, torch.randn draws",
+        "config": {"workload": f"C4 predict: ER N={n}, {args.edges} edges, m={m}, L={L}, p_halt={p}; "
+                               f"{n_tr} train / {n_te} test nodes, n_samples={S}, noise {noise}, cg_tolerance 1",
+                   "cg_iterations": its[0], "nnz_phi_train": nnz_tr,
+                   "parallelism": f"independent sample batches x{world}"},
+        "roofline": {"bound": "hbm", "achieved": alg / (per_it_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": alg / (per_it_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "CG iteration (2 column-tiled spmm_kernel passes + 3 cg_* kernels)",
+                     "kernel_ms": per_it_ms, "algorithmic_bytes": alg,
+                     "gather_TBps": gathers / (per_it_ms * 1e-3) / 1e12,
+                     "gather_note": "X rows gathered per CSR entry (L2/Infinity-Cache served; MI355X_MICROARCH.md "
+                                    "'Indexed rows': ~17 TB/s L2-resident, ~8.6 TB/s Infinity Cache)"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_predict(_phi_host(phi), perm[:n_tr], perm[n_tr:n_tr + n_te],
+                                                   y.cpu().numpy().astype(np.float64), noise, S, its[0])
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _phi_host(phi):
+    n = phi.n_rows
+    return sp.csr_matrix((phi.val32.cpu().numpy().astype(np.float64), phi.idx.cpu().numpy(), phi.ptr.cpu().numpy()),
+                         shape=(n, phi.n_cols))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -127,7 +269,13 @@ def main():
                     help="rows: K row blocks after a Phi all-gather (default); allreduce: the north star's literal "
                          "option -- per-rank partial K over an inner-dimension slice + bucketed RCCL all-reduce, "
                          "K replicated on every rank (SURVEY.md §8e)")
+    ap.add_argument("--workload", choices=["kernel", "predict"], default="kernel",
+                    help="kernel: K = Phi Phi^T (headline); predict: pathwise-conditioning posterior samples")
+    ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
+    ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
+    if args.workload == "predict":
+        return main_predict(args)
 
     import torch
     import torch.distributed as dist
