@@ -469,15 +469,11 @@ extern "C" {
 
 size_t grf_gram_workspace_bytes(void) { return 256; }
 
-static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t rows, bool sym, int64_t k_begin,
-                                  int64_t k_end, const int64_t *ptr,
-                                  const int32_t *idx, const float *val, int64_t band_width, const uint32_t *t_desc,
-                                  const void *t_rec, const int32_t *t_rowshift, float *K, int64_t ldk,
-                                  hipStream_t st) {
-    const int64_t nb = cdiv<int64_t>(n_total, band_width);
-    const GramTiles tl{rows, band_width, nb, sym, (int32_t)k_begin, (int32_t)k_end};
-    const int64_t n_tiles = tl.total();
-    if (n_tiles == 0) return GRF_OK;
+// tiles [t_first, t_last) of one Gram call
+static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramTiles &tl, int64_t t_first,
+                                 int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
+                                 const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
+                                 int64_t ldk, hipStream_t st) {
     // tuning knobs (defaults = measured best on MI355X): gathers in flight per wave, waves per tile
     static const int knobs = [] {
         const char *e = getenv("GRF_GRAM_UNROLL"), *w = getenv("GRF_GRAM_WAVES");
@@ -485,11 +481,11 @@ static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t ro
         return ((u == 4 || u == 8 || u == 16) ? u : 8) * 10 + (ww == 8 ? 8 : 4);
     }();
     const int unroll = knobs / 10, waves = knobs % 10, halves = waves == 8 ? 1 : 2;
-    const size_t lds = gram_lds_bytes(band_width, waves, halves);
+    const size_t lds = gram_lds_bytes(tl.W, waves, halves);
     // one launch covers at most 2^32 - 1 work-items: split the tile range
     const int64_t max_tiles = ((1ll << 32) - 1) / (64 * waves);
-    for (int64_t t0 = 0; t0 < n_tiles; t0 += max_tiles) {
-        const int64_t nt = (n_tiles - t0) < max_tiles ? (n_tiles - t0) : max_tiles;
+    for (int64_t t0 = t_first; t0 < t_last; t0 += max_tiles) {
+        const int64_t nt = (t_last - t0) < max_tiles ? (t_last - t0) : max_tiles;
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     gram_sparse_kernel<WV, H, U><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx, val,   \
                                                                      reinterpret_cast<const uint2 *>(t_desc),     \
@@ -507,6 +503,19 @@ static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t ro
         GRF_CHECK_LAUNCH("gram_sparse_kernel");
     }
     return GRF_OK;
+}
+
+static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t rows, bool sym, int64_t k_begin,
+                                  int64_t k_end, const int64_t *ptr,
+                                  const int32_t *idx, const float *val, int64_t band_width, const uint32_t *t_desc,
+                                  const void *t_rec, const int32_t *t_rowshift, float *K, int64_t ldk,
+                                  hipStream_t st) {
+    const int64_t nb = cdiv<int64_t>(n_total, band_width);
+    const GramTiles tl{rows, band_width, nb, sym, (int32_t)k_begin, (int32_t)k_end};
+    const int64_t n_tiles = tl.total();
+    if (n_tiles == 0) return GRF_OK;
+    return gram_tiles_launch(n_total, row_begin, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, t_rowshift, K, ldk,
+                             st);
 }
 
 static int32_t gram_sparse_check(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
