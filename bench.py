@@ -302,9 +302,8 @@ def main():
     allreduce = args.mode == "allreduce"
     k_rows = n if allreduce else e - b
     K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    gram_ms = []
-    nnz_phi = [0]
+    gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
+    last = [None]
 
     def step(record: bool):
         G = eng.laplacian(A_dev)
@@ -313,14 +312,16 @@ def main():
         tws = eng.transpose_workspace(n, n) if world == 1 else None
         local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
                                          band_width=DEFAULT_BAND_WIDTH if tws is not None else 0),
-                            want64=False, want32=True)
+                            want64=False, want32=True, sync_free=world == 1)
         if world > 1:
             ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32)
             phi = DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))
         else:
-            phi = DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
-        tr = eng.transpose_banded(phi, counted_ws=tws)
+            phi = local
+        # (one GPU: sizes from bounds, no host round trip inside the step)
+        tr = eng.transpose_banded(phi, counted_ws=tws, nnz_bound=local.nnz_bound if world == 1 else None)
         if record:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         if allreduce:
             eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
@@ -330,13 +331,10 @@ def main():
             eng.gram_sparse(phi, tr, b, e, out=K)
         if record:
             ev[1].record()
-            ev[1].synchronize()
-            gram_ms.append(ev[0].elapsed_time(ev[1]))
+            gram_ev.append(ev)
         if allreduce:
             allreduce_buckets(K[:, :n])
-        nnz_phi[0] = phi.nnz
-        local_nnz = local.nnz
-        return local_nnz
+        last[0] = (phi, local)
 
     for _ in range(args.warmup):
         step(False)
@@ -344,13 +342,13 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    local_nnz = 0
     for _ in range(args.steps):
-        local_nnz = step(True)
+        step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
+    gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
     if world > 1:
         tt = torch.tensor([t], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -362,6 +360,8 @@ def main():
         gram_avg = float(np.mean(gram_ms))
 
     ms_per_step = 1000.0 * t / args.steps
+    nnz_phi = [last[0][0].nnz]
+    local_nnz = last[0][1].nnz
     # algorithmic bytes of the K assembly (gram_sparse_kernel [+ gram_mirror_kernel]): write this
     # rank's K rows once, read its Phi rows (col int32 + val fp32) and every Phi^T entry once
     rows = e - b

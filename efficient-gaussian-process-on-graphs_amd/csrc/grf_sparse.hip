@@ -189,6 +189,232 @@ __global__ void tr_pad_fill_kernel(int64_t n, const uint2 *desc, const int32_t *
     }
 }
 
+
+// ---------------------------------------------------- staged (binned) transpose fill
+// tr_fill_kernel places every record with a global atomic on its bucket's cursor and two
+// scattered sub-line stores (43.5 M atomics and partially written lines at C4).  The staged
+// fill moves the entries in two passes whose global writes are whole lines:
+//   1. tr_bin_kernel: a workgroup takes kBinRows rows of one band, counting-sorts their
+//      entries by region = (band, cr-column range) in LDS and writes them back over its own
+//      CSR range of the staging buffer as {u16 8 * row-in-band, u16 column-in-region, f32
+//      value}, plus its per-region offsets (table row of nreg + 1 ints).
+//   2. tr_place_kernel: a workgroup per region gathers the region's sub-runs from the band's
+//      binning workgroups, builds the region's records (a contiguous range of lines: buckets
+//      are ordered by (band, column)) in LDS with LDS cursors -- the odd buckets' padding is
+//      the zero fill -- and writes the image with 16-byte stores.  A region whose image
+//      exceeds the LDS cap falls back to global cursors.
+constexpr int kRegionCols = 128;          // columns per region (at least; see tr_region_cols)
+constexpr int kPlaceCap = 48 * 1024;      // LDS image cap of one region
+constexpr int kBinRows = 16;              // rows per binning workgroup (divides every band: band_width % 64 == 0)
+constexpr int kBinCap = 8192;             // entries of one binning workgroup sorted in LDS (64 KiB)
+
+__global__ __launch_bounds__(256) void tr_bin_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, int32_t cr,
+                                                     int32_t nreg, const int64_t *ptr, const int32_t *idx,
+                                                     const float *val, uint2 *staging, int32_t *tab,
+                                                     float *wg_max, float *row_max, double *row_sum) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char tb_smem[];
+    uint2 *img = reinterpret_cast<uint2 *>(tb_smem);                        // [kBinCap]
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(img + kBinCap);            // [nreg] counts, then cursors
+    int32_t *rp = reinterpret_cast<int32_t *>(cnt + nreg);                  // [kBinRows + 1]
+    int32_t *scratch = rp + kBinRows + 1;                                   // [8]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * kBinRows, r1 = min<int64_t>(n_rows, r0 + kBinRows);
+    const int nr = (int)(r1 - r0);
+    const int64_t band = r0 / bw;
+    const int64_t E0 = ptr[r0];
+    const int32_t nE = (int32_t)(ptr[r1] - E0);
+    for (int g = tid; g < nreg; g += 256) cnt[g] = 0u;
+    for (int i = tid; i <= nr; i += 256) rp[i] = (int32_t)(ptr[r0 + i] - E0);
+    __syncthreads();
+    // the workgroup's entries: in registers (all loads in flight at once) when they fit
+    constexpr int kPerT = kBinCap / 256;
+    const bool in_lds = nE <= kBinCap;
+    int32_t kr[kPerT];
+    float vr[kPerT];
+    if (in_lds) {
+#pragma unroll
+        for (int q = 0; q < kPerT; ++q) {
+            const int32_t e = tid + q * 256;
+            kr[q] = e < nE ? idx[E0 + e] : -1;
+            vr[q] = e < nE ? val[E0 + e] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < kPerT; ++q)
+            if (kr[q] >= 0) atomicAdd(&cnt[kr[q] / cr], 1u);
+    } else {
+        for (int32_t e = tid; e < nE; e += 256) atomicAdd(&cnt[idx[E0 + e] / cr], 1u);
+    }
+    // per-row max / sum of |values| (one wave per row, fixed order: deterministic shifts)
+    float wmx = 0.f;
+    for (int i = wave; i < nr; i += 4) {
+        float mx = 0.f;
+        double sm = 0.0;
+        for (int32_t e = rp[i] + lane; e < rp[i + 1]; e += 64) {
+            const float a = fabsf(val[E0 + e]);
+            mx = fmaxf(mx, a);
+            sm += (double)a;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        sm = wave_sum<double>(sm);
+        if (lane == 0) {
+            row_max[r0 + i] = mx;
+            row_sum[r0 + i] = sm;
+        }
+        wmx = fmaxf(wmx, mx);
+    }
+    // the workgroup's max |value| (one store; reduced by tr_maxabs_kernel -- one global atomic per
+    // row on a single word serialised the old fill)
+    if (lane == 0) scratch[wave] = (int32_t)__float_as_uint(wmx);
+    __syncthreads();
+    if (tid == 0) {
+        float m = 0.f;
+        for (int q = 0; q < 4; ++q) m = fmaxf(m, __uint_as_float((uint32_t)scratch[q]));
+        wg_max[blockIdx.x] = m;
+    }
+    __syncthreads();
+    // exclusive offsets of the regions (thread t owns regions [t * per, (t + 1) * per))
+    const int per = (nreg + 255) / 256;
+    int32_t sum = 0;
+    for (int q = 0; q < per; ++q) {
+        const int g = tid * per + q;
+        if (g < nreg) sum += (int32_t)cnt[g];
+    }
+    int32_t total;
+    int32_t run = block_exclusive_scan<int32_t>(sum, scratch, &total);
+    int32_t *trow = tab + (int64_t)blockIdx.x * (nreg + 1);
+    for (int q = 0; q < per; ++q) {
+        const int g = tid * per + q;
+        if (g < nreg) {
+            const int32_t c = (int32_t)cnt[g];
+            trow[g] = run;
+            cnt[g] = (uint32_t)run;  // cursor
+            run += c;
+        }
+    }
+    if (tid == 0) trow[nreg] = total;
+    __syncthreads();
+    const uint32_t jr0 = (uint32_t)(r0 - band * bw);
+    uint2 *out = staging + E0;
+    auto row_of = [&](int32_t e) {  // the entry's row: the last i with rp[i] <= e
+        int lo = 0, hi = nr;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (rp[mid] <= e) lo = mid;
+            else hi = mid;
+        }
+        return lo;
+    };
+    if (in_lds) {
+#pragma unroll
+        for (int q = 0; q < kPerT; ++q) {
+            const int32_t e = tid + q * 256, k = kr[q];
+            if (k >= 0) {
+                const int g = k / cr;
+                const uint32_t s = atomicAdd(&cnt[g], 1u);
+                img[s] = make_uint2(((jr0 + (uint32_t)row_of(e)) * 8u) | ((uint32_t)(k - g * cr) << 16),
+                                    __float_as_uint(vr[q]));
+            }
+        }
+    } else {
+        for (int32_t e = tid; e < nE; e += 256) {
+            const int32_t k = idx[E0 + e];
+            const int g = k / cr;
+            const uint32_t s = atomicAdd(&cnt[g], 1u);
+            out[s] = make_uint2(((jr0 + (uint32_t)row_of(e)) * 8u) | ((uint32_t)(k - g * cr) << 16),
+                                __float_as_uint(val[E0 + e]));
+        }
+    }
+    if (in_lds) {
+        __syncthreads();
+        for (int32_t e = tid; e < nE; e += 256) out[e] = img[e];
+    }
+}
+
+// max over the binning workgroups' maxima (one workgroup)
+__global__ __launch_bounds__(1024) void tr_maxabs_kernel(int64_t n, const float *wg_max, float *maxabs) {
+    __shared__ float red[16];
+    float m = 0.f;
+    for (int64_t i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, wg_max[i]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < 16; ++q) m = fmaxf(m, red[q]);
+        *maxabs = fmaxf(m, red[0]);
+    }
+}
+
+__global__ __launch_bounds__(256) void tr_place_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, int32_t cr,
+                                                       int32_t nreg, const int64_t *ptr, const uint2 *desc,
+                                                       const int64_t *ent_off, const uint2 *staging,
+                                                       const int32_t *tab, int32_t *gcur, unsigned char *t_rec) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char tp_smem[];
+    const int tid = threadIdx.x;
+    const int64_t band = blockIdx.x / nreg, g = blockIdx.x - band * nreg;
+    const int64_t c0 = g * cr, c1 = min<int64_t>(n_cols, c0 + cr);
+    const int64_t b0 = band * n_cols + c0, b1 = band * n_cols + c1;
+    const int64_t L0 = desc[b0].x, L1 = desc[b1].x;  // (desc[nbk].x = total lines, low word)
+    const int64_t img = (L1 - L0) * kLineBytes;
+    if (ent_off[b1] == ent_off[b0]) return;
+    // the band's binning workgroups
+    const int64_t w0 = band * bw / kBinRows, w1 = cdiv<int64_t>(min<int64_t>(n_rows, (band + 1) * bw), kBinRows);
+    const bool lds = img <= kPlaceCap;
+    uint32_t *lcur = reinterpret_cast<uint32_t *>(tp_smem);   // [cr]
+    uint32_t *lline = lcur + cr;                               // [cr] first byte of each bucket in the image
+    unsigned char *image = tp_smem + 8 * cr;                   // [img]
+    if (lds) {
+        for (int i = tid; i < c1 - c0; i += 256) {
+            lcur[i] = 0u;
+            lline[i] = (uint32_t)((desc[b0 + i].x - L0) * kLineBytes);
+        }
+        for (int64_t i = tid; i < img / 16; i += 256) reinterpret_cast<uint4 *>(image)[i] = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+    }
+    for (int64_t w = w0 + tid; w < w1; w += 256) {
+        const int32_t *trow = tab + w * (nreg + 1);
+        const int32_t o0 = trow[g], o1 = trow[g + 1];
+        const uint2 *run = staging + ptr[w * kBinRows];
+        for (int32_t o = o0; o < o1; ++o) {
+            const uint2 x = run[o];
+            const uint32_t kk = x.x >> 16;
+            if (lds) {
+                const uint32_t s = atomicAdd(&lcur[kk], 1u);
+                unsigned char *pair = image + lline[kk] + kPairBytes * (s >> 1);
+                reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(x.x & 0xffffu);
+                reinterpret_cast<uint32_t *>(pair + 4)[s & 1] = x.y;
+            } else {  // oversized region: global cursors (zeroed by the caller)
+                const int64_t b = b0 + kk;
+                const int32_t s = atomicAdd(&gcur[b], 1);
+                unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (s >> 1);
+                reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(x.x & 0xffffu);
+                reinterpret_cast<uint32_t *>(pair + 4)[s & 1] = x.y;
+            }
+        }
+    }
+    if (lds) {
+        __syncthreads();
+        uint4 *dst = reinterpret_cast<uint4 *>(t_rec + L0 * kLineBytes);
+        for (int64_t i = tid; i < img / 16; i += 256) dst[i] = reinterpret_cast<const uint4 *>(image)[i];
+        return;
+    }
+    for (int64_t b = b0 + tid; b < b1; b += 256) {  // pad the odd buckets
+        const int32_t c = (int32_t)(ent_off[b + 1] - ent_off[b]);
+        if (c & 1) {
+            unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (c >> 1);
+            reinterpret_cast<uint16_t *>(pair)[1] = 0;
+            reinterpret_cast<float *>(pair + 4)[1] = 0.f;
+        }
+    }
+}
+
+static int32_t tr_region_cols(int64_t n_cols) {
+    int64_t cr = kRegionCols;
+    while (cdiv<int64_t>(n_cols, cr) > 4096) cr *= 2;
+    return (int32_t)cr;
+}
+
 }  // namespace grf
 
 using namespace grf;
@@ -293,6 +519,74 @@ int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_w
     GRF_REQUIRE_GRID(cdiv<int64_t>(nbk, 256), 256, "tr_pad_fill_kernel");
     tr_pad_fill_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, desc, cursor, (unsigned char *)t_rec);
     GRF_CHECK_LAUNCH("tr_pad_fill_kernel");
+    return GRF_OK;
+}
+
+
+size_t grf_transpose_staging_bytes(int64_t n_rows, int64_t n_cols, int64_t band_width, int64_t nnz) {
+    if (n_cols <= 0 || band_width <= 0) return 0;
+    const int64_t nreg = cdiv<int64_t>(n_cols, tr_region_cols(n_cols)), nwg = cdiv<int64_t>(n_rows, kBinRows);
+    return tr_align((size_t)nnz * 8) + tr_align((size_t)std::max<int64_t>(n_rows, 1) * 8) +
+           tr_align((size_t)std::max<int64_t>(nwg, 1) * (nreg + 1) * 4) + tr_align((size_t)std::max<int64_t>(nwg, 1) * 4);
+}
+
+int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
+                                         const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
+                                         int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
+                                         void *workspace, size_t workspace_bytes, int64_t nnz, void *staging,
+                                         size_t staging_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && val && t_desc &&
+                    t_rec && t_maxabs && t_rowshift && t_rec_bytes >= 0 && staging,
+                GRF_EINVAL, "grf_transpose_banded_fill_staged: bad arguments");
+    GRF_REQUIRE(band_width % 64 == 0, GRF_EUNSUPPORTED,
+                "grf_transpose_banded_fill_staged: band_width must be a multiple of 64");
+    GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL,
+                "grf_transpose_banded_fill_staged: t_rec must be 128-byte aligned");
+    const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
+    const int32_t cr = tr_region_cols(n_cols);
+    GRF_REQUIRE(cr <= 65536, GRF_EUNSUPPORTED, "grf_transpose_banded_fill_staged: too many columns");
+    const int32_t nreg = (int32_t)cdiv<int64_t>(n_cols, cr);
+    GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,
+                "grf_transpose_banded_fill_staged: workspace too small");
+    GRF_REQUIRE(nnz >= 0 && staging_bytes >= grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz), GRF_EINVAL,
+                "grf_transpose_banded_fill_staged: staging too small (%zu < %zu)", staging_bytes,
+                grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz));
+    hipStream_t st = S(stream);
+    // workspace: [cnt: bucket counts from the plan | row_max | ent_off (nbk + 1) | scan scratch]
+    char *w = (char *)workspace;
+    int32_t *cnt = (int32_t *)w;
+    float *row_max = (float *)(w + tr_align((size_t)nbk * 4));
+    int64_t *ent_off = (int64_t *)(w + 2 * tr_align((size_t)nbk * 4));
+    void *scan_ws = w + 2 * tr_align((size_t)nbk * 4) + tr_align((size_t)(nbk + 1) * 8);
+    char *sg = (char *)staging;
+    uint2 *ent = (uint2 *)sg;
+    double *row_sum = (double *)(sg + tr_align((size_t)nnz * 8));
+    int32_t *tab = (int32_t *)(sg + tr_align((size_t)nnz * 8) + tr_align((size_t)std::max<int64_t>(n_rows, 1) * 8));
+    const int64_t nwg = cdiv<int64_t>(n_rows, kBinRows);
+    float *wg_max = (float *)((char *)tab + tr_align((size_t)std::max<int64_t>(nwg, 1) * (nreg + 1) * 4));
+    const uint2 *desc = reinterpret_cast<const uint2 *>(t_desc);
+    int32_t rc = scan_counts_i32(nbk, cnt, ent_off, scan_ws, scan_ws_bytes(nbk), st);  // entries before each bucket
+    if (rc != GRF_OK) return rc;
+    GRF_CHECK_HIP(hipMemsetAsync(t_maxabs, 0, sizeof(float), st));
+    if (n_rows == 0) return GRF_OK;
+    const size_t lds1 = (size_t)kBinCap * 8 + (size_t)nreg * 4 + (kBinRows + 1 + 8) * 4;
+    GRF_REQUIRE_GRID(nwg, 256, "tr_bin_kernel");
+    tr_bin_kernel<<<(unsigned)nwg, 256, lds1, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr, idx, val, ent, tab,
+                                                    wg_max, row_max, row_sum);
+    GRF_CHECK_LAUNCH("tr_bin_kernel");
+    tr_maxabs_kernel<<<1, 1024, 0, st>>>(nwg, wg_max, t_maxabs);
+    GRF_CHECK_LAUNCH("tr_maxabs_kernel");
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 256), 256, "tr_rowshift_kernel");
+    tr_rowshift_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 256), 256, 0, st>>>(n_rows, row_max, row_sum, t_maxabs,
+                                                                            t_rowshift);
+    GRF_CHECK_LAUNCH("tr_rowshift_kernel");
+    GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));  // fallback cursors
+    const int64_t n_regions = nb * nreg;
+    const size_t lds2 = (size_t)8 * cr + kPlaceCap;
+    GRF_REQUIRE_GRID(n_regions, 256, "tr_place_kernel");
+    tr_place_kernel<<<(unsigned)n_regions, 256, lds2, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr, desc, ent_off,
+                                                            ent, tab, cnt, (unsigned char *)t_rec);
+    GRF_CHECK_LAUNCH("tr_place_kernel");
     return GRF_OK;
 }
 

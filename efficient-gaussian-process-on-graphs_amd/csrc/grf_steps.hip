@@ -44,7 +44,9 @@ __global__ __launch_bounds__(256) void steps_kernel(int64_t m, int32_t norm, int
         key[t] = k;
     }
     __syncthreads();
+#ifndef GRF_EXP_NOSORT
     block_bitonic_sort(key, P);
+#endif
     // contiguous chunk per thread
     const int T = blockDim.x;
     const int per = P >= T ? P / T : 1;
@@ -191,7 +193,9 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         }
     }
     __syncthreads();
+#ifndef GRF_EXP_NOSORT
     block_bitonic_sort(key, P);
+#endif
 
     // ---- step values at (node, step) run heads: loads in walk order from 0.0 (the run is
     //      read 8 keys / loads per LDS round trip; the source's step-0 run is m long)

@@ -279,13 +279,16 @@ class GRFEngine:
         return self.phi(self.steps(slots, norm), f)
 
     # ------------------------------------------------------ sparse utilities
-    def compact(self, rows: PaddedRows, want64: bool = True, want32: bool = True) -> DeviceCSR:
+    def compact(self, rows: PaddedRows, want64: bool = True, want32: bool = True,
+                sync_free: bool = False) -> DeviceCSR:
+        """Compact CSR of padded rows.  sync_free: size the outputs by the padded capacity instead of
+        reading nnz back (no host synchronisation; nnz is read lazily if asked for)."""
         n = rows.n_rows
         ptr = self._empty(n + 1, torch.int64)
         ws = self._ws(self.lib.grf_scan_workspace_bytes(n))
         C.check(self.lib.grf_scan_counts(n, _p(rows.cnt), _p(ptr), _p(ws), ws.numel(), self.stream),
                 "grf_scan_counts")
-        nnz = int(ptr[-1].item())
+        nnz = n * rows.cap if sync_free else int(ptr[-1].item())
         idx = self._empty(nnz, torch.int32)
         v64 = self._empty(nnz, torch.float64) if want64 else None
         v32 = self._empty(nnz, torch.float32) if (want32 and rows.val32 is not None) else None
@@ -293,7 +296,9 @@ class GRFEngine:
                                           _p(rows.val if want64 else None),
                                           _p(rows.val32 if v32 is not None else None), _p(idx), _p(v64),
                                           _p(v32), self.stream), "grf_compact_rows")
-        return DeviceCSR(n, rows.n_cols, ptr, idx, v64, v32, nnz)
+        out = DeviceCSR(n, rows.n_cols, ptr, idx, v64, v32, None if sync_free else nnz)
+        out.nnz_bound = nnz
+        return out
 
     def step_matrices(self, st: StepRows) -> list[DeviceCSR]:
         """Per-step CSR matrices (rows = the sources of this step block)."""
@@ -319,8 +324,12 @@ class GRFEngine:
         return ws
 
     def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH,
-                         counted_ws: Optional[torch.Tensor] = None) -> Banded:
-        """Banded transpose of Phi.  counted_ws: workspace whose bucket counts ``walk_phi`` filled."""
+                         counted_ws: Optional[torch.Tensor] = None, staged: Optional[bool] = None,
+                         nnz_bound: Optional[int] = None) -> Banded:
+        """Banded transpose of Phi.  counted_ws: workspace whose bucket counts ``walk_phi`` filled.
+        staged: two-pass binned fill (default when band_width % 64 == 0) or the atomic fill.
+        nnz_bound: an upper bound of nnz(Phi) (e.g. ``compact(..., sync_free=True)``'s): the record
+        buffer is then sized from bounds and no size is read back (no host synchronisation)."""
         n_rows, n_cols = phi.n_rows, phi.n_cols
         nb = -(-n_rows // band_width)
         nbk = nb * n_cols
@@ -331,19 +340,36 @@ class GRFEngine:
         C.check(self.lib.grf_transpose_banded_plan(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(t_desc),
                                                    int(counted_ws is not None), _p(ws), ws.numel(), self.stream),
                 "grf_transpose_banded_plan")
-        # band starts (first line of bucket (band, 0)) and the total: the Gram kernel addresses a
-        # band's records with 32-bit byte offsets
-        starts = torch.cat([t_desc[0:2 * nbk:2 * n_cols], t_desc[2 * nbk:2 * nbk + 1]]).cpu().numpy()
-        starts = starts.view(np.uint32).astype(np.int64)
-        tail = t_desc[2 * nbk:].cpu().numpy().view(np.uint32).astype(np.int64)
-        lines = int(tail[0] + (tail[1] << 32))
-        starts[-1] = lines
-        if nb and int(np.diff(starts).max(initial=0)) * 128 >= 2 ** 31:
-            raise NotImplementedError("a transpose band holds >= 2 GiB of records; use a smaller band_width")
+        # the Gram kernel addresses a band's records with 32-bit byte offsets.  A bucket of c entries
+        # takes ceil(12 ceil(c / 2) / 128) <= 0.047 c + 1.1 lines, so a band of rows with at most
+        # `row_cap` entries each holds < 6 bw row_cap + 141 n_cols bytes.
+        row_cap = min(n_cols, max(1, -(-(nnz_bound or 0) // max(n_rows, 1)))) if nnz_bound is not None else None
+        if nnz_bound is not None and nb and 6 * band_width * row_cap + 141 * n_cols < 2 ** 31:
+            lines = int(0.047 * nnz_bound + 1.1 * nbk) + 1  # bound: no read-back
+        else:
+            # band starts (first line of bucket (band, 0)) and the total, read back
+            starts = torch.cat([t_desc[0:2 * nbk:2 * n_cols], t_desc[2 * nbk:2 * nbk + 1]]).cpu().numpy()
+            starts = starts.view(np.uint32).astype(np.int64)
+            tail = t_desc[2 * nbk:].cpu().numpy().view(np.uint32).astype(np.int64)
+            lines = int(tail[0] + (tail[1] << 32))
+            starts[-1] = lines
+            if nb and int(np.diff(starts).max(initial=0)) * 128 >= 2 ** 31:
+                raise NotImplementedError("a transpose band holds >= 2 GiB of records; use a smaller band_width")
         t_rec = self._empty(max(lines, 1) * 128, torch.uint8)  # torch allocations are 256-B aligned
-        C.check(self.lib.grf_transpose_banded_fill(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx),
-                                                   _p(phi.val32), _p(t_desc), _p(t_rec), t_rec.numel(), _p(t_max),
-                                                   _p(t_shift), _p(ws), ws.numel(), self.stream), "grf_transpose_banded_fill")
+        if staged is None:
+            staged = band_width % 64 == 0 and os.environ.get("GRF_TRANSPOSE_STAGED", "1") != "0"
+        if staged:
+            nnz = nnz_bound if nnz_bound is not None else phi.nnz
+            sg = self._ws(self.lib.grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz))
+            C.check(self.lib.grf_transpose_banded_fill_staged(
+                n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(t_desc), _p(t_rec),
+                t_rec.numel(), _p(t_max), _p(t_shift), _p(ws), ws.numel(), nnz, _p(sg), sg.numel(), self.stream),
+                "grf_transpose_banded_fill_staged")
+        else:
+            C.check(self.lib.grf_transpose_banded_fill(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx),
+                                                       _p(phi.val32), _p(t_desc), _p(t_rec), t_rec.numel(),
+                                                       _p(t_max), _p(t_shift), _p(ws), ws.numel(), self.stream),
+                    "grf_transpose_banded_fill")
         return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols)
 
     # ----------------------------------------------------------------- Gram

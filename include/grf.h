@@ -192,6 +192,16 @@ int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_w
                                   int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift, void *workspace,
                                   size_t workspace_bytes, grf_stream_t stream);
 size_t grf_transpose_workspace_bytes(int64_t n_buckets);
+/* The same fill in two coalesced passes (entries binned by (band, 128-column region) into
+ * `staging`, then each region's records built in LDS and written whole); band_width must be
+ * a multiple of 64, nnz = ptr[n_rows].  Record order inside a bucket is unspecified in both
+ * fills (the Gram's fixed-point sum does not depend on it). */
+int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
+                                         const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
+                                         int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
+                                         void *workspace, size_t workspace_bytes, int64_t nnz, void *staging,
+                                         size_t staging_bytes, grf_stream_t stream);
+size_t grf_transpose_staging_bytes(int64_t n_rows, int64_t n_cols, int64_t band_width, int64_t nnz);
 
 /* ---------------------------------------------------------------------- Gram
  * Replaces `Phi @ Phi.T` of fast_grf_kernel_general.py:55 (sparse) and :39 (dense).
