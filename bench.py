@@ -29,6 +29,8 @@ for _p in (ROOT, os.path.join(ROOT, "efficient-gaussian-process-on-graphs_amd"))
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+from grf_amd.graphs import er_graph_exact_edges, powerlaw_graph, snap_graph  # noqa: E402,F401
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh -> tools/pmc_summary.py), committed
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
@@ -52,24 +54,29 @@ def pmc_traffic(kernels):
     return total
 
 
-def er_graph_exact_edges(n: int, n_edges: int, seed: int = 0) -> sp.csr_matrix:
-    """Undirected Erdos-Renyi graph with exactly n_edges distinct edges, unit weights, no self-loops."""
-    rng = np.random.default_rng(seed)
-    keys = np.empty(0, np.int64)
-    while keys.size < n_edges:
-        k = n_edges - keys.size
-        u = rng.integers(0, n, int(k * 1.2) + 16)
-        v = rng.integers(0, n, int(k * 1.2) + 16)
-        lo, hi = np.minimum(u, v), np.maximum(u, v)
-        cand = (lo * n + hi)[lo != hi]
-        keys = np.concatenate([keys, cand])
-        _, first = np.unique(keys, return_index=True)
-        keys = keys[np.sort(first)]
-    keys = keys[:n_edges]
-    u, v = keys // n, keys % n
-    A = sp.coo_matrix((np.ones(2 * n_edges), (np.r_[u, v], np.r_[v, u])), shape=(n, n)).tocsr()
-    A.sort_indices()
-    return A
+def make_graph(args):
+    """The adjacency of the configured workload (scipy CSR, unit weights)."""
+    if args.graph == "er":
+        return er_graph_exact_edges(args.n, args.edges, seed=0)
+    if args.graph == "powerlaw":
+        return powerlaw_graph(args.n, args.avg_degree, 2.5, seed=0)
+    return snap_graph(args.graph)
+
+
+def workload_name(args, A):
+    n, nnz = A.shape[0], A.nnz
+    if args.graph == "er":
+        return {"short": f"N={n // 1000}k ER graph" if n % 1000 == 0 else f"N={n} ER graph",
+                "long": f"C4: ER N={n}, {args.edges} undirected edges",
+                "data": "synthetic Erdos-Renyi graph (seed 0), unit weights"}
+    if args.graph == "powerlaw":
+        return {"short": f"N={n // 1000}k power-law graph",
+                "long": f"C5: Chung-Lu power-law N={n}, exponent 2.5, mean degree {nnz / n:.2f} "
+                        f"(max {int(np.diff(A.indptr).max())})",
+                "data": "synthetic Chung-Lu power-law graph (seed 0), unit weights"}
+    return {"short": f"{args.graph} N={n}",
+            "long": f"SNAP {args.graph} social graph shipped with the reference, N={n}, {nnz} adjacency entries",
+            "data": f"real graph: the reference's {args.graph} edge list (tests/golden/snap.npz)"}
 
 
 def diffusion_modulator(L: int, beta: float = 1.0) -> np.ndarray:
@@ -77,8 +84,9 @@ def diffusion_modulator(L: int, beta: float = 1.0) -> np.ndarray:
     return np.array([(-beta) ** l / (2 ** l * math.factorial(l)) for l in range(L)])
 
 
-def cpu_baseline(A, f, m, p, L, budget_rows: int, n_threads: int):
-    """Reference algorithm on the host (C oracle, PCG64 reference stream), bounded sample."""
+def cpu_baseline(A, f, m, p, L, budget_rows: int, n_threads: int, k_rows: int = 0):
+    """Reference algorithm on the host (C oracle, PCG64 reference stream), bounded sample.
+    k_rows: the unit is K rows (Phi of all nodes + k_rows rows of K per step) instead of whole K's."""
     from oracle import oracle as O
 
     n = A.shape[0]
@@ -97,16 +105,18 @@ def cpu_baseline(A, f, m, p, L, budget_rows: int, n_threads: int):
     rows = min(budget_rows, n)
     O.gram_rows(phi, 0, rows, n_threads=n_threads)
     t4 = time.perf_counter()
-    t_full = (t1 - t0) + (t2 - t1) + (t3 - t2) + (t4 - t3) * n / rows
+    target = min(k_rows, n) if k_rows else n
+    t_full = (t1 - t0) + (t2 - t1) + (t3 - t2) + (t4 - t3) * target / rows
     return {
-        "value": 1.0 / t_full,
-        "unit": "K-matrices/s",
+        "value": (target if k_rows else 1.0) / t_full,
+        "unit": "K-rows/s" if k_rows else "K-matrices/s",
         "cores": n_threads,
         "kind": "port",
         "sample": (f"C oracle (reference algorithm: PCG64 stream, {n_threads} chunks) on {n_threads} host threads: "
                    f"full Laplacian+walks+step reduction+Phi ({t3 - t0:.2f} s) + K rows 0..{rows} "
-                   f"({t4 - t3:.2f} s) extrapolated x{n / rows:.1f} to all {n} rows; fp64"),
-        "stages_s": {"laplacian": t1 - t0, "walks": t2 - t1, "phi": t3 - t2, "gram_extrapolated": (t4 - t3) * n / rows},
+                   f"({t4 - t3:.2f} s) extrapolated x{target / rows:.2f} to {target} rows; fp64"),
+        "stages_s": {"laplacian": t1 - t0, "walks": t2 - t1, "phi": t3 - t2,
+                     "gram_extrapolated": (t4 - t3) * target / rows},
     }
 
 
@@ -155,8 +165,8 @@ def main_predict(args):
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     eng = GRFEngine(f"cuda:{local_rank}")
-    n, m, L, p, S = args.n, args.walks, args.length, args.p_halt, args.samples
-    A = er_graph_exact_edges(n, args.edges, seed=0)
+    A = make_graph(args)
+    n, m, L, p, S = A.shape[0], args.walks, args.length, args.p_halt, args.samples
     f = diffusion_modulator(L, 1.0)
     G = eng.laplacian(DeviceCSR.from_scipy(A, eng.device))
     phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42), want64=False)
@@ -213,7 +223,8 @@ def main_predict(args):
     alg = 2 * 8.0 * nnz_tr + elem * S * (n_tr + n + n + 3 * n_tr)
     gathers = 2.0 * nnz_tr * S * elem
     out = {
-        "metric": "GRF pathwise-conditioning posterior sample batches/s (SparseGraphGP.predict, N=100k, 64 samples)",
+        "metric": (f"GRF pathwise-conditioning posterior sample batches/s (SparseGraphGP.predict, "
+                   f"{workload_name(args, A)['short']}, {S} samples)"),
         "value": world * args.steps / t,
         "unit": "posterior-sample-batches/s",
         "n_gpus": world,
@@ -224,8 +235,8 @@ def main_predict(args):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": ("fp64" if elem == 8 else "fp32") + " CG vectors, fp32 Phi",
-        "data": "synthetic Erdos-Renyi graph (seed 0), random targets, torch.randn draws",
-        "config": {"workload": f"C4 predict: ER N={n}, {args.edges} edges, m={m}, L={L}, p_halt={p}; "
+        "data": workload_name(args, A)["data"] + "; random targets, torch.randn draws",
+        "config": {"workload": f"{workload_name(args, A)['long']} predict: m={m}, L={L}, p_halt={p}; "
                                f"{n_tr} train / {n_te} test nodes, n_samples={S}, noise {noise}, cg_tolerance 1",
                    "cg_iterations": its[0], "nnz_phi_train": nnz_tr,
                    "parallelism": f"independent sample batches x{world}"},
@@ -269,11 +280,24 @@ def main():
                     help="rows: K row blocks after a Phi all-gather (default); allreduce: the north star's literal "
                          "option -- per-rank partial K over an inner-dimension slice + bucketed RCCL all-reduce, "
                          "K replicated on every rank (SURVEY.md §8e)")
-    ap.add_argument("--workload", choices=["kernel", "predict"], default="kernel",
-                    help="kernel: K = Phi Phi^T (headline); predict: pathwise-conditioning posterior samples")
+    ap.add_argument("--workload", choices=["kernel", "predict", "c5"], default="kernel",
+                    help="kernel: K = Phi Phi^T (headline); predict: pathwise-conditioning posterior samples; "
+                         "c5: SURVEY.md C5 -- N=1M power-law graph, m=64, Phi + a K row block per GPU")
+    ap.add_argument("--graph", choices=["er", "powerlaw", "facebook", "enron"], default="er",
+                    help="er: Erdos-Renyi with --edges edges (C4); powerlaw: Chung-Lu, exponent 2.5, mean degree "
+                         "--avg-degree (C5); facebook / enron: the reference's shipped social graphs")
+    ap.add_argument("--avg-degree", type=float, default=10.0, help="powerlaw: expected mean degree")
+    ap.add_argument("--k-rows", type=int, default=0,
+                    help="compute only the first R rows of every rank's K row block (0 = all rows); "
+                         "the unit becomes K rows/s")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
     ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
+    if args.workload == "c5":
+        args.n, args.graph, args.walks = 1_000_000, "powerlaw", 64
+        args.k_rows = args.k_rows or 8192
+    if args.graph in ("facebook", "enron"):
+        args.n = None
     if args.workload == "predict":
         return main_predict(args)
 
@@ -293,14 +317,17 @@ def main():
     eng = GRFEngine(f"cuda:{local_rank}")
     dev = eng.device
 
-    n, m, L, p = args.n, args.walks, args.length, args.p_halt
-    A = er_graph_exact_edges(n, args.edges, seed=0)
+    A = make_graph(args)
+    n, m, L, p = A.shape[0], args.walks, args.length, args.p_halt
     f = diffusion_modulator(L, 1.0)
     A_dev = DeviceCSR.from_scipy(A, dev)
     b, e = shard_range(n, rank, world)
     ldk = eng.leading_dim(n)
     allreduce = args.mode == "allreduce"
-    k_rows = n if allreduce else e - b
+    if args.k_rows and allreduce:
+        raise SystemExit("--k-rows applies to the row mode only")
+    kr_end = min(e, b + args.k_rows) if args.k_rows else e  # this rank's K rows [b, kr_end)
+    k_rows = n if allreduce else kr_end - b
     K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     last = [None]
@@ -325,10 +352,10 @@ def main():
             ev[0].record()
         if allreduce:
             eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
-        elif world == 1 and not args.no_sym:
+        elif world == 1 and not args.no_sym and not args.k_rows:
             eng.gram_sparse_sym(phi, tr, out=K)  # upper band tiles + mirror
         else:
-            eng.gram_sparse(phi, tr, b, e, out=K)
+            eng.gram_sparse(phi, tr, b, kr_end, out=K)
         if record:
             ev[1].record()
             gram_ev.append(ev)
@@ -364,33 +391,45 @@ def main():
     local_nnz = last[0][1].nnz
     # algorithmic bytes of the K assembly (gram_sparse_kernel [+ gram_mirror_kernel]): write this
     # rank's K rows once, read its Phi rows (col int32 + val fp32) and every Phi^T entry once
-    rows = e - b
-    alg_bytes = 4.0 * rows * n + 8.0 * local_nnz + 8.0 * nnz_phi[0]
+    rows = kr_end - b
+    alg_bytes = 4.0 * rows * n + 8.0 * local_nnz * rows / max(e - b, 1) + 8.0 * nnz_phi[0]
     if allreduce:  # every K entry written; all of Phi scanned, the slice's share of Phi^T read
         alg_bytes = 4.0 * n * n + 8.0 * nnz_phi[0] + 8.0 * nnz_phi[0] * rows / n
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
-    sym = world == 1 and not args.no_sym and not allreduce
+    sym = world == 1 and not args.no_sym and not allreduce and not args.k_rows
     kernels = ["grf::gram_sparse_kernel", "grf::gram_mirror_kernel"] if sym else ["grf::gram_sparse_kernel"]
     traffic = None
-    if (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and world == 1 and not allreduce:
+    if (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and args.graph == "er" and world == 1 and sym:
         traffic = pmc_traffic(kernels)
+    wl = workload_name(args, A)
+    if args.k_rows:
+        metric = (f"GRF kernel rows/sec ({wl['short']}, m={m} walks: Phi of all N nodes + a {args.k_rows}-row "
+                  f"fp32 K block per GPU, every step)")
+        unit, value, scaling = "K-rows/s", world * rows * args.steps / t, "weak"
+    else:
+        metric = "GRF kernel-matrices/sec (N=100k graph, m=128 walks; + achieved HBM GB/s of the Gram kernel)"
+        if args.graph != "er" or (n, args.edges, m, L, p) != DEFAULT_WORKLOAD:
+            metric = f"GRF kernel-matrices/sec ({wl['short']}, m={m} walks; + achieved HBM GB/s of the Gram kernel)"
+        unit, value, scaling = "K-matrices/s", args.steps / t, "strong"
     out = {
-        "metric": "GRF kernel-matrices/sec (N=100k graph, m=128 walks; + achieved HBM GB/s of the Gram kernel)",
-        "value": args.steps / t,
-        "unit": "K-matrices/s",
+        "metric": metric,
+        "value": value,
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "fp64 walks/Phi, fp32 K",
-        "data": "synthetic Erdos-Renyi graph (seed 0), unit weights",
-        "config": {"workload": f"C4: ER N={n}, {args.edges} undirected edges, walks_per_node={m}, "
-                               f"max_walk_length={L}, p_halt={p}, diffusion modulator beta=1, Philox seed 42, "
-                               f"dense fp32 K resident in HBM",
-                   "n_nodes": n, "n_edges": args.edges, "walks_per_node": m, "max_walk_length": L,
+        "data": wl["data"],
+        "config": {"workload": f"{wl['long']}, walks_per_node={m}, max_walk_length={L}, p_halt={p}, diffusion "
+                               f"modulator beta=1, Philox seed 42, dense fp32 K "
+                               + (f"rows [r0, r0+{args.k_rows}) of every rank's block" if args.k_rows else "")
+                               + " resident in HBM",
+                   "n_nodes": n, "n_edges": int(A.nnz // 2), "walks_per_node": m, "max_walk_length": L,
+                   "k_rows_per_gpu": rows,
                    "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
                                    f"RCCL all-reduce (K replicated)") if allreduce else
                                   f"source-sharded x{world}, Phi all-gather, K row blocks"},
@@ -405,7 +444,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(A, f, m, p, L, args.cpu_rows, threads)
+        out["cpu_baseline"] = cpu_baseline(A, f, m, p, L, args.cpu_rows, threads, k_rows=args.k_rows)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -22,3 +22,16 @@ def digest(M) -> str:
     for x in (np.asarray(M.indptr, np.int64), np.asarray(M.indices, np.int32), np.asarray(M.data, np.float64)):
         h.update(np.ascontiguousarray(x).tobytes())
     return h.hexdigest()
+
+
+def snap_adjacency(d, name):
+    """Unit-weight CSR adjacency of a SNAP fixture (tests/golden/make_snap.py)."""
+    ip, ix = d[name + "_indptr"], d[name + "_indices"]
+    n = len(ip) - 1
+    return sp.csr_matrix((np.ones(len(ix)), ix, ip), shape=(n, n))
+
+
+def snap_k_rows(d, name, n):
+    """The fixture's K rows (the reference's fp64 Phi[rows] Phi^T) as a dense array."""
+    ip, ix, dx = d[name + "_K_rows_indptr"], d[name + "_K_rows_indices"], d[name + "_K_rows_data"]
+    return sp.csr_matrix((dx, ix, ip), shape=(len(ip) - 1, n)).toarray()

@@ -395,3 +395,87 @@ def test_walk_phi_fused_bitexact(eng, n, deg, m, L, p, rule):
     K1 = eng.gram_sparse(phi, eng.transpose_banded(phi, bw, counted_ws=ws)).cpu().numpy()
     K2 = eng.gram_sparse(phi, eng.transpose_banded(phi, bw)).cpu().numpy()
     assert np.array_equal(K1, K2)
+
+
+# ------------------------------------------------- real graphs
+def _diffusion(L):
+    return np.array([(-1.0) ** l / (2.0 ** l * float(np.prod(np.arange(1, l + 1)))) for l in range(L)])
+
+
+def _k_bound_close(Krows, phi64, rows, Kref):
+    """|dK| <= 3e-5 (|Phi||Phi|^T) + the fixed-point resolution, on selected rows."""
+    absphi = abs(phi64)
+    bound = (absphi[rows] @ absphi.T).toarray()
+    rowmax = np.asarray(absphi.max(axis=1).todense()).ravel()
+    fx = 1e-12 * np.maximum(rowmax[rows][:, None], rowmax[None, :]) * absphi.max()
+    err = np.abs(np.asarray(Krows, np.float64) - Kref)
+    return bool(np.all(err <= 3e-5 * bound + fx + 1e-30)), float(err.max())
+
+
+@pytest.mark.parametrize("name", ["facebook", "enron"])
+def test_snap_graph_reference_stream(eng, golden, name):
+    """Facebook / Enron (self-loops, heavy-tailed degrees): Laplacian, the 8 step matrices and Phi
+    bit-identical to the reference's own sparse path; K rows (hubs included) within tolerance."""
+    from golden_util import digest, snap_adjacency, snap_k_rows
+    d = golden("snap")
+    A = snap_adjacency(d, name)
+    n = A.shape[0]
+    m, p, L = (int(d[f"{name}_walk"][0]), float(d[f"{name}_walk"][1]), int(d[f"{name}_walk"][2]))
+    G = eng.laplacian(A)
+    assert digest(G.to_scipy()) == str(d[f"{name}_L_digest"][0])
+    slots = eng.walk(G, m, p, L, rng=0, seed=42, n_chunks=8)
+    mats = eng.step_matrices(eng.steps(slots, norm=1))
+    assert [digest(M.to_scipy()) for M in mats] == [str(x) for x in d[f"{name}_step_digests"]]
+    phi = eng.compact(eng.features(slots, _diffusion(L)))
+    phi64 = phi.to_scipy()
+    assert digest(phi64) == str(d[f"{name}_phi_digest"][0])
+    rows = d[f"{name}_K_rows"].astype(np.int64)
+    K = eng.gram(phi, "sparse")
+    import torch
+    Kr = K[torch.from_numpy(rows).to(K.device)].cpu().numpy()
+    ok, e = _k_bound_close(Kr, phi64, rows, snap_k_rows(d, name, n))
+    assert ok, e
+    diag = K.diagonal().cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(diag, d[f"{name}_K_diag"], rtol=3e-5)
+    del K
+
+
+@pytest.mark.parametrize("name", ["enron", "powerlaw"])
+def test_bench_path_heavy_tailed_graphs(eng, golden, name):
+    """The bench's path (fused Philox walk -> Phi with bucket counting, sync-free compaction, staged
+    transpose, symmetric Gram + mirror) on heavy-tailed graphs -- the real Enron graph and a C5-style
+    Chung-Lu power-law graph: Phi bit-exact against the oracle, K exactly symmetric, the symmetric
+    and row modes bit-identical, rows (hubs included) within tolerance."""
+    import torch
+    from golden_util import snap_adjacency
+    from grf_amd.engine import DEFAULT_BAND_WIDTH
+    from grf_amd.graphs import powerlaw_graph
+    A = snap_adjacency(golden("snap"), name) if name != "powerlaw" else powerlaw_graph(50_000, 10.0, 2.5, seed=3)
+    n = A.shape[0]
+    m, p, L = 64, 0.1, 8
+    f = _diffusion(L)
+    G = eng.laplacian(A)
+    tws = eng.transpose_workspace(n, n)
+    rows_p = eng.walk_phi(G, m, p, L, f, seed=42, count_ws=tws, band_width=DEFAULT_BAND_WIDTH)
+    phi = eng.compact(rows_p, want64=True, want32=True, sync_free=True)
+    Ls, _ = O.laplacian_sparse(A)
+    ip, ix, dx = O._csr_arrays(Ls)
+    node, load = O.walk_slots(ip, ix, dx, m, p, L, rng=O.RNG_PHILOX, seed=42)
+    ref_phi = O.phi_sparse(O.reduce_steps(node, load, O.NORM_MUL_RECIP), f)
+    phi64 = phi.to_scipy()
+    assert same_csr(phi64, ref_phi)
+    tr = eng.transpose_banded(phi, counted_ws=tws, nnz_bound=phi.nnz_bound)
+    K = eng.gram_sparse_sym(phi, tr)
+    sample = np.r_[0, 1, np.argsort(-np.diff(A.indptr), kind="stable")[:4], n - 1].astype(np.int64)
+    si = torch.from_numpy(sample).to(K.device)
+    Ks = K[si].cpu().numpy()
+    ok, e = _k_bound_close(Ks, ref_phi, sample, (ref_phi[sample] @ ref_phi.T).toarray())
+    assert ok, e
+    assert torch.equal(K[:, :2048][:2048], K[:2048, :2048].t())  # exact symmetry (a diagonal block)
+    assert torch.equal(K[si, :].t().contiguous(), K[:, si].contiguous())
+    # row mode = symmetric mode on and above the diagonal (the mirror carries the upper triangle)
+    for r0, r1 in ((0, 4096), (n - 5000, n)):
+        Kr = eng.gram_sparse(phi, tr, r0, r1)
+        up = torch.triu(torch.ones(r1 - r0, n, dtype=torch.bool, device=K.device), diagonal=r0)
+        assert torch.equal(Kr[up], K[r0:r1][up])
+    del K, Kr

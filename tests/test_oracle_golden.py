@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
-from golden_util import csr, digest, same_csr
+from golden_util import csr, digest, same_csr, snap_adjacency, snap_k_rows
 from oracle import oracle as O
 
 
@@ -160,3 +160,24 @@ def test_philox_walk_is_deterministic_and_chunk_free(rule):
     b = O.walk_slots(ip, ix, dx, 16, 0.2, 5, rng=O.RNG_PHILOX, load_rule=rule, seed=9, n_threads=8)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
     assert (a[0][:, 0, :] == np.arange(50)[:, None]).all()
+
+
+@pytest.mark.parametrize("name", ["facebook", "enron"])
+def test_snap_graphs(golden, name):
+    """Real social graphs the reference ships: the oracle reproduces the reference's
+    Laplacian, step matrices and Phi bit-exactly (8 chunks), and its K rows (tests/golden/make_snap.py)."""
+    d = golden("snap")
+    A = snap_adjacency(d, name)
+    m, p, L = d[f"{name}_walk"]
+    Lc, _ = O.laplacian_sparse(A)
+    assert digest(Lc) == str(d[f"{name}_L_digest"][0])
+    mats = O.sparse_random_walk(Lc, int(m), float(p), int(L), n_processes=8)
+    assert [digest(M) for M in mats] == [str(x) for x in d[f"{name}_step_digests"]]
+    f = np.array([(-1.0) ** l / (2.0 ** l * float(np.prod(np.arange(1, l + 1)))) for l in range(int(L))])
+    phi = O.phi_sparse(mats, f)
+    assert digest(phi) == str(d[f"{name}_phi_digest"][0])
+    rows = d[f"{name}_K_rows"]
+    Kref = snap_k_rows(d, name, A.shape[0])
+    for i, r in enumerate(rows):
+        np.testing.assert_allclose(O.gram_rows(phi, int(r), int(r) + 1)[0], Kref[i], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(np.asarray(phi.multiply(phi).sum(axis=1)).ravel(), d[f"{name}_K_diag"], rtol=1e-12)
