@@ -83,47 +83,77 @@ __global__ void lap_deg_kernel(int64_t n, const int64_t *ptr, const double *val,
     dinv[i] = isinf(v) ? 0.0 : v;
 }
 
-// One row of D^-1/2 (D - A) D^-1/2 in scipy order.  EMIT=false counts.
+// One row of D^-1/2 (D - A) D^-1/2 in scipy order, one wave per row (a power-law hub row of
+// thousands of entries is spread over the 64 lanes instead of serialising one thread).
+// The row's virtual sequence is A's entries in column order with the diagonal merged into an
+// explicit (i, i) entry (value d - a_ii) or inserted before the first column > i (value d);
+// sp.diags drops a zero diagonal, so d == 0 inserts nothing and an explicit a_ii stays -a_ii.
+// Every element is computed independently with the serial code's exact arithmetic
+// (u = (dinv_i v) dinv_j, exact zeros dropped), then compacted in order by ballot counts.
+// EMIT=false counts.
 template <bool EMIT>
-__global__ void lap_row_kernel(int64_t n, const int64_t *ptr, const int32_t *idx, const double *val,
-                               const double *deg, const double *dinv, int32_t *cnt, const int64_t *l_ptr,
-                               int32_t *l_idx, double *l_val, int64_t l_cap) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void lap_row_kernel(int64_t n, const int64_t *ptr, const int32_t *idx,
+                                                      const double *val, const double *deg, const double *dinv,
+                                                      int32_t *cnt, const int64_t *l_ptr, int32_t *l_idx,
+                                                      double *l_val, int64_t l_cap) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
+    const int lane = threadIdx.x & 63;
     const double d = deg[i], di = dinv[i];
-    int64_t a = ptr[i];
-    const int64_t ae = ptr[i + 1];
-    bool diag_done = (d == 0.0);  // sp.diags drops a zero diagonal
+    const int64_t b = ptr[i], e = ptr[i + 1];
+    // first entry with column >= i (columns ascending)
+    int64_t lo = b, hi = e;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (idx[mid] < i) lo = mid + 1;
+        else hi = mid;
+    }
+    const int64_t pd = lo - b;  // position of the diagonal in the virtual sequence
+    const bool has_diag = d != 0.0;
+    const bool expl = lo < e && idx[lo] == i;
+    const bool insert = has_diag && !expl;
+    const int64_t total = (e - b) + (insert ? 1 : 0);
     int64_t out = EMIT ? l_ptr[i] : 0;
     int32_t c = 0;
-    for (;;) {
-        int64_t col;
-        double v;
-        if (!diag_done && (a >= ae || idx[a] > i)) {
-            col = i; v = d; diag_done = true;
-        } else if (a < ae) {
-            col = idx[a];
-            if (!diag_done && col == i) { v = d - val[a]; diag_done = true; }
-            else v = 0.0 - val[a];
-            ++a;
-        } else {
-            break;
+    for (int64_t base = 0; base < total; base += 64) {
+        const int64_t k = base + lane;
+        bool keep = false;
+        int64_t col = 0;
+        double u = 0.0;
+        if (k < total) {
+            double v;
+            if (insert && k == pd) {
+                col = i;
+                v = d;
+            } else {
+                const int64_t a = b + ((insert && k > pd) ? k - 1 : k);
+                col = idx[a];
+                v = (has_diag && col == i) ? d - val[a] : 0.0 - val[a];
+            }
+            if (v != 0.0 && di != 0.0) {
+                const double t = di * v;
+                if (t != 0.0) {
+                    const double dj = dinv[col];
+                    if (dj != 0.0) {
+                        u = t * dj;
+                        keep = u != 0.0;
+                    }
+                }
+            }
         }
-        if (v == 0.0 || di == 0.0) continue;
-        double t = di * v;
-        if (t == 0.0) continue;
-        double dj = dinv[col];
-        if (dj == 0.0) continue;
-        double u = t * dj;
-        if (u == 0.0) continue;
+        const uint64_t m = __ballot(keep);
         if (EMIT) {
-            if (out < l_cap) { l_idx[out] = (int32_t)col; l_val[out] = u; }
-            ++out;
+            const int64_t o = out + __popcll(m & ((1ull << lane) - 1ull));
+            if (keep && o < l_cap) {
+                l_idx[o] = (int32_t)col;
+                l_val[o] = u;
+            }
+            out += __popcll(m);
         } else {
-            ++c;
+            c += __popcll(m);
         }
     }
-    if (!EMIT) cnt[i] = c;
+    if (!EMIT && lane == 0) cnt[i] = c;
 }
 
 // ------------------------------------------------------------------- dense
@@ -214,13 +244,14 @@ int32_t grf_laplacian_csr(int64_t n, const int64_t *a_ptr, const int32_t *a_idx,
     GRF_REQUIRE_GRID(g, 256, "lap_deg_kernel");
     lap_deg_kernel<<<g, 256, 0, st>>>(n, a_ptr, a_val, deg, dinv);
     GRF_CHECK_LAUNCH("lap_deg_kernel");
-    GRF_REQUIRE_GRID(g, 256, "lap_row_kernel");
-    lap_row_kernel<false><<<g, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
+    const unsigned gw = (unsigned)cdiv<int64_t>(n, 4);  // one wave per row
+    GRF_REQUIRE_GRID(gw, 256, "lap_row_kernel");
+    lap_row_kernel<false><<<gw, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
     GRF_CHECK_LAUNCH("lap_row_kernel<count>");
     int32_t rc = scan_counts_i32(n, cnt, l_ptr, (char *)workspace + cnt_bytes, workspace_bytes - cnt_bytes, st);
     if (rc != GRF_OK) return rc;
-    GRF_REQUIRE_GRID(g, 256, "lap_row_kernel");
-    lap_row_kernel<true><<<g, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
+    GRF_REQUIRE_GRID(gw, 256, "lap_row_kernel");
+    lap_row_kernel<true><<<gw, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
     GRF_CHECK_LAUNCH("lap_row_kernel<fill>");
     return GRF_OK;
 }
