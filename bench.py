@@ -305,7 +305,7 @@ def main():
     import torch.distributed as dist
 
     from grf_amd import _lib as C
-    from grf_amd.dist import allgather_csr_rows, allreduce_buckets, shard_range
+    from grf_amd.dist import allreduce_buckets, gather_phi, shard_range
     from grf_amd.engine import DEFAULT_BAND_WIDTH, DeviceCSR, GRFEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -329,24 +329,22 @@ def main():
     kr_end = min(e, b + args.k_rows) if args.k_rows else e  # this rank's K rows [b, kr_end)
     k_rows = n if allreduce else kr_end - b
     K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
+    rows_cap = max(1, min(m * L, n))  # walk_phi's padded row capacity
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     last = [None]
 
     def step(record: bool):
         G = eng.laplacian(A_dev)
         # Philox walks of this rank's sources straight to Phi rows (one kernel, no slot round trip);
-        # on one GPU the same kernel counts the banded transpose's buckets
-        tws = eng.transpose_workspace(n, n) if world == 1 else None
+        # the same kernel counts this rank's buckets of the banded transpose (summed over the ranks
+        # by one all-reduce in gather_phi)
+        tws = eng.transpose_workspace(n, n)
         local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
-                                         band_width=DEFAULT_BAND_WIDTH if tws is not None else 0),
+                                         band_width=DEFAULT_BAND_WIDTH),
                             want64=False, want32=True, sync_free=world == 1)
-        if world > 1:
-            ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32)
-            phi = DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))
-        else:
-            phi = local
-        # (one GPU: sizes from bounds, no host round trip inside the step)
-        tr = eng.transpose_banded(phi, counted_ws=tws, nnz_bound=local.nnz_bound if world == 1 else None)
+        phi = gather_phi(eng, local, tws) if world > 1 else local
+        # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
+        tr = eng.transpose_banded(phi, counted_ws=tws, nnz_bound=n * rows_cap)
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()

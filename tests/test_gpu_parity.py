@@ -479,3 +479,46 @@ def test_bench_path_heavy_tailed_graphs(eng, golden, name):
         up = torch.triu(torch.ones(r1 - r0, n, dtype=torch.bool, device=K.device), diagonal=r0)
         assert torch.equal(Kr[up], K[r0:r1][up])
     del K, Kr
+
+
+def test_sharded_counts_and_phi_equal_single_gpu(eng):
+    """The multi-GPU assembly, emulated in one process: per-shard fused walk -> Phi with bucket
+    counting, counts summed (the all-reduce of dist.gather_phi) and rows concatenated (the
+    all-gather) give the single-GPU transpose bit for bit, and the row-block Grams match K."""
+    import torch
+    from grf_amd.dist import shard_range
+    from grf_amd.engine import DEFAULT_BAND_WIDTH, DeviceCSR
+    n = 20000
+    A = er_graph(n, 10, 11)
+    G = eng.laplacian(A)
+    m, L = 32, 6
+    f = [1.0, -0.5, 0.125, -0.02, 0.003, -0.0004]
+    nbk = -(-n // DEFAULT_BAND_WIDTH) * n
+    ws1 = eng.transpose_workspace(n, n)
+    one = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=5, count_ws=ws1, band_width=DEFAULT_BAND_WIDTH),
+                      want64=False)
+    cnt1 = ws1[:4 * nbk].clone()  # (the transpose reuses its workspace)
+    tr1 = eng.transpose_banded(one, counted_ws=ws1, nnz_bound=n * m * L)
+    K1 = eng.gram_sparse(one, tr1)
+    world = 3
+    wsum = eng.transpose_workspace(n, n)
+    parts = []
+    for r in range(world):
+        b, e = shard_range(n, r, world)
+        ws = eng.transpose_workspace(n, n)
+        loc = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=5, src_begin=b, src_end=e, count_ws=ws,
+                                       band_width=DEFAULT_BAND_WIDTH), want64=False)
+        wsum[:4 * nbk].view(torch.int32).add_(ws[:4 * nbk].view(torch.int32))
+        parts.append(loc)
+    cnt = torch.cat([p.ptr[1:] - p.ptr[:-1] for p in parts])
+    ptr = torch.zeros(n + 1, dtype=torch.int64, device=cnt.device)
+    ptr[1:] = torch.cumsum(cnt, 0)
+    phi = DeviceCSR(n, n, ptr, torch.cat([p.idx[:p.nnz] for p in parts]), None,
+                    torch.cat([p.val32[:p.nnz] for p in parts]), int(ptr[-1].item()))
+    assert torch.equal(wsum[:4 * nbk], cnt1)
+    assert torch.equal(phi.ptr, one.ptr) and torch.equal(phi.idx, one.idx[:one.nnz])
+    tr = eng.transpose_banded(phi, counted_ws=wsum, nnz_bound=n * m * L)
+    assert torch.equal(tr.t_desc, tr1.t_desc) and torch.equal(tr.t_rowshift, tr1.t_rowshift)
+    for r in range(world):
+        b, e = shard_range(n, r, world)
+        assert torch.equal(eng.gram_sparse(phi, tr, b, e), K1[b:e])

@@ -128,6 +128,40 @@ def _allreduce_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _gather_phi_worker(rank, world, port, q):
+    """gather_phi: Phi rows all-gathered and the per-rank bucket counts summed in place."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import scipy.sparse as sp
+        from grf_amd.dist import gather_phi, shard_range
+        from grf_amd.engine import DEFAULT_BAND_WIDTH, DeviceCSR
+        n = 5000
+        full = sp.random(n, n, density=0.002, random_state=7, format="csr", dtype=np.float32)
+        full.sort_indices()
+        b, e = shard_range(n, rank, world)
+        part = full[b:e]
+        local = DeviceCSR(e - b, n, torch.from_numpy(part.indptr.astype(np.int64)),
+                          torch.from_numpy(part.indices.astype(np.int32)), None,
+                          torch.from_numpy(part.data.astype(np.float32)), int(part.nnz))
+        nbk = -(-n // DEFAULT_BAND_WIDTH) * n
+        cnt = np.zeros(nbk + 16, np.int32)  # (the workspace is longer than its count head)
+        rows = np.repeat(np.arange(b, e), np.diff(part.indptr))
+        np.add.at(cnt, (rows // DEFAULT_BAND_WIDTH) * n + part.indices, 1)
+        ws = torch.from_numpy(cnt.view(np.uint8).copy())
+        phi = gather_phi(None, local, ws)
+        want = np.zeros(nbk, np.int64)
+        allrows = np.repeat(np.arange(n), np.diff(full.indptr))
+        np.add.at(want, (allrows // DEFAULT_BAND_WIDTH) * n + full.indices, 1)
+        got = ws.numpy().view(np.int32)
+        ok = (np.array_equal(phi.ptr.numpy(), full.indptr) and np.array_equal(phi.idx.numpy(), full.indices)
+              and np.array_equal(phi.val32.numpy(), full.data) and np.array_equal(got[:nbk], want)
+              and np.array_equal(got[nbk:], cnt[nbk:]))
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
 def _spawn(target, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -144,6 +178,11 @@ def _spawn(target, world):
 @pytest.mark.parametrize("world", [2, 3])
 def test_allreduce_buckets_gloo(world):
     assert _spawn(_allreduce_worker, world) == [(r, True) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_phi_sums_bucket_counts_gloo(world):
+    assert _spawn(_gather_phi_worker, world) == [(r, True) for r in range(world)]
 
 
 @pytest.mark.parametrize("world", [2, 3])
