@@ -310,7 +310,7 @@ def main():
 
     from grf_amd import _lib as C
     from grf_amd.dist import allreduce_buckets, gather_phi, shard_range
-    from grf_amd.engine import DEFAULT_BAND_WIDTH, DeviceCSR, GRFEngine
+    from grf_amd.engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, DeviceCSR, GRFEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -334,6 +334,8 @@ def main():
     k_rows = n if allreduce else kr_end - b
     K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
     rows_cap = max(1, min(m * L, n))  # walk_phi's padded row capacity
+    sym_mode = world == 1 and not args.no_sym and not args.k_rows and not allreduce
+    bw = DEFAULT_BAND_WIDTH if sym_mode else ROWS_BAND_WIDTH  # (engine.py: measured per mode)
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     last = [None]
 
@@ -346,13 +348,13 @@ def main():
         # Philox walks of this rank's sources straight to Phi rows (one kernel, no slot round trip);
         # the same kernel counts this rank's buckets of the banded transpose (summed over the ranks
         # by one all-reduce in gather_phi)
-        tws = eng.transpose_workspace(n, n)
+        tws = eng.transpose_workspace(n, n, bw)
         local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
-                                         band_width=DEFAULT_BAND_WIDTH),
+                                         band_width=bw),
                             want64=False, want32=True, sync_free=world == 1)
-        phi = gather_phi(eng, local, tws) if world > 1 else local
+        phi = gather_phi(eng, local, tws, band_width=bw) if world > 1 else local
         # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
-        tr = eng.transpose_banded(phi, counted_ws=tws, nnz_bound=n * rows_cap)
+        tr = eng.transpose_banded(phi, bw, counted_ws=tws, nnz_bound=n * rows_cap)
         return phi, tr, local
 
     def back(fr, record: bool):
@@ -363,7 +365,7 @@ def main():
             ev[0].record()
         if allreduce:
             eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
-        elif world == 1 and not args.no_sym and not args.k_rows:
+        elif sym_mode:
             eng.gram_sparse_sym(phi, tr, out=K)  # upper band tiles + mirror
         else:
             eng.gram_sparse(phi, tr, b, kr_end, out=K)
@@ -449,7 +451,7 @@ def main():
     if allreduce:  # every K entry written; all of Phi scanned, the slice's share of Phi^T read
         alg_bytes = 4.0 * n * n + 8.0 * nnz_phi[0] + 8.0 * nnz_phi[0] * rows / n
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
-    sym = world == 1 and not args.no_sym and not allreduce and not args.k_rows
+    sym = sym_mode
     kernels = ["grf::gram_sparse_kernel", "grf::gram_mirror_kernel"] if sym else ["grf::gram_sparse_kernel"]
     traffic = None
     if (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and args.graph == "er" and world == 1 and sym:

@@ -235,7 +235,7 @@ struct GramTiles {
 // id (bucket-start markers propagated by a running maximum, one LDS read); the gathers of kGramUnroll
 // windows of 64 pairs are in flight together.  Tiles are dispatched band-major, so the
 // tiles in flight share one band's records (L2 / Infinity Cache).
-template <int kWaves, int kHalves, int kGramUnroll>
+template <int kWaves, int kHalves, int kGramUnroll, bool kTailExact>
 __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
@@ -313,7 +313,24 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             int32_t w0 = c0;
             for (; w0 + 64 * kGramUnroll <= cend; w0 += 64 * kGramUnroll)
                 gram_windows<kGramUnroll, false>(gs, w0, c0, cend, lane);
-            if (w0 < cend) gram_windows<kGramUnroll, true>(gs, w0, c0, cend, lane);  // masked last group
+            if (w0 < cend) {
+                // last group: exactly the windows left (a group of kGramUnroll would issue up to
+                // kGramUnroll - 1 all-masked windows of loads and LDS adds per batch)
+                if (kTailExact) {
+                    switch ((cend - w0 + 63) >> 6) {
+                        case 1: gram_windows<1, true>(gs, w0, c0, cend, lane); break;
+                        case 2: gram_windows<2, true>(gs, w0, c0, cend, lane); break;
+                        case 3: gram_windows<3, true>(gs, w0, c0, cend, lane); break;
+                        case 4: gram_windows<4, true>(gs, w0, c0, cend, lane); break;
+                        case 5: gram_windows<kGramUnroll < 5 ? kGramUnroll : 5, true>(gs, w0, c0, cend, lane); break;
+                        case 6: gram_windows<kGramUnroll < 6 ? kGramUnroll : 6, true>(gs, w0, c0, cend, lane); break;
+                        case 7: gram_windows<kGramUnroll < 7 ? kGramUnroll : 7, true>(gs, w0, c0, cend, lane); break;
+                        default: gram_windows<kGramUnroll, true>(gs, w0, c0, cend, lane); break;
+                    }
+                } else {
+                    gram_windows<kGramUnroll, true>(gs, w0, c0, cend, lane);  // masked last group
+                }
+            }
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -476,21 +493,30 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
                                  int64_t ldk, hipStream_t st) {
     // tuning knobs (defaults = measured best on MI355X): gathers in flight per wave, waves per tile
     static const int knobs = [] {
-        const char *e = getenv("GRF_GRAM_UNROLL"), *w = getenv("GRF_GRAM_WAVES");
-        const int u = e ? atoi(e) : 8, ww = w ? atoi(w) : 4;
-        return ((u == 4 || u == 8 || u == 16) ? u : 8) * 10 + (ww == 8 ? 8 : 4);
+        const char *e = getenv("GRF_GRAM_UNROLL"), *w = getenv("GRF_GRAM_WAVES"), *t = getenv("GRF_GRAM_TAIL");
+        const int u = e ? atoi(e) : 8, ww = w ? atoi(w) : 0, tt = t ? atoi(t) : 1;
+        return (tt ? 1000 : 0) + ((u == 4 || u == 8 || u == 16) ? u : 8) * 10 + (ww == 8 ? 8 : ww == 4 ? 4 : 0);
     }();
-    const int unroll = knobs / 10, waves = knobs % 10, halves = waves == 8 ? 1 : 2;
+    const bool tail_exact = knobs >= 1000;
+    // waves per tile: 4 for W <= 4096 (4 tiles of 40 KiB per CU), 8 for wider bands (2 tiles of
+    // 76 KiB per CU: 16 waves per CU either way); measured best at both widths (GRF_GRAM_WAVES overrides)
+    const int waves = knobs % 10 ? knobs % 10 : (tl.W > 4096 ? 8 : 4);
+    const int unroll = (knobs % 1000) / 10, halves = waves == 8 ? 1 : 2;
     const size_t lds = gram_lds_bytes(tl.W, waves, halves);
     // one launch covers at most 2^32 - 1 work-items: split the tile range
     const int64_t max_tiles = ((1ll << 32) - 1) / (64 * waves);
     for (int64_t t0 = t_first; t0 < t_last; t0 += max_tiles) {
         const int64_t nt = (t_last - t0) < max_tiles ? (t_last - t0) : max_tiles;
-#define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
-    gram_sparse_kernel<WV, H, U><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx, val,   \
+#define GRF_GRAM_LAUNCH_T(WV, H, U, T)                                                                            \
+    gram_sparse_kernel<WV, H, U, T><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx, val,\
                                                                      reinterpret_cast<const uint2 *>(t_desc),     \
                                                                      reinterpret_cast<const unsigned char *>(t_rec), \
                                                                      t_rowshift, K, ldk)
+#define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
+    do {                                                                                                          \
+        if (tail_exact) GRF_GRAM_LAUNCH_T(WV, H, U, true);                                                        \
+        else GRF_GRAM_LAUNCH_T(WV, H, U, false);                                                                  \
+    } while (0)
         if (waves == 8) {
             if (unroll == 4) GRF_GRAM_LAUNCH(8, 1, 4);
             else GRF_GRAM_LAUNCH(8, 1, 8);
@@ -500,6 +526,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
             else GRF_GRAM_LAUNCH(4, 2, 8);
         }
 #undef GRF_GRAM_LAUNCH
+#undef GRF_GRAM_LAUNCH_T
         GRF_CHECK_LAUNCH("gram_sparse_kernel");
     }
     return GRF_OK;

@@ -79,19 +79,19 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
     return full_ptr, torch.cat(parts_i), torch.cat(parts_v)
 
 
-def gather_phi(engine, local, count_ws=None, group=None):
+def gather_phi(engine, local, count_ws=None, group=None, band_width=None):
     """All ranks' Phi rows (CSR, float32) from this rank's compacted rows ``local``.
 
     count_ws: this rank's transpose workspace in which ``walk_phi`` counted the banded transpose's
-    buckets for its own rows (global band ids).  The per-rank counts are summed in place with one
-    all-reduce (n_bands * n int32, 10 MB at N = 100k), so the caller's ``transpose_banded(...,
-    counted_ws=count_ws)`` skips the counting pass over the gathered Phi -- the same workspace a
-    single GPU's fused count leaves."""
+    buckets for its own rows (global band ids, bands of ``band_width``).  The per-rank counts are
+    summed in place with one all-reduce (n_bands * n int32, 5-10 MB at N = 100k), so the caller's
+    ``transpose_banded(..., counted_ws=count_ws)`` skips the counting pass over the gathered Phi --
+    the same workspace a single GPU's fused count leaves."""
     from .engine import DEFAULT_BAND_WIDTH, DeviceCSR
 
     n = local.n_cols
     if count_ws is not None and dist.get_world_size(group) > 1:
-        nbk = -(-n // DEFAULT_BAND_WIDTH) * n
+        nbk = -(-n // (band_width or DEFAULT_BAND_WIDTH)) * n
         dist.all_reduce(count_ws[:4 * nbk].view(torch.int32), group=group)
     if dist.get_world_size(group) == 1:
         return local
@@ -128,24 +128,25 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
         raise NotImplementedError("sharded walks use Philox (shard-invariant); PCG64 replay is single-GPU")
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    from .engine import DEFAULT_BAND_WIDTH
+    from .engine import ROWS_BAND_WIDTH
 
     G = engine.laplacian(A)
     n = G.n_rows
     b, e = shard_range(n, rank, world)
+    bw = ROWS_BAND_WIDTH  # (row-mode Grams: the wide bands)
     tws = None
     if walks_per_node * max_walk_length <= 4096:
         # fused walk -> Phi, counting this rank's buckets of the banded transpose on the way
-        tws = engine.transpose_workspace(n, n)
+        tws = engine.transpose_workspace(n, n, bw)
         rows = engine.walk_phi(G, walks_per_node, p_halt, max_walk_length, f, seed=seed, src_begin=b, src_end=e,
-                               count_ws=tws, band_width=DEFAULT_BAND_WIDTH)
+                               count_ws=tws, band_width=bw)
     else:
         rows = engine.features(engine.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed,
                                            src_begin=b, src_end=e), f)
     local = engine.compact(rows, want64=False, want32=True)
-    phi = gather_phi(engine, local, tws, group) if world > 1 else \
+    phi = gather_phi(engine, local, tws, group, band_width=bw) if world > 1 else \
         DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
-    tr = engine.transpose_banded(phi, counted_ws=tws)
+    tr = engine.transpose_banded(phi, bw, counted_ws=tws)
     if mode == "allreduce":
         K = engine.gram_sparse_kslice(phi, tr, b, e)
         allreduce_buckets(K, group=group)

@@ -254,6 +254,9 @@ def test_gram_sparse_band_invariance(eng):
     K_wide = eng.gram_sparse(phi, eng.transpose_banded(phi, 4096)).cpu().numpy()
     K_narrow = eng.gram_sparse(phi, eng.transpose_banded(phi, 64)).cpu().numpy()
     assert np.array_equal(K_wide, K_narrow)
+    # 8192-wide bands run 8-wave tiles (76 KiB of LDS): the same bits
+    K_8k = eng.gram_sparse(phi, eng.transpose_banded(phi, 8192)).cpu().numpy()
+    assert np.array_equal(K_wide, K_8k)
     ok, fro = gram_close(K_wide[:16], phi.to_scipy(), (0, 16))
     assert ok, fro
 
