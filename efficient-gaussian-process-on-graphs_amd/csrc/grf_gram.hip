@@ -239,8 +239,8 @@ template <int kWaves, int kHalves, int kGramUnroll, bool kTailExact>
 __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
-    const unsigned char *__restrict__ t_rec, const int32_t *__restrict__ rowshift, float *__restrict__ K,
-    int64_t ldk) {
+    const unsigned char *__restrict__ t_rec, int32_t unit, const int32_t *__restrict__ rowshift,
+    float *__restrict__ K, int64_t ldk) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t W = tl.W;
@@ -258,8 +258,8 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     const int64_t e0 = ptr[row], e1 = ptr[row + 1];
     const int64_t boff = J * n_total;
     const int sh = rowshift[row];
-    const int32_t line0 = (int32_t)t_desc[boff].x;
-    const unsigned char *brec = t_rec + (int64_t)line0 * 128;  // the band's records
+    const int32_t line0 = (int32_t)t_desc[boff].x;                  // the band's first unit
+    const unsigned char *brec = t_rec + (int64_t)line0 * unit;  // the band's records
 
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     u64x2 *acc2 = reinterpret_cast<u64x2 *>(acc);
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             if (k < tl.k_begin || k >= tl.k_end) k = -1;  // (k-slice mode)
             av[h] = k >= 0 ? val[e] : 0.f;
             const uint2 d = k >= 0 ? t_desc[boff + k] : make_uint2((uint32_t)line0, 0u);
-            t0[h] = ((int32_t)d.x - line0) * 128;  // bucket byte offset within the band
+            t0[h] = ((int32_t)d.x - line0) * unit;  // bucket byte offset within the band
             cnt[h] = (int32_t)d.y;                 // pairs
         }
         int32_t total = 0;
@@ -489,8 +489,8 @@ size_t grf_gram_workspace_bytes(void) { return 256; }
 // tiles [t_first, t_last) of one Gram call
 static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramTiles &tl, int64_t t_first,
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
-                                 const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
-                                 int64_t ldk, hipStream_t st) {
+                                 const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
+                                 float *K, int64_t ldk, hipStream_t st) {
     // tuning knobs (defaults = measured best on MI355X): gathers in flight per wave, waves per tile
     static const int knobs = [] {
         const char *e = getenv("GRF_GRAM_UNROLL"), *w = getenv("GRF_GRAM_WAVES"), *t = getenv("GRF_GRAM_TAIL");
@@ -511,7 +511,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
     gram_sparse_kernel<WV, H, U, T><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx, val,\
                                                                      reinterpret_cast<const uint2 *>(t_desc),     \
                                                                      reinterpret_cast<const unsigned char *>(t_rec), \
-                                                                     t_rowshift, K, ldk)
+                                                                     unit, t_rowshift, K, ldk)
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     do {                                                                                                          \
         if (tail_exact) GRF_GRAM_LAUNCH_T(WV, H, U, true);                                                        \
@@ -533,21 +533,22 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
 }
 
 static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t rows, bool sym, int64_t k_begin,
-                                  int64_t k_end, const int64_t *ptr,
-                                  const int32_t *idx, const float *val, int64_t band_width, const uint32_t *t_desc,
-                                  const void *t_rec, const int32_t *t_rowshift, float *K, int64_t ldk,
-                                  hipStream_t st) {
+                                  int64_t k_end, const int64_t *ptr, const int32_t *idx, const float *val,
+                                  int64_t band_width, int32_t unit, const uint32_t *t_desc, const void *t_rec,
+                                  const int32_t *t_rowshift, float *K, int64_t ldk, hipStream_t st) {
     const int64_t nb = cdiv<int64_t>(n_total, band_width);
     const GramTiles tl{rows, band_width, nb, sym, (int32_t)k_begin, (int32_t)k_end};
     const int64_t n_tiles = tl.total();
     if (n_tiles == 0) return GRF_OK;
-    return gram_tiles_launch(n_total, row_begin, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, t_rowshift, K, ldk,
-                             st);
+    return gram_tiles_launch(n_total, row_begin, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, unit, t_rowshift, K,
+                             ldk, st);
 }
 
 static int32_t gram_sparse_check(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
-                                 int64_t band_width, const uint32_t *t_desc, const void *t_rec,
+                                 int64_t band_width, int32_t unit, const uint32_t *t_desc, const void *t_rec,
                                  const int32_t *t_rowshift, float *K, int64_t ldk) {
+    GRF_REQUIRE(unit == GRF_REC_LINE || unit == GRF_REC_PACKED, GRF_EINVAL,
+                "grf_gram_sparse: rec_unit must be GRF_REC_LINE or GRF_REC_PACKED");
     GRF_REQUIRE(n_total >= 0 && 0 <= row_begin && row_begin <= row_end && row_end <= n_total && ptr && t_desc && K &&
                     t_rowshift && t_rec,
                 GRF_EINVAL, "grf_gram_sparse: bad arguments");
@@ -559,35 +560,37 @@ static int32_t gram_sparse_check(int64_t n_total, int64_t row_begin, int64_t row
 }
 
 int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
-                        const float *val, int64_t band_width, const uint32_t *t_desc, const void *t_rec,
-                        const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
-                        grf_stream_t stream) {
-    int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, t_desc, t_rec, t_rowshift, K, ldk);
+                        const float *val, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
+                        const void *t_rec, const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
+                        size_t workspace_bytes, grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift,
+                                   K, ldk);
     if (rc != GRF_OK) return rc;
     if (row_end == row_begin || n_total == 0) return GRF_OK;
     return gram_sparse_launch(n_total, row_begin, row_end - row_begin, false, 0, n_total, ptr, idx, val, band_width,
-                              t_desc, t_rec,
-                              t_rowshift, K, ldk, S(stream));
+                              rec_unit, t_desc, t_rec, t_rowshift, K, ldk, S(stream));
 }
 
 int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
-                            int64_t band_width, const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift,
-                            float *K, int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
-    int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, t_desc, t_rec, t_rowshift, K, ldk);
+                            int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                            const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
+                            grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
     if (rc != GRF_OK) return rc;
     if (n_total == 0) return GRF_OK;
-    rc = gram_sparse_launch(n_total, 0, n_total, true, 0, n_total, ptr, idx, val, band_width, t_desc, t_rec,
-                            t_rowshift, K, ldk,
-                            S(stream));
+    rc = gram_sparse_launch(n_total, 0, n_total, true, 0, n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec,
+                            t_rowshift, K, ldk, S(stream));
     if (rc != GRF_OK) return rc;
     return grf_gram_mirror(n_total, K, ldk, stream);
 }
 
 int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,
                                const int64_t *ptr, const int32_t *idx, const float *val, int64_t band_width,
-                               const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
-                               int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
-    int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, t_desc, t_rec, t_rowshift, K, ldk);
+                               int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                               const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
+                               size_t workspace_bytes, grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift,
+                                   K, ldk);
     if (rc != GRF_OK) return rc;
     GRF_REQUIRE(0 <= k_begin && k_begin <= k_end && k_end <= n_total, GRF_EINVAL,
                 "grf_gram_sparse_kslice: bad column slice [%lld, %lld)", (long long)k_begin, (long long)k_end);
@@ -595,7 +598,7 @@ int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_e
     (void)workspace;
     (void)workspace_bytes;
     return gram_sparse_launch(n_total, row_begin, row_end - row_begin, false, k_begin, k_end, ptr, idx, val,
-                              band_width, t_desc, t_rec, t_rowshift, K, ldk, S(stream));
+                              band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk, S(stream));
 }
 
 int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, grf_stream_t stream) {

@@ -113,9 +113,12 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(int64_t n_rows, int64
 // Bucket b = band * n_cols + k holds the entries Phi[j, k], j in the band, as PAIRS of
 // records packed in 12 bytes: {u16 8 (j0 - band start), u16 8 (j1 - band start), f32 v0, f32 v1}
 // (the row is stored as the byte offset of its int64 counter in the Gram tile).
-// Every bucket starts on a 128-byte line (the Gram kernel reads a bucket as one short
-// segment; aligned, a segment of <= 10 pairs is one line instead of two).
-constexpr int kPairBytes = 12, kLineBytes = 128;
+// Record unit u (bytes): GRF_REC_LINE (128) starts every bucket on a 128-byte line (the Gram
+// kernel reads a bucket as one short segment; aligned, a segment of <= 10 pairs is one line
+// instead of two) -- for the dense-bucket regime (C4: ~9 pairs per bucket); GRF_REC_PACKED (12)
+// packs the buckets pair after pair -- for sparse buckets (C5: ~0.7 pairs per bucket, where a
+// line per bucket is ~15x the records' bytes).  Descriptors count units of u bytes.
+constexpr int kPairBytes = 12;
 
 __global__ __launch_bounds__(256) void tr_count_kernel(int64_t n_rows, int64_t n_cols, int64_t bw,
                                                        const int64_t *ptr, const int32_t *idx, int32_t *cnt) {
@@ -126,9 +129,9 @@ __global__ __launch_bounds__(256) void tr_count_kernel(int64_t n_rows, int64_t n
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) atomicAdd(&cnt[band_off + idx[e]], 1);
 }
 
-__global__ void tr_lines_kernel(int64_t n, const int32_t *cnt, int32_t *lines) {
+__global__ void tr_lines_kernel(int64_t n, const int32_t *cnt, int32_t *lines, int32_t unit) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) lines[i] = (kPairBytes * ((cnt[i] + 1) >> 1) + kLineBytes - 1) / kLineBytes;
+    if (i < n) lines[i] = (kPairBytes * ((cnt[i] + 1) >> 1) + unit - 1) / unit;
 }
 
 __global__ void tr_desc_kernel(int64_t n, const int32_t *cnt, const int64_t *line_off, uint2 *desc) {
@@ -139,7 +142,7 @@ __global__ void tr_desc_kernel(int64_t n, const int32_t *cnt, const int64_t *lin
 
 __global__ __launch_bounds__(256) void tr_fill_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, const int64_t *ptr,
                                                       const int32_t *idx, const float *val, const uint2 *desc,
-                                                      int32_t *cursor, unsigned char *t_rec,
+                                                      int32_t *cursor, unsigned char *t_rec, int32_t unit,
                                                       unsigned int *maxabs_bits, float *row_max, double *row_sum) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n_rows) return;
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(256) void tr_fill_kernel(int64_t n_rows, int64_t n_
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) {
         const int64_t b = band_off + idx[e];
         const int32_t s = atomicAdd(&cursor[b], 1);
-        unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (s >> 1);
+        unsigned char *pair = t_rec + (int64_t)desc[b].x * unit + (int64_t)kPairBytes * (s >> 1);
         reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(jr * 8u);  // byte offset of the int64 counter
         reinterpret_cast<float *>(pair + 4)[s & 1] = val[e];
         mx = fmaxf(mx, fabsf(val[e]));
@@ -180,10 +183,11 @@ __global__ void tr_rowshift_kernel(int64_t n_rows, const float *row_max, const d
 }
 
 // odd buckets: the second record of the last pair is (col 0, +0.0) -- adds exactly 0
-__global__ void tr_pad_fill_kernel(int64_t n, const uint2 *desc, const int32_t *cursor, unsigned char *t_rec) {
+__global__ void tr_pad_fill_kernel(int64_t n, const uint2 *desc, const int32_t *cursor, unsigned char *t_rec,
+                                   int32_t unit) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b < n && (cursor[b] & 1)) {
-        unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (cursor[b] >> 1);
+        unsigned char *pair = t_rec + (int64_t)desc[b].x * unit + (int64_t)kPairBytes * (cursor[b] >> 1);
         reinterpret_cast<uint16_t *>(pair)[1] = 0;
         reinterpret_cast<float *>(pair + 4)[1] = 0.f;
     }
@@ -349,27 +353,28 @@ __global__ __launch_bounds__(1024) void tr_maxabs_kernel(int64_t n, const float 
 __global__ __launch_bounds__(256) void tr_place_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, int32_t cr,
                                                        int32_t nreg, const int64_t *ptr, const uint2 *desc,
                                                        const int64_t *ent_off, const uint2 *staging,
-                                                       const int32_t *tab, int32_t *gcur, unsigned char *t_rec) {
+                                                       const int32_t *tab, int32_t *gcur, unsigned char *t_rec,
+                                                       int32_t unit) {
     extern __shared__ __attribute__((aligned(16))) unsigned char tp_smem[];
     const int tid = threadIdx.x;
     const int64_t band = blockIdx.x / nreg, g = blockIdx.x - band * nreg;
     const int64_t c0 = g * cr, c1 = min<int64_t>(n_cols, c0 + cr);
     const int64_t b0 = band * n_cols + c0, b1 = band * n_cols + c1;
     const int64_t L0 = desc[b0].x, L1 = desc[b1].x;  // (desc[nbk].x = total lines, low word)
-    const int64_t img = (L1 - L0) * kLineBytes;
+    const int64_t img = (L1 - L0) * unit;
     if (ent_off[b1] == ent_off[b0]) return;
     // the band's binning workgroups
     const int64_t w0 = band * bw / kBinRows, w1 = cdiv<int64_t>(min<int64_t>(n_rows, (band + 1) * bw), kBinRows);
-    const bool lds = img <= kPlaceCap;
+    const bool lds = (img + 15) / 16 * 16 <= kPlaceCap;
     uint32_t *lcur = reinterpret_cast<uint32_t *>(tp_smem);   // [cr]
     uint32_t *lline = lcur + cr;                               // [cr] first byte of each bucket in the image
     unsigned char *image = tp_smem + 8 * cr;                   // [img]
     if (lds) {
         for (int i = tid; i < c1 - c0; i += 256) {
             lcur[i] = 0u;
-            lline[i] = (uint32_t)((desc[b0 + i].x - L0) * kLineBytes);
+            lline[i] = (uint32_t)((desc[b0 + i].x - L0) * unit);
         }
-        for (int64_t i = tid; i < img / 16; i += 256) reinterpret_cast<uint4 *>(image)[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int64_t i = tid; i < (img + 15) / 16; i += 256) reinterpret_cast<uint4 *>(image)[i] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
     }
     for (int64_t w = w0 + tid; w < w1; w += 256) {
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(256) void tr_place_kernel(int64_t n_rows, int64_t n
             } else {  // oversized region: global cursors (zeroed by the caller)
                 const int64_t b = b0 + kk;
                 const int32_t s = atomicAdd(&gcur[b], 1);
-                unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (s >> 1);
+                unsigned char *pair = t_rec + (int64_t)desc[b].x * unit + (int64_t)kPairBytes * (s >> 1);
                 reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(x.x & 0xffffu);
                 reinterpret_cast<uint32_t *>(pair + 4)[s & 1] = x.y;
             }
@@ -395,14 +400,19 @@ __global__ __launch_bounds__(256) void tr_place_kernel(int64_t n_rows, int64_t n
     }
     if (lds) {
         __syncthreads();
-        uint4 *dst = reinterpret_cast<uint4 *>(t_rec + L0 * kLineBytes);
-        for (int64_t i = tid; i < img / 16; i += 256) dst[i] = reinterpret_cast<const uint4 *>(image)[i];
+        if ((L0 * unit) % 16 == 0 && img % 16 == 0) {  // whole lines: 16-byte stores
+            uint4 *dst = reinterpret_cast<uint4 *>(t_rec + L0 * unit);
+            for (int64_t i = tid; i < img / 16; i += 256) dst[i] = reinterpret_cast<const uint4 *>(image)[i];
+        } else {  // packed records: the region's exact byte range (a multiple of 4 at a 4-byte offset)
+            uint32_t *dst = reinterpret_cast<uint32_t *>(t_rec + L0 * unit);
+            for (int64_t i = tid; i < img / 4; i += 256) dst[i] = reinterpret_cast<const uint32_t *>(image)[i];
+        }
         return;
     }
     for (int64_t b = b0 + tid; b < b1; b += 256) {  // pad the odd buckets
         const int32_t c = (int32_t)(ent_off[b + 1] - ent_off[b]);
         if (c & 1) {
-            unsigned char *pair = t_rec + (int64_t)desc[b].x * kLineBytes + (int64_t)kPairBytes * (c >> 1);
+            unsigned char *pair = t_rec + (int64_t)desc[b].x * unit + (int64_t)kPairBytes * (c >> 1);
             reinterpret_cast<uint16_t *>(pair)[1] = 0;
             reinterpret_cast<float *>(pair + 4)[1] = 0.f;
         }
@@ -452,11 +462,13 @@ size_t grf_transpose_workspace_bytes(int64_t n_buckets) {
            scan_ws_bytes(n_buckets);
 }
 
-int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                                  const int32_t *idx, uint32_t *t_desc, int32_t counted, void *workspace,
-                                  size_t workspace_bytes, grf_stream_t stream) {
+int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                  const int64_t *ptr, const int32_t *idx, uint32_t *t_desc, int32_t counted,
+                                  void *workspace, size_t workspace_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && t_desc,
                 GRF_EINVAL, "grf_transpose_banded_plan: bad arguments");
+    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED, GRF_EINVAL,
+                "grf_transpose_banded_plan: rec_unit must be GRF_REC_LINE or GRF_REC_PACKED");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
     GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,
                 "grf_transpose_banded_plan: workspace too small (%zu < %zu)", workspace_bytes,
@@ -475,7 +487,7 @@ int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_w
         GRF_CHECK_LAUNCH("tr_count_kernel");
     }
     GRF_REQUIRE_GRID(cdiv<int64_t>(nbk, 256), 256, "tr_lines_kernel");
-    tr_lines_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, cnt, lines);
+    tr_lines_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, cnt, lines, rec_unit);
     GRF_CHECK_LAUNCH("tr_lines_kernel");
     int32_t rc = scan_counts_i32(nbk, lines, line_off, scan_ws, scan_ws_bytes(nbk), st);
     if (rc != GRF_OK) return rc;
@@ -486,13 +498,15 @@ int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_w
     return GRF_OK;
 }
 
-int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                                  const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
-                                  int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift, void *workspace,
-                                  size_t workspace_bytes, grf_stream_t stream) {
+int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                  const int64_t *ptr, const int32_t *idx, const float *val, const uint32_t *t_desc,
+                                  void *t_rec, int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
+                                  void *workspace, size_t workspace_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && val && t_desc &&
                     t_rec && t_maxabs && t_rowshift && t_rec_bytes >= 0,
                 GRF_EINVAL, "grf_transpose_banded_fill: bad arguments");
+    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED, GRF_EINVAL,
+                "grf_transpose_banded_fill: rec_unit must be GRF_REC_LINE or GRF_REC_PACKED");
     GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_transpose_banded_fill: t_rec must be 128-byte aligned");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
     GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,
@@ -508,7 +522,7 @@ int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_w
     if (n_rows > 0) {
         GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "tr_fill_kernel");
         tr_fill_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, st>>>(
-            n_rows, n_cols, band_width, ptr, idx, val, desc, cursor, (unsigned char *)t_rec,
+            n_rows, n_cols, band_width, ptr, idx, val, desc, cursor, (unsigned char *)t_rec, rec_unit,
             reinterpret_cast<unsigned int *>(t_maxabs), row_max, row_sum);
         GRF_CHECK_LAUNCH("tr_fill_kernel");
         GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 256), 256, "tr_rowshift_kernel");
@@ -517,7 +531,8 @@ int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_w
         GRF_CHECK_LAUNCH("tr_rowshift_kernel");
     }
     GRF_REQUIRE_GRID(cdiv<int64_t>(nbk, 256), 256, "tr_pad_fill_kernel");
-    tr_pad_fill_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, desc, cursor, (unsigned char *)t_rec);
+    tr_pad_fill_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, desc, cursor, (unsigned char *)t_rec,
+                                                                          rec_unit);
     GRF_CHECK_LAUNCH("tr_pad_fill_kernel");
     return GRF_OK;
 }
@@ -530,14 +545,16 @@ size_t grf_transpose_staging_bytes(int64_t n_rows, int64_t n_cols, int64_t band_
            tr_align((size_t)std::max<int64_t>(nwg, 1) * (nreg + 1) * 4) + tr_align((size_t)std::max<int64_t>(nwg, 1) * 4);
 }
 
-int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                                         const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
-                                         int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
-                                         void *workspace, size_t workspace_bytes, int64_t nnz, void *staging,
-                                         size_t staging_bytes, grf_stream_t stream) {
+int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                         const int64_t *ptr, const int32_t *idx, const float *val,
+                                         const uint32_t *t_desc, void *t_rec, int64_t t_rec_bytes, float *t_maxabs,
+                                         int32_t *t_rowshift, void *workspace, size_t workspace_bytes, int64_t nnz,
+                                         void *staging, size_t staging_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && val && t_desc &&
                     t_rec && t_maxabs && t_rowshift && t_rec_bytes >= 0 && staging,
                 GRF_EINVAL, "grf_transpose_banded_fill_staged: bad arguments");
+    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED, GRF_EINVAL,
+                "grf_transpose_banded_fill_staged: rec_unit must be GRF_REC_LINE or GRF_REC_PACKED");
     GRF_REQUIRE(band_width % 64 == 0, GRF_EUNSUPPORTED,
                 "grf_transpose_banded_fill_staged: band_width must be a multiple of 64");
     GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL,
@@ -585,7 +602,7 @@ int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t
     const size_t lds2 = (size_t)8 * cr + kPlaceCap;
     GRF_REQUIRE_GRID(n_regions, 256, "tr_place_kernel");
     tr_place_kernel<<<(unsigned)n_regions, 256, lds2, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr, desc, ent_off,
-                                                            ent, tab, cnt, (unsigned char *)t_rec);
+                                                            ent, tab, cnt, (unsigned char *)t_rec, rec_unit);
     GRF_CHECK_LAUNCH("tr_place_kernel");
     return GRF_OK;
 }

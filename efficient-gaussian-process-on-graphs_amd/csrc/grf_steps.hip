@@ -14,6 +14,8 @@
 // (node, walk) keys in LDS gives those orders without atomics.
 #include <algorithm>
 
+#include <stdlib.h>
+
 #include "grf_block.h"
 #include "grf_philox.h"
 
@@ -337,7 +339,17 @@ int32_t grf_steps(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32
     GRF_REQUIRE(m <= 16384, GRF_EUNSUPPORTED, "grf_steps: walks_per_node > 16384 not supported by this build");
     if (n_src == 0) return GRF_OK;
     const int P = (int)next_pow2_u32((uint32_t)m);
-    const int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
+    // threads per source: P / 4 up to 256, and at most two per walk -- measured (tools/walkphi_ab.py):
+    // m = 128 (C4) 256 threads 3.37 ms vs 128 4.20; m = 64 (C5) 128 threads 14.3 ms vs 256 19.6 (idle
+    // waves hold the source's slot while the walk runs); GRF_PHI_THREADS caps it for experiments
+    static const int t_env = [] {
+        const char *e = getenv("GRF_PHI_THREADS");
+        const int v = e ? atoi(e) : 0;
+        return (v == 64 || v == 128 || v == 256) ? v : 0;
+    }();
+    const int t_cap = t_env ? t_env : (int)std::min<int64_t>(256, std::max<int64_t>(64, 2 * ((m + 63) / 64) * 64));
+    int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
+    while (T > t_cap && P / (T / 2) <= kPhiMaxPer) T /= 2;
     const size_t lds = (size_t)P * sizeof(uint64_t) + 128;
     GRF_REQUIRE_GRID((n_src * L), T, "steps_kernel");
     steps_kernel<<<(unsigned)(n_src * L), T, lds, S(stream)>>>(m, norm, P, slot_node, slot_load, step_cnt, step_idx,
@@ -379,7 +391,17 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     const int wbits = ceil_log2((uint64_t)m), lbits = ceil_log2((uint64_t)L) > 0 ? ceil_log2((uint64_t)L) : 1;
     GRF_REQUIRE(wbits + lbits <= 32, GRF_EUNSUPPORTED, "grf_phi_fused: key overflow");
     const size_t lds = (size_t)P * 8 + (size_t)E * 8 + (size_t)P * 8 + 64 * 8 + 128;
-    const int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
+    // threads per source: P / 4 up to 256, and at most two per walk -- measured (tools/walkphi_ab.py):
+    // m = 128 (C4) 256 threads 3.37 ms vs 128 4.20; m = 64 (C5) 128 threads 14.3 ms vs 256 19.6 (idle
+    // waves hold the source's slot while the walk runs); GRF_PHI_THREADS caps it for experiments
+    static const int t_env = [] {
+        const char *e = getenv("GRF_PHI_THREADS");
+        const int v = e ? atoi(e) : 0;
+        return (v == 64 || v == 128 || v == 256) ? v : 0;
+    }();
+    const int t_cap = t_env ? t_env : (int)std::min<int64_t>(256, std::max<int64_t>(64, 2 * ((m + 63) / 64) * 64));
+    int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
+    while (T > t_cap && P / (T / 2) <= kPhiMaxPer) T /= 2;
     GRF_REQUIRE(n_f <= 64 || L <= 64, GRF_EUNSUPPORTED, "grf_phi_fused: max_walk_length > 64");
     GRF_REQUIRE(P / T <= kPhiMaxPer, GRF_EUNSUPPORTED, "grf_phi_fused: too many positions per thread");
     const int32_t Lf = n_f < L ? n_f : L;

@@ -23,6 +23,7 @@ LAP_SCIPY, LAP_NUMPY, LAP_NUMPY_SAFE, LAP_COMBINATORIAL, LAP_NONE = 0, 1, 2, 3, 
 RNG_PCG64, RNG_PHILOX = 0, 1
 LOAD_CUMULATIVE, LOAD_NONCUMULATIVE, LOAD_ABLATION = 0, 1, 2
 NORM_DIV, NORM_MUL_RECIP = 0, 1
+REC_LINE, REC_PACKED = 128, 12
 
 
 class GrfWalkParams(ctypes.Structure):
@@ -62,15 +63,16 @@ SIGNATURES = {
     "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_scan_workspace_bytes": (_sz, [_i64]),
     "grf_compact_rows": (_i32, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "grf_transpose_banded_plan": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
-    "grf_transpose_banded_fill": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "grf_transpose_banded_plan": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
+    "grf_transpose_banded_fill": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz,
+                                         _vp]),
     "grf_transpose_workspace_bytes": (_sz, [_i64]),
-    "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
+    "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_workspace_bytes": (_sz, []),
-    "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
+    "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _vp]),
-    "grf_transpose_banded_fill_staged": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz,
-                                                _i64, _vp, _sz, _vp]),
+    "grf_transpose_banded_fill_staged": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                                _sz, _i64, _vp, _sz, _vp]),
     "grf_transpose_staging_bytes": (_sz, [_i64, _i64, _i64, _i64]),
     "grf_csr_transpose_workspace_bytes": (_sz, [_i64, _i64]),
     "grf_csr_transpose": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -81,8 +83,8 @@ SIGNATURES = {
     "grf_cg_workspace_bytes": (_sz, [_i64, _i64, _i32]),
     "grf_cg_gram_solve": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _dbl, _vp, _i64, _i32, _dbl, _i32,
                                  _vp, _i64, _vp, _sz, _vp, _vp, _vp]),
-    "grf_gram_sparse_kslice": (_i32, [_i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64,
-                                      _vp, _sz, _vp]),
+    "grf_gram_sparse_kslice": (_i32, [_i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp,
+                                      _i64, _vp, _sz, _vp]),
     "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
 }

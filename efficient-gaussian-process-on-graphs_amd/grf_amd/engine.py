@@ -122,13 +122,22 @@ class PaddedRows:
 
 @dataclass
 class Banded:
-    t_desc: torch.Tensor  # int32 [2 * (n_bands * n_cols + 1)]: per bucket {first 128-B line, pairs}
-    t_rec: torch.Tensor   # uint8 [lines * 128]: 12-byte record pairs {u16 j0 | u16 j1, f32 v0, f32 v1}
+    t_desc: torch.Tensor  # int32 [2 * (n_bands * n_cols + 1)]: per bucket {first unit, pairs}
+    t_rec: torch.Tensor   # uint8 [units * rec_unit]: 12-byte record pairs {u16 j0 | u16 j1, f32 v0, f32 v1}
     t_maxabs: torch.Tensor  # float32 [1], max |Phi|
     t_rowshift: torch.Tensor  # int32 [n_rows], Gram fixed-point scale exponent per row
     band_width: int
     n_rows: int
     n_cols: int
+    rec_unit: int = C.REC_LINE  # bucket alignment: 128-byte lines or packed 12-byte pairs
+
+
+def choose_rec_unit(nnz: int, n_rows: int, n_cols: int, band_width: int) -> int:
+    """Line-aligned buckets when a bucket averages >= 8 entries (C4: ~18 at W = 4096), packed
+    pairs below that (C5: ~1.4 at W = 8192, where a 128-byte line per bucket would be ~15x
+    the records' bytes)."""
+    per_bucket = nnz / max(1, n_rows) * band_width / max(1, n_cols)
+    return C.REC_LINE if per_bucket >= 8.0 else C.REC_PACKED
 
 
 class GRFEngine:
@@ -329,7 +338,7 @@ class GRFEngine:
 
     def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH,
                          counted_ws: Optional[torch.Tensor] = None, staged: Optional[bool] = None,
-                         nnz_bound: Optional[int] = None) -> Banded:
+                         nnz_bound: Optional[int] = None, rec_unit: Optional[int] = None) -> Banded:
         """Banded transpose of Phi.  counted_ws: workspace whose bucket counts ``walk_phi`` filled.
         staged: two-pass binned fill (default when band_width % 64 == 0) or the atomic fill.
         nnz_bound: an upper bound of nnz(Phi) (e.g. ``compact(..., sync_free=True)``'s): the record
@@ -341,40 +350,49 @@ class GRFEngine:
         t_max = self._empty(1, torch.float32)
         t_shift = self._empty(max(n_rows, 1), torch.int32)
         ws = counted_ws if counted_ws is not None else self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
-        C.check(self.lib.grf_transpose_banded_plan(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(t_desc),
-                                                   int(counted_ws is not None), _p(ws), ws.numel(), self.stream),
-                "grf_transpose_banded_plan")
+        if rec_unit is None:
+            rec_unit = choose_rec_unit(phi.nnz if phi._nnz is not None or nnz_bound is None else nnz_bound,
+                                       n_rows, n_cols, band_width)
+        u = int(rec_unit)
+        C.check(self.lib.grf_transpose_banded_plan(n_rows, n_cols, band_width, u, _p(phi.ptr), _p(phi.idx),
+                                                   _p(t_desc), int(counted_ws is not None), _p(ws), ws.numel(),
+                                                   self.stream), "grf_transpose_banded_plan")
         # the Gram kernel addresses a band's records with 32-bit byte offsets.  A bucket of c entries
-        # takes ceil(12 ceil(c / 2) / 128) <= 0.047 c + 1.1 lines, so a band of rows with at most
-        # `row_cap` entries each holds < 6 bw row_cap + 141 n_cols bytes.
+        # takes ceil(12 ceil(c / 2) / u) units: lines (u = 128) <= 0.047 c + 1.1, pairs (u = 12)
+        # <= c, so a band of rows with at most `row_cap` entries each holds < 6 bw row_cap +
+        # 141 n_cols bytes (lines) or 12 bw row_cap bytes (pairs).
         row_cap = min(n_cols, max(1, -(-(nnz_bound or 0) // max(n_rows, 1)))) if nnz_bound is not None else None
-        if nnz_bound is not None and nb and 6 * band_width * row_cap + 141 * n_cols < 2 ** 31:
-            lines = int(0.047 * nnz_bound + 1.1 * nbk) + 1  # bound: no read-back
+        band_bytes = (None if row_cap is None else
+                      6 * band_width * row_cap + 141 * n_cols if u == C.REC_LINE else 12 * band_width * row_cap)
+        if nnz_bound is not None and nb and band_bytes < 2 ** 31:
+            # bound: no read-back
+            units = int(0.047 * nnz_bound + 1.1 * nbk) + 1 if u == C.REC_LINE else int(nnz_bound) + 1
         else:
-            # band starts (first line of bucket (band, 0)) and the total, read back
+            # band starts (first unit of bucket (band, 0)) and the total, read back
             starts = torch.cat([t_desc[0:2 * nbk:2 * n_cols], t_desc[2 * nbk:2 * nbk + 1]]).cpu().numpy()
             starts = starts.view(np.uint32).astype(np.int64)
             tail = t_desc[2 * nbk:].cpu().numpy().view(np.uint32).astype(np.int64)
-            lines = int(tail[0] + (tail[1] << 32))
-            starts[-1] = lines
-            if nb and int(np.diff(starts).max(initial=0)) * 128 >= 2 ** 31:
+            units = int(tail[0] + (tail[1] << 32))
+            starts[-1] = units
+            if nb and int(np.diff(starts).max(initial=0)) * u >= 2 ** 31:
                 raise NotImplementedError("a transpose band holds >= 2 GiB of records; use a smaller band_width")
-        t_rec = self._empty(max(lines, 1) * 128, torch.uint8)  # torch allocations are 256-B aligned
+        # (+128 B: a masked Gram lane reads the first pair of an empty last band)
+        t_rec = self._empty(max(units, 1) * u + 128, torch.uint8)  # torch allocations are 256-B aligned
         if staged is None:
             staged = band_width % 64 == 0 and os.environ.get("GRF_TRANSPOSE_STAGED", "1") != "0"
         if staged:
             nnz = nnz_bound if nnz_bound is not None else phi.nnz
             sg = self._ws(self.lib.grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz))
             C.check(self.lib.grf_transpose_banded_fill_staged(
-                n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(t_desc), _p(t_rec),
+                n_rows, n_cols, band_width, u, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(t_desc), _p(t_rec),
                 t_rec.numel(), _p(t_max), _p(t_shift), _p(ws), ws.numel(), nnz, _p(sg), sg.numel(), self.stream),
                 "grf_transpose_banded_fill_staged")
         else:
-            C.check(self.lib.grf_transpose_banded_fill(n_rows, n_cols, band_width, _p(phi.ptr), _p(phi.idx),
+            C.check(self.lib.grf_transpose_banded_fill(n_rows, n_cols, band_width, u, _p(phi.ptr), _p(phi.idx),
                                                        _p(phi.val32), _p(t_desc), _p(t_rec), t_rec.numel(),
                                                        _p(t_max), _p(t_shift), _p(ws), ws.numel(), self.stream),
                     "grf_transpose_banded_fill")
-        return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols)
+        return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols, u)
 
     # ----------------------------------------------------------------- Gram
     @staticmethod
@@ -390,7 +408,8 @@ class GRFEngine:
         if out is None:
             out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_gram_sparse(n, row_begin, row_end, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
-                                         tr.band_width, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out),
+                                         tr.band_width, tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec),
+                                         _p(tr.t_rowshift), _p(out),
                                          out.stride(0), _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse")
         return out[:, :n]
@@ -404,7 +423,8 @@ class GRFEngine:
         if out is None:
             out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_gram_sparse_kslice(n, row_begin, row_end, k_begin, k_end, _p(phi.ptr), _p(phi.idx),
-                                                _p(phi.val32), tr.band_width, _p(tr.t_desc), _p(tr.t_rec),
+                                                _p(phi.val32), tr.band_width, tr.rec_unit, _p(tr.t_desc),
+                                                _p(tr.t_rec),
                                                 _p(tr.t_rowshift), _p(out), out.stride(0), _p(self._gram_ws),
                                                 self._gram_ws.numel(), self.stream), "grf_gram_sparse_kslice")
         return out[:, :n]
@@ -416,7 +436,7 @@ class GRFEngine:
         if out is None:
             out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_gram_sparse_sym(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
-                                             _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out), out.stride(0),
+                                             tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out), out.stride(0),
                                              _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_sym")
         return out[:, :n]

@@ -33,6 +33,12 @@ enum grf_status {
     GRF_EUNSUPPORTED = -4 /* size outside what this build handles                   */
 };
 
+/* Record unit of the banded transpose (bytes per descriptor unit) */
+enum grf_rec_unit {
+    GRF_REC_LINE = 128,  /* every bucket starts on a 128-byte line: dense buckets (C4)      */
+    GRF_REC_PACKED = 12  /* buckets packed pair after pair: sparse buckets (C5, N = 1M)     */
+};
+
 /* Laplacian semantics */
 enum grf_laplacian_mode {
     GRF_LAP_SCIPY = 0,         /* utils_sparse/graph_utils.py:5-30  (D^-1/2 (D-A) D^-1/2, scipy order) */
@@ -174,33 +180,34 @@ int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const 
 /* Banded transpose for the Gram kernel: entries (j, k, v) of Phi (CSR rows j)
  * bucketed by (band = j / band_width, k):  bucket id b = band * n_cols + k.
  * A bucket is a run of 12-byte record PAIRS {u16 8 (j0 - band start), u16 8 (j1 - band start)
- * (low / high half of one word), f32 v0, f32 v1}, starting on a 128-byte line; an odd
- * bucket ends with the pad record (0, +0.0).  Two calls:
- *   plan: t_desc[2 * (n_bands * n_cols + 1)] = per bucket {first line, pairs}; the last
- *         entry holds the total line count (lo, hi words).  counted = 1: the bucket counts
+ * (low / high half of one word), f32 v0, f32 v1}, starting on a unit boundary (rec_unit =
+ * GRF_REC_LINE: a 128-byte line; GRF_REC_PACKED: right after the previous bucket); an odd
+ * bucket ends with the pad record (0, +0.0).  Two calls (and the Gram) take the same rec_unit:
+ *   plan: t_desc[2 * (n_bands * n_cols + 1)] = per bucket {first unit, pairs}; the last
+ *         entry holds the total unit count (lo, hi words).  counted = 1: the bucket counts
  *         are already in the workspace (from grf_walk_phi over all rows), skip counting.
- *   fill: t_rec (>= total lines * 128 bytes, 128-byte aligned), t_maxabs[1] = max |Phi| and
+ *   fill: t_rec (>= total units * rec_unit bytes, 128-byte aligned), t_maxabs[1] = max |Phi| and
  *         t_rowshift[n_rows]: the Gram kernel's per-row fixed-point scale 2^shift (every term
  *         < 2^51, the row's sum of |terms| < 2^62).
  * workspace >= grf_transpose_workspace_bytes(n_bands * n_cols), shared by both calls.
  * band_width <= 8192. */
-int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                                  const int32_t *idx, uint32_t *t_desc, int32_t counted, void *workspace,
-                                  size_t workspace_bytes, grf_stream_t stream);
-int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                                  const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
-                                  int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift, void *workspace,
-                                  size_t workspace_bytes, grf_stream_t stream);
+int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                  const int64_t *ptr, const int32_t *idx, uint32_t *t_desc, int32_t counted,
+                                  void *workspace, size_t workspace_bytes, grf_stream_t stream);
+int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                  const int64_t *ptr, const int32_t *idx, const float *val, const uint32_t *t_desc,
+                                  void *t_rec, int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
+                                  void *workspace, size_t workspace_bytes, grf_stream_t stream);
 size_t grf_transpose_workspace_bytes(int64_t n_buckets);
 /* The same fill in two coalesced passes (entries binned by (band, 128-column region) into
  * `staging`, then each region's records built in LDS and written whole); band_width must be
  * a multiple of 64, nnz = ptr[n_rows].  Record order inside a bucket is unspecified in both
  * fills (the Gram's fixed-point sum does not depend on it). */
-int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t band_width, const int64_t *ptr,
-                                         const int32_t *idx, const float *val, const uint32_t *t_desc, void *t_rec,
-                                         int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
-                                         void *workspace, size_t workspace_bytes, int64_t nnz, void *staging,
-                                         size_t staging_bytes, grf_stream_t stream);
+int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                         const int64_t *ptr, const int32_t *idx, const float *val,
+                                         const uint32_t *t_desc, void *t_rec, int64_t t_rec_bytes, float *t_maxabs,
+                                         int32_t *t_rowshift, void *workspace, size_t workspace_bytes, int64_t nnz,
+                                         void *staging, size_t staging_bytes, grf_stream_t stream);
 size_t grf_transpose_staging_bytes(int64_t n_rows, int64_t n_cols, int64_t band_width, int64_t nnz);
 
 /* ---------------------------------------------------------------------- Gram
@@ -214,9 +221,9 @@ size_t grf_transpose_staging_bytes(int64_t n_rows, int64_t n_cols, int64_t band_
  * power-of-two scale), so K does not depend on summation order: it is
  * bit-reproducible run to run, across row splits and GPU counts. */
 int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr, const int32_t *idx,
-                        const float *val, int64_t band_width, const uint32_t *t_desc, const void *t_rec,
-                        const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
-                        grf_stream_t stream);
+                        const float *val, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
+                        const void *t_rec, const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
+                        size_t workspace_bytes, grf_stream_t stream);
 /* device workspace of one grf_gram_sparse / grf_gram_sparse_sym call (reserved for a tile
  * work counter; this build does not touch it and accepts NULL) */
 size_t grf_gram_workspace_bytes(void);
@@ -227,16 +234,18 @@ size_t grf_gram_workspace_bytes(void);
  * row_begin = 0, row_end = n_total, except that the mirrored entries carry the
  * fixed-point rounding of row i (K is exactly symmetric).  band_width multiple of 64. */
 int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
-                            int64_t band_width, const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift,
-                            float *K, int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+                            int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                            const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
+                            grf_stream_t stream);
 
 /* Partial Gram over a slice of the inner dimension: K[r, :] = sum over k in [k_begin, k_end)
  * of Phi[r, k] Phi[:, k] (same fixed-point rule as grf_gram_sparse).  The partial Grams of
  * disjoint slices sum to K -- the "partial K + all-reduce" multi-GPU option. */
 int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,
                                const int64_t *ptr, const int32_t *idx, const float *val, int64_t band_width,
-                               const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
-                               int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+                               int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                               const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
+                               size_t workspace_bytes, grf_stream_t stream);
 
 /* The mirror pass of grf_gram_sparse_sym alone: K[j, i] = K[i, j] for every j > i. */
 int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, grf_stream_t stream);

@@ -261,17 +261,20 @@ def test_gram_sparse_band_invariance(eng):
     assert ok, fro
 
 
+@pytest.mark.parametrize("unit", [128, 12])
 @pytest.mark.parametrize("n,deg,m,L,bw", [(20000, 10, 32, 6, 4096), (5000, 10, 64, 8, 64), (3000, 20, 128, 8, 4096),
                                           (4100, 6, 16, 4, 1024)])
-def test_transpose_staged_fill_matches_atomic_fill(eng, n, deg, m, L, bw):
+def test_transpose_staged_fill_matches_atomic_fill(eng, n, deg, m, L, bw, unit):
     """The binned two-pass fill (LDS region images; the dense 3000-node case overflows the LDS
     cap and takes the global-cursor fallback) gives the same descriptors, the same multiset of
-    records per bucket, the same row shifts -- hence bit-identical K."""
+    records per bucket, the same row shifts -- hence bit-identical K -- in both record layouts
+    (buckets on 128-byte lines and packed 12-byte pairs), and the two layouts give the same K."""
     A = er_graph(n, deg, n + 7)
     G = eng.laplacian(A)
     phi = eng.compact(eng.walk_phi(G, m, 0.15, L, [1.0, -0.5, 0.25, -0.125, 0.1, -0.05, 0.02, -0.01][:L], seed=4))
-    ta = eng.transpose_banded(phi, bw, staged=False)
-    ts = eng.transpose_banded(phi, bw, staged=True)
+    ta = eng.transpose_banded(phi, bw, staged=False, rec_unit=unit)
+    ts = eng.transpose_banded(phi, bw, staged=True, rec_unit=unit)
+    assert ta.rec_unit == ts.rec_unit == unit
     assert np.array_equal(ta.t_desc.cpu().numpy(), ts.t_desc.cpu().numpy())
     assert np.array_equal(ta.t_rowshift.cpu().numpy(), ts.t_rowshift.cpu().numpy())
     assert ta.t_maxabs.item() == ts.t_maxabs.item()
@@ -284,7 +287,7 @@ def test_transpose_staged_fill_matches_atomic_fill(eng, n, deg, m, L, bw):
         if pairs == 0:
             continue
         def recs(buf):
-            seg = buf[line * 128: line * 128 + 12 * pairs].reshape(pairs, 12)
+            seg = buf[line * unit: line * unit + 12 * pairs].reshape(pairs, 12)
             cols = seg[:, :4].copy().view(np.uint16).reshape(pairs, 2)
             vals = seg[:, 4:].copy().view(np.float32).reshape(pairs, 2)
             return sorted(zip(cols.ravel().tolist(), vals.ravel().tolist()))
@@ -292,6 +295,10 @@ def test_transpose_staged_fill_matches_atomic_fill(eng, n, deg, m, L, bw):
     Ka = eng.gram_sparse(phi, ta, 0, 300).cpu().numpy()
     Ks = eng.gram_sparse(phi, ts, 0, 300).cpu().numpy()
     assert np.array_equal(Ka, Ks)
+    other = eng.transpose_banded(phi, bw, rec_unit=140 - unit)  # the other layout
+    assert np.array_equal(eng.gram_sparse(phi, other, 0, 300).cpu().numpy(), Ka)
+    if bw % 64 == 0:
+        assert np.array_equal(eng.gram_sparse_sym(phi, other).cpu().numpy(), eng.gram_sparse_sym(phi, ts).cpu().numpy())
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
