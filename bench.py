@@ -6,7 +6,10 @@ in HBM: normalised Laplacian -> 12.8M Philox random walks (L = 8, p_halt = 0.1)
 dense float32 N x N matrix in HBM (40 GB at N = 100k).  With --gpus N (launched
 by torch.distributed.run) every rank walks its source range, the Phi rows are
 all-gathered over RCCL and each rank writes its row block of K (strong scaling:
-one K per step for the whole job).
+one K per step for the whole job).  On one GPU the steps are pipelined over two HIP
+streams: step s+1's front (Laplacian, walks, Phi, transpose) starts when step s's Gram
+tiles finish and runs beside step s's HBM-bound mirror pass; every step still runs its
+whole path, and `serial_ms_per_step` reports the un-pipelined latency beside `value`.
 
 Prints ONE JSON line on rank 0 (contract in the task description) with a
 `roofline` object for the dominant kernel (gram_sparse) and a `cpu_baseline`
@@ -290,10 +293,12 @@ def main():
     ap.add_argument("--k-rows", type=int, default=0,
                     help="compute only the first R rows of every rank's K row block (0 = all rows); "
                          "the unit becomes K rows/s")
-    ap.add_argument("--overlap", action="store_true",
-                    help="pipeline the steps: step s+1's Laplacian/walks/Phi/transpose on a second HIP stream "
-                         "beside step s's K assembly (measured: 27.3 vs 27.5 ms per step -- the Gram stretches by "
-                         "the front's share of the GPU, so the default runs the steps one after another)")
+    ap.add_argument("--overlap", dest="overlap", action="store_true", default=None,
+                    help="pipeline the steps on two HIP streams: step s+1's Laplacian/walks/Phi/transpose start "
+                         "when step s's Gram tiles finish and run beside its HBM-bound mirror pass (default for "
+                         "the single-GPU symmetric K: 25.9 vs 27.5 ms per step; beside the gather-bound Gram of "
+                         "the row modes it gains nothing, so those default to serial steps)")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false", help="serial steps")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
     ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
@@ -335,6 +340,8 @@ def main():
     K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
     rows_cap = max(1, min(m * L, n))  # walk_phi's padded row capacity
     sym_mode = world == 1 and not args.no_sym and not args.k_rows and not allreduce
+    if args.overlap is None:
+        args.overlap = sym_mode
     bw = DEFAULT_BAND_WIDTH if sym_mode else ROWS_BAND_WIDTH  # (engine.py: measured per mode)
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     last = [None]
@@ -357,8 +364,9 @@ def main():
         tr = eng.transpose_banded(phi, bw, counted_ws=tws, nnz_bound=n * rows_cap)
         return phi, tr, local
 
-    def back(fr, record: bool):
-        """The K assembly of one step (its front's outputs)."""
+    def back(fr, record: bool, after_gram=None):
+        """The K assembly of one step (its front's outputs).  after_gram: called between the Gram
+        tiles and the mirror of the symmetric mode (the pipelined run issues the next front there)."""
         phi, tr, local = fr
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -366,7 +374,10 @@ def main():
         if allreduce:
             eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
         elif sym_mode:
-            eng.gram_sparse_sym(phi, tr, out=K)  # upper band tiles + mirror
+            eng.gram_sparse_upper(phi, tr, out=K)  # upper band tiles ...
+            if after_gram is not None:
+                after_gram()
+            eng.gram_mirror(K, n)  # ... + mirror (= grf_gram_sparse_sym)
         else:
             eng.gram_sparse(phi, tr, b, kr_end, out=K)
         if record:
@@ -376,15 +387,19 @@ def main():
             allreduce_buckets(K[:, :n])
         last[0] = (phi, local)
 
-    def front_on_side():
-        side.wait_stream(main)  # (inputs and the previous use of its buffers are ordered)
+    def front_on_side(after=None):
+        # (after: an event on `main`; default: everything issued on `main` so far)
+        if after is None:
+            side.wait_stream(main)
+        else:
+            side.wait_event(after)
         with torch.cuda.stream(side):
             fr = front()
             done = torch.cuda.Event()
             done.record(side)
         return fr, done
 
-    def back_on_main(frd, record):
+    def back_on_main(frd, record, after_gram=None):
         fr, done = frd
         main.wait_event(done)
         phi, tr, local = fr
@@ -392,7 +407,7 @@ def main():
             for v in vars(obj).values():
                 if torch.is_tensor(v) and v.is_cuda:
                     v.record_stream(main)
-        back(fr, record)
+        back(fr, record, after_gram)
 
     def run(steps: int, record: bool):
         """`steps` whole steps.  Pipelined (--overlap): step s+1's front is issued on the side
@@ -405,9 +420,23 @@ def main():
             return
         cur = front_on_side()
         for s_ in range(steps):
-            nxt = front_on_side() if s_ + 1 < steps else None
-            back_on_main(cur, record)
-            cur = nxt
+            if sym_mode:
+                # the next front starts when this step's Gram tiles are done: it runs beside the
+                # HBM-bound mirror instead of the gather-bound Gram
+                nxt = [None]
+
+                def issue_next(last=s_ + 1 >= steps):
+                    if not last:
+                        ev = torch.cuda.Event()
+                        ev.record(main)
+                        nxt[0] = front_on_side(ev)
+
+                back_on_main(cur, record, issue_next)
+                cur = nxt[0]
+            else:
+                nxt = front_on_side() if s_ + 1 < steps else None
+                back_on_main(cur, record)
+                cur = nxt
 
     run(args.warmup, False)
     torch.cuda.synchronize()

@@ -584,6 +584,17 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
     return grf_gram_mirror(n_total, K, ldk, stream);
 }
 
+int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                              int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                              const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
+                              size_t workspace_bytes, grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
+    if (rc != GRF_OK) return rc;
+    if (n_total == 0) return GRF_OK;
+    return gram_sparse_launch(n_total, 0, n_total, true, 0, n_total, ptr, idx, val, band_width, rec_unit, t_desc,
+                              t_rec, t_rowshift, K, ldk, S(stream));
+}
+
 int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,
                                const int64_t *ptr, const int32_t *idx, const float *val, int64_t band_width,
                                int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,

@@ -238,6 +238,15 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
                             const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
                             grf_stream_t stream);
 
+/* The Gram half of grf_gram_sparse_sym alone: the tiles K[i, band >= band(i)] (the lower parts
+ * of the diagonal band tiles are written too and are overwritten by the mirror).  Followed by
+ * grf_gram_mirror on the same stream it is grf_gram_sparse_sym; split so that other work can be
+ * scheduled against the HBM-bound mirror. */
+int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                              int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                              const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
+                              size_t workspace_bytes, grf_stream_t stream);
+
 /* Partial Gram over a slice of the inner dimension: K[r, :] = sum over k in [k_begin, k_end)
  * of Phi[r, k] Phi[:, k] (same fixed-point rule as grf_gram_sparse).  The partial Grams of
  * disjoint slices sum to K -- the "partial K + all-reduce" multi-GPU option. */

@@ -237,6 +237,11 @@ def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
     # symmetric mode: the upper triangle is the same bits; the lower triangle is its mirror
     Ks = eng.gram_sparse_sym(phi, tr).cpu().numpy()
     assert np.array_equal(Ks, Ks.T)
+    if bw % 64 == 0:  # the two halves of the symmetric mode, as the pipelined bench issues them
+        import torch
+        Ku = torch.empty((n, eng.leading_dim(n)), dtype=torch.float32, device=eng.device)
+        eng.gram_sparse_upper(phi, tr, Ku)
+        assert np.array_equal(eng.gram_mirror(Ku, n).cpu().numpy(), Ks)
     upper = np.triu(np.ones((n, n), bool))
     assert np.array_equal(Ks[upper], K[upper])
     ok, fro = gram_close(Ks, phi.to_scipy())
