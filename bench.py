@@ -269,7 +269,7 @@ def _phi_host(phi):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=100_000)
     ap.add_argument("--edges", type=int, default=1_000_000)
@@ -299,6 +299,8 @@ def main():
                          "the single-GPU symmetric K: 25.9 vs 27.5 ms per step; beside the gather-bound Gram of "
                          "the row modes it gains nothing, so those default to serial steps)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false", help="serial steps")
+    ap.add_argument("--front-at", type=float, default=1.0,
+                    help="pipelined: the next front starts after this fraction of the Gram tiles (1 = at the mirror)")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
     ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
@@ -374,10 +376,23 @@ def main():
         if allreduce:
             eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
         elif sym_mode:
-            eng.gram_sparse_upper(phi, tr, out=K)  # upper band tiles ...
+            # upper band tiles (the pipelined run lets the next front start at the Gram's tail) ...
+            tiles_done = None
+            if after_gram is not None and args.front_at < 1.0:
+                cut = int(round(args.front_at * 1000))
+                eng.gram_sparse_upper(phi, tr, out=K, parts=(0, cut, 1000))
+                tiles_done = torch.cuda.Event()
+                tiles_done.record(main)
+                eng.gram_sparse_upper(phi, tr, out=K, parts=(cut, 1000, 1000))
+            else:
+                eng.gram_sparse_upper(phi, tr, out=K)
+                if after_gram is not None:
+                    tiles_done = torch.cuda.Event()
+                    tiles_done.record(main)
+            # ... + mirror (= grf_gram_sparse_sym); pipelined: a 3-per-CU grid leaves slots to the next front
+            eng.gram_mirror(K, n, 768 if after_gram is not None else 0)
             if after_gram is not None:
-                after_gram()
-            eng.gram_mirror(K, n)  # ... + mirror (= grf_gram_sparse_sym)
+                after_gram(tiles_done)  # (issued after the mirror: the host's launch time does not delay it)
         else:
             eng.gram_sparse(phi, tr, b, kr_end, out=K)
         if record:
@@ -425,11 +440,9 @@ def main():
                 # HBM-bound mirror instead of the gather-bound Gram
                 nxt = [None]
 
-                def issue_next(last=s_ + 1 >= steps):
+                def issue_next(tiles_done, last=s_ + 1 >= steps):
                     if not last:
-                        ev = torch.cuda.Event()
-                        ev.record(main)
-                        nxt[0] = front_on_side(ev)
+                        nxt[0] = front_on_side(tiles_done)
 
                 back_on_main(cur, record, issue_next)
                 cur = nxt[0]
@@ -453,11 +466,12 @@ def main():
         # latency of one un-pipelined step (reported beside the throughput; not part of `value`)
         ov = args.overlap
         args.overlap = False
+        run(1, False)  # (warm-up of the serial order)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        run(max(1, min(args.steps, 3)), False)
+        run(3, False)
         torch.cuda.synchronize()
-        serial_ms = 1000.0 * (time.perf_counter() - t1) / max(1, min(args.steps, 3))
+        serial_ms = 1000.0 * (time.perf_counter() - t1) / 3
         args.overlap = ov
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
     if world > 1:

@@ -357,15 +357,9 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     }
 }
 
-// Symmetric completion: K[j, i] = K[i, j] for every j > i (the Gram launch in symmetric
-// mode wrote the tiles K[i, band >= band(i)], which cover the upper triangle; the lower
-// parts of the diagonal band tiles are overwritten, so K is exactly symmetric).  One
-// workgroup per upper-triangle 64 x 64 block (triangular grid: no idle workgroups) moves
-// it through LDS with 16-byte loads and 16-byte non-temporal stores.
-__global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, int64_t nt, float *__restrict__ K, int64_t ldk) {
-    __shared__ float tile[64][65];
+__device__ __forceinline__ void gram_mirror_block(int64_t n, int64_t nt, int64_t b, float *__restrict__ K, int64_t ldk,
+                                                  float (*tile)[65]) {
     // block b -> (bi, bj), bj >= bi, row-major over the upper triangle of the nt x nt grid
-    const int64_t b = blockIdx.x;
     int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
     auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };  // first block of block-row i
     if (bi < 0) bi = 0;
@@ -406,6 +400,21 @@ __global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, int64_t nt,
                 if (j < n && i < n && j > i) K[j * ldk + i] = tile[x + c][y];
             }
         }
+    }
+}
+
+// Symmetric completion: K[j, i] = K[i, j] for every j > i (the Gram launch in symmetric
+// mode wrote the tiles K[i, band >= band(i)], which cover the upper triangle; the lower
+// parts of the diagonal band tiles are overwritten, so K is exactly symmetric).  One
+// workgroup per upper-triangle 64 x 64 block (triangular grid: no idle workgroups) moves
+// it through LDS with 16-byte loads and 16-byte non-temporal stores.  A bounded grid
+// (grid-stride over the blocks) leaves CU slots to work on another stream.
+__global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, int64_t nt, int64_t nblocks,
+                                                          float *__restrict__ K, int64_t ldk) {
+    __shared__ float tile[64][65];
+    for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        gram_mirror_block(n, nt, b, K, ldk, tile);
+        __syncthreads();  // (the tile is reused by the next block)
     }
 }
 
@@ -581,18 +590,25 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
     rc = gram_sparse_launch(n_total, 0, n_total, true, 0, n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec,
                             t_rowshift, K, ldk, S(stream));
     if (rc != GRF_OK) return rc;
-    return grf_gram_mirror(n_total, K, ldk, stream);
+    return grf_gram_mirror(n_total, K, ldk, 0, stream);
 }
 
 int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                               int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                              const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
-                              size_t workspace_bytes, grf_stream_t stream) {
+                              const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                              int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
+                              grf_stream_t stream) {
     int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
     if (rc != GRF_OK) return rc;
-    if (n_total == 0) return GRF_OK;
-    return gram_sparse_launch(n_total, 0, n_total, true, 0, n_total, ptr, idx, val, band_width, rec_unit, t_desc,
-                              t_rec, t_rowshift, K, ldk, S(stream));
+    GRF_REQUIRE(n_parts >= 1 && 0 <= part_begin && part_begin <= part_end && part_end <= n_parts, GRF_EINVAL,
+                "grf_gram_sparse_upper: bad tile parts [%d, %d) of %d", part_begin, part_end, n_parts);
+    if (n_total == 0 || part_begin == part_end) return GRF_OK;
+    const GramTiles tl{n_total, band_width, cdiv<int64_t>(n_total, band_width), true, 0, (int32_t)n_total};
+    const int64_t total = tl.total();
+    const int64_t t0 = total * part_begin / n_parts, t1 = total * part_end / n_parts;
+    if (t1 <= t0) return GRF_OK;
+    return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
+                             S(stream));
 }
 
 int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,
@@ -612,12 +628,20 @@ int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_e
                               band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk, S(stream));
 }
 
-int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, grf_stream_t stream) {
+int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups, grf_stream_t stream) {
     GRF_REQUIRE(n >= 0 && K && ldk >= n, GRF_EINVAL, "grf_gram_mirror: bad arguments");
     if (n == 0) return GRF_OK;
     const int64_t nt = cdiv<int64_t>(n, 64), blocks = nt * (nt + 1) / 2;
-    GRF_REQUIRE_GRID(blocks, 256, "gram_mirror_kernel");
-    gram_mirror_kernel<<<(unsigned)blocks, 256, 0, S(stream)>>>(n, nt, K, ldk);
+    // workgroups: one per block (max_workgroups <= 0), or a bounded grid-stride grid that leaves CU
+    // slots to another stream (GRF_MIRROR_WGS overrides, for experiments)
+    static const int64_t env_cap = [] {
+        const char *e = getenv("GRF_MIRROR_WGS");
+        return e ? (int64_t)atoll(e) : (int64_t)-1;
+    }();
+    const int64_t cap = env_cap >= 0 ? env_cap : max_workgroups;
+    const int64_t grid = cap > 0 && cap < blocks ? cap : blocks;
+    GRF_REQUIRE_GRID(grid, 256, "gram_mirror_kernel");
+    gram_mirror_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
     GRF_CHECK_LAUNCH("gram_mirror_kernel");
     return GRF_OK;
 }

@@ -441,18 +441,21 @@ class GRFEngine:
                 "grf_gram_sparse_sym")
         return out[:, :n]
 
-    def gram_sparse_upper(self, phi: DeviceCSR, tr: Banded, out: torch.Tensor) -> torch.Tensor:
-        """The Gram half of ``gram_sparse_sym`` (tiles K[i, band >= band(i)]); ``gram_mirror`` completes K."""
+    def gram_sparse_upper(self, phi: DeviceCSR, tr: Banded, out: torch.Tensor, parts=(0, 1, 1)) -> torch.Tensor:
+        """The Gram half of ``gram_sparse_sym`` (tiles K[i, band >= band(i)]); ``gram_mirror`` completes K.
+        parts = (begin, end, n): only those parts of the band-major tile sequence cut into n."""
         n = tr.n_rows
         C.check(self.lib.grf_gram_sparse_upper(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
                                                tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out),
-                                               out.stride(0), _p(self._gram_ws), self._gram_ws.numel(), self.stream),
+                                               out.stride(0), int(parts[0]), int(parts[1]), int(parts[2]),
+                                               _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_upper")
         return out[:, :n]
 
-    def gram_mirror(self, K: torch.Tensor, n: int) -> torch.Tensor:
-        """K[j, i] = K[i, j] for every j > i (the second half of ``gram_sparse_sym``)."""
-        C.check(self.lib.grf_gram_mirror(n, _p(K), K.stride(0), self.stream), "grf_gram_mirror")
+    def gram_mirror(self, K: torch.Tensor, n: int, max_workgroups: int = 0) -> torch.Tensor:
+        """K[j, i] = K[i, j] for every j > i (the second half of ``gram_sparse_sym``).
+        max_workgroups > 0 bounds the grid (leaves CU slots to work on another stream)."""
+        C.check(self.lib.grf_gram_mirror(n, _p(K), K.stride(0), int(max_workgroups), self.stream), "grf_gram_mirror")
         return K[:, :n]
 
     def densify(self, phi: DeviceCSR) -> torch.Tensor:

@@ -239,13 +239,15 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
                             grf_stream_t stream);
 
 /* The Gram half of grf_gram_sparse_sym alone: the tiles K[i, band >= band(i)] (the lower parts
- * of the diagonal band tiles are written too and are overwritten by the mirror).  Followed by
- * grf_gram_mirror on the same stream it is grf_gram_sparse_sym; split so that other work can be
- * scheduled against the HBM-bound mirror. */
+ * of the diagonal band tiles are written too and are overwritten by the mirror), restricted to
+ * the parts [part_begin, part_end) of the band-major tile sequence cut into n_parts equal parts
+ * (0, 1, 1 = all).  All parts followed by grf_gram_mirror on one stream is grf_gram_sparse_sym;
+ * split so that other work can be scheduled against the Gram's tail and the HBM-bound mirror. */
 int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                               int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                              const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
-                              size_t workspace_bytes, grf_stream_t stream);
+                              const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                              int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
+                              grf_stream_t stream);
 
 /* Partial Gram over a slice of the inner dimension: K[r, :] = sum over k in [k_begin, k_end)
  * of Phi[r, k] Phi[:, k] (same fixed-point rule as grf_gram_sparse).  The partial Grams of
@@ -256,8 +258,11 @@ int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_e
                                const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
                                size_t workspace_bytes, grf_stream_t stream);
 
-/* The mirror pass of grf_gram_sparse_sym alone: K[j, i] = K[i, j] for every j > i. */
-int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, grf_stream_t stream);
+/* The mirror pass of grf_gram_sparse_sym alone: K[j, i] = K[i, j] for every j > i.
+ * max_workgroups <= 0: one workgroup per 64 x 64 block (fastest alone); > 0: at most that many
+ * workgroups striding over the blocks, which leaves CU slots to work on another stream (768 =
+ * 3 per CU was best beside the next step's walks: tools/gpu_mirror_ab.sh). */
+int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups, grf_stream_t stream);
 
 /* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
  * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */

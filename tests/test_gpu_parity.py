@@ -240,8 +240,9 @@ def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
     if bw % 64 == 0:  # the two halves of the symmetric mode, as the pipelined bench issues them
         import torch
         Ku = torch.empty((n, eng.leading_dim(n)), dtype=torch.float32, device=eng.device)
-        eng.gram_sparse_upper(phi, tr, Ku)
-        assert np.array_equal(eng.gram_mirror(Ku, n).cpu().numpy(), Ks)
+        eng.gram_sparse_upper(phi, tr, Ku, parts=(0, 7, 10))
+        eng.gram_sparse_upper(phi, tr, Ku, parts=(7, 10, 10))
+        assert np.array_equal(eng.gram_mirror(Ku, n, max_workgroups=37).cpu().numpy(), Ks)  # (grid-stride)
     upper = np.triu(np.ones((n, n), bool))
     assert np.array_equal(Ks[upper], K[upper])
     ok, fro = gram_close(Ks, phi.to_scipy())

@@ -50,7 +50,7 @@ for mode in modes:
         out["sym_ms"] = timed(lambda: eng.gram_sparse_sym(phi, tr, out=K))
         out["sym_digest"] = digest()
     elif mode == "mirror":
-        out["mirror_ms"] = timed(lambda: eng.lib.grf_gram_mirror(n, K.data_ptr(), K.stride(0), eng.stream))
+        out["mirror_ms"] = timed(lambda: eng.gram_mirror(K, n))
     elif mode == "rows":
         out["rows_ms"] = timed(lambda: eng.gram_sparse(phi, tr, out=K))
         out["rows_digest"] = digest()
