@@ -250,11 +250,15 @@ static int64_t spmm_tile_bytes() {
 // Budget 8 MiB -> X tiles of <= 4 MiB (one XCD L2).  Measured at C4 (CG iteration, S = 64):
 // fp32 1.63 ms untiled -> 1.36 ms; fp64 3.39 -> 2.25 ms (2 MiB tiles: 1.45 / 2.18 ms;
 // 1 MiB: 1.72 / 2.82 ms -- per-tile overheads; 8 MiB: 1.51 / 2.89 ms -- spills past L2).
+// At most 16 tiles: every tile launch visits every output row, so with many tiles a sparse row
+// has ~1 entry per tile (C5, N = 1M, S = 64 fp64: 123 L2-sized tiles took 40.9 ms per CG
+// iteration, 8 tiles of 64 MiB 19.8 ms, untiled 20.1 ms).
 static int32_t spmm_tile_rows(int64_t n_in, int32_t S, size_t elem) {
     const int64_t tb = spmm_tile_bytes();
     if (tb <= 0) return 0;
     int64_t tw = 64;
     while (tw * 2 * S * (int64_t)elem <= tb) tw *= 2;
+    while (cdiv<int64_t>(n_in, tw) > 16) tw *= 2;
     return tw >= n_in ? 0 : (int32_t)tw;
 }
 
