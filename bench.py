@@ -57,6 +57,23 @@ def pmc_traffic(kernels):
     return total
 
 
+def init_distributed(local_rank: int) -> int:
+    """One process per GPU over RCCL (backend "nccl").  GRF_DIST_BACKEND=gloo rehearses the same
+    multi-process path with several ranks on one GPU (device tensors staged through host memory
+    in grf_amd.dist); the returned device index is local_rank modulo the visible GPUs."""
+    import torch
+    import torch.distributed as dist
+
+    backend = os.environ.get("GRF_DIST_BACKEND", "nccl")
+    dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group(backend)
+    return dev
+
+
 def make_graph(args):
     """The adjacency of the configured workload (scipy CSR, unit weights)."""
     if args.graph == "er":
@@ -165,8 +182,9 @@ def main_predict(args):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+        from grf_amd.dist import all_reduce as dist_all_reduce
+        local_rank = init_distributed(local_rank)
     eng = GRFEngine(f"cuda:{local_rank}")
     A = make_graph(args)
     n, m, L, p, S = A.shape[0], args.walks, args.length, args.p_halt, args.samples
@@ -216,7 +234,7 @@ def main_predict(args):
     t = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([t], dtype=torch.float64, device=eng.device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dist_all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
     nnz_tr = int((phi.ptr[tr + 1] - phi.ptr[tr]).sum().item())
     elem = 8 if dtype == torch.float64 else 4
@@ -271,7 +289,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--n", "--n-nodes", dest="n", type=int, default=100_000)
     ap.add_argument("--edges", type=int, default=1_000_000)
     ap.add_argument("--walks", type=int, default=128)
     ap.add_argument("--length", type=int, default=8)
@@ -316,6 +334,7 @@ def main():
     import torch.distributed as dist
 
     from grf_amd import _lib as C
+    from grf_amd.dist import all_reduce as dist_all_reduce
     from grf_amd.dist import allreduce_buckets, gather_phi, shard_range
     from grf_amd.engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, DeviceCSR, GRFEngine
 
@@ -323,8 +342,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        local_rank = init_distributed(local_rank)
     eng = GRFEngine(f"cuda:{local_rank}")
     dev = eng.device
 
@@ -476,10 +494,10 @@ def main():
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
     if world > 1:
         tt = torch.tensor([t], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dist_all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
         gm = torch.tensor([float(np.mean(gram_ms))], dtype=torch.float64, device=dev)
-        dist.all_reduce(gm, op=dist.ReduceOp.MAX)
+        dist_all_reduce(gm, op=dist.ReduceOp.MAX)
         gram_avg = float(gm.item())
     else:
         gram_avg = float(np.mean(gram_ms))

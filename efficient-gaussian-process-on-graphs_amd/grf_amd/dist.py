@@ -26,6 +26,42 @@ import torch
 import torch.distributed as dist
 
 
+def _host_staged(group=None) -> bool:
+    """gloo has no all-gather for device tensors, so it moves them through host memory (this is how
+    the multi-process path is rehearsed with several ranks on one GPU: GRF_DIST_BACKEND=gloo in
+    bench.py).  RCCL ("nccl") works on the device tensors directly."""
+    return dist.get_backend(group) == "gloo"
+
+
+def _all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None):
+    if out.is_cuda and _host_staged(group):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def _all_gather_list(outs, inp: torch.Tensor, group=None):
+    if inp.is_cuda and _host_staged(group):
+        o = [x.cpu() for x in outs]
+        dist.all_gather(o, inp.cpu(), group=group)
+        for x, y in zip(outs, o):
+            x.copy_(y)
+    else:
+        dist.all_gather(outs, inp, group=group)
+
+
+def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None):
+    """In-place all-reduce of a device (or host) tensor; host-staged under gloo."""
+    if t.is_cuda and _host_staged(group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     """Contiguous source range of ``rank`` (np.array_split boundaries)."""
     base, extra = divmod(n, world)
@@ -46,7 +82,7 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
     nnz_local = int(ptr[-1].item()) if n_local >= 0 else 0
     sizes = torch.tensor([n_local, nnz_local], dtype=torch.int64, device=dev)
     all_sizes = [torch.empty_like(sizes) for _ in range(world)]
-    dist.all_gather(all_sizes, sizes, group=group)
+    _all_gather_list(all_sizes, sizes, group=group)
     all_sizes = torch.stack(all_sizes).cpu()
     n_max, nnz_max = int(all_sizes[:, 0].max()), int(all_sizes[:, 1].max())
 
@@ -62,9 +98,9 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
     g_counts = torch.empty(world * n_max, dtype=torch.int64, device=dev)
     g_idx = torch.empty(world * z, dtype=idx.dtype, device=dev)
     g_val = torch.empty(world * z, dtype=val.dtype, device=dev)
-    dist.all_gather_into_tensor(g_counts, counts, group=group)
-    dist.all_gather_into_tensor(g_idx, idx_pad, group=group)
-    dist.all_gather_into_tensor(g_val, val_pad, group=group)
+    _all_gather_into(g_counts, counts, group=group)
+    _all_gather_into(g_idx, idx_pad, group=group)
+    _all_gather_into(g_val, val_pad, group=group)
     g_counts, g_idx, g_val = g_counts.view(world, n_max), g_idx.view(world, z), g_val.view(world, z)
 
     parts_c, parts_i, parts_v = [], [], []
@@ -92,7 +128,7 @@ def gather_phi(engine, local, count_ws=None, group=None, band_width=None):
     n = local.n_cols
     if count_ws is not None and dist.get_world_size(group) > 1:
         nbk = -(-n // (band_width or DEFAULT_BAND_WIDTH)) * n
-        dist.all_reduce(count_ws[:4 * nbk].view(torch.int32), group=group)
+        all_reduce(count_ws[:4 * nbk].view(torch.int32), group=group)
     if dist.get_world_size(group) == 1:
         return local
     ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32, group)
@@ -108,7 +144,7 @@ def allreduce_buckets(t: torch.Tensor, bucket_bytes: int = 1 << 30, group=None) 
     rows_per = max(1, bucket_bytes // max(1, t.stride(0) * t.element_size()))
     base = t.as_strided((t.shape[0], t.stride(0)), (t.stride(0), 1)) if t.dim() == 2 else t.view(-1, 1)
     for r0 in range(0, base.shape[0], rows_per):
-        dist.all_reduce(base[r0:r0 + rows_per], group=group)
+        all_reduce(base[r0:r0 + rows_per], group=group)
     return t
 
 
