@@ -68,9 +68,10 @@ __device__ inline T block_exclusive_scan_fast(T v, T *scratch, T *total) {
     return before + inc - v;
 }
 
-// In-LDS bitonic sort (ascending) of P = power-of-two 64-bit keys by the whole
+// In-LDS bitonic sort (ascending) of P = power-of-two 32- or 64-bit keys by the whole
 // workgroup.  Caller must __syncthreads() before (keys written) and after.
-__device__ inline void block_bitonic_sort(uint64_t *key, int P) {
+template <typename KT>
+__device__ inline void block_bitonic_sort(KT *key, int P) {
     for (int k = 2; k <= P; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = threadIdx.x; i < (P >> 1); i += blockDim.x) {
@@ -78,7 +79,7 @@ __device__ inline void block_bitonic_sort(uint64_t *key, int P) {
                 int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
                 int hi = lo | j;
                 bool asc = (lo & k) == 0;
-                uint64_t a = key[lo], b = key[hi];
+                const KT a = key[lo], b = key[hi];
                 if ((a > b) == asc) {
                     key[lo] = b;
                     key[hi] = a;

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void steps_kernel(int64_t m, int32_t norm, int
     }
     __syncthreads();
 #ifndef GRF_EXP_NOSORT
-    block_bitonic_sort(key, P);
+    block_bitonic_sort<uint64_t>(key, P);
 #endif
     // contiguous chunk per thread
     const int T = blockDim.x;
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void phi_merge_kernel(int64_t n_src, int64_t m
 // workgroup (kWalk = true, grf_walk_phi: no slot round trip through HBM).
 constexpr int kPhiMaxPer = 16;  // sorted positions per thread (P <= 4096, 256 threads)
 
-template <bool kWalk, int kPer>  // kPer = P / blockDim.x sorted positions per thread
+template <bool kWalk, int kPer, typename KT>  // kPer = P / blockDim.x sorted positions per thread
 __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, int32_t norm, int32_t P, int32_t wbits,
                                                         int32_t lbits, const int32_t *__restrict__ slot_node,
                                                         const double *__restrict__ slot_load,
@@ -152,24 +152,28 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         double *__restrict__ phi_val, float *__restrict__ phi_val32,
                                                         int32_t *__restrict__ t_count, int64_t band_width,
                                                         int64_t n_cols) {
+    // LDS: ld [E] loads by slot (later the compacted step values), fl [64] the modulator,
+    // scratch (2 x 16 ints), key [P] the sorted keys (later the compacted step keys).  32-bit
+    // keys when (node, step, walk) fits 32 bits (C4 / C5): half the sort's LDS traffic and a
+    // third of the footprint of the 64-bit layout with its separate head-value array.
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int E = (int)(m * L), T = (int)blockDim.x, tid = (int)threadIdx.x;
-    uint64_t *key = smem;                               // [P]  sorted keys, later compacted step keys
-    double *ld = reinterpret_cast<double *>(smem + P);  // [E]  loads by slot, later compacted step values
-    double *mv = ld + E;                                // [P]  step values at (node, step) run heads
-    double *fl = mv + P;                                // [64] the modulator
-    int32_t *scratch = reinterpret_cast<int32_t *>(fl + 64);  // block-scan scratch (2 x 16 ints)
+    double *ld = reinterpret_cast<double *>(smem);             // [E]
+    double *fl = ld + E;                                        // [64]
+    int32_t *scratch = reinterpret_cast<int32_t *>(fl + 64);    // [32]
+    KT *key = reinterpret_cast<KT *>(scratch + 32);             // [P]
+    const KT kNone = (KT)~(KT)0;
     const int64_t s = blockIdx.x;
     const int sh = wbits + lbits;
-    const uint64_t wmask = (1ull << wbits) - 1ull, lmask = (1ull << lbits) - 1ull;
+    const KT wmask = (KT)(((KT)1 << wbits) - 1), lmask = (KT)(((KT)1 << lbits) - 1);
     auto make_key = [&](int32_t node, int l, int64_t w) {
-        return ((uint64_t)(uint32_t)node << sh) | ((uint64_t)l << wbits) | (uint64_t)w;
+        return (KT)(((KT)(uint32_t)node << sh) | ((KT)l << wbits) | (KT)w);
     };
 
     for (int l = tid; l < Lf; l += T) fl[l] = f[l];
     // ---- slots -> keys
     if (kWalk) {
-        for (int t = tid; t < P; t += T) key[t] = ~0ull;
+        for (int t = tid; t < P; t += T) key[t] = kNone;
         __syncthreads();
         const int64_t src = src_begin + s;
         for (int64_t w = tid; w < m; w += T)
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         const int32_t *nd = slot_node + s * E;
         const double *sl = slot_load + s * E;
         for (int t = tid; t < P; t += T) {
-            uint64_t k = ~0ull;
+            KT k = kNone;
             if (t < E) {
                 const int32_t v = nd[t];
                 if (v >= 0) {
@@ -196,60 +200,53 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     }
     __syncthreads();
 #ifndef GRF_EXP_NOSORT
-    block_bitonic_sort(key, P);
+    block_bitonic_sort<KT>(key, P);
 #endif
 
-    // ---- step values at (node, step) run heads: loads in walk order from 0.0 (the run is
-    //      read 8 keys / loads per LDS round trip; the source's step-0 run is m long)
-    for (int i = tid; i < P; i += T) {
-        const uint64_t k = key[i];
-        if (k == ~0ull || (i > 0 && (key[i - 1] >> wbits) == (k >> wbits))) continue;
-        const uint64_t hk = k >> wbits;
-        const uint64_t k1 = i + 1 < P ? key[i + 1] : ~0ull;
-        double acc = 0.0 + ld[((k >> wbits) & lmask) * m + (k & wmask)];
-        if ((k1 >> wbits) == hk) {  // a run of more than one visit: 8 keys / loads per round trip
-            acc += ld[((k1 >> wbits) & lmask) * m + (k1 & wmask)];
-            for (int j = i + 2;; j += 8) {
-                uint64_t kk[8];
-                double lv[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) kk[q] = j + q < P ? key[j + q] : ~0ull;
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    lv[q] = (kk[q] >> wbits) == hk ? ld[((kk[q] >> wbits) & lmask) * m + (kk[q] & wmask)] : 0.0;
-                bool more = true;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    if ((kk[q] >> wbits) == hk) acc += lv[q];  // keys are sorted: the run is contiguous
-                    else more = false;
-                }
-                if (!more) break;
-            }
-        }
-        mv[i] = normalise(acc, norm, m);
-    }
-    __syncthreads();
-
-    // ---- compact the step heads (sorted order): key -> key[rank], value -> ld[rank]
+    // ---- step values at (node, step) run heads, kept in registers: loads in walk order from
+    //      0.0 (the run is read 8 keys / loads per LDS round trip; the source's step-0 run is m
+    //      long); thread t owns the sorted positions [t kPer, (t + 1) kPer)
     const int i0 = tid * kPer;
-    uint64_t hk_[kPer];
+    KT hk_[kPer];
     double hv_[kPer];
     int c = 0;
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
         const int i = i0 + q;
-        const uint64_t k = key[i];
-        const bool head = k != ~0ull && (i == 0 || (key[i - 1] >> wbits) != (k >> wbits));
-        if (head) {
+        const KT k = key[i];
+        if (k == kNone || (i > 0 && (key[i - 1] >> wbits) == (k >> wbits))) continue;
+        const KT hk = k >> wbits;
+        const KT k1 = i + 1 < P ? key[i + 1] : kNone;
+        double acc = 0.0 + ld[((k >> wbits) & lmask) * m + (k & wmask)];
+        if ((k1 >> wbits) == hk) {  // a run of more than one visit: 8 keys / loads per round trip
+            acc += ld[((k1 >> wbits) & lmask) * m + (k1 & wmask)];
+            for (int j = i + 2;; j += 8) {
+                KT kk[8];
+                double lv[8];
 #pragma unroll
-            for (int e = 0; e < kPer; ++e)  // static register indexing
-                if (e == c) {
-                    hk_[e] = k;
-                    hv_[e] = mv[i];
+                for (int r = 0; r < 8; ++r) kk[r] = j + r < P ? key[j + r] : kNone;
+#pragma unroll
+                for (int r = 0; r < 8; ++r)
+                    lv[r] = (kk[r] >> wbits) == hk ? ld[((kk[r] >> wbits) & lmask) * m + (kk[r] & wmask)] : 0.0;
+                bool more = true;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    if ((kk[r] >> wbits) == hk) acc += lv[r];  // keys are sorted: the run is contiguous
+                    else more = false;
                 }
-            ++c;
+                if (!more) break;
+            }
         }
+        const double v = normalise(acc, norm, m);
+#pragma unroll
+        for (int e = 0; e < kPer; ++e)  // static register indexing
+            if (e == c) {
+                hk_[e] = k;
+                hv_[e] = v;
+            }
+        ++c;
     }
+    // ---- compact the step heads (sorted order): key -> key[rank], value -> ld[rank]
     int32_t n_heads;
     const int32_t rank0 = block_exclusive_scan_fast<int32_t>(c, scratch, &n_heads);  // (barrier: reads done)
 #pragma unroll
@@ -270,7 +267,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     for (int qq = 0; qq < per2; ++qq) {
         const int q = q0 + qq;
         if (q >= n_heads) break;
-        const uint64_t k = key[q];
+        const KT k = key[q];
         if (q > 0 && (key[q - 1] >> sh) == (k >> sh)) continue;  // not a node head
         double acc = 0.0;
         bool present = false;
@@ -390,7 +387,10 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     const int P = std::max(64, (int)next_pow2_u32((uint32_t)E));
     const int wbits = ceil_log2((uint64_t)m), lbits = ceil_log2((uint64_t)L) > 0 ? ceil_log2((uint64_t)L) : 1;
     GRF_REQUIRE(wbits + lbits <= 32, GRF_EUNSUPPORTED, "grf_phi_fused: key overflow");
-    const size_t lds = (size_t)P * 8 + (size_t)E * 8 + (size_t)P * 8 + 64 * 8 + 128;
+    // 32-bit keys when every key (node << (wbits + lbits) | step | walk) < the sentinel 2^32 - 1:
+    // needs the node-id bound n_cols, known for the walking kernel (the slots path stays 64-bit)
+    const bool key32 = walk && n_cols > 0 && ((uint64_t)n_cols << (wbits + lbits)) <= 0xffffffffull;
+    const size_t lds = (size_t)E * 8 + 64 * 8 + 32 * 4 + (size_t)P * (key32 ? 4 : 8);
     // threads per source: P / 4 up to 256, and at most two per walk -- measured (tools/walkphi_ab.py):
     // m = 128 (C4) 256 threads 3.37 ms vs 128 4.20; m = 64 (C5) 128 threads 14.3 ms vs 256 19.6 (idle
     // waves hold the source's slot while the walk runs); GRF_PHI_THREADS caps it for experiments
@@ -406,11 +406,16 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     GRF_REQUIRE(P / T <= kPhiMaxPer, GRF_EUNSUPPORTED, "grf_phi_fused: too many positions per thread");
     const int32_t Lf = n_f < L ? n_f : L;
     GRF_REQUIRE_GRID(n_src, T, "phi_fused_kernel");
-#define GRF_PHI_LAUNCH(W, K)                                                                                      \
-    phi_fused_kernel<W, K><<<(unsigned)n_src, T, lds, st>>>(                                                      \
+#define GRF_PHI_LAUNCH_KT(W, K, KT)                                                                               \
+    phi_fused_kernel<W, K, KT><<<(unsigned)n_src, T, lds, st>>>(                                                  \
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val, p_halt, rule, (uint32_t)seed,    \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
         n_cols)
+#define GRF_PHI_LAUNCH(W, K)                                                                                      \
+    do {                                                                                                          \
+        if (key32) GRF_PHI_LAUNCH_KT(W, K, uint32_t);                                                             \
+        else GRF_PHI_LAUNCH_KT(W, K, uint64_t);                                                                   \
+    } while (0)
 #define GRF_PHI_PER(W)                                                                                            \
     switch (P / T) {                                                                                              \
         case 1: GRF_PHI_LAUNCH(W, 1); break;                                                                      \
@@ -422,6 +427,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     if (walk) { GRF_PHI_PER(true) } else { GRF_PHI_PER(false) }
 #undef GRF_PHI_PER
 #undef GRF_PHI_LAUNCH
+#undef GRF_PHI_LAUNCH_KT
     GRF_CHECK_LAUNCH("phi_fused_kernel");
     return GRF_OK;
 }

@@ -23,9 +23,10 @@ bw = int(os.environ.get("GRF_BW", DEFAULT_BAND_WIDTH))
 tws = eng.transpose_workspace(n, n, bw)
 phi = eng.compact(eng.walk_phi(G, 128, 0.1, 8, diffusion_modulator(8), seed=42, count_ws=tws,
                                band_width=bw), want64=False, sync_free=True)
-tr = eng.transpose_banded(phi, bw, counted_ws=tws, nnz_bound=phi.nnz_bound)
+ru = int(os.environ["GRF_REC_UNIT"]) if "GRF_REC_UNIT" in os.environ else None
+tr = eng.transpose_banded(phi, bw, counted_ws=tws, nnz_bound=phi.nnz_bound, rec_unit=ru)
 K = torch.empty((n, eng.leading_dim(n)), dtype=torch.float32, device=eng.device)
-out = {"n": n, "bw": bw}
+out = {"n": n, "bw": bw, "rec_unit": tr.rec_unit, "t_rec_MB": tr.t_rec.numel() / 1e6}
 
 
 def timed(fn):
