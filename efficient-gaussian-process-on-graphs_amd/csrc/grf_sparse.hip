@@ -419,9 +419,15 @@ __global__ __launch_bounds__(256) void tr_place_kernel(int64_t n_rows, int64_t n
     }
 }
 
-static int32_t tr_region_cols(int64_t n_cols) {
+// Region width: at most 4096 regions per band, and every placing workgroup reads one table
+// entry per binning workgroup of its band, n_rows * n_cols / (16 cr) scattered reads in all --
+// kept <= 32 M (C4: cr = 128, 4.9 M; C5, N = 1M: cr = 2048 instead of 256, where 244 M reads
+// took 4.9 ms of the placing pass).
+static int32_t tr_region_cols(int64_t n_rows, int64_t n_cols) {
     int64_t cr = kRegionCols;
-    while (cdiv<int64_t>(n_cols, cr) > 4096) cr *= 2;
+    while (cr < 65536 && (cdiv<int64_t>(n_cols, cr) > 4096 ||
+                          (double)std::max<int64_t>(n_rows, 1) * (double)n_cols / (16.0 * (double)cr) > 32e6))
+        cr *= 2;
     return (int32_t)cr;
 }
 
@@ -540,7 +546,7 @@ int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_w
 
 size_t grf_transpose_staging_bytes(int64_t n_rows, int64_t n_cols, int64_t band_width, int64_t nnz) {
     if (n_cols <= 0 || band_width <= 0) return 0;
-    const int64_t nreg = cdiv<int64_t>(n_cols, tr_region_cols(n_cols)), nwg = cdiv<int64_t>(n_rows, kBinRows);
+    const int64_t nreg = cdiv<int64_t>(n_cols, tr_region_cols(n_rows, n_cols)), nwg = cdiv<int64_t>(n_rows, kBinRows);
     return tr_align((size_t)nnz * 8) + tr_align((size_t)std::max<int64_t>(n_rows, 1) * 8) +
            tr_align((size_t)std::max<int64_t>(nwg, 1) * (nreg + 1) * 4) + tr_align((size_t)std::max<int64_t>(nwg, 1) * 4);
 }
@@ -560,7 +566,7 @@ int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t
     GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL,
                 "grf_transpose_banded_fill_staged: t_rec must be 128-byte aligned");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
-    const int32_t cr = tr_region_cols(n_cols);
+    const int32_t cr = tr_region_cols(n_rows, n_cols);
     GRF_REQUIRE(cr <= 65536, GRF_EUNSUPPORTED, "grf_transpose_banded_fill_staged: too many columns");
     const int32_t nreg = (int32_t)cdiv<int64_t>(n_cols, cr);
     GRF_REQUIRE(workspace_bytes >= grf_transpose_workspace_bytes(nbk), GRF_EINVAL,

@@ -336,15 +336,16 @@ int32_t grf_steps(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32
     GRF_REQUIRE(m <= 16384, GRF_EUNSUPPORTED, "grf_steps: walks_per_node > 16384 not supported by this build");
     if (n_src == 0) return GRF_OK;
     const int P = (int)next_pow2_u32((uint32_t)m);
-    // threads per source: P / 4 up to 256, and at most two per walk -- measured (tools/walkphi_ab.py):
-    // m = 128 (C4) 256 threads 3.37 ms vs 128 4.20; m = 64 (C5) 128 threads 14.3 ms vs 256 19.6 (idle
-    // waves hold the source's slot while the walk runs); GRF_PHI_THREADS caps it for experiments
+    // threads per source: P / 4 up to 256, and at most one per walk -- measured (tools/walkphi_ab.py)
+    // with the 12.9 KB LDS layout: m = 128 (C4) 128 threads 2.85 ms vs 256 3.28; m = 64 (C5) 64
+    // threads 11.2 ms vs 128 13.0 (idle waves hold the source's slot while its walks run, and LDS
+    // no longer caps the sources per CU); GRF_PHI_THREADS caps it for experiments
     static const int t_env = [] {
         const char *e = getenv("GRF_PHI_THREADS");
         const int v = e ? atoi(e) : 0;
         return (v == 64 || v == 128 || v == 256) ? v : 0;
     }();
-    const int t_cap = t_env ? t_env : (int)std::min<int64_t>(256, std::max<int64_t>(64, 2 * ((m + 63) / 64) * 64));
+    const int t_cap = t_env ? t_env : (int)std::min<int64_t>(256, std::max<int64_t>(64, ((m + 63) / 64) * 64));
     int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
     while (T > t_cap && P / (T / 2) <= kPhiMaxPer) T /= 2;
     const size_t lds = (size_t)P * sizeof(uint64_t) + 128;
@@ -391,15 +392,16 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     // needs the node-id bound n_cols, known for the walking kernel (the slots path stays 64-bit)
     const bool key32 = walk && n_cols > 0 && ((uint64_t)n_cols << (wbits + lbits)) <= 0xffffffffull;
     const size_t lds = (size_t)E * 8 + 64 * 8 + 32 * 4 + (size_t)P * (key32 ? 4 : 8);
-    // threads per source: P / 4 up to 256, and at most two per walk -- measured (tools/walkphi_ab.py):
-    // m = 128 (C4) 256 threads 3.37 ms vs 128 4.20; m = 64 (C5) 128 threads 14.3 ms vs 256 19.6 (idle
-    // waves hold the source's slot while the walk runs); GRF_PHI_THREADS caps it for experiments
+    // threads per source: P / 4 up to 256, and at most one per walk -- measured (tools/walkphi_ab.py)
+    // with the 12.9 KB LDS layout: m = 128 (C4) 128 threads 2.85 ms vs 256 3.28; m = 64 (C5) 64
+    // threads 11.2 ms vs 128 13.0 (idle waves hold the source's slot while its walks run, and LDS
+    // no longer caps the sources per CU); GRF_PHI_THREADS caps it for experiments
     static const int t_env = [] {
         const char *e = getenv("GRF_PHI_THREADS");
         const int v = e ? atoi(e) : 0;
         return (v == 64 || v == 128 || v == 256) ? v : 0;
     }();
-    const int t_cap = t_env ? t_env : (int)std::min<int64_t>(256, std::max<int64_t>(64, 2 * ((m + 63) / 64) * 64));
+    const int t_cap = t_env ? t_env : (int)std::min<int64_t>(256, std::max<int64_t>(64, ((m + 63) / 64) * 64));
     int T = P >= 512 ? 256 : (P >= 128 ? P / 2 : 64);
     while (T > t_cap && P / (T / 2) <= kPhiMaxPer) T /= 2;
     GRF_REQUIRE(n_f <= 64 || L <= 64, GRF_EUNSUPPORTED, "grf_phi_fused: max_walk_length > 64");

@@ -538,3 +538,22 @@ def test_sharded_counts_and_phi_equal_single_gpu(eng):
     for r in range(world):
         b, e = shard_range(n, r, world)
         assert torch.equal(eng.gram_sparse(phi, tr, b, e), K1[b:e])
+
+
+@pytest.mark.parametrize("unit", [128, 12])
+def test_transpose_wide_regions(eng, unit):
+    """A graph large enough that the staged fill widens its column regions (n_rows * n_cols / (16 cr)
+    above 32 M: cr = 256 at 300k nodes) gives the atomic fill's descriptors and the same K rows."""
+    n = 300_000
+    A = er_graph(n, 4, 21)
+    G = eng.laplacian(A)
+    phi = eng.compact(eng.walk_phi(G, 4, 0.2, 3, [1.0, -0.5, 0.25], seed=8))
+    ta = eng.transpose_banded(phi, 8192, staged=False, rec_unit=unit)
+    ts = eng.transpose_banded(phi, 8192, staged=True, rec_unit=unit)
+    assert np.array_equal(ta.t_desc.cpu().numpy(), ts.t_desc.cpu().numpy())
+    assert np.array_equal(ta.t_rowshift.cpu().numpy(), ts.t_rowshift.cpu().numpy())
+    for r0 in (0, n - 200):
+        Ka = eng.gram_sparse(phi, ta, r0, r0 + 200).cpu().numpy()
+        assert np.array_equal(Ka, eng.gram_sparse(phi, ts, r0, r0 + 200).cpu().numpy())
+    ok, fro = gram_close(eng.gram_sparse(phi, ts, 0, 50).cpu().numpy(), phi.to_scipy(), (0, 50))
+    assert ok, fro
