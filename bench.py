@@ -407,8 +407,8 @@ def main():
                 if after_gram is not None:
                     tiles_done = torch.cuda.Event()
                     tiles_done.record(main)
-            # ... + mirror (= grf_gram_sparse_sym); pipelined: a 3-per-CU grid leaves slots to the next front
-            eng.gram_mirror(K, n, 768 if after_gram is not None else 0)
+            # ... + mirror (= grf_gram_sparse_sym); pipelined: a 4-per-CU grid leaves slots to the next front
+            eng.gram_mirror(K, n, 1024 if after_gram is not None else 0)
             if after_gram is not None:
                 after_gram(tiles_done)  # (issued after the mirror: the host's launch time does not delay it)
         else:

@@ -260,8 +260,8 @@ int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_e
 
 /* The mirror pass of grf_gram_sparse_sym alone: K[j, i] = K[i, j] for every j > i.
  * max_workgroups <= 0: one workgroup per 64 x 64 block (fastest alone); > 0: at most that many
- * workgroups striding over the blocks, which leaves CU slots to work on another stream (768 =
- * 3 per CU was best beside the next step's walks: tools/gpu_mirror_ab.sh). */
+ * workgroups striding over the blocks, which leaves CU slots to work on another stream (1024 =
+ * 4 per CU was best beside the next step's walks: tools/gpu_mirror_ab.sh). */
 int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups, grf_stream_t stream);
 
 /* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
