@@ -228,3 +228,31 @@ def test_gptorch_kernels_on_golden_steps(golden):
     np.testing.assert_allclose(fm, ref, rtol=1e-6)
     Phi = sum(fl * M for fl, M in zip(fm, dense))
     np.testing.assert_allclose(dk().detach().numpy(), Phi @ Phi.T, rtol=1e-5, atol=1e-6)
+
+
+def test_record_unit_choice():
+    """Line-aligned buckets for dense buckets (C4), packed pairs for sparse ones (C5)."""
+    from grf_amd import _lib as C
+    from grf_amd.engine import choose_rec_unit
+    assert choose_rec_unit(43_484_870, 100_000, 100_000, 4096) == C.REC_LINE      # C4: ~18 entries per bucket
+    assert choose_rec_unit(100_000 * 1024, 100_000, 100_000, 8192) == C.REC_LINE  # C4 bound, row mode
+    assert choose_rec_unit(1_000_000 * 512, 1_000_000, 1_000_000, 8192) == C.REC_PACKED  # C5 bound: ~4 entries
+    assert choose_rec_unit(0, 10, 10, 64) == C.REC_PACKED
+
+
+def test_powerlaw_graph_is_simple_and_heavy_tailed():
+    from grf_amd.graphs import powerlaw_graph
+    A = powerlaw_graph(20_000, 10.0, 2.5, seed=1)
+    assert (A != A.T).nnz == 0 and A.diagonal().sum() == 0 and A.data.min() == 1.0
+    deg = np.diff(A.indptr)
+    assert 8.0 < deg.mean() < 10.5 and deg.max() > 20 * deg.mean()  # hubs
+    assert np.array_equal(A.indices, powerlaw_graph(20_000, 10.0, 2.5, seed=1).indices)  # seeded
+
+
+def test_snap_graphs_load():
+    from grf_amd.graphs import snap_graph
+    fb, en = snap_graph("facebook"), snap_graph("enron")
+    assert fb.shape == (22470, 22470) and en.shape == (36692, 36692)
+    assert (fb != fb.T).nnz == 0 and (en != en.T).nnz == 0
+    with pytest.raises(ValueError):
+        snap_graph("youtube")
