@@ -314,8 +314,9 @@ def main():
     ap.add_argument("--overlap", dest="overlap", action="store_true", default=None,
                     help="pipeline the steps on two HIP streams: step s+1's Laplacian/walks/Phi/transpose start "
                          "when step s's Gram tiles finish and run beside its HBM-bound mirror pass (default for "
-                         "the single-GPU symmetric K: 25.9 vs 27.5 ms per step; beside the gather-bound Gram of "
-                         "the row modes it gains nothing, so those default to serial steps)")
+                         "the single-GPU symmetric K: 24.3 vs 26.5 ms per step); with N > 1 (default) the next "
+                         "front, with its RCCL collectives, runs beside this step's Gram; single-GPU row modes "
+                         "gain ~1 % and default to serial steps")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false", help="serial steps")
     ap.add_argument("--front-at", type=float, default=1.0,
                     help="pipelined: the next front starts after this fraction of the Gram tiles (1 = at the mirror)")
@@ -361,7 +362,10 @@ def main():
     rows_cap = max(1, min(m * L, n))  # walk_phi's padded row capacity
     sym_mode = world == 1 and not args.no_sym and not args.k_rows and not allreduce
     if args.overlap is None:
-        args.overlap = sym_mode
+        # one GPU, whole K: the next front beside the mirror; N > 1 row blocks: the next front's
+        # collectives beside this step's Gram (the compute of a front beside a Gram gains ~1 %:
+        # single-GPU row modes stay serial)
+        args.overlap = sym_mode or (world > 1 and not allreduce)
     bw = DEFAULT_BAND_WIDTH if sym_mode else ROWS_BAND_WIDTH  # (engine.py: measured per mode)
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     last = [None]
@@ -420,9 +424,13 @@ def main():
             allreduce_buckets(K[:, :n])
         last[0] = (phi, local)
 
-    def front_on_side(after=None):
-        # (after: an event on `main`; default: everything issued on `main` so far)
-        if after is None:
+    def front_on_side(after=None, independent=False):
+        # after: an event on `main`; default: everything issued on `main` so far.  independent: no
+        # wait at all (a front reads only the resident adjacency and writes fresh buffers; buffers
+        # freed on `main` are recorded there, so the allocator does not hand them out early)
+        if independent:
+            pass
+        elif after is None:
             side.wait_stream(main)
         else:
             side.wait_event(after)
@@ -465,9 +473,11 @@ def main():
                 back_on_main(cur, record, issue_next)
                 cur = nxt[0]
             else:
-                nxt = front_on_side() if s_ + 1 < steps else None
+                # row modes: this step's Gram is issued first, then the next front, which overlaps
+                # it (its host synchronisations -- row counts, the all-gather sizes -- then no
+                # longer hold back the Gram's launch; with N > 1 the collectives run beside it)
                 back_on_main(cur, record)
-                cur = nxt
+                cur = front_on_side(independent=True) if s_ + 1 < steps else None
 
     run(args.warmup, False)
     torch.cuda.synchronize()
