@@ -278,6 +278,108 @@ def main_predict(args):
         dist.destroy_process_group()
 
 
+MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
+
+
+def cora_adjacency() -> np.ndarray:
+    """Cora (experiments/dense/cora/data/cora/cora.cites, 2,708 nodes) as the symmetric 0/1 dense
+    adjacency of tests/golden/cora.npz (made by tests/golden/make_golden.py from the reference's file)."""
+    d = np.load(os.path.join(ROOT, "tests", "golden", "cora.npz"), allow_pickle=False)
+    n = len(d["A_indptr"]) - 1
+    return sp.csr_matrix((d["A_data"], d["A_indices"], d["A_indptr"]), shape=(n, n)).toarray()
+
+
+def main_c3(args):
+    """C3: the reference's DENSE path on Cora (graph_kernels/fast_grf_kernel_general.py:11-39) --
+    numpy-semantics dense Laplacian of the dense adjacency (resident in HBM) -> Philox walks
+    (m = 128, L = 8) -> step rows (dense sampler's divide-by-m rule) -> Phi = F f -> dense
+    float32 Phi -> K = Phi Phi^T on the MFMA (gram_dense_kernel, v_mfma_f32_32x32x2_f32).
+    The roofline is the MFMA Gram's (+ its mirror pass): N (N + 1) k flops (the symmetric
+    product's unique entries) against the fp32 matrix peak."""
+    import torch
+
+    from grf_amd import _lib as C
+    from grf_amd.engine import GRFEngine
+
+    eng = GRFEngine("cuda:0")
+    W = cora_adjacency()
+    n, m, L, p = W.shape[0], args.walks, args.length, args.p_halt
+    f = diffusion_modulator(L, 1.0)
+    Wt = torch.from_numpy(W).to(eng.device)
+    gram_ev = []
+
+    def step(record):
+        G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY)
+        slots = eng.walk(G, m, p, L, rng=C.RNG_PHILOX, seed=42)
+        phi = eng.compact(eng.features(slots, f, C.NORM_DIV), want64=False)
+        dense = eng.densify(phi)
+        if record:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        K = eng.gram_dense(dense, n)
+        if record:
+            ev[1].record()
+            gram_ev.append(ev)
+        return K
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    gram_ms = float(np.mean([a.elapsed_time(b) for a, b in gram_ev]))
+    kpad = -(-n // 16) * 16
+    # the symmetric product's unique entries, 2 k flops each (the kernel computes the tiles on and
+    # above the diagonal and mirrors them; counting 2 n^2 k would credit work it does not do)
+    flops = 1.0 * n * (n + 1) * kpad
+    tfs = flops / (gram_ms * 1e-3) / 1e12
+    out = {
+        "metric": "GRF kernel-matrices/sec (Cora N=2708, dense path, m=128 walks; MFMA utilisation of the Gram)",
+        "value": args.steps / t,
+        "unit": "K-matrices/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * t / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp64 walks/Phi, fp32 MFMA Gram",
+        "data": "real graph: Cora citation graph shipped with the reference (tests/golden/cora.npz)",
+        "config": {"workload": f"C3: Cora N={n} dense adjacency resident in HBM, dense numpy-semantics Laplacian, "
+                               f"walks_per_node={m}, max_walk_length={L}, p_halt={p}, diffusion modulator beta=1, "
+                               f"Philox seed 42, dense fp32 Phi and K", "n_nodes": n},
+        "roofline": {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": tfs / MFMA_F32_PEAK_TFS, "traffic": None, "kernel": "gram_dense_kernel",
+                     "kernel_ms": gram_ms, "algorithmic_flops": flops},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_dense(W, f, m, p, L,
+                                                 int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+                                                 or min(16, os.cpu_count() or 1))
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_dense(W, f, m, p, L, n_threads):
+    """The reference's dense path restated on the host (C oracle: numpy Laplacian, PCG64 pool walks
+    on n_threads chunks, step tensor F, Phi = F f, K = Phi Phi^T with numpy's BLAS)."""
+    from oracle import oracle as O
+
+    t0 = time.perf_counter()
+    Ld = O.laplacian_dense(W, 0)
+    F = O.dense_random_walk(Ld, m, p, L, n_processes=n_threads, n_threads=n_threads)
+    phi = F @ np.asarray(f)
+    K = phi @ phi.T
+    t = time.perf_counter() - t0
+    del K
+    return {"value": 1.0 / t, "unit": "K-matrices/s", "cores": n_threads, "kind": "port",
+            "sample": f"C oracle dense path (reference algorithm, PCG64 stream, {n_threads} chunks) on {n_threads} "
+                      f"host threads, the whole K ({t:.2f} s); fp64"}
+
+
 def _phi_host(phi):
     n = phi.n_rows
     return sp.csr_matrix((phi.val32.cpu().numpy().astype(np.float64), phi.idx.cpu().numpy(), phi.ptr.cpu().numpy()),
@@ -301,9 +403,10 @@ def main():
                     help="rows: K row blocks after a Phi all-gather (default); allreduce: the north star's literal "
                          "option -- per-rank partial K over an inner-dimension slice + bucketed RCCL all-reduce, "
                          "K replicated on every rank (SURVEY.md §8e)")
-    ap.add_argument("--workload", choices=["kernel", "predict", "c5"], default="kernel",
+    ap.add_argument("--workload", choices=["kernel", "predict", "c5", "c3"], default="kernel",
                     help="kernel: K = Phi Phi^T (headline); predict: pathwise-conditioning posterior samples; "
-                         "c5: SURVEY.md C5 -- N=1M power-law graph, m=64, Phi + a K row block per GPU")
+                         "c5: SURVEY.md C5 -- N=1M power-law graph, m=64, Phi + a K row block per GPU; "
+                         "c3: Cora dense path with the MFMA Gram")
     ap.add_argument("--graph", choices=["er", "powerlaw", "facebook", "enron"], default="er",
                     help="er: Erdos-Renyi with --edges edges (C4); powerlaw: Chung-Lu, exponent 2.5, mean degree "
                          "--avg-degree (C5); facebook / enron: the reference's shipped social graphs")
@@ -330,6 +433,8 @@ def main():
         args.n = None
     if args.workload == "predict":
         return main_predict(args)
+    if args.workload == "c3":
+        return main_c3(args)
 
     import torch
     import torch.distributed as dist

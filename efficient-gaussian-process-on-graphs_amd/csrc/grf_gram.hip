@@ -421,59 +421,94 @@ __global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, int64_t nt,
 __global__ void absmax_reset_kernel(float *m) { *m = 0.f; }
 
 // ------------------------------------------------------------------ dense MFMA
-constexpr int kBM = 128, kBK = 16, kPad = 4;
+// K = A A^T (A: n x k_dim fp32, row-major) on v_mfma_f32_32x32x2f32 (exact f32 FMA chains).
+// Symmetric: only the tiles on and above the diagonal are computed (the mirror pass copies the
+// upper triangle down), so a launch does n^2 k instead of 2 n^2 k flops.  A workgroup of 4 waves
+// (2 x 2) owns a BM x BM tile, each wave (BM/2)^2 as (BM/64)^2 MFMA blocks of 32 x 32; the
+// k-tiles (BK deep, staged k-major through LDS) are software-pipelined: the next tile's global
+// loads are in flight in registers while the current one feeds the MFMAs.  BM = 64 for small n
+// (more workgroups than CUs), 128 otherwise.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kDensePad = 4;
 
-__global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t k_dim, const float *__restrict__ A,
-                                                         int64_t lda, float *__restrict__ K, int64_t ldk) {
-    __shared__ __attribute__((aligned(16))) float As[kBK][kBM + kPad];
-    __shared__ __attribute__((aligned(16))) float Bs[kBK][kBM + kPad];
+template <int BM, int BK>
+__global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, int64_t k_dim,
+                                                         const float *__restrict__ A, int64_t lda,
+                                                         float *__restrict__ K, int64_t ldk) {
+    constexpr int NB = BM / 64;          // 32 x 32 MFMA blocks per wave and dimension
+    constexpr int F4 = BM * BK / 4 / 256;  // float4 loads per thread and operand per k-tile
+    __shared__ __attribute__((aligned(16))) float As[BK][BM + kDensePad];
+    __shared__ __attribute__((aligned(16))) float Bs[BK][BM + kDensePad];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    const int64_t m0 = (int64_t)blockIdx.y * kBM, n0 = (int64_t)blockIdx.x * kBM;
-    f32x16 c[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) c[a][b][q] = 0.f;
+    // block -> (bi, bj), bj >= bi, row-major over the upper triangle of the nt x nt tile grid
+    const int64_t b = blockIdx.x;
+    int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
+    auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };
+    if (bi < 0) bi = 0;
+    if (bi > nt - 1) bi = nt - 1;
+    while (bi > 0 && first(bi) > b) --bi;
+    while (bi < nt - 1 && first(bi + 1) <= b) ++bi;
+    const int64_t bj = bi + (b - first(bi));
+    const int64_t m0 = bi * BM, n0 = bj * BM;
 
-    for (int64_t k0 = 0; k0 < k_dim; k0 += kBK) {
-        // stage: 128 rows x 16 k of A (M tile) and of A (N tile), transposed to [k][row]
+    f32x16 c[NB][NB];
 #pragma unroll
-        for (int it = 0; it < 2; ++it) {
-            const int idx = tid + it * 256;        // 0..511 float4 slots
-            const int row = idx >> 2, kq = (idx & 3) * 4;
-            float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
-            if (m0 + row < n) va = *reinterpret_cast<const float4 *>(A + (m0 + row) * lda + k0 + kq);
-            if (n0 + row < n) vb = *reinterpret_cast<const float4 *>(A + (n0 + row) * lda + k0 + kq);
-            As[kq + 0][row] = va.x; As[kq + 1][row] = va.y; As[kq + 2][row] = va.z; As[kq + 3][row] = va.w;
-            Bs[kq + 0][row] = vb.x; Bs[kq + 1][row] = vb.y; Bs[kq + 2][row] = vb.z; Bs[kq + 3][row] = vb.w;
+    for (int x = 0; x < NB; ++x)
+#pragma unroll
+        for (int y = 0; y < NB; ++y)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) c[x][y][q] = 0.f;
+
+    float4 ra[F4], rb[F4];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int it = 0; it < F4; ++it) {
+            const int idx = tid + it * 256;
+            const int row = idx / (BK / 4), kq = (idx % (BK / 4)) * 4;
+            ra[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rb[it] = ra[it];
+            if (m0 + row < n) ra[it] = *reinterpret_cast<const float4 *>(A + (m0 + row) * lda + k0 + kq);
+            if (n0 + row < n) rb[it] = *reinterpret_cast<const float4 *>(A + (n0 + row) * lda + k0 + kq);
+        }
+    };
+    load(0);
+    for (int64_t k0 = 0; k0 < k_dim; k0 += BK) {
+        __syncthreads();  // (the previous tile's MFMA reads are done)
+#pragma unroll
+        for (int it = 0; it < F4; ++it) {
+            const int idx = tid + it * 256;
+            const int row = idx / (BK / 4), kq = (idx % (BK / 4)) * 4;
+            As[kq + 0][row] = ra[it].x; As[kq + 1][row] = ra[it].y; As[kq + 2][row] = ra[it].z; As[kq + 3][row] = ra[it].w;
+            Bs[kq + 0][row] = rb[it].x; Bs[kq + 1][row] = rb[it].y; Bs[kq + 2][row] = rb[it].z; Bs[kq + 3][row] = rb[it].w;
         }
         __syncthreads();
+        if (k0 + BK < k_dim) load(k0 + BK);  // in flight during the MFMAs below
 #pragma unroll
-        for (int kk = 0; kk < kBK; kk += 2) {
+        for (int kk = 0; kk < BK; kk += 2) {
             const int kr = kk + (lane >> 5), rc = lane & 31;
-            float a0 = As[kr][wm * 64 + rc], a1 = As[kr][wm * 64 + 32 + rc];
-            float b0 = Bs[kr][wn * 64 + rc], b1 = Bs[kr][wn * 64 + 32 + rc];
-            c[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, c[0][0], 0, 0, 0);
-            c[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, c[0][1], 0, 0, 0);
-            c[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, c[1][0], 0, 0, 0);
-            c[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, c[1][1], 0, 0, 0);
+            float a[NB], bv[NB];
+#pragma unroll
+            for (int x = 0; x < NB; ++x) {
+                a[x] = As[kr][wm * (BM / 2) + x * 32 + rc];
+                bv[x] = Bs[kr][wn * (BM / 2) + x * 32 + rc];
+            }
+#pragma unroll
+            for (int x = 0; x < NB; ++x)
+#pragma unroll
+                for (int y = 0; y < NB; ++y) c[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], bv[y], c[x][y], 0, 0, 0);
         }
-        __syncthreads();
     }
     // C/D map (32x32): col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int x = 0; x < NB; ++x)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int y = 0; y < NB; ++y)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int64_t row = m0 + wm * 64 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
-                const int64_t col = n0 + wn * 64 + b * 32 + (lane & 31);
-                if (row < n && col < n) K[row * ldk + col] = c[a][b][q];
+                const int64_t row = m0 + wm * (BM / 2) + x * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+                const int64_t col = n0 + wn * (BM / 2) + y * 32 + (lane & 31);
+                if (row < n && col < n) K[row * ldk + col] = c[x][y][q];
             }
 }
 
@@ -653,13 +688,19 @@ int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, fl
     GRF_REQUIRE(lda % 16 == 0 && ((uintptr_t)A & 15) == 0, GRF_EINVAL,
                 "grf_gram_dense: lda must be a multiple of 16 and A 16-byte aligned");
     if (n == 0) return GRF_OK;
-    const int64_t kpad = cdiv<int64_t>(k_dim, kBK) * kBK;
-    GRF_REQUIRE(kpad <= lda, GRF_EINVAL, "grf_gram_dense: lda must cover k_dim rounded up to 16");
-    const int64_t tiles = cdiv<int64_t>(n, kBM);
-    dim3 grid((unsigned)tiles, (unsigned)tiles);
-    gram_dense_kernel<<<grid, 256, 0, S(stream)>>>(n, kpad, A, lda, K, ldk);
+    // tile: 128 when the upper triangle of 128-tiles gives >= 2 workgroups per CU (n >= ~4.5 k), else 64
+    const int64_t nt128 = cdiv<int64_t>(n, 128);
+    const bool big = nt128 * (nt128 + 1) / 2 >= 512;
+    const int bk = (!big && lda % 32 == 0) ? 32 : 16;  // (zero padding up to lda covers the last k-tile)
+    const int64_t kpad = cdiv<int64_t>(k_dim, bk) * bk;
+    GRF_REQUIRE(kpad <= lda, GRF_EINVAL, "grf_gram_dense: lda must cover k_dim rounded up to %d", bk);
+    const int64_t nt = cdiv<int64_t>(n, big ? 128 : 64), tiles = nt * (nt + 1) / 2;
+    GRF_REQUIRE_GRID(tiles, 256, "gram_dense_kernel");
+    if (big) gram_dense_kernel<128, 16><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
+    else if (bk == 32) gram_dense_kernel<64, 32><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
+    else gram_dense_kernel<64, 16><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
     GRF_CHECK_LAUNCH("gram_dense_kernel");
-    return GRF_OK;
+    return grf_gram_mirror(n, K, ldk, 0, stream);  // the lower triangle
 }
 
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,

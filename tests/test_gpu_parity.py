@@ -339,7 +339,7 @@ def test_gram_kslice_partials_sum_to_K(eng, world):
                           eng.gram_sparse_kslice(phi, tr, kb, ke).cpu().numpy()[100:400])
 
 
-@pytest.mark.parametrize("n", [1, 31, 128, 1000, 2708])
+@pytest.mark.parametrize("n", [1, 31, 64, 65, 128, 1000, 2708, 4500])
 def test_gram_dense_mfma_vs_oracle(eng, n):
     A = er_graph(max(n, 2), 6, n + 1)[:n, :n]
     G = eng.laplacian(A)
@@ -348,6 +348,7 @@ def test_gram_dense_mfma_vs_oracle(eng, n):
     K = eng.gram(phi, "dense").cpu().numpy()
     ok, fro = gram_close(K, phi.to_scipy())
     assert ok, fro
+    assert np.array_equal(K, K.T)  # (upper tiles + mirror: exactly symmetric)
 
 
 def test_gram_dense_asymmetric_layout(eng):
