@@ -429,7 +429,11 @@ __global__ void absmax_reset_kernel(float *m) { *m = 0.f; }
 // loads are in flight in registers while the current one feeds the MFMAs.  BM = 64 for small n
 // (more workgroups than CUs), 128 otherwise.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int kDensePad = 4;
+// k-major LDS image, row pitch BM + 32 (the two k-rows one MFMA operand read spans fall on
+// disjoint bank halves) and rows XOR-swizzled by the k group: the transposing stores (8 k-groups
+// x 8 rows per wave) and the operand reads are both conflict-free
+constexpr int kDensePad = 32;
+__device__ __forceinline__ int dense_swz(int k) { return ((k >> 2) & 7) << 3; }
 
 template <int BM, int BK>
 __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, int64_t k_dim,
@@ -479,19 +483,20 @@ __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, 
         for (int it = 0; it < F4; ++it) {
             const int idx = tid + it * 256;
             const int row = idx / (BK / 4), kq = (idx % (BK / 4)) * 4;
-            As[kq + 0][row] = ra[it].x; As[kq + 1][row] = ra[it].y; As[kq + 2][row] = ra[it].z; As[kq + 3][row] = ra[it].w;
-            Bs[kq + 0][row] = rb[it].x; Bs[kq + 1][row] = rb[it].y; Bs[kq + 2][row] = rb[it].z; Bs[kq + 3][row] = rb[it].w;
+            const int sr = row ^ dense_swz(kq);
+            As[kq + 0][sr] = ra[it].x; As[kq + 1][sr] = ra[it].y; As[kq + 2][sr] = ra[it].z; As[kq + 3][sr] = ra[it].w;
+            Bs[kq + 0][sr] = rb[it].x; Bs[kq + 1][sr] = rb[it].y; Bs[kq + 2][sr] = rb[it].z; Bs[kq + 3][sr] = rb[it].w;
         }
         __syncthreads();
         if (k0 + BK < k_dim) load(k0 + BK);  // in flight during the MFMAs below
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 2) {
-            const int kr = kk + (lane >> 5), rc = lane & 31;
+            const int kr = kk + (lane >> 5), rc = lane & 31, sw = dense_swz(kr);
             float a[NB], bv[NB];
 #pragma unroll
             for (int x = 0; x < NB; ++x) {
-                a[x] = As[kr][wm * (BM / 2) + x * 32 + rc];
-                bv[x] = Bs[kr][wn * (BM / 2) + x * 32 + rc];
+                a[x] = As[kr][(wm * (BM / 2) + x * 32 + rc) ^ sw];
+                bv[x] = Bs[kr][(wn * (BM / 2) + x * 32 + rc) ^ sw];
             }
 #pragma unroll
             for (int x = 0; x < NB; ++x)
