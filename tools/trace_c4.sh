@@ -1,0 +1,9 @@
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+O=$R/gpurun_out/c4trace
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
+    python3 $R/bench.py --steps 6 --warmup 1 --no-cpu-baseline > $O/trace.log 2>&1 && echo TRACE_OK
+find $O -name "*kernel_trace.csv" | head -1 | xargs -I{} cp {} $O/kernel_trace.csv
+find $O -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/kernel_stats.csv
