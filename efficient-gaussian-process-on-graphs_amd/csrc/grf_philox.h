@@ -79,4 +79,44 @@ __device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const i
     return L;
 }
 
+// The same walk over the "augmented" walk matrix: aug[e] = {target node, its row start (32 bits),
+// its row length, 0} for every entry e, so a step is ONE dependent round trip (the chosen entry's
+// record and weight) instead of two (the chosen entry's target, then the target's row bounds).
+// Same draws, same choices, same loads: bit-identical to philox_walk.  Needs nnz < 2^32.
+template <typename Visit>
+__device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, const int4 *__restrict__ aug,
+                                          const double *__restrict__ g_val, int64_t s, uint32_t w, double p,
+                                          int32_t L, int32_t rule, uint32_t k0, uint32_t k1, Visit visit) {
+    int64_t cur = s;
+    double load = 1.0;
+    int64_t rs = g_ptr[s];
+    int64_t deg = g_ptr[s + 1] - rs;
+    int32_t l = 0;
+    for (; l < L; ++l) {
+        visit(l, (int32_t)cur, load);
+        if (deg == 0) return l + 1;
+        uint32_t x0, x1, x2, x3;
+        philox4x32_10((uint32_t)l, w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
+        const double h = (double)((((uint64_t)x0 << 32) | x1) >> 11) * (1.0 / 9007199254740992.0);
+        if (h < p) return l + 1;
+        const uint32_t d = (uint32_t)deg;
+        uint32_t k = 0;
+        if (d > 1) {
+            uint64_t mm = (uint64_t)x2 * d;
+            if ((uint32_t)mm < d) {
+                const uint32_t thr = (0u - d) % d;
+                if ((uint32_t)mm < thr) mm = philox_lemire_retry(d, thr, x3, (uint32_t)l, w, (uint32_t)s, k0, k1);
+            }
+            k = (uint32_t)(mm >> 32);
+        }
+        const int4 a = aug[rs + k];
+        const double wt = g_val[rs + k];
+        load = load_update(rule, load, deg, wt, p);
+        cur = a.x;
+        rs = (int64_t)(uint32_t)a.y;
+        deg = a.z;
+    }
+    return L;
+}
+
 }  // namespace grf

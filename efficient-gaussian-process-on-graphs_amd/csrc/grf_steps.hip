@@ -145,7 +145,8 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         const double *__restrict__ slot_load,
                                                         const int64_t *__restrict__ g_ptr,
                                                         const int32_t *__restrict__ g_idx,
-                                                        const double *__restrict__ g_val, double p_halt, int32_t rule,
+                                                        const double *__restrict__ g_val,
+                                                        const int4 *__restrict__ g_aug, double p_halt, int32_t rule,
                                                         uint32_t k0, uint32_t k1, int64_t src_begin,
                                                         const double *__restrict__ f, int32_t Lf, int64_t cap,
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
@@ -176,12 +177,14 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         for (int t = tid; t < P; t += T) key[t] = kNone;
         __syncthreads();
         const int64_t src = src_begin + s;
-        for (int64_t w = tid; w < m; w += T)
-            philox_walk(g_ptr, g_idx, g_val, src, (uint32_t)w, p_halt, L, rule, k0, k1,
-                        [&](int32_t l, int32_t node, double load) {
-                            key[l * m + w] = make_key(node, l, w);
-                            ld[l * m + w] = load;
-                        });
+        for (int64_t w = tid; w < m; w += T) {
+            auto visit = [&](int32_t l, int32_t node, double load) {
+                key[l * m + w] = make_key(node, l, w);
+                ld[l * m + w] = load;
+            };
+            if (g_aug) philox_walk_aug(g_ptr, g_aug, g_val, src, (uint32_t)w, p_halt, L, rule, k0, k1, visit);
+            else philox_walk(g_ptr, g_idx, g_val, src, (uint32_t)w, p_halt, L, rule, k0, k1, visit);
+        }
     } else {
         const int32_t *nd = slot_node + s * E;
         const double *sl = slot_load + s * E;
@@ -305,6 +308,21 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     if (tid == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
 }
 
+// ---------------------------------------------- augmented walk matrix (philox_walk_aug)
+// aug[e] = {target v, row start of v (32 bits), row length of v, 0} for every entry e of the
+// walk matrix; one wave per row.
+__global__ __launch_bounds__(256) void walk_aug_kernel(int64_t n, const int64_t *__restrict__ g_ptr,
+                                                       const int32_t *__restrict__ g_idx, int4 *__restrict__ aug) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const int lane = threadIdx.x & 63;
+    for (int64_t e = g_ptr[row] + lane; e < g_ptr[row + 1]; e += 64) {
+        const int32_t v = g_idx[e];
+        const int64_t rs = g_ptr[v];
+        aug[e] = make_int4(v, (int32_t)(uint32_t)rs, (int32_t)(g_ptr[v + 1] - rs), 0);
+    }
+}
+
 // ------------------------------------------------------- dense (N, N, L) out
 __global__ __launch_bounds__(256) void steps_densify_kernel(int64_t n_src, int64_t m, int32_t L, int64_t n_cols,
                                                             const int32_t *__restrict__ step_cnt,
@@ -375,7 +393,8 @@ int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, co
 
 static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, int32_t norm,
                                 const int32_t *slot_node, const double *slot_load, const int64_t *g_ptr,
-                                const int32_t *g_idx, const double *g_val, double p_halt, int32_t rule, uint64_t seed,
+                                const int32_t *g_idx, const double *g_val, const void *g_aug, double p_halt,
+                                int32_t rule, uint64_t seed,
                                 int64_t src_begin, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
                                 int32_t *phi_idx, double *phi_val, float *phi_val32, int32_t *t_count,
                                 int64_t band_width, int64_t n_cols, hipStream_t st) {
@@ -410,7 +429,8 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     GRF_REQUIRE_GRID(n_src, T, "phi_fused_kernel");
 #define GRF_PHI_LAUNCH_KT(W, K, KT)                                                                               \
     phi_fused_kernel<W, K, KT><<<(unsigned)n_src, T, lds, st>>>(                                                  \
-        m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val, p_halt, rule, (uint32_t)seed,    \
+        m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val,                                   \
+        reinterpret_cast<const int4 *>(g_aug), p_halt, rule, (uint32_t)seed,                                      \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
         n_cols)
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
@@ -439,11 +459,12 @@ int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const i
                       int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream) {
     GRF_REQUIRE(n_src >= 0 && m >= 1 && L >= 1 && slot_node && slot_load && phi_cnt && phi_idx && phi_val,
                 GRF_EINVAL, "grf_phi_fused: bad arguments");
-    return phi_fused_launch(false, n_src, m, L, norm, slot_node, slot_load, nullptr, nullptr, nullptr, 0.0, 0, 0, 0, f,
+    return phi_fused_launch(false, n_src, m, L, norm, slot_node, slot_load, nullptr, nullptr, nullptr, nullptr, 0.0, 0,
+                            0, 0, f,
                             n_f, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, nullptr, 1, 0, S(stream));
 }
 
-int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
+int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
                      const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
                      int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
                      float *phi_val32, int32_t *t_count, int64_t band_width, grf_stream_t stream) {
@@ -461,9 +482,23 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
     GRF_REQUIRE(!t_count || (band_width >= 1 &&
                              phi_cap >= std::min<int64_t>(P.walks_per_node * (int64_t)P.max_walk_length, n)),
                 GRF_EINVAL, "grf_walk_phi: counting needs band_width >= 1 and phi_cap that never truncates a row");
+    GRF_REQUIRE(!g_aug || ((uintptr_t)g_aug & 15) == 0, GRF_EINVAL, "grf_walk_phi: g_aug must be 16-byte aligned");
     return phi_fused_launch(true, src_end - src_begin, P.walks_per_node, P.max_walk_length, norm, nullptr, nullptr,
-                            g_ptr, g_idx, g_val, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, phi_cnt,
+                            g_ptr, g_idx, g_val, g_aug, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, phi_cnt,
                             phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream));
+}
+
+size_t grf_walk_aug_bytes(int64_t nnz) { return (size_t)(nnz > 0 ? nnz : 0) * sizeof(int4); }
+
+int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, void *g_aug, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && g_ptr && g_idx && g_aug, GRF_EINVAL, "grf_walk_aug: bad arguments");
+    GRF_REQUIRE(((uintptr_t)g_aug & 15) == 0, GRF_EINVAL, "grf_walk_aug: g_aug must be 16-byte aligned");
+    if (n == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n, 4), 256, "walk_aug_kernel");
+    walk_aug_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, S(stream)>>>(n, g_ptr, g_idx,
+                                                                         reinterpret_cast<int4 *>(g_aug));
+    GRF_CHECK_LAUNCH("walk_aug_kernel");
+    return GRF_OK;
 }
 
 int32_t grf_steps_densify(int64_t n_src, int64_t m, int32_t L, int64_t n_cols, const int32_t *step_cnt,

@@ -185,7 +185,9 @@ class GRFEngine:
         C.check(self.lib.grf_laplacian_csr(n, _p(A.ptr), _p(A.idx), _p(A.val), C.LAP_SCIPY, _p(lp), _p(li), _p(lv),
                                            cap, _p(deg), _p(dinv), _p(ws), ws.numel(), self.stream),
                 "grf_laplacian_csr")
-        return DeviceCSR(n, n, lp, li, lv)
+        G = DeviceCSR(n, n, lp, li, lv)
+        G.nnz_bound = cap  # (sizes the augmented walk matrix without reading nnz back)
+        return G
 
     def walk_matrix_dense(self, W, mode: int) -> DeviceCSR:
         """Dense-input walk matrix (numpy Laplacian variants or the matrix itself) as CSR."""
@@ -274,7 +276,7 @@ class GRFEngine:
     def walk_phi(self, G: DeviceCSR, walks_per_node: int, p_halt: float, max_walk_length: int, f, *,
                  seed: int = 42, load_rule: int = C.LOAD_CUMULATIVE, norm: int = C.NORM_MUL_RECIP,
                  src_begin: int = 0, src_end: Optional[int] = None, want32: bool = True,
-                 count_ws: Optional[torch.Tensor] = None, band_width: int = 0) -> PaddedRows:
+                 count_ws: Optional[torch.Tensor] = None, band_width: int = 0, use_aug: bool = True) -> PaddedRows:
         """Philox walks straight to Phi rows (one kernel; identical to walk + features).
 
         count_ws: a zeroed transpose workspace (``transpose_workspace``) in which the kernel also
@@ -292,10 +294,26 @@ class GRFEngine:
         val = self._empty(ns * cap, torch.float64)
         v32 = self._empty(ns * cap, torch.float32) if want32 else None
         prm = C.GrfWalkParams(m, float(p_halt), L, int(load_rule), C.RNG_PHILOX, 0, 1, int(seed) & 0xFFFFFFFFFFFFFFFF)
-        C.check(self.lib.grf_walk_phi(n, _p(G.ptr), _p(G.idx), _p(G.val), ctypes.byref(prm), src_begin, src_end,
+        aug = self.walk_aug(G) if use_aug else None
+        C.check(self.lib.grf_walk_phi(n, _p(G.ptr), _p(G.idx), _p(G.val), _p(aug), ctypes.byref(prm), src_begin,
+                                      src_end,
                                       norm, _p(ft), ft.numel(), cap, _p(cnt), _p(idx), _p(val), _p(v32),
                                       _p(count_ws), int(band_width), self.stream), "grf_walk_phi")
         return PaddedRows(cnt, idx, val, v32, cap, n)
+
+    def walk_aug(self, G: DeviceCSR) -> Optional[torch.Tensor]:
+        """The augmented walk matrix of G (grf_walk_aug), built once per DeviceCSR; None when
+        nnz >= 2^32 (the walk then reads the row bounds per step)."""
+        aug = getattr(G, "_aug", None)
+        if aug is not None:
+            return aug
+        nnz = G.nnz_bound if getattr(G, "nnz_bound", None) is not None else G.nnz
+        if nnz >= 2 ** 32:
+            return None
+        aug = torch.empty(max(int(self.lib.grf_walk_aug_bytes(nnz)), 16), dtype=torch.uint8, device=self.device)
+        C.check(self.lib.grf_walk_aug(G.n_rows, _p(G.ptr), _p(G.idx), _p(aug), self.stream), "grf_walk_aug")
+        G._aug = aug
+        return aug
 
     def features(self, slots: Slots, f, norm: int = C.NORM_MUL_RECIP) -> PaddedRows:
         """Phi rows; the fused kernel when m*L fits LDS, else steps + merge (bit-identical)."""

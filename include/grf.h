@@ -157,11 +157,18 @@ int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, co
  * followed by grf_phi_fused.  Requires m * L <= 4096.
  * Optional (t_count != NULL): also count the banded transpose's buckets of the rows written,
  * t_count[(row / band_width) * n + col] += 1 -- pass the transpose workspace (zeroed) and then
- * grf_transpose_banded_plan(..., counted = 1, ...); phi_cap must not truncate rows. */
-int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
+ * grf_transpose_banded_plan(..., counted = 1, ...); phi_cap must not truncate rows.
+ * Optional (g_aug != NULL, from grf_walk_aug on the same walk matrix, nnz < 2^32): each step of a
+ * walk is one dependent memory round trip instead of two -- same draws, same Phi bits. */
+int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
                      const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
                      int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
                      float *phi_val32, int32_t *t_count, int64_t band_width, grf_stream_t stream);
+/* The augmented walk matrix of grf_walk_phi: g_aug[e] = {target v, row start of v (low 32 bits),
+ * row length of v, 0} (int32 x 4) for every entry e of the CSR walk matrix (g_ptr, g_idx);
+ * grf_walk_aug_bytes(nnz) bytes, 16-byte aligned. */
+int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, void *g_aug, grf_stream_t stream);
+size_t grf_walk_aug_bytes(int64_t nnz);
 int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
                       const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
                       int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream);

@@ -558,3 +558,29 @@ def test_transpose_wide_regions(eng, unit):
         assert np.array_equal(Ka, eng.gram_sparse(phi, ts, r0, r0 + 200).cpu().numpy())
     ok, fro = gram_close(eng.gram_sparse(phi, ts, 0, 50).cpu().numpy(), phi.to_scipy(), (0, 50))
     assert ok, fro
+
+
+@pytest.mark.parametrize("rule", [0, 1, 2])
+def test_walk_phi_augmented_matrix_bitexact(eng, rule):
+    """One-round-trip walks over the augmented walk matrix (grf_walk_aug) take the same draws and
+    give the same Phi bits as the two-round-trip walks, on a weighted heavy-tailed graph with
+    isolated nodes; and both match the oracle."""
+    import torch
+    from grf_amd.graphs import powerlaw_graph
+    A = powerlaw_graph(6000, 6.0, 2.2, seed=5)
+    A.data = np.random.default_rng(1).uniform(0.2, 3.0, A.nnz)
+    A = ((A + A.T) * 0.5).tocsr()
+    A.sort_indices()
+    G = eng.laplacian(A)
+    f = [1.0, -0.5, 0.125, -0.02, 0.003]
+    a = eng.walk_phi(G, 40, 0.15, 5, f, seed=11, load_rule=rule, use_aug=True)
+    b = eng.walk_phi(G, 40, 0.15, 5, f, seed=11, load_rule=rule, use_aug=False)
+    assert torch.equal(a.cnt, b.cnt)
+    mask = torch.arange(a.cap, device=a.cnt.device)[None, :] < a.cnt[:, None]
+    assert torch.equal(a.idx.view(-1, a.cap)[mask], b.idx.view(-1, b.cap)[mask])
+    assert torch.equal(a.val.view(-1, a.cap)[mask], b.val.view(-1, b.cap)[mask])
+    Ls, _ = O.laplacian_sparse(A)
+    ip, ix, dx = O._csr_arrays(Ls)
+    node, load = O.walk_slots(ip, ix, dx, 40, 0.15, 5, rng=O.RNG_PHILOX, load_rule=rule, seed=11)
+    ref = O.phi_sparse(O.reduce_steps(node, load, O.NORM_MUL_RECIP), f)
+    assert same_csr(eng.compact(a).to_scipy(), ref)
