@@ -310,8 +310,8 @@ def main_c3(args):
 
     def step(record):
         G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY)
-        slots = eng.walk(G, m, p, L, rng=C.RNG_PHILOX, seed=42)
-        phi = eng.compact(eng.features(slots, f, C.NORM_DIV), want64=False)
+        # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule
+        phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV), want64=False)
         dense = eng.densify(phi)
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

@@ -202,7 +202,9 @@ class GRFEngine:
         ws = self._ws(self.lib.grf_laplacian_dense_workspace_bytes(n))
         C.check(self.lib.grf_laplacian_dense(n, _p(Wt), mode, _p(lp), _p(li), _p(lv), cap, _p(deg), _p(ws),
                                              ws.numel(), self.stream), "grf_laplacian_dense")
-        return DeviceCSR(n, n, lp, li, lv)
+        G = DeviceCSR(n, n, lp, li, lv)
+        G.nnz_bound = cap
+        return G
 
     # ---------------------------------------------------------------- walks
     def walk(self, G: DeviceCSR, walks_per_node: int, p_halt: float, max_walk_length: int, *, rng: int = C.RNG_PHILOX,
