@@ -72,15 +72,118 @@ __device__ double np_pairwise(const double *a, int64_t n) {
     return ret;
 }
 
+// numpy pairwise_sum_DOUBLE of a[0 .. n) by one wave, bit for bit: the recursion's leaves (runs
+// of <= 128 values, split points n2 = n/2 - (n/2) % 8) are listed by lane 0, summed by the 64 lanes
+// in parallel with the leaf's own 8-accumulator order, and combined by lane 0 in the recursion's
+// order.  `leaf` is per-wave LDS scratch for kPwLeaves leaves; longer inputs fall back to lane 0.
+// Every lane returns the sum.  (A hub row of thousands of entries, or a dense row, no longer
+// costs one lane thousands of dependent adds.)
+constexpr int kPwLeaves = 128;
+struct PwLeaf { int64_t off; int64_t n; double sum; };
+
+__device__ double wave_np_pairwise(const double *a, int64_t n, PwLeaf *leaf) {
+    const int lane = threadIdx.x & 63;
+    if (n <= 128) {
+        // one leaf: lanes 0..7 own the accumulators r_j (a[j], a[j + 8], ...), then the fixed tree
+        double r = 0.0;
+        if (n < 8) {
+            double t = 0.0;
+            if (lane == 0)
+                for (int64_t i = 0; i < n; ++i) t += a[i];
+            return __shfl(t, 0, 64);
+        }
+        const int64_t nb = n - (n % 8);
+        if (lane < 8) {
+            r = a[lane];
+            for (int64_t i = 8 + lane; i < nb; i += 8) r += a[i];
+        }
+        const double r0 = __shfl(r, 0, 64), r1 = __shfl(r, 1, 64), r2 = __shfl(r, 2, 64), r3 = __shfl(r, 3, 64);
+        const double r4 = __shfl(r, 4, 64), r5 = __shfl(r, 5, 64), r6 = __shfl(r, 6, 64), r7 = __shfl(r, 7, 64);
+        double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        for (int64_t i = nb; i < n; ++i) res += a[i];
+        return res;
+    }
+    // list the leaves (lane 0, the recursion's explicit stack), left to right
+    int32_t nl = 0;
+    if (lane == 0) {
+        int64_t so[64], sn[64];
+        int sp = 0;
+        so[0] = 0;
+        sn[0] = n;
+        while (sp >= 0) {
+            const int64_t o = so[sp], m = sn[sp];
+            --sp;
+            if (m <= 128) {
+                if (nl < kPwLeaves) leaf[nl] = PwLeaf{o, m, 0.0};
+                ++nl;
+                continue;
+            }
+            int64_t n2 = m / 2;
+            n2 -= n2 % 8;
+            // push right then left: the left subtree's leaves come first
+            ++sp; so[sp] = o + n2; sn[sp] = m - n2;
+            ++sp; so[sp] = o; sn[sp] = n2;
+        }
+    }
+    nl = __shfl(nl, 0, 64);
+    if (nl > kPwLeaves) {
+        const double t = lane == 0 ? np_pairwise(a, n) : 0.0;
+        return __shfl(t, 0, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int l = lane; l < nl; l += 64) leaf[l].sum = pw_leaf(a + leaf[l].off, leaf[l].n);
+    __builtin_amdgcn_wave_barrier();
+    // combine in the recursion's order (lane 0): the same stack machine with leaf sums in order
+    double total = 0.0;
+    if (lane == 0) {
+        struct Frame { int64_t n; int state; double left; };
+        Frame st[64];
+        int sp = 0, next = 0;
+        st[0] = {n, 0, 0.0};
+        double ret = 0.0;
+        while (sp >= 0) {
+            Frame &f = st[sp];
+            if (f.n <= 128) {
+                ret = leaf[next++].sum;
+                --sp;
+                continue;
+            }
+            int64_t n2 = f.n / 2;
+            n2 -= n2 % 8;
+            if (f.state == 0) {
+                f.state = 1;
+                st[sp + 1] = {n2, 0, 0.0};
+                ++sp;
+            } else if (f.state == 1) {
+                f.left = ret;
+                f.state = 2;
+                st[sp + 1] = {f.n - n2, 0, 0.0};
+                ++sp;
+            } else {
+                ret = f.left + ret;
+                --sp;
+            }
+        }
+        total = ret;
+    }
+    return __shfl(total, 0, 64);
+}
+
 // ------------------------------------------------------------------- scipy
-__global__ void lap_deg_kernel(int64_t n, const int64_t *ptr, const double *val, double *deg, double *dinv) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// degrees a_ii... : deg = a0 + pairwise(rest) per row (np.add.reduceat), one wave per row
+__global__ __launch_bounds__(256) void lap_deg_kernel(int64_t n, const int64_t *ptr, const double *val, double *deg,
+                                                      double *dinv) {
+    __shared__ PwLeaf leaves[4][kPwLeaves];
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
     const int64_t b = ptr[i], e = ptr[i + 1];
-    double d = e > b ? val[b] + np_pairwise(val + b + 1, e - b - 1) : 0.0;
-    deg[i] = d;
-    double v = 1.0 / sqrt(d);
-    dinv[i] = isinf(v) ? 0.0 : v;
+    const double rest = e - b > 1 ? wave_np_pairwise(val + b + 1, e - b - 1, leaves[threadIdx.x >> 6]) : 0.0;
+    if ((threadIdx.x & 63) == 0) {
+        const double d = e > b ? val[b] + rest : 0.0;
+        deg[i] = d;
+        const double v = 1.0 / sqrt(d);
+        dinv[i] = isinf(v) ? 0.0 : v;
+    }
 }
 
 // One row of D^-1/2 (D - A) D^-1/2 in scipy order, one wave per row (a power-law hub row of
@@ -157,13 +260,17 @@ __global__ __launch_bounds__(256) void lap_row_kernel(int64_t n, const int64_t *
 }
 
 // ------------------------------------------------------------------- dense
-__global__ void lapd_deg_kernel(int64_t n, const double *W, int32_t mode, double *deg, double *dinv) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void lapd_deg_kernel(int64_t n, const double *W, int32_t mode, double *deg,
+                                                       double *dinv) {
+    __shared__ PwLeaf leaves[4][kPwLeaves];
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per row
     if (i >= n) return;
-    double d = np_pairwise(W + i * n, n);
-    deg[i] = d;
-    if (mode == GRF_LAP_NUMPY) dinv[i] = d > 0.0 ? 1.0 / sqrt(d) : 0.0;
-    else dinv[i] = 1.0 / sqrt(d > 0.0 ? d : 1.0);
+    const double d = wave_np_pairwise(W + i * n, n, leaves[threadIdx.x >> 6]);
+    if ((threadIdx.x & 63) == 0) {
+        deg[i] = d;
+        if (mode == GRF_LAP_NUMPY) dinv[i] = d > 0.0 ? 1.0 / sqrt(d) : 0.0;
+        else dinv[i] = 1.0 / sqrt(d > 0.0 ? d : 1.0);
+    }
 }
 
 __device__ inline double lapd_value(int32_t mode, int64_t i, int64_t j, double w, const double *deg,
@@ -240,7 +347,7 @@ int32_t grf_laplacian_csr(int64_t n, const int64_t *a_ptr, const int32_t *a_idx,
         GRF_CHECK_HIP(hipMemsetAsync(l_ptr, 0, sizeof(int64_t), st));
         return GRF_OK;
     }
-    const unsigned g = (unsigned)cdiv<int64_t>(n, 256);
+    const unsigned g = (unsigned)cdiv<int64_t>(n, 4);  // one wave per row
     GRF_REQUIRE_GRID(g, 256, "lap_deg_kernel");
     lap_deg_kernel<<<g, 256, 0, st>>>(n, a_ptr, a_val, deg, dinv);
     GRF_CHECK_LAUNCH("lap_deg_kernel");
@@ -275,8 +382,8 @@ int32_t grf_laplacian_dense(int64_t n, const double *W, int32_t mode, int64_t *l
     double *dinv = (double *)workspace;
     int32_t *cnt = (int32_t *)((char *)workspace + dinv_bytes);
     void *scan_ws = (char *)workspace + dinv_bytes + cnt_bytes;
-    GRF_REQUIRE_GRID(cdiv<int64_t>(n, 128), 128, "lapd_deg_kernel");
-    lapd_deg_kernel<<<(unsigned)cdiv<int64_t>(n, 128), 128, 0, st>>>(n, W, mode, deg, dinv);
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n, 4), 256, "lapd_deg_kernel");
+    lapd_deg_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, st>>>(n, W, mode, deg, dinv);
     GRF_CHECK_LAUNCH("lapd_deg_kernel");
     const unsigned g = (unsigned)cdiv<int64_t>(n, 4);
     GRF_REQUIRE_GRID(g, 256, "lapd_row_kernel");
