@@ -197,6 +197,7 @@ struct GramTiles {
     int64_t rows, W, nb;
     bool sym;
     int32_t k_begin, k_end;  // only the nonzeros Phi[i, k] with k in [k_begin, k_end) contribute
+    int64_t J_off = 0;       // the launch's bands are the global bands J_off .. J_off + nb - 1
     __host__ __device__ int64_t count(int64_t J) const {
         if (!sym) return rows;
         const int64_t c = (J + 1) * W;
@@ -252,6 +253,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
 
     int64_t J, r;
     tl.locate(t_begin + (int64_t)blockIdx.x, J, r);
+    J += tl.J_off;  // global band
     const int64_t row = row_begin + r;
     const int64_t j0 = J * W;
     const int64_t wlen = (n_total - j0) < W ? (n_total - j0) : W;
@@ -649,6 +651,42 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
     if (t1 <= t0) return GRF_OK;
     return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
                              S(stream));
+}
+
+// K rows [row_begin, row_end) of the whole K using the symmetry inside the row block: the bands
+// that lie inside the block ("interior", rows [B0, B1)) are computed only on and above the
+// diagonal for the block's interior rows and mirrored; everything else is the row mode.
+int32_t grf_gram_sparse_block(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                              const int32_t *idx, const float *val, int64_t band_width, int32_t rec_unit,
+                              const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
+                              int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift,
+                                   K, ldk);
+    if (rc != GRF_OK) return rc;
+    if (row_end == row_begin || n_total == 0) return GRF_OK;
+    hipStream_t st = S(stream);
+    const int64_t W = band_width, nb = cdiv<int64_t>(n_total, W);
+    const int64_t J0 = cdiv<int64_t>(row_begin, W);
+    const int64_t J1 = row_end == n_total ? nb : row_end / W;
+    if (J1 <= J0) {
+        return gram_sparse_launch(n_total, row_begin, row_end - row_begin, false, 0, n_total, ptr, idx, val, W,
+                                  rec_unit, t_desc, t_rec, t_rowshift, K, ldk, st);
+    }
+    const int64_t B0 = J0 * W, B1 = std::min<int64_t>(J1 * W, n_total);
+    auto launch = [&](int64_t r0, int64_t r1, int64_t ja, int64_t jb, bool sym) -> int32_t {
+        if (r1 <= r0 || jb <= ja) return GRF_OK;
+        GramTiles tl{r1 - r0, W, jb - ja, sym, 0, (int32_t)n_total};
+        tl.J_off = ja;
+        const int64_t n_tiles = tl.total();
+        return gram_tiles_launch(n_total, r0, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift,
+                                 K + (r0 - row_begin) * ldk, ldk, st);
+    };
+    if ((rc = launch(B0, B1, J0, J1, true)) != GRF_OK) return rc;            // interior, symmetric
+    if ((rc = launch(row_begin, row_end, 0, J0, false)) != GRF_OK) return rc;  // bands before
+    if ((rc = launch(row_begin, row_end, J1, nb, false)) != GRF_OK) return rc; // bands after
+    if ((rc = launch(row_begin, B0, J0, J1, false)) != GRF_OK) return rc;     // edge rows x interior
+    if ((rc = launch(B1, row_end, J0, J1, false)) != GRF_OK) return rc;
+    return grf_gram_mirror(B1 - B0, K + (B0 - row_begin) * ldk + B0, ldk, 0, stream);
 }
 
 int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,

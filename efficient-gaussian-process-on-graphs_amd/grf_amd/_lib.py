@@ -70,6 +70,8 @@ SIGNATURES = {
                                          _vp]),
     "grf_transpose_workspace_bytes": (_sz, [_i64]),
     "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
+    "grf_gram_sparse_block": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz,
+                                     _vp]),
     "grf_gram_workspace_bytes": (_sz, []),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _i64, _vp]),

@@ -448,6 +448,19 @@ class GRFEngine:
                 "grf_gram_sparse")
         return out[:, :n]
 
+    def gram_sparse_block(self, phi: DeviceCSR, tr: Banded, row_begin: int, row_end: int,
+                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """K[row_begin:row_end, :] (float32) using the symmetry inside the row block (grf_gram_sparse_block)."""
+        n = tr.n_rows
+        ldk = self.leading_dim(n)
+        if out is None:
+            out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
+        C.check(self.lib.grf_gram_sparse_block(n, row_begin, row_end, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
+                                               tr.band_width, tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec),
+                                               _p(tr.t_rowshift), _p(out), out.stride(0), _p(self._gram_ws),
+                                               self._gram_ws.numel(), self.stream), "grf_gram_sparse_block")
+        return out[:, :n]
+
     def gram_sparse_kslice(self, phi: DeviceCSR, tr: Banded, k_begin: int, k_end: int, row_begin: int = 0,
                            row_end: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Partial K[row_begin:row_end, :] over the inner-dimension slice [k_begin, k_end) (float32)."""

@@ -256,6 +256,15 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
                               int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                               grf_stream_t stream);
 
+/* K rows [row_begin, row_end) (as grf_gram_sparse) using the symmetry inside the row block: the
+ * bands lying wholly inside the block are computed only on and above the diagonal for the block's
+ * rows in them, then mirrored (entries below the diagonal there carry row j's fixed-point rounding,
+ * as in grf_gram_sparse_sym); all other tiles are the row mode's.  The multi-GPU row blocks. */
+int32_t grf_gram_sparse_block(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                              const int32_t *idx, const float *val, int64_t band_width, int32_t rec_unit,
+                              const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
+                              int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+
 /* Partial Gram over a slice of the inner dimension: K[r, :] = sum over k in [k_begin, k_end)
  * of Phi[r, k] Phi[:, k] (same fixed-point rule as grf_gram_sparse).  The partial Grams of
  * disjoint slices sum to K -- the "partial K + all-reduce" multi-GPU option. */

@@ -267,6 +267,31 @@ def test_gram_sparse_band_invariance(eng):
     assert ok, fro
 
 
+@pytest.mark.parametrize("n,bw,blocks", [(20000, 4096, [(0, 10000), (10000, 20000)]),
+                                          (20000, 1024, [(0, 5000), (5000, 10000), (10000, 15000), (15000, 20000)]),
+                                          (5000, 64, [(0, 1667), (1667, 3334), (3334, 5000)]),
+                                          (9000, 4096, [(0, 4500), (4500, 9000), (100, 8200), (0, 9000)]),
+                                          (3000, 4096, [(0, 1500), (1500, 3000)])])
+def test_gram_block_symmetric_row_blocks(eng, n, bw, blocks):
+    """The multi-GPU row-block Gram with the symmetry inside the block: every entry is the row
+    mode's bits except in the block's interior square (whole bands inside the block) below the
+    diagonal, which holds the mirrored upper entry -- as the symmetric mode fills it."""
+    A = er_graph(n, 8, n + 1)
+    G = eng.laplacian(A)
+    phi = eng.compact(eng.walk_phi(G, 32, 0.15, 5, [1.0, -0.5, 0.25, -0.125, 0.1], seed=6))
+    tr = eng.transpose_banded(phi, bw)
+    K = eng.gram_sparse(phi, tr).cpu().numpy()
+    for b0, b1 in blocks:
+        Kb = eng.gram_sparse_block(phi, tr, b0, b1).cpu().numpy()
+        exp = K[b0:b1].copy()
+        i0 = -(-b0 // bw) * bw
+        i1 = n if b1 == n else (b1 // bw) * bw
+        if i1 > i0:
+            sq = K[i0:i1, i0:i1]
+            exp[i0 - b0:i1 - b0, i0:i1] = np.triu(sq) + np.triu(sq, 1).T
+        assert np.array_equal(Kb, exp), (b0, b1)
+
+
 @pytest.mark.parametrize("unit", [128, 12])
 @pytest.mark.parametrize("n,deg,m,L,bw", [(20000, 10, 32, 6, 4096), (5000, 10, 64, 8, 64), (3000, 20, 128, 8, 4096),
                                           (4100, 6, 16, 4, 1024)])
