@@ -399,8 +399,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=2048)
     ap.add_argument("--no-sym", action="store_true", help="single GPU: compute every K tile (no symmetric mode)")
-    ap.add_argument("--mode", choices=["rows", "allreduce"], default="rows",
-                    help="rows: K row blocks after a Phi all-gather (default); allreduce: the north star's literal "
+    ap.add_argument("--mode", choices=["cols", "rows", "allreduce"], default="cols",
+                    help="cols (default; N > 1): K column blocks K[:, R_r] (= the row blocks, K symmetric) from a "
+                         "transpose of the rank's own Phi rows after a Phi all-gather; rows: K row blocks from a "
+                         "transpose of all of Phi (one GPU always runs rows / symmetric); allreduce: the north star's literal "
                          "option -- per-rank partial K over an inner-dimension slice + bucketed RCCL all-reduce, "
                          "K replicated on every rank (SURVEY.md §8e)")
     ap.add_argument("--workload", choices=["kernel", "predict", "c5", "c3"], default="kernel",
@@ -442,7 +444,7 @@ def main():
     from grf_amd import _lib as C
     from grf_amd.dist import all_reduce as dist_all_reduce
     from grf_amd.dist import allreduce_buckets, gather_phi, shard_range
-    from grf_amd.engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, DeviceCSR, GRFEngine
+    from grf_amd.engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, DeviceCSR, GRFEngine, cols_band_width
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -459,11 +461,17 @@ def main():
     b, e = shard_range(n, rank, world)
     ldk = eng.leading_dim(n)
     allreduce = args.mode == "allreduce"
+    # N > 1 column blocks K[:, b:e] (each rank transposes only its own rows); one GPU: row blocks
+    cols = args.mode == "cols" and world > 1 and not args.k_rows
     if args.k_rows and allreduce:
         raise SystemExit("--k-rows applies to the row mode only")
     kr_end = min(e, b + args.k_rows) if args.k_rows else e  # this rank's K rows [b, kr_end)
     k_rows = n if allreduce else kr_end - b
-    K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
+    if cols:
+        wl = cols_band_width(e - b)
+        K = torch.empty((n, eng.leading_dim(e - b)), dtype=torch.float32, device=dev)  # K[:, b:e], reused
+    else:
+        K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
     rows_cap = max(1, min(m * L, n))  # walk_phi's padded row capacity
     sym_mode = world == 1 and not args.no_sym and not args.k_rows and not allreduce
     if args.overlap is None:
@@ -484,6 +492,15 @@ def main():
         # Philox walks of this rank's sources straight to Phi rows (one kernel, no slot round trip);
         # the same kernel counts this rank's buckets of the banded transpose (summed over the ranks
         # by one all-reduce in gather_phi)
+        if cols:
+            # (counting the rank's own-rows transpose: no count all-reduce, and a 1/N-size transpose)
+            tws = eng.transpose_workspace(e - b, n, wl)
+            local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
+                                             band_width=wl, count_origin=b),
+                                want64=False, want32=True, sync_free=True)
+            phi = gather_phi(eng, local)
+            tr = eng.transpose_banded(local, wl, counted_ws=tws, nnz_bound=(e - b) * rows_cap)
+            return phi, (tr, eng.phi_row_shifts(phi)), local
         tws = eng.transpose_workspace(n, n, bw)
         local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
                                          band_width=bw),
@@ -500,7 +517,9 @@ def main():
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if allreduce:
+        if cols:
+            eng.gram_sparse_cols(phi, tr[1], tr[0], out=K)  # K[:, b:e] = Phi Phi[b:e]^T
+        elif allreduce:
             eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
         elif sym_mode:
             # upper band tiles (the pipelined run lets the next front start at the Gram's tail) ...
@@ -549,8 +568,8 @@ def main():
         fr, done = frd
         main.wait_event(done)
         phi, tr, local = fr
-        for obj in (phi, tr, local):  # allocated on `side`, used on `main`
-            for v in vars(obj).values():
+        for obj in (phi, *(tr if isinstance(tr, tuple) else (tr,)), local):  # allocated on `side`, used on `main`
+            for v in ([obj] if torch.is_tensor(obj) else vars(obj).values()):
                 if torch.is_tensor(v) and v.is_cuda:
                     v.record_stream(main)
         back(fr, record, after_gram)
@@ -663,6 +682,8 @@ def main():
                    "k_rows_per_gpu": rows,
                    "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
                                    f"RCCL all-reduce (K replicated)") if allreduce else
+                                  (f"source-sharded x{world}, Phi all-gather, K column blocks K[:, R_r] from each "
+                                   f"rank's own-rows transpose") if cols else
                                   f"source-sharded x{world}, Phi all-gather, K row blocks"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

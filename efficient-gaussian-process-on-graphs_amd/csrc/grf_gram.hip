@@ -198,6 +198,7 @@ struct GramTiles {
     bool sym;
     int32_t k_begin, k_end;  // only the nonzeros Phi[i, k] with k in [k_begin, k_end) contribute
     int64_t J_off = 0;       // the launch's bands are the global bands J_off .. J_off + nb - 1
+    int64_t t_rows = -1;     // rows of the transposed matrix (< 0: n_total, the square case)
     __host__ __device__ int64_t count(int64_t J) const {
         if (!sym) return rows;
         const int64_t c = (J + 1) * W;
@@ -256,7 +257,8 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     J += tl.J_off;  // global band
     const int64_t row = row_begin + r;
     const int64_t j0 = J * W;
-    const int64_t wlen = (n_total - j0) < W ? (n_total - j0) : W;
+    const int64_t t_rows = tl.t_rows < 0 ? n_total : tl.t_rows;  // (n_total: Phi's columns)
+    const int64_t wlen = (t_rows - j0) < W ? (t_rows - j0) : W;
     const int64_t e0 = ptr[row], e1 = ptr[row + 1];
     const int64_t boff = J * n_total;
     const int sh = rowshift[row];
@@ -651,6 +653,32 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
     if (t1 <= t0) return GRF_OK;
     return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
                              S(stream));
+}
+
+// Column block: K[r - row_begin, 0 : t_rows] = sum_k Phi[r, k] Phi_B[:, k] for the rows r of Phi
+// against the t_rows rows of another matrix Phi_B (a rank's own rows) whose banded transpose is
+// given; the row shifts come from grf_phi_row_shifts over all of Phi.  With Phi_B = Phi[b:e] this
+// is K[:, b:e] -- entry for entry the row mode's K[r, b + j] -- so a rank transposes only its rows.
+int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                             const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
+                             int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec, float *K,
+                             int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n_cols > 0 && 0 <= row_begin && row_begin <= row_end && ptr && idx && val && row_shift &&
+                    t_rows >= 0 && t_desc && t_rec && K && ldk >= t_rows,
+                GRF_EINVAL, "grf_gram_sparse_cols: bad arguments");
+    GRF_REQUIRE(band_width >= 64 && band_width % 64 == 0 && band_width <= 8192, GRF_EUNSUPPORTED,
+                "grf_gram_sparse_cols: band_width must be a multiple of 64 in [64, 8192]");
+    GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_gram_sparse_cols: t_rec must be 128-byte aligned");
+    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED, GRF_EINVAL,
+                "grf_gram_sparse_cols: bad rec_unit");
+    (void)workspace;
+    (void)workspace_bytes;
+    if (row_end == row_begin || t_rows == 0) return GRF_OK;
+    GramTiles tl{row_end - row_begin, band_width, cdiv<int64_t>(t_rows, band_width), false, 0, (int32_t)n_cols};
+    tl.t_rows = t_rows;
+    // (the kernel reads row_shift[row] for row = row_begin + r: the shifts of Phi's rows)
+    return gram_tiles_launch(n_cols, row_begin, tl, 0, tl.total(), ptr, idx, val, t_desc, t_rec, rec_unit, row_shift,
+                             K, ldk, S(stream));
 }
 
 // K rows [row_begin, row_end) of the whole K using the symmetry inside the row block: the bands

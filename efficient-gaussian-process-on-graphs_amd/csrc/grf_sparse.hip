@@ -350,6 +350,35 @@ __global__ __launch_bounds__(1024) void tr_maxabs_kernel(int64_t n, const float 
     }
 }
 
+// Per-row max / sum of |values| over a whole CSR (one wave per row, the loop order of the
+// transpose's binning kernel) and each workgroup's max: the Gram row shifts of rows that are not
+// in the transpose (the column-block Gram of the multi-GPU path).
+__global__ __launch_bounds__(256) void phi_row_stats_kernel(int64_t n_rows, const int64_t *ptr, const float *val,
+                                                            float *wg_max, float *row_max, double *row_sum) {
+    __shared__ float red[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+    float mx = 0.f;
+    if (r < n_rows) {
+        double sm = 0.0;
+        for (int64_t e = ptr[r] + lane; e < ptr[r + 1]; e += 64) {
+            const float a = fabsf(val[e]);
+            mx = fmaxf(mx, a);
+            sm += (double)a;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        sm = wave_sum<double>(sm);
+        if (lane == 0) {
+            row_max[r] = mx;
+            row_sum[r] = sm;
+        }
+    }
+    if (lane == 0) red[wave] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) wg_max[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 __global__ __launch_bounds__(256) void tr_place_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, int32_t cr,
                                                        int32_t nreg, const int64_t *ptr, const uint2 *desc,
                                                        const int64_t *ent_off, const uint2 *staging,
@@ -610,6 +639,36 @@ int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t
     tr_place_kernel<<<(unsigned)n_regions, 256, lds2, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr, desc, ent_off,
                                                             ent, tab, cnt, (unsigned char *)t_rec, rec_unit);
     GRF_CHECK_LAUNCH("tr_place_kernel");
+    return GRF_OK;
+}
+
+size_t grf_phi_row_shifts_workspace_bytes(int64_t n_rows) {
+    const int64_t n = std::max<int64_t>(n_rows, 1);
+    return tr_align((size_t)n * 4) + tr_align((size_t)n * 8) + tr_align((size_t)cdiv<int64_t>(n, 4) * 4);
+}
+
+int32_t grf_phi_row_shifts(int64_t n_rows, const int64_t *ptr, const float *val, float *maxabs, int32_t *row_shift,
+                           void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && ptr && val && maxabs && row_shift && workspace, GRF_EINVAL,
+                "grf_phi_row_shifts: bad arguments");
+    GRF_REQUIRE(workspace_bytes >= grf_phi_row_shifts_workspace_bytes(n_rows), GRF_EINVAL,
+                "grf_phi_row_shifts: workspace too small");
+    hipStream_t st = S(stream);
+    GRF_CHECK_HIP(hipMemsetAsync(maxabs, 0, sizeof(float), st));
+    if (n_rows == 0) return GRF_OK;
+    char *w = (char *)workspace;
+    float *row_max = (float *)w;
+    double *row_sum = (double *)(w + tr_align((size_t)n_rows * 4));
+    float *wg_max = (float *)(w + tr_align((size_t)n_rows * 4) + tr_align((size_t)n_rows * 8));
+    const int64_t nwg = cdiv<int64_t>(n_rows, 4);
+    GRF_REQUIRE_GRID(nwg, 256, "phi_row_stats_kernel");
+    phi_row_stats_kernel<<<(unsigned)nwg, 256, 0, st>>>(n_rows, ptr, val, wg_max, row_max, row_sum);
+    GRF_CHECK_LAUNCH("phi_row_stats_kernel");
+    tr_maxabs_kernel<<<1, 1024, 0, st>>>(nwg, wg_max, maxabs);
+    GRF_CHECK_LAUNCH("tr_maxabs_kernel");
+    tr_rowshift_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 256), 256, 0, st>>>(n_rows, row_max, row_sum, maxabs,
+                                                                            row_shift);
+    GRF_CHECK_LAUNCH("tr_rowshift_kernel");
     return GRF_OK;
 }
 

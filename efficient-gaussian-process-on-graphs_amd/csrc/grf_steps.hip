@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
                                                         double *__restrict__ phi_val, float *__restrict__ phi_val32,
                                                         int32_t *__restrict__ t_count, int64_t band_width,
-                                                        int64_t n_cols) {
+                                                        int64_t n_cols, int64_t count_row0) {
     // LDS: ld [E] loads by slot (later the compacted step values), fl [64] the modulator,
     // scratch (2 x 16 ints), key [P] the sorted keys (later the compacted step keys).  32-bit
     // keys when (node, step, walk) fits 32 bits (C4 / C5): half the sort's LDS traffic and a
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
             phi_val[obase + rank + q] = pv_[q];
             if (phi_val32) phi_val32[obase + rank + q] = (float)pv_[q];
             // the banded transpose's bucket counts of this row's entries (grf_transpose_banded_plan)
-            if (t_count) atomicAdd(&t_count[((src_begin + s) / band_width) * n_cols + pn_[q]], 1);
+            if (t_count) atomicAdd(&t_count[((src_begin + s - count_row0) / band_width) * n_cols + pn_[q]], 1);
         }
     }
     if (tid == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
@@ -397,7 +397,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
                                 int32_t rule, uint64_t seed,
                                 int64_t src_begin, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
                                 int32_t *phi_idx, double *phi_val, float *phi_val32, int32_t *t_count,
-                                int64_t band_width, int64_t n_cols, hipStream_t st) {
+                                int64_t band_width, int64_t n_cols, hipStream_t st, int64_t count_row0 = 0) {
     GRF_REQUIRE(norm == GRF_NORM_DIV || norm == GRF_NORM_MUL_RECIP, GRF_EINVAL, "grf_phi_fused: bad norm");
     GRF_REQUIRE(n_f >= 0 && (n_f == 0 || f), GRF_EINVAL, "grf_phi_fused: bad modulator");
     GRF_REQUIRE(m * (int64_t)L <= 4096, GRF_EUNSUPPORTED, "grf_phi_fused: needs walks_per_node * L <= 4096");
@@ -432,7 +432,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val,                                   \
         reinterpret_cast<const int4 *>(g_aug), p_halt, rule, (uint32_t)seed,                                      \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
-        n_cols)
+        n_cols, count_row0)
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
     do {                                                                                                          \
         if (key32) GRF_PHI_LAUNCH_KT(W, K, uint32_t);                                                             \
@@ -467,7 +467,8 @@ int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const i
 int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
                      const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
                      int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
-                     float *phi_val32, int32_t *t_count, int64_t band_width, grf_stream_t stream) {
+                     float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
+                     grf_stream_t stream) {
     GRF_REQUIRE(params != nullptr, GRF_EINVAL, "grf_walk_phi: params is NULL");
     const grf_walk_params P = *params;
     GRF_REQUIRE(n >= 0 && g_ptr && phi_cnt && phi_idx && phi_val, GRF_EINVAL, "grf_walk_phi: bad arguments");
@@ -482,10 +483,12 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
     GRF_REQUIRE(!t_count || (band_width >= 1 &&
                              phi_cap >= std::min<int64_t>(P.walks_per_node * (int64_t)P.max_walk_length, n)),
                 GRF_EINVAL, "grf_walk_phi: counting needs band_width >= 1 and phi_cap that never truncates a row");
+    GRF_REQUIRE(!t_count || (0 <= count_row0 && count_row0 <= src_begin), GRF_EINVAL,
+                "grf_walk_phi: count_row0 must be in [0, src_begin]");
     GRF_REQUIRE(!g_aug || ((uintptr_t)g_aug & 15) == 0, GRF_EINVAL, "grf_walk_phi: g_aug must be 16-byte aligned");
     return phi_fused_launch(true, src_end - src_begin, P.walks_per_node, P.max_walk_length, norm, nullptr, nullptr,
                             g_ptr, g_idx, g_val, g_aug, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, phi_cnt,
-                            phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream));
+                            phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream), count_row0);
 }
 
 size_t grf_walk_aug_bytes(int64_t nnz) { return (size_t)(nnz > 0 ? nnz : 0) * sizeof(int4); }

@@ -60,7 +60,7 @@ SIGNATURES = {
     "grf_walk_aug": (_i32, [_i64, _vp, _vp, _vp, _vp]),
     "grf_walk_aug_bytes": (_sz, [_i64]),
     "grf_walk_phi": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32, _i64,
-                             _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+                             _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
     "grf_phi_fused": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_scan_workspace_bytes": (_sz, [_i64]),
@@ -73,6 +73,10 @@ SIGNATURES = {
     "grf_gram_sparse_block": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz,
                                      _vp]),
     "grf_gram_workspace_bytes": (_sz, []),
+    "grf_gram_sparse_cols": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _vp,
+                                    _sz, _vp]),
+    "grf_phi_row_shifts_workspace_bytes": (_sz, [_i64]),
+    "grf_phi_row_shifts": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _i64, _vp]),
     "grf_gram_sparse_upper": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32,

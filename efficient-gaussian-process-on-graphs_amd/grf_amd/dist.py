@@ -152,10 +152,13 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
                           rng=None, mode: str = "rows"):
     """This rank's row block of K = Phi Phi^T (float32, on the engine's device), and its row range.
 
+    ``mode="cols"``: this rank's column block K[:, b:e] (n x (e - b)) instead -- the same numbers
+    as the row block (K is symmetric; entry for entry the row mode's K[i, b + j]), computed from a
+    transpose of the rank's own Phi rows only (no replicated transpose, no bucket-count all-reduce).
     ``mode="allreduce"``: every rank returns the whole K (row range (0, n)), assembled as the
     all-reduced sum of per-rank partial Grams over inner-dimension slices."""
-    if mode not in ("rows", "allreduce"):
-        raise ValueError(f"mode must be 'rows' or 'allreduce', got {mode!r}")
+    if mode not in ("rows", "cols", "allreduce"):
+        raise ValueError(f"mode must be 'rows', 'cols' or 'allreduce', got {mode!r}")
     from . import _lib as C
     from .engine import DeviceCSR
 
@@ -170,6 +173,10 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
     n = G.n_rows
     b, e = shard_range(n, rank, world)
     bw = ROWS_BAND_WIDTH  # (row-mode Grams: the wide bands)
+    if mode == "cols":
+        from .engine import cols_band_width
+        return _cols_block(engine, G, f, walks_per_node, p_halt, max_walk_length, seed, rng, b, e, group,
+                           cols_band_width(e - b)), (b, e)
     tws = None
     if walks_per_node * max_walk_length <= 4096:
         # fused walk -> Phi, counting this rank's buckets of the banded transpose on the way
@@ -188,3 +195,25 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
         allreduce_buckets(K, group=group)
         return K, (0, n)
     return engine.gram_sparse(phi, tr, b, e), (b, e)
+
+
+def _cols_block(engine, G, f, m, p_halt, L, seed, rng, b, e, group, wl):
+    """K[:, b:e] from this rank's rows: walks -> Phi rows (counting the local transpose's buckets)
+    -> Phi all-gather -> transpose of the local rows -> column-block Gram with all rows' shifts."""
+    from .engine import DeviceCSR
+
+    n = G.n_rows
+    tws = None
+    if m * L <= 4096:
+        tws = engine.transpose_workspace(e - b, n, wl)
+        rows = engine.walk_phi(G, m, p_halt, L, f, seed=seed, src_begin=b, src_end=e, count_ws=tws, band_width=wl,
+                               count_origin=b)
+    else:
+        rows = engine.features(engine.walk(G, m, p_halt, L, rng=rng, seed=seed, src_begin=b, src_end=e), f)
+    local = engine.compact(rows, want64=False, want32=True)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    phi = gather_phi(engine, local, None, group) if world > 1 else \
+        DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
+    tr = engine.transpose_banded(local, wl, counted_ws=tws)
+    return engine.gram_sparse_cols(phi, engine.phi_row_shifts(phi), tr)
+

@@ -132,6 +132,13 @@ class Banded:
     rec_unit: int = C.REC_LINE  # bucket alignment: 128-byte lines or packed 12-byte pairs
 
 
+def cols_band_width(rows: int, max_width: int = ROWS_BAND_WIDTH) -> int:
+    """Band width of a rank's own-rows transpose (column-block Gram): the rows in the fewest bands
+    of at most ``max_width``, split evenly and rounded up to a multiple of 64."""
+    nb = max(1, -(-rows // max_width))
+    return max(64, -(-(-(-rows // nb)) // 64) * 64)
+
+
 def choose_rec_unit(nnz: int, n_rows: int, n_cols: int, band_width: int) -> int:
     """Line-aligned buckets when a bucket averages >= 8 entries (C4: ~18 at W = 4096), packed
     pairs below that (C5: ~1.4 at W = 8192, where a 128-byte line per bucket would be ~15x
@@ -280,11 +287,13 @@ class GRFEngine:
     def walk_phi(self, G: DeviceCSR, walks_per_node: int, p_halt: float, max_walk_length: int, f, *,
                  seed: int = 42, load_rule: int = C.LOAD_CUMULATIVE, norm: int = C.NORM_MUL_RECIP,
                  src_begin: int = 0, src_end: Optional[int] = None, want32: bool = True,
-                 count_ws: Optional[torch.Tensor] = None, band_width: int = 0, use_aug: bool = True) -> PaddedRows:
+                 count_ws: Optional[torch.Tensor] = None, band_width: int = 0, use_aug: bool = True,
+                 count_origin: int = 0) -> PaddedRows:
         """Philox walks straight to Phi rows (one kernel; identical to walk + features).
 
         count_ws: a zeroed transpose workspace (``transpose_workspace``) in which the kernel also
-        counts the banded transpose's buckets, for ``transpose_banded(..., counted_ws=...)``."""
+        counts the banded transpose's buckets, for ``transpose_banded(..., counted_ws=...)``;
+        count_origin: the transposed matrix's first row (0: all of Phi; src_begin: these rows alone)."""
         n = G.n_rows
         src_end = n if src_end is None else src_end
         m, L = int(walks_per_node), int(max_walk_length)
@@ -302,7 +311,8 @@ class GRFEngine:
         C.check(self.lib.grf_walk_phi(n, _p(G.ptr), _p(G.idx), _p(G.val), _p(aug), ctypes.byref(prm), src_begin,
                                       src_end,
                                       norm, _p(ft), ft.numel(), cap, _p(cnt), _p(idx), _p(val), _p(v32),
-                                      _p(count_ws), int(band_width), self.stream), "grf_walk_phi")
+                                      _p(count_ws), int(band_width), int(count_origin), self.stream),
+                "grf_walk_phi")
         return PaddedRows(cnt, idx, val, v32, cap, n)
 
     def walk_aug(self, G: DeviceCSR) -> Optional[torch.Tensor]:
@@ -460,6 +470,35 @@ class GRFEngine:
                                                _p(tr.t_rowshift), _p(out), out.stride(0), _p(self._gram_ws),
                                                self._gram_ws.numel(), self.stream), "grf_gram_sparse_block")
         return out[:, :n]
+
+    def phi_row_shifts(self, phi: DeviceCSR) -> torch.Tensor:
+        """The Gram fixed-point shifts of every row of Phi (int32 [n_rows]; grf_phi_row_shifts): the
+        same values as ``transpose_banded(phi).t_rowshift``, for rows that are not in the transpose."""
+        n = phi.n_rows
+        shift = self._empty(max(n, 1), torch.int32)
+        mx = self._empty(1, torch.float32)
+        ws = self._ws(self.lib.grf_phi_row_shifts_workspace_bytes(n))
+        C.check(self.lib.grf_phi_row_shifts(n, _p(phi.ptr), _p(phi.val32), _p(mx), _p(shift), _p(ws), ws.numel(),
+                                            self.stream), "grf_phi_row_shifts")
+        return shift
+
+    def gram_sparse_cols(self, phi: DeviceCSR, row_shift: torch.Tensor, tr_b: Banded, row_begin: int = 0,
+                         row_end: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Column block K[row_begin:row_end, B] = Phi[rows] Phi_B^T (float32) from the banded transpose
+        ``tr_b`` of another row set Phi_B (grf_gram_sparse_cols); row_shift = ``phi_row_shifts(phi)``.
+        With Phi_B = Phi[b:e] this is K[:, b:e], bit-identical to ``gram_sparse(...)[:, b:e]``."""
+        n = phi.n_rows
+        row_end = n if row_end is None else row_end
+        t_rows = tr_b.n_rows
+        if out is None:
+            out = torch.empty((row_end - row_begin, self.leading_dim(max(t_rows, 1))), dtype=torch.float32,
+                              device=self.device)
+        C.check(self.lib.grf_gram_sparse_cols(phi.n_cols, row_begin, row_end, _p(phi.ptr), _p(phi.idx),
+                                              _p(phi.val32), _p(row_shift), t_rows, tr_b.band_width, tr_b.rec_unit,
+                                              _p(tr_b.t_desc), _p(tr_b.t_rec), _p(out), out.stride(0),
+                                              _p(self._gram_ws), self._gram_ws.numel(), self.stream),
+                "grf_gram_sparse_cols")
+        return out[:, :t_rows]
 
     def gram_sparse_kslice(self, phi: DeviceCSR, tr: Banded, k_begin: int, k_end: int, row_begin: int = 0,
                            row_end: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -156,14 +156,17 @@ int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, co
  * visit slots never touch HBM): bit-identical to grf_walk (params->rng = GRF_RNG_PHILOX)
  * followed by grf_phi_fused.  Requires m * L <= 4096.
  * Optional (t_count != NULL): also count the banded transpose's buckets of the rows written,
- * t_count[(row / band_width) * n + col] += 1 -- pass the transpose workspace (zeroed) and then
- * grf_transpose_banded_plan(..., counted = 1, ...); phi_cap must not truncate rows.
+ * t_count[((row - count_row0) / band_width) * n + col] += 1 -- pass the transpose workspace (zeroed)
+ * and then grf_transpose_banded_plan(..., counted = 1, ...); phi_cap must not truncate rows.
+ * count_row0 (<= src_begin) is the first row of the transposed matrix: 0 for all of Phi, src_begin
+ * for a transpose of these rows alone (the column-block multi-GPU Gram). 
  * Optional (g_aug != NULL, from grf_walk_aug on the same walk matrix, nnz < 2^32): each step of a
  * walk is one dependent memory round trip instead of two -- same draws, same Phi bits. */
 int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
                      const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
                      int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
-                     float *phi_val32, int32_t *t_count, int64_t band_width, grf_stream_t stream);
+                     float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
+                     grf_stream_t stream);
 /* The augmented walk matrix of grf_walk_phi: g_aug[e] = {target v, row start of v (low 32 bits),
  * row length of v, 0} (int32 x 4) for every entry e of the CSR walk matrix (g_ptr, g_idx);
  * grf_walk_aug_bytes(nnz) bytes, 16-byte aligned. */
@@ -255,6 +258,25 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
                               const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
                               int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                               grf_stream_t stream);
+
+/* Column block of K against another row set: K[r - row_begin, 0 : t_rows] = sum_k Phi[r, k] Phi_B[:, k]
+ * for the rows r in [row_begin, row_end) of Phi (CSR ptr/idx/val, n_cols columns), where Phi_B
+ * (t_rows rows, the same n_cols columns) is given by its banded transpose (grf_transpose_banded_*
+ * of Phi_B) and row_shift holds the fixed-point shifts of Phi's rows (grf_phi_row_shifts over all
+ * of Phi).  With Phi_B = Phi[b:e] the block is K[:, b:e], entry for entry the row mode's K[r, b + j]
+ * (bit-identical to grf_gram_sparse): the multi-GPU path in which each rank transposes only its
+ * own rows.  band_width: a multiple of 64 in [64, 8192]; ldk >= t_rows. */
+int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                             const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
+                             int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec, float *K,
+                             int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+
+/* The Gram fixed-point row shifts of a CSR (n_rows rows; float values) and its max |value|
+ * (*maxabs, device): the same rule and the same per-row summation order as the banded transpose's
+ * t_rowshift / t_maxabs, so grf_gram_sparse_cols reproduces grf_gram_sparse's bits. */
+size_t grf_phi_row_shifts_workspace_bytes(int64_t n_rows);
+int32_t grf_phi_row_shifts(int64_t n_rows, const int64_t *ptr, const float *val, float *maxabs, int32_t *row_shift,
+                           void *workspace, size_t workspace_bytes, grf_stream_t stream);
 
 /* K rows [row_begin, row_end) (as grf_gram_sparse) using the symmetry inside the row block: the
  * bands lying wholly inside the block are computed only on and above the diagonal for the block's

@@ -566,6 +566,34 @@ def test_sharded_counts_and_phi_equal_single_gpu(eng):
         assert torch.equal(eng.gram_sparse(phi, tr, b, e), K1[b:e])
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_column_block_gram_from_local_transpose(eng, world):
+    """The column-block multi-GPU Gram: each rank transposes only its own Phi rows and computes
+    K[:, b:e] against all (gathered) rows with the row shifts of the whole Phi -- bit-identical to
+    the single-GPU row mode's columns, for any band width of the local transpose and row subset."""
+    import torch
+    from grf_amd.dist import shard_range
+    n = 20000
+    A = er_graph(n, 10, 12)
+    G = eng.laplacian(A)
+    m, L = 32, 6
+    f = [1.0, -0.5, 0.125, -0.02, 0.003, -0.0004]
+    phi = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=8), want64=False)
+    tr = eng.transpose_banded(phi, 8192)
+    K = eng.gram_sparse(phi, tr)
+    shift = eng.phi_row_shifts(phi)
+    assert torch.equal(shift[:n], tr.t_rowshift[:n])
+    for r in range(world):
+        b, e = shard_range(n, r, world)
+        loc = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=8, src_begin=b, src_end=e), want64=False)
+        assert loc.n_rows == e - b and loc.n_cols == n
+        for bw in (64, 4096, 8192):
+            Kc = eng.gram_sparse_cols(phi, shift, eng.transpose_banded(loc, bw))
+            assert torch.equal(Kc, K[:, b:e]), (r, bw)
+        Kp = eng.gram_sparse_cols(phi, shift, eng.transpose_banded(loc, 4096), 123, 4567)
+        assert torch.equal(Kp, K[123:4567, b:e])
+
+
 @pytest.mark.parametrize("unit", [128, 12])
 def test_transpose_wide_regions(eng, unit):
     """A graph large enough that the staged fill widens its column regions (n_rows * n_cols / (16 cr)
@@ -609,3 +637,50 @@ def test_walk_phi_augmented_matrix_bitexact(eng, rule):
     node, load = O.walk_slots(ip, ix, dx, 40, 0.15, 5, rng=O.RNG_PHILOX, load_rule=rule, seed=11)
     ref = O.phi_sparse(O.reduce_steps(node, load, O.NORM_MUL_RECIP), f)
     assert same_csr(eng.compact(a).to_scipy(), ref)
+
+
+def _sharded_worker(rank, world, port, mode, q):
+    """One rank of a gloo group on cuda:0 (device tensors staged through host memory)."""
+    import os
+
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from grf_amd.dist import sharded_kernel_matrix
+        from grf_amd.engine import GRFEngine
+        eng = GRFEngine("cuda:0")
+        n = 6000
+        A = er_graph(n, 8, 21)
+        f = [1.0, -0.5, 0.125, -0.02, 0.003]
+        Kb, (b, e) = sharded_kernel_matrix(eng, A, f, 24, 0.15, 5, seed=3, mode=mode)
+        phi = eng.compact(eng.walk_phi(eng.laplacian(A), 24, 0.15, 5, f, seed=3), want64=False)
+        K = eng.gram_sparse(phi, eng.transpose_banded(phi, 8192))
+        want = K[:, b:e] if mode == "cols" else K[b:e]
+        q.put((rank, bool(torch.equal(Kb, want))))
+    except Exception as exc:  # (reported through the queue: a hung peer would hide it)
+        q.put((rank, repr(exc)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["cols", "rows"])
+def test_sharded_kernel_matrix_two_ranks_gloo(mode):
+    """The multi-GPU assembly end to end with two ranks on one GPU: each rank's block (row block,
+    or the column block from its own-rows transpose) equals the single-GPU K's, bit for bit."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+    assert res == [(0, True), (1, True)], res

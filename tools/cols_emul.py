@@ -1,0 +1,76 @@
+"""Per-rank compute of the multi-GPU step at C4, emulated on one GPU (no collectives: the gathered
+Phi is precomputed): the row-block mode (replicated transpose of all of Phi, K[b:e, :]) against the
+column-block mode (transpose of the rank's own rows, K[:, b:e]).  Prints one JSON line per world size.
+
+usage: python tools/cols_emul.py [worlds=2,4,8] [reps=3]"""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "efficient-gaussian-process-on-graphs_amd")]
+from bench import diffusion_modulator  # noqa: E402
+from grf_amd.dist import shard_range  # noqa: E402
+from grf_amd.engine import ROWS_BAND_WIDTH, DeviceCSR, GRFEngine, cols_band_width  # noqa: E402
+from grf_amd.graphs import er_graph_exact_edges  # noqa: E402
+
+worlds = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "2,4,8").split(",")]
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+eng = GRFEngine("cuda:0")
+n, m, L, p = 100_000, 128, 8, 0.1
+f = diffusion_modulator(L)
+G = eng.laplacian(DeviceCSR.from_scipy(er_graph_exact_edges(n, 1_000_000, 0), eng.device))
+bw = ROWS_BAND_WIDTH
+nbk = -(-n // bw) * n
+ws_full = eng.transpose_workspace(n, n, bw)
+phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, count_ws=ws_full, band_width=bw), want64=False)
+counts = ws_full[:4 * nbk].clone()  # the all-reduced bucket counts of the row mode
+K_ref = eng.gram_sparse(phi, eng.transpose_banded(phi, bw))
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        out = fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps, out
+
+
+for world in worlds:
+    res = {"world": world}
+    for r in sorted({0, world // 2, world - 1}):
+        b, e = shard_range(n, r, world)
+        K = torch.empty((e - b, eng.leading_dim(n)), dtype=torch.float32, device=eng.device)
+        ws = eng.transpose_workspace(n, n, bw)
+
+        def rows_step():
+            eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=ws, band_width=bw),
+                        want64=False, sync_free=True)
+            ws[:4 * nbk].copy_(counts)  # (stands in for the counts all-reduce)
+            tr = eng.transpose_banded(phi, bw, counted_ws=ws, nnz_bound=n * m * L)
+            return eng.gram_sparse(phi, tr, b, e, out=K)
+
+        wl = cols_band_width(e - b)
+        Kc = torch.empty((n, eng.leading_dim(e - b)), dtype=torch.float32, device=eng.device)
+        ws_l = eng.transpose_workspace(e - b, n, wl)
+
+        def cols_step():
+            loc = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=ws_l,
+                                           band_width=wl, count_origin=b), want64=False, sync_free=True)
+            shift = eng.phi_row_shifts(phi)
+            tr = eng.transpose_banded(loc, wl, counted_ws=ws_l, nnz_bound=(e - b) * m * L)
+            return eng.gram_sparse_cols(phi, shift, tr, out=Kc)
+
+        t_rows, Kr = timed(rows_step)
+        t_cols, Kcc = timed(cols_step)
+        res[f"r{r}"] = {"rows_ms": round(t_rows, 3), "cols_ms": round(t_cols, 3), "cols_band": wl,
+                        "rows_equal": bool(torch.equal(Kr, K_ref[b:e])),
+                        "cols_equal": bool(torch.equal(Kcc, K_ref[:, b:e]))}
+        print(json.dumps({world: res[f"r{r}"]}), flush=True)
+    print(json.dumps(res), flush=True)

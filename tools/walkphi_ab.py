@@ -24,19 +24,28 @@ f = diffusion_modulator(8)
 tws = eng.transpose_workspace(n, n, bw)
 
 
-def run():
-    return eng.walk_phi(G, m, 0.1, 8, f, seed=42, count_ws=tws, band_width=bw)
-
-
-rows = run()
-torch.cuda.synchronize()
-ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-reps = 5
-ev[0].record()
-for _ in range(reps):
+modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["count"]
+fns = {
+    "count": lambda: eng.walk_phi(G, m, 0.1, 8, f, seed=42, count_ws=tws, band_width=bw),  # (the bench's call)
+    "nocount": lambda: eng.walk_phi(G, m, 0.1, 8, f, seed=42),
+    "noaug": lambda: eng.walk_phi(G, m, 0.1, 8, f, seed=42, count_ws=tws, band_width=bw, use_aug=False),
+    "walk": lambda: eng.walk(G, m, 0.1, 8, rng=1, seed=42),  # slots only (no sort, no Phi)
+}
+out = {"cfg": cfg}
+for mode in modes:
+    run = fns[mode]
     rows = run()
-ev[1].record()
-torch.cuda.synchronize()
-cnt = rows.cnt.sum().item()
-print(json.dumps({"cfg": cfg, "walk_phi_ms": ev[0].elapsed_time(ev[1]) / reps, "nnz": int(cnt),
-                  "idx_sum": int(rows.idx.view(-1)[:1000].sum().item())}), flush=True)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 5
+    ev[0].record()
+    for _ in range(reps):
+        rows = run()
+    ev[1].record()
+    torch.cuda.synchronize()
+    out[mode + "_ms"] = ev[0].elapsed_time(ev[1]) / reps
+    if mode == "count":
+        out["nnz"] = int(rows.cnt.sum().item())
+        out["idx_sum"] = int(rows.idx.view(-1)[:1000].sum().item())
+    print(json.dumps({mode: out[mode + "_ms"]}), flush=True)
+print(json.dumps(out), flush=True)
