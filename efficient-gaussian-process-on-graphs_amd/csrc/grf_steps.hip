@@ -153,15 +153,15 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         double *__restrict__ phi_val, float *__restrict__ phi_val32,
                                                         int32_t *__restrict__ t_count, int64_t band_width,
                                                         int64_t n_cols, int64_t count_row0) {
-    // LDS: ld [E] loads by slot (later the compacted step values), fl [64] the modulator,
+    // LDS: ld [E] loads by slot (later the compacted step values), fl [Lf] the modulator,
     // scratch (2 x 16 ints), key [P] the sorted keys (later the compacted step keys).  32-bit
     // keys when (node, step, walk) fits 32 bits (C4 / C5): half the sort's LDS traffic and a
     // third of the footprint of the 64-bit layout with its separate head-value array.
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int E = (int)(m * L), T = (int)blockDim.x, tid = (int)threadIdx.x;
     double *ld = reinterpret_cast<double *>(smem);             // [E]
-    double *fl = ld + E;                                        // [64]
-    int32_t *scratch = reinterpret_cast<int32_t *>(fl + 64);    // [32]
+    double *fl = ld + E;                                        // [Lf rounded up to even]
+    int32_t *scratch = reinterpret_cast<int32_t *>(fl + ((Lf + 1) & ~1));  // [32]
     KT *key = reinterpret_cast<KT *>(scratch + 32);             // [P]
     const KT kNone = (KT)~(KT)0;
     const int64_t s = blockIdx.x;
@@ -410,7 +410,12 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     // 32-bit keys when every key (node << (wbits + lbits) | step | walk) < the sentinel 2^32 - 1:
     // needs the node-id bound n_cols, known for the walking kernel (the slots path stays 64-bit)
     const bool key32 = walk && n_cols > 0 && ((uint64_t)n_cols << (wbits + lbits)) <= 0xffffffffull;
-    const size_t lds = (size_t)E * 8 + 64 * 8 + 32 * 4 + (size_t)P * (key32 ? 4 : 8);
+    const int32_t Lf_ = n_f < L ? n_f : L;
+    static const size_t lds_pad = [] {  // (experiments: extra LDS per source, GRF_PHI_LDS_PAD bytes)
+        const char *e = getenv("GRF_PHI_LDS_PAD");
+        return e ? (size_t)atoll(e) : (size_t)0;
+    }();
+    const size_t lds = (size_t)E * 8 + (size_t)((Lf_ + 1) & ~1) * 8 + 32 * 4 + (size_t)P * (key32 ? 4 : 8) + lds_pad;
     // threads per source: P / 4 up to 256, and at most one per walk -- measured (tools/walkphi_ab.py)
     // with the 12.9 KB LDS layout: m = 128 (C4) 128 threads 2.85 ms vs 256 3.28; m = 64 (C5) 64
     // threads 11.2 ms vs 128 13.0 (idle waves hold the source's slot while its walks run, and LDS
