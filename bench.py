@@ -398,7 +398,8 @@ def main():
     ap.add_argument("--p-halt", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=2048)
-    ap.add_argument("--no-sym", action="store_true", help="single GPU: compute every K tile (no symmetric mode)")
+    ap.add_argument("--no-sym", action="store_true", help="compute every K tile (one GPU: no symmetric mode; N > 1 "
+                    "column blocks: no symmetric square K[b:e, b:e])")
     ap.add_argument("--mode", choices=["cols", "rows", "allreduce"], default="cols",
                     help="cols (default; N > 1): K column blocks K[:, R_r] (= the row blocks, K symmetric) from a "
                          "transpose of the rank's own Phi rows after a Phi all-gather; rows: K row blocks from a "
@@ -469,6 +470,7 @@ def main():
     k_rows = n if allreduce else kr_end - b
     if cols:
         wl = cols_band_width(e - b)
+        cols_sym = not args.no_sym and 4 * (e - b) >= n
         K = torch.empty((n, eng.leading_dim(e - b)), dtype=torch.float32, device=dev)  # K[:, b:e], reused
     else:
         K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
@@ -518,7 +520,10 @@ def main():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         if cols:
-            eng.gram_sparse_cols(phi, tr[1], tr[0], out=K)  # K[:, b:e] = Phi Phi[b:e]^T
+            # K[:, b:e] = Phi Phi[b:e]^T; the square K[b:e, b:e] on and above its diagonal + mirror
+            # (the square pays from N <= 4: per-rank emulation N = 2 14.9 -> 14.1 ms, N = 4 7.95 -> 7.85 ms,
+            # N = 8 4.13 -> 4.19 ms)
+            eng.gram_sparse_cols(phi, tr[1], tr[0], out=K, sym_row0=b if cols_sym else None)
         elif allreduce:
             eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
         elif sym_mode:

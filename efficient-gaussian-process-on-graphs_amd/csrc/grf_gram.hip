@@ -661,8 +661,9 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
 // is K[:, b:e] -- entry for entry the row mode's K[r, b + j] -- so a rank transposes only its rows.
 int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
                              const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
-                             int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec, float *K,
-                             int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+                             int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
+                             const void *t_rec, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
+                             grf_stream_t stream) {
     GRF_REQUIRE(n_cols > 0 && 0 <= row_begin && row_begin <= row_end && ptr && idx && val && row_shift &&
                     t_rows >= 0 && t_desc && t_rec && K && ldk >= t_rows,
                 GRF_EINVAL, "grf_gram_sparse_cols: bad arguments");
@@ -671,14 +672,29 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
     GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_gram_sparse_cols: t_rec must be 128-byte aligned");
     GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED, GRF_EINVAL,
                 "grf_gram_sparse_cols: bad rec_unit");
+    GRF_REQUIRE(sym_row0 < 0 || (row_begin <= sym_row0 && sym_row0 + t_rows <= row_end), GRF_EINVAL,
+                "grf_gram_sparse_cols: the symmetric square [sym_row0, sym_row0 + t_rows) must lie in the rows");
     (void)workspace;
     (void)workspace_bytes;
     if (row_end == row_begin || t_rows == 0) return GRF_OK;
-    GramTiles tl{row_end - row_begin, band_width, cdiv<int64_t>(t_rows, band_width), false, 0, (int32_t)n_cols};
-    tl.t_rows = t_rows;
+    const int64_t nb = cdiv<int64_t>(t_rows, band_width);
+    hipStream_t st = S(stream);
     // (the kernel reads row_shift[row] for row = row_begin + r: the shifts of Phi's rows)
-    return gram_tiles_launch(n_cols, row_begin, tl, 0, tl.total(), ptr, idx, val, t_desc, t_rec, rec_unit, row_shift,
-                             K, ldk, S(stream));
+    auto launch = [&](int64_t r0, int64_t r1, bool sym) -> int32_t {
+        if (r1 <= r0) return GRF_OK;
+        GramTiles tl{r1 - r0, band_width, nb, sym, 0, (int32_t)n_cols};
+        tl.t_rows = t_rows;
+        return gram_tiles_launch(n_cols, r0, tl, 0, tl.total(), ptr, idx, val, t_desc, t_rec, rec_unit, row_shift,
+                                 K + (r0 - row_begin) * ldk, ldk, st);
+    };
+    if (sym_row0 < 0) return launch(row_begin, row_end, false);
+    // Phi_B = Phi[sym_row0, sym_row0 + t_rows): the square K[B, B] is symmetric and its bands start at
+    // sym_row0, so only its tiles on and above the diagonal run (symmetric enumeration), then a mirror
+    int32_t rc = launch(sym_row0, sym_row0 + t_rows, true);
+    if (rc == GRF_OK) rc = launch(row_begin, sym_row0, false);
+    if (rc == GRF_OK) rc = launch(sym_row0 + t_rows, row_end, false);
+    if (rc != GRF_OK) return rc;
+    return grf_gram_mirror(t_rows, K + (sym_row0 - row_begin) * ldk, ldk, 0, stream);
 }
 
 // K rows [row_begin, row_end) of the whole K using the symmetry inside the row block: the bands

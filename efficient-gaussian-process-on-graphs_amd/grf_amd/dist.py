@@ -153,7 +153,8 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
     """This rank's row block of K = Phi Phi^T (float32, on the engine's device), and its row range.
 
     ``mode="cols"``: this rank's column block K[:, b:e] (n x (e - b)) instead -- the same numbers
-    as the row block (K is symmetric; entry for entry the row mode's K[i, b + j]), computed from a
+    as the row block (K is symmetric; entry for entry the row mode's K[i, b + j], except that for
+    world <= 4 the square K[b:e, b:e] is computed on and above its diagonal and mirrored), from a
     transpose of the rank's own Phi rows only (no replicated transpose, no bucket-count all-reduce).
     ``mode="allreduce"``: every rank returns the whole K (row range (0, n)), assembled as the
     all-reduced sum of per-rank partial Grams over inner-dimension slices."""
@@ -215,5 +216,8 @@ def _cols_block(engine, G, f, m, p_halt, L, seed, rng, b, e, group, wl):
     phi = gather_phi(engine, local, None, group) if world > 1 else \
         DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
     tr = engine.transpose_banded(local, wl, counted_ws=tws)
-    return engine.gram_sparse_cols(phi, engine.phi_row_shifts(phi), tr)
+    # the square K[b:e, b:e] on and above its diagonal, then mirrored, when it is a large enough share
+    # of the block to pay for the mirror (N <= 4)
+    sym = 4 * (e - b) >= n
+    return engine.gram_sparse_cols(phi, engine.phi_row_shifts(phi), tr, sym_row0=b if sym else None)
 

@@ -483,10 +483,13 @@ class GRFEngine:
         return shift
 
     def gram_sparse_cols(self, phi: DeviceCSR, row_shift: torch.Tensor, tr_b: Banded, row_begin: int = 0,
-                         row_end: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                         row_end: Optional[int] = None, out: Optional[torch.Tensor] = None,
+                         sym_row0: Optional[int] = None) -> torch.Tensor:
         """Column block K[row_begin:row_end, B] = Phi[rows] Phi_B^T (float32) from the banded transpose
         ``tr_b`` of another row set Phi_B (grf_gram_sparse_cols); row_shift = ``phi_row_shifts(phi)``.
-        With Phi_B = Phi[b:e] this is K[:, b:e], bit-identical to ``gram_sparse(...)[:, b:e]``."""
+        With Phi_B = Phi[b:e] this is K[:, b:e], bit-identical to ``gram_sparse(...)[:, b:e]``;
+        sym_row0 = b says so, and the square K[b:e, b:e] is then computed on and above its diagonal
+        and mirrored (the symmetric mode's bits there)."""
         n = phi.n_rows
         row_end = n if row_end is None else row_end
         t_rows = tr_b.n_rows
@@ -494,7 +497,8 @@ class GRFEngine:
             out = torch.empty((row_end - row_begin, self.leading_dim(max(t_rows, 1))), dtype=torch.float32,
                               device=self.device)
         C.check(self.lib.grf_gram_sparse_cols(phi.n_cols, row_begin, row_end, _p(phi.ptr), _p(phi.idx),
-                                              _p(phi.val32), _p(row_shift), t_rows, tr_b.band_width, tr_b.rec_unit,
+                                              _p(phi.val32), _p(row_shift), t_rows,
+                                              -1 if sym_row0 is None else int(sym_row0), tr_b.band_width, tr_b.rec_unit,
                                               _p(tr_b.t_desc), _p(tr_b.t_rec), _p(out), out.stride(0),
                                               _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_cols")

@@ -265,11 +265,15 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
  * of Phi_B) and row_shift holds the fixed-point shifts of Phi's rows (grf_phi_row_shifts over all
  * of Phi).  With Phi_B = Phi[b:e] the block is K[:, b:e], entry for entry the row mode's K[r, b + j]
  * (bit-identical to grf_gram_sparse): the multi-GPU path in which each rank transposes only its
- * own rows.  band_width: a multiple of 64 in [64, 8192]; ldk >= t_rows. */
+ * own rows.  band_width: a multiple of 64 in [64, 8192]; ldk >= t_rows.
+ * sym_row0 >= 0 declares Phi_B = Phi[sym_row0, sym_row0 + t_rows) (inside [row_begin, row_end)):
+ * the square K[B, B] is then computed on and above its diagonal only and mirrored (its entries
+ * below the diagonal carry the upper entry's bits, as in grf_gram_sparse_sym); sym_row0 < 0: none. */
 int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
                              const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
-                             int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec, float *K,
-                             int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+                             int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
+                             const void *t_rec, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
+                             grf_stream_t stream);
 
 /* The Gram fixed-point row shifts of a CSR (n_rows rows; float values) and its max |value|
  * (*maxabs, device): the same rule and the same per-row summation order as the banded transpose's

@@ -566,6 +566,15 @@ def test_sharded_counts_and_phi_equal_single_gpu(eng):
         assert torch.equal(eng.gram_sparse(phi, tr, b, e), K1[b:e])
 
 
+def _sym_square(Kc, b, e):
+    """Kc = K[:, b:e] with its square K[b:e, b:e] made symmetric from its upper triangle."""
+    import torch
+    out = Kc.clone()
+    sq = Kc[b:e]
+    out[b:e] = torch.triu(sq) + torch.triu(sq, 1).T
+    return out
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_column_block_gram_from_local_transpose(eng, world):
     """The column-block multi-GPU Gram: each rank transposes only its own Phi rows and computes
@@ -587,9 +596,13 @@ def test_column_block_gram_from_local_transpose(eng, world):
         b, e = shard_range(n, r, world)
         loc = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=8, src_begin=b, src_end=e), want64=False)
         assert loc.n_rows == e - b and loc.n_cols == n
+        want_sym = _sym_square(K[:, b:e], b, e)
         for bw in (64, 4096, 8192):
-            Kc = eng.gram_sparse_cols(phi, shift, eng.transpose_banded(loc, bw))
+            tb = eng.transpose_banded(loc, bw)
+            Kc = eng.gram_sparse_cols(phi, shift, tb)
             assert torch.equal(Kc, K[:, b:e]), (r, bw)
+            # the symmetric square K[b:e, b:e]: upper tiles + mirror
+            assert torch.equal(eng.gram_sparse_cols(phi, shift, tb, sym_row0=b), want_sym), (r, bw)
         Kp = eng.gram_sparse_cols(phi, shift, eng.transpose_banded(loc, 4096), 123, 4567)
         assert torch.equal(Kp, K[123:4567, b:e])
 
@@ -657,7 +670,7 @@ def _sharded_worker(rank, world, port, mode, q):
         Kb, (b, e) = sharded_kernel_matrix(eng, A, f, 24, 0.15, 5, seed=3, mode=mode)
         phi = eng.compact(eng.walk_phi(eng.laplacian(A), 24, 0.15, 5, f, seed=3), want64=False)
         K = eng.gram_sparse(phi, eng.transpose_banded(phi, 8192))
-        want = K[:, b:e] if mode == "cols" else K[b:e]
+        want = _sym_square(K[:, b:e], b, e) if mode == "cols" else K[b:e]  # (2 ranks: the square is mirrored)
         q.put((rank, bool(torch.equal(Kb, want))))
     except Exception as exc:  # (reported through the queue: a hung peer would hide it)
         q.put((rank, repr(exc)))

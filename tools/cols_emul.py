@@ -65,12 +65,19 @@ for world in worlds:
                                            band_width=wl, count_origin=b), want64=False, sync_free=True)
             shift = eng.phi_row_shifts(phi)
             tr = eng.transpose_banded(loc, wl, counted_ws=ws_l, nnz_bound=(e - b) * m * L)
-            return eng.gram_sparse_cols(phi, shift, tr, out=Kc)
+            return eng.gram_sparse_cols(phi, shift, tr, out=Kc, sym_row0=b if sym else None)
 
         t_rows, Kr = timed(rows_step)
+        sym = False
         t_cols, Kcc = timed(cols_step)
-        res[f"r{r}"] = {"rows_ms": round(t_rows, 3), "cols_ms": round(t_cols, 3), "cols_band": wl,
-                        "rows_equal": bool(torch.equal(Kr, K_ref[b:e])),
-                        "cols_equal": bool(torch.equal(Kcc, K_ref[:, b:e]))}
+        cols_equal = bool(torch.equal(Kcc, K_ref[:, b:e]))
+        sym = True
+        t_sym, Kcs = timed(cols_step)
+        sq = K_ref[b:e, b:e]
+        sym_equal = bool(torch.equal(Kcs[b:e], torch.triu(sq) + torch.triu(sq, 1).T)
+                         and torch.equal(Kcs[:b], K_ref[:b, b:e]) and torch.equal(Kcs[e:], K_ref[e:, b:e]))
+        res[f"r{r}"] = {"rows_ms": round(t_rows, 3), "cols_ms": round(t_cols, 3), "cols_sym_ms": round(t_sym, 3),
+                        "cols_band": wl, "rows_equal": bool(torch.equal(Kr, K_ref[b:e])),
+                        "cols_equal": cols_equal, "cols_sym_equal": sym_equal}
         print(json.dumps({world: res[f"r{r}"]}), flush=True)
     print(json.dumps(res), flush=True)
