@@ -194,3 +194,45 @@ def test_philox_mode_through_api_matches_oracle():
     ref = O.reduce_steps(node, load, O.NORM_MUL_RECIP)
     for a, b in zip(mats, ref):
         assert same_csr(a, b)
+
+
+def _degenerate_graphs():
+    """Edge cases the path has to survive: one node, no edges, a star (one hub of degree n - 1),
+    disjoint components with isolated nodes, a path, a weighted pair."""
+    r = np.random.default_rng(0)
+    star = np.zeros((200, 200))
+    star[0, 1:] = star[1:, 0] = 1.0
+    comp = np.zeros((60, 60))
+    for a, b in [(0, 1), (1, 2), (2, 0), (10, 11), (30, 31), (31, 32), (32, 33)]:
+        comp[a, b] = comp[b, a] = 1.0
+    path = np.diag(np.ones(39), 1)
+    path = path + path.T
+    pair = np.array([[0.0, 2.5], [2.5, 0.0]])
+    er = (r.random((90, 90)) < 0.04).astype(float)
+    er = np.triu(er, 1)
+    er = er + er.T
+    return {"single": np.zeros((1, 1)), "empty": np.zeros((50, 50)), "star": star, "components": comp,
+            "path": path, "pair": pair, "er_sparse": er}
+
+
+@pytest.mark.parametrize("name", list(_degenerate_graphs()))
+def test_degenerate_graphs_match_oracle(name):
+    """Both drop-in entry points on degenerate graphs (reference stream, 3 chunks) against the C
+    oracle's restatement of the reference: sparse K within the fp32 Gram tolerance, dense K too."""
+    from efficient_graph_gp.graph_kernels.fast_grf_kernel_general import fast_general_grf_kernel as dense_k
+    from efficient_graph_gp_sparse.graph_kernels_sparse.fast_grf_kernel_general import fast_general_grf_kernel as sk
+    from oracle import oracle as O
+    A = _degenerate_graphs()[name]
+    f = [1.0, -0.5, 0.25, -0.125]
+    m, p, L, nproc = 16, 0.2, 4, 3
+    Ls, _ = O.laplacian_sparse(sp.csr_matrix(A))
+    phi = O.phi_sparse(O.sparse_random_walk(Ls, m, p, L, n_processes=nproc, seed=None), f)
+    ref = O.gram_rows(phi)
+    K = sk(sp.csr_matrix(A), f, walks_per_node=m, p_halt=p, max_walk_length=L, n_processes=nproc)
+    assert K.shape == A.shape
+    np.testing.assert_allclose(K.toarray(), ref, rtol=3e-5, atol=1e-6 * max(np.abs(ref).max(), 1e-30))
+    if A.shape[0] >= 2 * nproc:  # (below that the dense reference takes its sequential path)
+        F = O.dense_random_walk(O.laplacian_dense(A, 0), m, p, L, n_processes=nproc, seed=42)
+        Phi = np.einsum("ijl,l->ij", F, np.asarray(f))
+        Kd = dense_k(A, f, walks_per_node=m, p_halt=p, max_walk_length=L, n_processes=nproc)
+        np.testing.assert_allclose(Kd, Phi @ Phi.T, rtol=3e-5, atol=1e-6 * max(np.abs(Phi @ Phi.T).max(), 1e-30))

@@ -697,3 +697,30 @@ def test_sharded_kernel_matrix_two_ranks_gloo(mode):
     for p in procs:
         p.join(timeout=30)
     assert res == [(0, True), (1, True)], res
+
+
+@pytest.mark.parametrize("name", ["single", "empty", "star", "components", "path", "pair", "er_sparse"])
+def test_bench_path_on_degenerate_graphs(eng, name):
+    """The bench's device path (fused Philox walks -> Phi -> banded transpose -> symmetric Gram +
+    mirror, row mode, and the column blocks with their symmetric square) on degenerate graphs:
+    Phi bit-exact against walk + features, every K mode against the fp64 oracle Gram."""
+    import torch
+    from test_gpu_api import _degenerate_graphs
+    A = sp.csr_matrix(_degenerate_graphs()[name])
+    n = A.shape[0]
+    G = eng.laplacian(A)
+    f = [1.0, -0.5, 0.25, -0.125]
+    phi = eng.compact(eng.walk_phi(G, 16, 0.2, 4, f, seed=4), want64=False)
+    ref = eng.compact(eng.features(eng.walk(G, 16, 0.2, 4, rng=1, seed=4), f))
+    assert same_csr(eng.compact(eng.walk_phi(G, 16, 0.2, 4, f, seed=4)).to_scipy(), ref.to_scipy())
+    tr = eng.transpose_banded(phi, 4096)
+    K = eng.gram_sparse(phi, tr)
+    ok, fro = gram_close(K.cpu().numpy(), ref.to_scipy())
+    assert ok, fro
+    Ks = eng.gram_sparse_sym(phi, tr)
+    assert torch.equal(Ks, Ks.T) and torch.equal(torch.triu(Ks), torch.triu(K))
+    b, e = n // 3, n - n // 4
+    if e > b:
+        loc = eng.compact(eng.walk_phi(G, 16, 0.2, 4, f, seed=4, src_begin=b, src_end=e), want64=False)
+        Kc = eng.gram_sparse_cols(phi, eng.phi_row_shifts(phi), eng.transpose_banded(loc, 64), sym_row0=b)
+        assert torch.equal(Kc, _sym_square(K[:, b:e], b, e))
