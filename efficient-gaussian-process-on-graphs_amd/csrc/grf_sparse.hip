@@ -49,6 +49,72 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(int64_t n, con
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) out[n] = run;
 }
 
+// Coalesced variants: the tile is loaded lane-striped (consecutive lanes, consecutive elements),
+// transposed through LDS to per-thread runs of kScanItems for the scan, and stored lane-striped
+// again (the kernels above give every lane its own 64-byte input run and 128-byte output run).
+// Padding one slot per 16 keeps the per-thread runs on distinct LDS banks.
+__device__ __forceinline__ int scan_pad(int i) { return i + (i >> 4); }
+constexpr int kScanLds = (int)kScanTile + (int)(kScanTile >> 4);
+
+template <typename TIn>
+__global__ __launch_bounds__(kScanThreads) void scan_reduce_striped_kernel(int64_t n, const TIn *in, int64_t *part) {
+    __shared__ int64_t scratch[kScanThreads / 64 + 1];
+    const int64_t blk = (int64_t)blockIdx.x * kScanTile;
+    int64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int64_t g = blk + k * kScanThreads + threadIdx.x;
+        if (g < n) s += (int64_t)in[g];  // (an integer sum: any order gives the same total)
+    }
+    int64_t tot;
+    block_exclusive_scan<int64_t>(s, scratch, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+template <typename TIn>
+__global__ __launch_bounds__(kScanThreads) void scan_apply_striped_kernel(int64_t n, const TIn *in,
+                                                                          const int64_t *offset, int64_t *out) {
+    __shared__ int64_t sh[kScanLds];
+    __shared__ int64_t scratch[kScanThreads / 64 + 1];
+    const int tid = threadIdx.x;
+    const int64_t blk = (int64_t)blockIdx.x * kScanTile;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int i = k * kScanThreads + tid;
+        sh[scan_pad(i)] = blk + i < n ? (int64_t)in[blk + i] : 0;
+    }
+    __syncthreads();
+    int64_t v[kScanItems];
+    int64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = sh[scan_pad(tid * kScanItems + k)];
+        s += v[k];
+    }
+    int64_t tot;
+    int64_t run = block_exclusive_scan<int64_t>(s, scratch, &tot) + (offset ? offset[blockIdx.x] : 0);
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        sh[scan_pad(tid * kScanItems + k)] = run;
+        run += v[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && tid == kScanThreads - 1) out[n] = run;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int i = k * kScanThreads + tid;
+        if (blk + i < n) out[blk + i] = sh[scan_pad(i)];
+    }
+}
+
+static bool scan_striped() {  // (GRF_SCAN_LEGACY=1: the per-lane-run kernels, for A/B runs)
+    static const bool v = [] {
+        const char *e = getenv("GRF_SCAN_LEGACY");
+        return !(e && atoi(e) != 0);
+    }();
+    return v;
+}
+
 static size_t scan_ws_elems(int64_t n) {
     int64_t nb = cdiv<int64_t>(n, kScanTile);
     if (nb <= 1) return 0;
@@ -62,20 +128,24 @@ static int32_t scan_exclusive(int64_t n, const TIn *in, int64_t *out, int64_t *w
         GRF_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), st));
         return GRF_OK;
     }
+    const bool striped = scan_striped();
     if (nb == 1) {
         GRF_REQUIRE_GRID(1, kScanThreads, "scan_apply_kernel");
-        scan_apply_kernel<TIn><<<1, kScanThreads, 0, st>>>(n, in, nullptr, out);
+        if (striped) scan_apply_striped_kernel<TIn><<<1, kScanThreads, 0, st>>>(n, in, nullptr, out);
+        else scan_apply_kernel<TIn><<<1, kScanThreads, 0, st>>>(n, in, nullptr, out);
         GRF_CHECK_LAUNCH("scan_apply_kernel");
         return GRF_OK;
     }
     int64_t *part = ws, *part_ex = ws + nb, *rest = ws + nb + nb + 1;
     GRF_REQUIRE_GRID(nb, kScanThreads, "scan_reduce_kernel");
-    scan_reduce_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part);
+    if (striped) scan_reduce_striped_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part);
+    else scan_reduce_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part);
     GRF_CHECK_LAUNCH("scan_reduce_kernel");
     int32_t rc = scan_exclusive<int64_t>(nb, part, part_ex, rest, st);
     if (rc != GRF_OK) return rc;
     GRF_REQUIRE_GRID(nb, kScanThreads, "scan_apply_kernel");
-    scan_apply_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part_ex, out);
+    if (striped) scan_apply_striped_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part_ex, out);
+    else scan_apply_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part_ex, out);
     GRF_CHECK_LAUNCH("scan_apply_kernel");
     return GRF_OK;
 }
