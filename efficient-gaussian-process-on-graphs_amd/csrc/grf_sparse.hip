@@ -13,67 +13,43 @@ constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int64_t kScanTile = (int64_t)kScanThreads * kScanItems;
 
-template <typename TIn>
-__global__ __launch_bounds__(kScanThreads) void scan_reduce_kernel(int64_t n, const TIn *in, int64_t *part) {
-    __shared__ int64_t scratch[kScanThreads / 64 + 1];
-    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-    int64_t s = 0;
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k)
-        if (base + k < n) s += (int64_t)in[base + k];
-    int64_t tot;
-    block_exclusive_scan<int64_t>(s, scratch, &tot);
-    if (threadIdx.x == 0) part[blockIdx.x] = tot;
-}
-
-// out[i] = offset[blockIdx] + exclusive prefix; out[n] = total (written by the last tile)
-template <typename TIn>
-__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(int64_t n, const TIn *in, const int64_t *offset,
-                                                                  int64_t *out) {
-    __shared__ int64_t scratch[kScanThreads / 64 + 1];
-    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-    int64_t v[kScanItems];
-    int64_t s = 0;
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        v[k] = base + k < n ? (int64_t)in[base + k] : 0;
-        s += v[k];
-    }
-    int64_t tot;
-    int64_t run = block_exclusive_scan<int64_t>(s, scratch, &tot) + (offset ? offset[blockIdx.x] : 0);
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        if (base + k < n) out[base + k] = run;
-        run += v[k];
-    }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) out[n] = run;
-}
-
-// Coalesced variants: the tile is loaded lane-striped (consecutive lanes, consecutive elements),
-// transposed through LDS to per-thread runs of kScanItems for the scan, and stored lane-striped
-// again (the kernels above give every lane its own 64-byte input run and 128-byte output run).
-// Padding one slot per 16 keeps the per-thread runs on distinct LDS banks.
+// Exclusive scans of n values map(in[i]) (int64 sums).  A tile of kScanTile values is loaded
+// lane-striped (consecutive lanes, consecutive elements), transposed through LDS to per-thread
+// runs of kScanItems for the scan, and handed to the output functor lane-striped again, so both
+// global sides are coalesced (a per-lane run layout gives every lane its own 64-byte input and
+// 128-byte output run: C5's 123 M-bucket scans ran at ~2 TB/s that way).  One padding slot per
+// 16 keeps the per-thread runs on distinct LDS banks.
 __device__ __forceinline__ int scan_pad(int i) { return i + (i >> 4); }
 constexpr int kScanLds = (int)kScanTile + (int)(kScanTile >> 4);
 
-template <typename TIn>
-__global__ __launch_bounds__(kScanThreads) void scan_reduce_striped_kernel(int64_t n, const TIn *in, int64_t *part) {
+struct ScanIdentity {
+    template <typename T>
+    __device__ int64_t operator()(T v) const { return (int64_t)v; }
+};
+struct ScanStore {  // out[i] = prefix, out[n] = total
+    int64_t *out;
+    __device__ void operator()(int64_t i, int64_t prefix) const { out[i] = prefix; }
+    __device__ void total(int64_t n, int64_t t) const { out[n] = t; }
+};
+
+template <typename TIn, typename Map>
+__global__ __launch_bounds__(kScanThreads) void scan_reduce_kernel(int64_t n, const TIn *in, Map map, int64_t *part) {
     __shared__ int64_t scratch[kScanThreads / 64 + 1];
     const int64_t blk = (int64_t)blockIdx.x * kScanTile;
     int64_t s = 0;
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
         const int64_t g = blk + k * kScanThreads + threadIdx.x;
-        if (g < n) s += (int64_t)in[g];  // (an integer sum: any order gives the same total)
+        if (g < n) s += map(in[g]);  // (an integer sum: any order gives the same total)
     }
     int64_t tot;
     block_exclusive_scan<int64_t>(s, scratch, &tot);
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-template <typename TIn>
-__global__ __launch_bounds__(kScanThreads) void scan_apply_striped_kernel(int64_t n, const TIn *in,
-                                                                          const int64_t *offset, int64_t *out) {
+template <typename TIn, typename Map, typename Out>
+__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(int64_t n, const TIn *in, Map map,
+                                                                  const int64_t *offset, Out out) {
     __shared__ int64_t sh[kScanLds];
     __shared__ int64_t scratch[kScanThreads / 64 + 1];
     const int tid = threadIdx.x;
@@ -81,7 +57,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_striped_kernel(int64_
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
         const int i = k * kScanThreads + tid;
-        sh[scan_pad(i)] = blk + i < n ? (int64_t)in[blk + i] : 0;
+        sh[scan_pad(i)] = blk + i < n ? map(in[blk + i]) : 0;
     }
     __syncthreads();
     int64_t v[kScanItems];
@@ -98,21 +74,13 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_striped_kernel(int64_
         sh[scan_pad(tid * kScanItems + k)] = run;
         run += v[k];
     }
-    if (blockIdx.x == gridDim.x - 1 && tid == kScanThreads - 1) out[n] = run;
+    if (blockIdx.x == gridDim.x - 1 && tid == kScanThreads - 1) out.total(n, run);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
         const int i = k * kScanThreads + tid;
-        if (blk + i < n) out[blk + i] = sh[scan_pad(i)];
+        if (blk + i < n) out(blk + i, sh[scan_pad(i)]);
     }
-}
-
-static bool scan_striped() {  // (GRF_SCAN_LEGACY=1: the per-lane-run kernels, for A/B runs)
-    static const bool v = [] {
-        const char *e = getenv("GRF_SCAN_LEGACY");
-        return !(e && atoi(e) != 0);
-    }();
-    return v;
 }
 
 static size_t scan_ws_elems(int64_t n) {
@@ -121,31 +89,26 @@ static size_t scan_ws_elems(int64_t n) {
     return (size_t)(nb + nb + 1) + scan_ws_elems(nb);
 }
 
-template <typename TIn>
-static int32_t scan_exclusive(int64_t n, const TIn *in, int64_t *out, int64_t *ws, hipStream_t st) {
-    int64_t nb = cdiv<int64_t>(n, kScanTile);
+template <typename TIn, typename Map, typename Out>
+static int32_t scan_exclusive(int64_t n, const TIn *in, Map map, Out out, int64_t *ws, hipStream_t st) {
+    const int64_t nb = cdiv<int64_t>(n, kScanTile);
     if (n == 0) {
-        GRF_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), st));
+        scan_apply_kernel<TIn, Map, Out><<<1, kScanThreads, 0, st>>>(0, in, map, nullptr, out);  // (the total, 0)
+        GRF_CHECK_LAUNCH("scan_apply_kernel");
         return GRF_OK;
     }
-    const bool striped = scan_striped();
     if (nb == 1) {
-        GRF_REQUIRE_GRID(1, kScanThreads, "scan_apply_kernel");
-        if (striped) scan_apply_striped_kernel<TIn><<<1, kScanThreads, 0, st>>>(n, in, nullptr, out);
-        else scan_apply_kernel<TIn><<<1, kScanThreads, 0, st>>>(n, in, nullptr, out);
+        scan_apply_kernel<TIn, Map, Out><<<1, kScanThreads, 0, st>>>(n, in, map, nullptr, out);
         GRF_CHECK_LAUNCH("scan_apply_kernel");
         return GRF_OK;
     }
     int64_t *part = ws, *part_ex = ws + nb, *rest = ws + nb + nb + 1;
     GRF_REQUIRE_GRID(nb, kScanThreads, "scan_reduce_kernel");
-    if (striped) scan_reduce_striped_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part);
-    else scan_reduce_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part);
+    scan_reduce_kernel<TIn, Map><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, map, part);
     GRF_CHECK_LAUNCH("scan_reduce_kernel");
-    int32_t rc = scan_exclusive<int64_t>(nb, part, part_ex, rest, st);
+    int32_t rc = scan_exclusive<int64_t>(nb, part, ScanIdentity{}, ScanStore{part_ex}, rest, st);
     if (rc != GRF_OK) return rc;
-    GRF_REQUIRE_GRID(nb, kScanThreads, "scan_apply_kernel");
-    if (striped) scan_apply_striped_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part_ex, out);
-    else scan_apply_kernel<TIn><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, part_ex, out);
+    scan_apply_kernel<TIn, Map, Out><<<(unsigned)nb, kScanThreads, 0, st>>>(n, in, map, part_ex, out);
     GRF_CHECK_LAUNCH("scan_apply_kernel");
     return GRF_OK;
 }
@@ -154,11 +117,11 @@ static int32_t scan_exclusive(int64_t n, const TIn *in, int64_t *out, int64_t *w
 int32_t scan_counts_i32(int64_t n, const int32_t *cnt, int64_t *out, void *ws, size_t ws_bytes, hipStream_t st) {
     GRF_REQUIRE(ws_bytes >= scan_ws_elems(n) * sizeof(int64_t), GRF_EINVAL, "scan workspace too small (%zu < %zu)",
                 ws_bytes, scan_ws_elems(n) * sizeof(int64_t));
-    return scan_exclusive<int32_t>(n, cnt, out, (int64_t *)ws, st);
+    return scan_exclusive<int32_t>(n, cnt, ScanIdentity{}, ScanStore{out}, (int64_t *)ws, st);
 }
 int32_t scan_counts_i64(int64_t n, const int64_t *cnt, int64_t *out, void *ws, size_t ws_bytes, hipStream_t st) {
     GRF_REQUIRE(ws_bytes >= scan_ws_elems(n) * sizeof(int64_t), GRF_EINVAL, "scan workspace too small");
-    return scan_exclusive<int64_t>(n, cnt, out, (int64_t *)ws, st);
+    return scan_exclusive<int64_t>(n, cnt, ScanIdentity{}, ScanStore{out}, (int64_t *)ws, st);
 }
 size_t scan_ws_bytes(int64_t n) { return scan_ws_elems(n) * sizeof(int64_t); }
 
@@ -199,16 +162,20 @@ __global__ __launch_bounds__(256) void tr_count_kernel(int64_t n_rows, int64_t n
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) atomicAdd(&cnt[band_off + idx[e]], 1);
 }
 
-__global__ void tr_lines_kernel(int64_t n, const int32_t *cnt, int32_t *lines, int32_t unit) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) lines[i] = (kPairBytes * ((cnt[i] + 1) >> 1) + unit - 1) / unit;
-}
-
-__global__ void tr_desc_kernel(int64_t n, const int32_t *cnt, const int64_t *line_off, uint2 *desc) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) desc[i] = make_uint2((uint32_t)line_off[i], (uint32_t)((cnt[i] + 1) >> 1));
-    if (i == n) desc[n] = make_uint2((uint32_t)line_off[n], (uint32_t)(line_off[n] >> 32));
-}
+// the transpose plan as one scan: units per bucket (map) -> descriptors {first unit, pairs} (output);
+// desc[n] = the total units as {low, high} 32-bit words
+struct TrUnitsMap {
+    int32_t unit;
+    __device__ int64_t operator()(int32_t c) const { return (kPairBytes * ((c + 1) >> 1) + unit - 1) / unit; }
+};
+struct TrDescOut {
+    const int32_t *cnt;
+    uint2 *desc;
+    __device__ void operator()(int64_t i, int64_t first) const {
+        desc[i] = make_uint2((uint32_t)first, (uint32_t)((cnt[i] + 1) >> 1));
+    }
+    __device__ void total(int64_t n, int64_t t) const { desc[n] = make_uint2((uint32_t)t, (uint32_t)(t >> 32)); }
+};
 
 __global__ __launch_bounds__(256) void tr_fill_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, const int64_t *ptr,
                                                       const int32_t *idx, const float *val, const uint2 *desc,
@@ -581,8 +548,7 @@ int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_w
     hipStream_t st = S(stream);
     char *w = (char *)workspace;
     int32_t *cnt = (int32_t *)w;
-    int32_t *lines = (int32_t *)(w + tr_align((size_t)nbk * 4));
-    int64_t *line_off = (int64_t *)(w + 2 * tr_align((size_t)nbk * 4));
+    // (the workspace layout is shared with the fills: [cnt | row_max | ent_off | scan scratch])
     void *scan_ws = w + 2 * tr_align((size_t)nbk * 4) + tr_align((size_t)(nbk + 1) * 8);
     if (!counted) GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)nbk * sizeof(int32_t), st));
     if (n_rows > 0 && !counted) {
@@ -591,16 +557,9 @@ int32_t grf_transpose_banded_plan(int64_t n_rows, int64_t n_cols, int64_t band_w
                                                                           cnt);
         GRF_CHECK_LAUNCH("tr_count_kernel");
     }
-    GRF_REQUIRE_GRID(cdiv<int64_t>(nbk, 256), 256, "tr_lines_kernel");
-    tr_lines_kernel<<<(unsigned)cdiv<int64_t>(nbk, 256), 256, 0, st>>>(nbk, cnt, lines, rec_unit);
-    GRF_CHECK_LAUNCH("tr_lines_kernel");
-    int32_t rc = scan_counts_i32(nbk, lines, line_off, scan_ws, scan_ws_bytes(nbk), st);
-    if (rc != GRF_OK) return rc;
-    GRF_REQUIRE_GRID(cdiv<int64_t>(nbk + 1, 256), 256, "tr_desc_kernel");
-    tr_desc_kernel<<<(unsigned)cdiv<int64_t>(nbk + 1, 256), 256, 0, st>>>(nbk, cnt, line_off,
-                                                                         reinterpret_cast<uint2 *>(t_desc));
-    GRF_CHECK_LAUNCH("tr_desc_kernel");
-    return GRF_OK;
+    // units per bucket -> exclusive scan -> descriptors, in one scan (no units / offsets arrays)
+    return scan_exclusive<int32_t>(nbk, cnt, TrUnitsMap{rec_unit}, TrDescOut{cnt, reinterpret_cast<uint2 *>(t_desc)},
+                                   (int64_t *)scan_ws, st);
 }
 
 int32_t grf_transpose_banded_fill(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
