@@ -90,4 +90,64 @@ __device__ inline void block_bitonic_sort(KT *key, int P) {
     }
 }
 
+// Bitonic sort (ascending) of P = R * blockDim.x keys with each thread holding the R consecutive
+// keys [tid R, (tid + 1) R) in registers: the stages whose partner is in the same thread (j < R)
+// run in registers, the ones whose partner thread is in the same wave through lane shuffles, and
+// only partners in another wave go through LDS -- against two LDS reads, up to two writes and a
+// barrier per pair and stage for block_bitonic_sort.  Same result (a sorting network; keys equal
+// only when interchangeable).  Reads its keys from key[] and writes the sorted keys back; the
+// caller must __syncthreads() before (keys written); the sorted key[] is visible on return.
+template <typename KT, int R>
+__device__ inline void block_bitonic_sort_regs(KT *key, int P) {
+    const int tid = threadIdx.x;
+    KT v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = key[tid * R + r];
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j >= R; j >>= 1) {  // partner thread tid ^ (j / R), same register
+            const int tj = j / R;
+            const bool lo = (tid & tj) == 0;
+            if (tj < 64) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const KT o = __shfl_xor(v[r], tj, 64);
+                    const bool asc = ((tid * R + r) & k) == 0;
+                    v[r] = (lo == asc) ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
+                }
+            } else {  // the partner is in another wave
+                __syncthreads();  // (key[] may still be read by a previous cross-wave stage)
+#pragma unroll
+                for (int r = 0; r < R; ++r) key[tid * R + r] = v[r];
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const KT o = key[(tid ^ tj) * R + r];
+                    const bool asc = ((tid * R + r) & k) == 0;
+                    v[r] = (lo == asc) ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
+                }
+            }
+        }
+#pragma unroll
+        for (int jj = R / 2; jj >= 1; jj >>= 1) {  // partner in this thread's registers (static indices)
+            if (jj < k) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int p = r ^ jj;
+                    if (p > r) {
+                        const bool asc = ((tid * R + r) & k) == 0;
+                        const KT a = v[r], b = v[p];
+                        const bool sw = (a > b) == asc;
+                        v[r] = sw ? b : a;
+                        v[p] = sw ? a : b;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();  // (cross-wave stages: every read of key[] done)
+#pragma unroll
+    for (int r = 0; r < R; ++r) key[tid * R + r] = v[r];
+    __syncthreads();
+}
+
 }  // namespace grf

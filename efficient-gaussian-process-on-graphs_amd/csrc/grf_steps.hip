@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
                                                         double *__restrict__ phi_val, float *__restrict__ phi_val32,
                                                         int32_t *__restrict__ t_count, int64_t band_width,
-                                                        int64_t n_cols, int64_t count_row0) {
+                                                        int64_t n_cols, int64_t count_row0, int32_t sort_lds) {
     // LDS: ld [E] loads by slot (later the compacted step values), fl [Lf] the modulator,
     // scratch (2 x 16 ints), key [P] the sorted keys (later the compacted step keys).  32-bit
     // keys when (node, step, walk) fits 32 bits (C4 / C5): half the sort's LDS traffic and a
@@ -203,7 +203,8 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     }
     __syncthreads();
 #ifndef GRF_EXP_NOSORT
-    block_bitonic_sort<KT>(key, P);
+    if (sort_lds) block_bitonic_sort<KT>(key, P);
+    else block_bitonic_sort_regs<KT, kPer>(key, P);  // (P == kPer * blockDim.x)
 #endif
 
     // ---- step values at (node, step) run heads, kept in registers: loads in walk order from
@@ -411,6 +412,10 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     // needs the node-id bound n_cols, known for the walking kernel (the slots path stays 64-bit)
     const bool key32 = walk && n_cols > 0 && ((uint64_t)n_cols << (wbits + lbits)) <= 0xffffffffull;
     const int32_t Lf_ = n_f < L ? n_f : L;
+    static const int32_t sort_lds = [] {  // (experiments: GRF_PHI_SORT_LDS=1, the all-LDS bitonic sort)
+        const char *e = getenv("GRF_PHI_SORT_LDS");
+        return (int32_t)(e && atoi(e) != 0);
+    }();
     static const size_t lds_pad = [] {  // (experiments: extra LDS per source, GRF_PHI_LDS_PAD bytes)
         const char *e = getenv("GRF_PHI_LDS_PAD");
         return e ? (size_t)atoll(e) : (size_t)0;
@@ -437,7 +442,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val,                                   \
         reinterpret_cast<const int4 *>(g_aug), p_halt, rule, (uint32_t)seed,                                      \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
-        n_cols, count_row0)
+        n_cols, count_row0, sort_lds)
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
     do {                                                                                                          \
         if (key32) GRF_PHI_LAUNCH_KT(W, K, uint32_t);                                                             \
