@@ -90,6 +90,38 @@ __device__ inline void block_bitonic_sort(KT *key, int P) {
     }
 }
 
+// v from lane (lane ^ TJ) of the wave: DPP quad permutes for 1 and 2 (no LDS pipe), ds_swizzle in
+// bitmask mode for 4..16 (within 32 lanes, no address operand), ds_bpermute for 32.
+template <int TJ>
+__device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v) {
+    if constexpr (TJ == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    else if constexpr (TJ == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    else if constexpr (TJ < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (TJ << 10));
+    else return (uint32_t)__shfl_xor((int)v, TJ, 64);
+}
+template <int TJ, typename KT>
+__device__ __forceinline__ KT lane_xor(KT v) {
+    if constexpr (sizeof(KT) == 4) {
+        return (KT)lane_xor_u32<TJ>((uint32_t)v);
+    } else {
+        const uint32_t lo = lane_xor_u32<TJ>((uint32_t)v), hi = lane_xor_u32<TJ>((uint32_t)((uint64_t)v >> 32));
+        return (KT)(((uint64_t)hi << 32) | lo);
+    }
+}
+
+template <int TJ, typename KT, int R>
+__device__ __forceinline__ void bitonic_lane_stage(KT (&v)[R], int tid, int k) {
+    if (TJ * R < k) {
+        const bool lo = (tid & TJ) == 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const KT o = lane_xor<TJ>(v[r]);
+            const bool asc = ((tid * R + r) & k) == 0;
+            v[r] = (lo == asc) ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
+        }
+    }
+}
+
 // Bitonic sort (ascending) of P = R * blockDim.x keys with each thread holding the R consecutive
 // keys [tid R, (tid + 1) R) in registers: the stages whose partner is in the same thread (j < R)
 // run in registers, the ones whose partner thread is in the same wave through lane shuffles, and
@@ -104,29 +136,27 @@ __device__ inline void block_bitonic_sort_regs(KT *key, int P) {
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = key[tid * R + r];
     for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j >= R; j >>= 1) {  // partner thread tid ^ (j / R), same register
+        for (int j = k >> 1; j >= 64 * R; j >>= 1) {  // partner thread tid ^ (j / R) in another wave
             const int tj = j / R;
             const bool lo = (tid & tj) == 0;
-            if (tj < 64) {
+            __syncthreads();  // (key[] may still be read by a previous cross-wave stage)
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const KT o = __shfl_xor(v[r], tj, 64);
-                    const bool asc = ((tid * R + r) & k) == 0;
-                    v[r] = (lo == asc) ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
-                }
-            } else {  // the partner is in another wave
-                __syncthreads();  // (key[] may still be read by a previous cross-wave stage)
+            for (int r = 0; r < R; ++r) key[tid * R + r] = v[r];
+            __syncthreads();
 #pragma unroll
-                for (int r = 0; r < R; ++r) key[tid * R + r] = v[r];
-                __syncthreads();
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const KT o = key[(tid ^ tj) * R + r];
-                    const bool asc = ((tid * R + r) & k) == 0;
-                    v[r] = (lo == asc) ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
-                }
+            for (int r = 0; r < R; ++r) {
+                const KT o = key[(tid ^ tj) * R + r];
+                const bool asc = ((tid * R + r) & k) == 0;
+                v[r] = (lo == asc) ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
             }
         }
+        // partner lane tid ^ tj in this wave
+        bitonic_lane_stage<32>(v, tid, k);
+        bitonic_lane_stage<16>(v, tid, k);
+        bitonic_lane_stage<8>(v, tid, k);
+        bitonic_lane_stage<4>(v, tid, k);
+        bitonic_lane_stage<2>(v, tid, k);
+        bitonic_lane_stage<1>(v, tid, k);
 #pragma unroll
         for (int jj = R / 2; jj >= 1; jj >>= 1) {  // partner in this thread's registers (static indices)
             if (jj < k) {
