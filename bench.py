@@ -414,6 +414,9 @@ def main():
                     help="er: Erdos-Renyi with --edges edges (C4); powerlaw: Chung-Lu, exponent 2.5, mean degree "
                          "--avg-degree (C5); facebook / enron: the reference's shipped social graphs")
     ap.add_argument("--avg-degree", type=float, default=10.0, help="powerlaw: expected mean degree")
+    ap.add_argument("--band-width", type=int, default=0,
+                    help="transpose band width of the single-GPU Gram (a multiple of 64, <= 8192; default: 4096 for "
+                         "the symmetric mode, 8192 for row modes)")
     ap.add_argument("--k-rows", type=int, default=0,
                     help="compute only the first R rows of every rank's K row block (0 = all rows); "
                          "the unit becomes K rows/s")
@@ -482,6 +485,8 @@ def main():
         # single-GPU row modes stay serial)
         args.overlap = sym_mode or (world > 1 and not allreduce)
     bw = DEFAULT_BAND_WIDTH if sym_mode else ROWS_BAND_WIDTH  # (engine.py: measured per mode)
+    if args.band_width:
+        bw = args.band_width
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     last = [None]
 
