@@ -555,7 +555,11 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
     // 76 KiB per CU: 16 waves per CU either way); measured best at both widths (GRF_GRAM_WAVES overrides)
     const int waves = knobs % 10 ? knobs % 10 : (tl.W > 4096 ? 8 : 4);
     const int unroll = (knobs % 1000) / 10, halves = waves == 8 ? 1 : 2;
-    const size_t lds = gram_lds_bytes(tl.W, waves, halves);
+    static const size_t lds_pad = [] {  // (experiments: GRF_GRAM_LDS_PAD bytes per tile -> fewer tiles per CU)
+        const char *e = getenv("GRF_GRAM_LDS_PAD");
+        return e ? (size_t)atoll(e) : (size_t)0;
+    }();
+    const size_t lds = gram_lds_bytes(tl.W, waves, halves) + lds_pad;
     // one launch covers at most 2^32 - 1 work-items: split the tile range
     const int64_t max_tiles = ((1ll << 32) - 1) / (64 * waves);
     for (int64_t t0 = t_first; t0 < t_last; t0 += max_tiles) {
