@@ -260,6 +260,110 @@ __global__ __launch_bounds__(256) void lap_row_kernel(int64_t n, const int64_t *
 }
 
 // ------------------------------------------------------------------- dense
+// Dense rows all have the same length n, so numpy's pairwise recursion over a row has the same
+// leaves and the same combining order for every row: the host lists them once (PwPlan, a kernel
+// argument) and the kernel sums leaf l with the 8 lanes of group l % 8 (lane j owns numpy's
+// accumulator r_j: a[j], a[j + 8], ... -- 64 contiguous bytes per group and load), folds the 8
+// accumulators in numpy's order ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), adds the leaf's
+// tail, and lane 0 combines the leaf sums with the recorded post-order program.  Bit-identical to
+// wave_np_pairwise (lane-0 leaf listing, one lane per leaf walking 128 strided loads).
+constexpr int kPwPlanLeaves = 64;  // rows of up to 64 leaves: n <= 8192
+struct PwPlan {
+    int32_t nl;                      // leaves
+    int32_t nprog;                   // program tokens
+    int32_t off[kPwPlanLeaves];      // leaf l: a[off, off + len)
+    int32_t len[kPwPlanLeaves];
+    int8_t prog[2 * kPwPlanLeaves];  // post-order: >= 0 push leaf sum, -1 pop two, push (left + right)
+};
+
+static bool pw_plan_build(int64_t n, PwPlan &p) {
+    p.nl = 0;
+    p.nprog = 0;
+    if (n <= 128) return false;  // (one leaf: the plain per-row path)
+    // the recursion of pairwise_sum: leaves in order, then the post-order combine program
+    struct F { int64_t o, m; int state; };
+    F st[64];
+    int sp = 0;
+    st[0] = {0, n, 0};
+    while (sp >= 0) {
+        F &f = st[sp];
+        if (f.m <= 128) {
+            if (p.nl >= kPwPlanLeaves) return false;
+            p.off[p.nl] = (int32_t)f.o;
+            p.len[p.nl] = (int32_t)f.m;
+            p.prog[p.nprog++] = (int8_t)p.nl;
+            ++p.nl;
+            --sp;
+            continue;
+        }
+        int64_t n2 = f.m / 2;
+        n2 -= n2 % 8;
+        if (f.state == 0) {
+            f.state = 1;
+            st[sp + 1] = {f.o, n2, 0};
+            ++sp;
+        } else if (f.state == 1) {
+            f.state = 2;
+            st[sp + 1] = {f.o + n2, f.m - n2, 0};
+            ++sp;
+        } else {
+            p.prog[p.nprog++] = -1;
+            --sp;
+        }
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void lapd_deg_plan_kernel(int64_t n, const double *W, int32_t mode, PwPlan plan,
+                                                            double *deg, double *dinv) {
+    __shared__ double sums[4][kPwPlanLeaves];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
+    const int64_t i = (int64_t)blockIdx.x * 4 + wave;  // one wave per row
+    if (i >= n) return;
+    const double *a = W + i * n;
+    for (int l0 = 0; l0 < plan.nl; l0 += 8) {
+        const int l = l0 + g;
+        double r = 0.0;
+        int32_t off = 0, len = 0, nb = 0;
+        if (l < plan.nl) {
+            off = plan.off[l];
+            len = plan.len[l];
+            nb = len - (len % 8);  // (leaves of a split row hold >= 64 values)
+            r = a[off + j];
+            for (int32_t q = 8 + j; q < nb; q += 8) r += a[off + q];
+        }
+        // numpy's fold of the 8 accumulators, then the leaf's tail in order
+        const double r1 = __shfl_xor(r, 1, 64);
+        const double p01 = (j & 1) ? r1 + r : r + r1;                  // (r0 + r1), (r2 + r3), ...
+        const double p23 = __shfl_xor(p01, 2, 64);
+        const double q = (j & 2) ? p23 + p01 : p01 + p23;             // ((r0 + r1) + (r2 + r3)), ...
+        const double q4 = __shfl_xor(q, 4, 64);
+        double res = (j & 4) ? q4 + q : q + q4;
+        if (j == 0 && l < plan.nl) {
+            for (int32_t t = nb; t < len; ++t) res += a[off + t];
+            sums[wave][l] = res;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        double stk[32];
+        int sp = -1;
+        for (int t = 0; t < plan.nprog; ++t) {
+            const int tok = plan.prog[t];
+            if (tok >= 0) {
+                stk[++sp] = sums[wave][tok];
+            } else {
+                const double rgt = stk[sp--];
+                stk[sp] = stk[sp] + rgt;
+            }
+        }
+        const double d = stk[0];
+        deg[i] = d;
+        if (mode == GRF_LAP_NUMPY) dinv[i] = d > 0.0 ? 1.0 / sqrt(d) : 0.0;
+        else dinv[i] = 1.0 / sqrt(d > 0.0 ? d : 1.0);
+    }
+}
+
 __global__ __launch_bounds__(256) void lapd_deg_kernel(int64_t n, const double *W, int32_t mode, double *deg,
                                                        double *dinv) {
     __shared__ PwLeaf leaves[4][kPwLeaves];
@@ -383,7 +487,12 @@ int32_t grf_laplacian_dense(int64_t n, const double *W, int32_t mode, int64_t *l
     int32_t *cnt = (int32_t *)((char *)workspace + dinv_bytes);
     void *scan_ws = (char *)workspace + dinv_bytes + cnt_bytes;
     GRF_REQUIRE_GRID(cdiv<int64_t>(n, 4), 256, "lapd_deg_kernel");
-    lapd_deg_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, st>>>(n, W, mode, deg, dinv);
+    PwPlan plan;
+    if (pw_plan_build(n, plan)) {
+        lapd_deg_plan_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, st>>>(n, W, mode, plan, deg, dinv);
+    } else {
+        lapd_deg_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, st>>>(n, W, mode, deg, dinv);
+    }
     GRF_CHECK_LAUNCH("lapd_deg_kernel");
     const unsigned g = (unsigned)cdiv<int64_t>(n, 4);
     GRF_REQUIRE_GRID(g, 256, "lapd_row_kernel");
