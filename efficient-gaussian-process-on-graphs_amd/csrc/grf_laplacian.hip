@@ -259,6 +259,184 @@ __global__ __launch_bounds__(256) void lap_row_kernel(int64_t n, const int64_t *
     if (!EMIT && lane == 0) cnt[i] = c;
 }
 
+// ---------------------------------------------- scipy, eight rows per wave
+// Most rows of a sparse graph are short (C5: mean degree ~10): a wave per row leaves 50+ lanes
+// idle.  These kernels give each row a group of 8 lanes (8 rows per wave); rows too long for a
+// group (degree sums over more than one numpy leaf, or more than kGroupRowMax entries) are done
+// afterwards by the whole wave with the one-row-per-wave code.  Same arithmetic, same bits.
+constexpr int kGroupRowMax = 64;
+
+// numpy pairwise sum of a[0 .. m), m <= 128 (one leaf), by the 8 lanes of a group (lane j owns
+// accumulator r_j); every lane of the wave must call it.  The group's lane 0 gets the sum.
+__device__ __forceinline__ double group_pw_leaf(const double *a, int64_t m, int j) {
+    const int64_t nb = m >= 8 ? m - (m % 8) : 0;
+    double r = 0.0;
+    if (m >= 8) {
+        r = a[j];
+        for (int64_t q = 8 + j; q < nb; q += 8) r += a[q];
+    }
+    const double r1 = __shfl_xor(r, 1, 64);
+    const double p01 = (j & 1) ? r1 + r : r + r1;
+    const double p23 = __shfl_xor(p01, 2, 64);
+    const double q = (j & 2) ? p23 + p01 : p01 + p23;
+    const double q4 = __shfl_xor(q, 4, 64);
+    double res = (j & 4) ? q4 + q : q + q4;
+    if (m < 8) res = 0.0;  // (numpy: res = 0; res += a[i] for short inputs)
+    if (j == 0)
+        for (int64_t t = nb; t < m; ++t) res += a[t];
+    return res;
+}
+
+__global__ __launch_bounds__(256) void lap_deg_group_kernel(int64_t n, const int64_t *ptr, const double *val,
+                                                            double *deg, double *dinv) {
+    __shared__ PwLeaf leaves[4][kPwLeaves];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 8;
+    if (r0 >= n) return;
+    const int64_t i = r0 + g;
+    int64_t b = 0, e = 0;
+    if (i < n) {
+        b = ptr[i];
+        e = ptr[i + 1];
+    }
+    const int64_t m = e - b > 1 ? e - b - 1 : 0;
+    const bool lng = m > 128;
+    const double rest = group_pw_leaf(val + b + 1, lng ? 0 : m, j);
+    if (j == 0 && i < n && !lng) {
+        const double d = e > b ? val[b] + rest : 0.0;
+        deg[i] = d;
+        const double v = 1.0 / sqrt(d);
+        dinv[i] = isinf(v) ? 0.0 : v;
+    }
+    uint64_t todo = __ballot(lng && j == 0 && i < n);
+    while (todo) {  // long rows: the whole wave, one at a time
+        const int gg = (__ffsll((long long)todo) - 1) >> 3;
+        todo &= todo - 1;
+        const int64_t ii = r0 + gg, bb = ptr[ii], ee = ptr[ii + 1];
+        const double rr = wave_np_pairwise(val + bb + 1, ee - bb - 1, leaves[wave]);
+        if (lane == 0) {
+            const double d = val[bb] + rr;
+            deg[ii] = d;
+            const double v = 1.0 / sqrt(d);
+            dinv[ii] = isinf(v) ? 0.0 : v;
+        }
+    }
+}
+
+// the row's virtual sequence (lap_row_kernel): element k -> (column, scaled value, kept)
+struct LapRow {
+    int64_t i, b, e, pd, total;
+    double d, di;
+    bool has_diag, insert;
+    __device__ void init(int64_t row, const int64_t *ptr, const int32_t *idx, const double *deg, const double *dinv) {
+        i = row;
+        d = deg[i];
+        di = dinv[i];
+        b = ptr[i];
+        e = ptr[i + 1];
+        int64_t lo = b, hi = e;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (idx[mid] < i) lo = mid + 1;
+            else hi = mid;
+        }
+        pd = lo - b;
+        has_diag = d != 0.0;
+        const bool expl = lo < e && idx[lo] == i;
+        insert = has_diag && !expl;
+        total = (e - b) + (insert ? 1 : 0);
+    }
+    __device__ bool element(int64_t k, const int32_t *idx, const double *val, const double *dinv, int64_t &col,
+                            double &u) const {
+        double v;
+        if (insert && k == pd) {
+            col = i;
+            v = d;
+        } else {
+            const int64_t a = b + ((insert && k > pd) ? k - 1 : k);
+            col = idx[a];
+            v = (has_diag && col == i) ? d - val[a] : 0.0 - val[a];
+        }
+        if (v != 0.0 && di != 0.0) {
+            const double t = di * v;
+            if (t != 0.0) {
+                const double dj = dinv[col];
+                if (dj != 0.0) {
+                    u = t * dj;
+                    return u != 0.0;
+                }
+            }
+        }
+        return false;
+    }
+};
+
+template <bool EMIT>
+__global__ __launch_bounds__(256) void lap_row_group_kernel(int64_t n, const int64_t *ptr, const int32_t *idx,
+                                                            const double *val, const double *deg, const double *dinv,
+                                                            int32_t *cnt, const int64_t *l_ptr, int32_t *l_idx,
+                                                            double *l_val, int64_t l_cap) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 8;
+    if (r0 >= n) return;
+    const int64_t i = r0 + g;
+    LapRow R;
+    R.total = 0;
+    if (i < n) R.init(i, ptr, idx, deg, dinv);
+    const bool lng = R.total > kGroupRowMax;
+    const int64_t mine = lng ? 0 : R.total;
+    int64_t it = (mine + 7) / 8;  // iterations of this group; the wave runs the max
+#pragma unroll
+    for (int off = 8; off < 64; off <<= 1) it = max(it, (int64_t)__shfl_xor(it, off, 64));
+    int64_t out = (EMIT && i < n && !lng) ? l_ptr[i] : 0;
+    int32_t c = 0;
+    for (int64_t t = 0; t < it; ++t) {
+        const int64_t k = t * 8 + j;
+        int64_t col = 0;
+        double u = 0.0;
+        const bool keep = k < mine && R.element(k, idx, val, dinv, col, u);
+        const uint32_t gm = (uint32_t)(__ballot(keep) >> (8 * g)) & 0xffu;
+        if (EMIT) {
+            const int64_t o = out + __popc(gm & ((1u << j) - 1u));
+            if (keep && o < l_cap) {
+                l_idx[o] = (int32_t)col;
+                l_val[o] = u;
+            }
+            out += __popc(gm);
+        } else {
+            c += __popc(gm);
+        }
+    }
+    if (!EMIT && j == 0 && i < n && !lng) cnt[i] = c;
+    uint64_t todo = __ballot(lng && j == 0);
+    while (todo) {  // long rows: the whole wave, 64 elements per step
+        const int gg = (__ffsll((long long)todo) - 1) >> 3;
+        todo &= todo - 1;
+        LapRow W;
+        W.init(r0 + gg, ptr, idx, deg, dinv);
+        int64_t o0 = EMIT ? l_ptr[W.i] : 0;
+        int32_t cc = 0;
+        for (int64_t base = 0; base < W.total; base += 64) {
+            const int64_t k = base + lane;
+            int64_t col = 0;
+            double u = 0.0;
+            const bool keep = k < W.total && W.element(k, idx, val, dinv, col, u);
+            const uint64_t m = __ballot(keep);
+            if (EMIT) {
+                const int64_t o = o0 + __popcll(m & ((1ull << lane) - 1ull));
+                if (keep && o < l_cap) {
+                    l_idx[o] = (int32_t)col;
+                    l_val[o] = u;
+                }
+                o0 += __popcll(m);
+            } else {
+                cc += __popcll(m);
+            }
+        }
+        if (!EMIT && lane == 0) cnt[W.i] = cc;
+    }
+}
+
 // ------------------------------------------------------------------- dense
 // Dense rows all have the same length n, so numpy's pairwise recursion over a row has the same
 // leaves and the same combining order for every row: the host lists them once (PwPlan, a kernel
@@ -451,18 +629,29 @@ int32_t grf_laplacian_csr(int64_t n, const int64_t *a_ptr, const int32_t *a_idx,
         GRF_CHECK_HIP(hipMemsetAsync(l_ptr, 0, sizeof(int64_t), st));
         return GRF_OK;
     }
-    const unsigned g = (unsigned)cdiv<int64_t>(n, 4);  // one wave per row
-    GRF_REQUIRE_GRID(g, 256, "lap_deg_kernel");
-    lap_deg_kernel<<<g, 256, 0, st>>>(n, a_ptr, a_val, deg, dinv);
+    // eight rows per wave (GRF_LAP_WAVE_ROWS=1: one row per wave, for A/B runs)
+    static const bool wave_rows = [] {
+        const char *e = getenv("GRF_LAP_WAVE_ROWS");
+        return e && atoi(e) != 0;
+    }();
+    const unsigned gw = (unsigned)cdiv<int64_t>(n, wave_rows ? 4 : 32);
+    GRF_REQUIRE_GRID(gw, 256, "lap_deg_kernel");
+    if (wave_rows) lap_deg_kernel<<<gw, 256, 0, st>>>(n, a_ptr, a_val, deg, dinv);
+    else lap_deg_group_kernel<<<gw, 256, 0, st>>>(n, a_ptr, a_val, deg, dinv);
     GRF_CHECK_LAUNCH("lap_deg_kernel");
-    const unsigned gw = (unsigned)cdiv<int64_t>(n, 4);  // one wave per row
-    GRF_REQUIRE_GRID(gw, 256, "lap_row_kernel");
-    lap_row_kernel<false><<<gw, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
+    if (wave_rows)
+        lap_row_kernel<false><<<gw, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
+    else
+        lap_row_group_kernel<false><<<gw, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, cnt, nullptr, nullptr,
+                                                        nullptr, 0);
     GRF_CHECK_LAUNCH("lap_row_kernel<count>");
     int32_t rc = scan_counts_i32(n, cnt, l_ptr, (char *)workspace + cnt_bytes, workspace_bytes - cnt_bytes, st);
     if (rc != GRF_OK) return rc;
-    GRF_REQUIRE_GRID(gw, 256, "lap_row_kernel");
-    lap_row_kernel<true><<<gw, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
+    if (wave_rows)
+        lap_row_kernel<true><<<gw, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
+    else
+        lap_row_group_kernel<true><<<gw, 256, 0, st>>>(n, a_ptr, a_idx, a_val, deg, dinv, nullptr, l_ptr, l_idx, l_val,
+                                                       l_cap);
     GRF_CHECK_LAUNCH("lap_row_kernel<fill>");
     return GRF_OK;
 }
