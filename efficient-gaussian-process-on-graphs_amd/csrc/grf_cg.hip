@@ -11,11 +11,10 @@
 // a wavefront gathers whole rows: lane c owns column c (S = 64 fills the wave).
 //
 // Kernels
-//   csr_tr_count / csr_tr_fill  deterministic CSR transpose of a row subset: rows
-//                               are split into chunks, one wave per chunk walks
-//                               its rows in order, cursors are private per
-//                               (column, chunk) -> every column lists its rows in
-//                               ascending order (no sort, no atomics races).
+//   csr_tr_gather / unpack      deterministic CSR transpose of a row subset: the
+//                               entries laid out in row order, a stable rocPRIM
+//                               radix sort by column -> every column lists its
+//                               rows in ascending order.
 //   spmm_kernel<SG>             Y = A[row_map] X (+ zc Z); one wave per row, 64/SG
 //                               lane groups split the nonzeros, fixed-order sums.
 //   cg_* kernels                column reductions (fp64, fixed order, last block
@@ -23,6 +22,7 @@
 // All CG kernels read a device `done` flag first: once the stopping rule fires
 // the rest of the enqueued iterations are no-ops, so the host only polls the
 // flag and never serialises the stream per iteration.
+#include <rocprim/device/device_radix_sort.hpp>
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -38,52 +38,62 @@ size_t scan_ws_bytes(int64_t n);
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // ------------------------------------------------------------ CSR transpose
-// chunk c = rows [c*rpc, min((c+1)*rpc, n_sel)) of the selection, one wave each
-__global__ __launch_bounds__(256) void csr_tr_count_kernel(int64_t n_sel, const int64_t *ptr, const int32_t *idx,
-                                                           const int32_t *row_map, int64_t n_chunks, int64_t rpc,
-                                                           int32_t *cnt) {
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= n_chunks) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t r1 = min(n_sel, (c + 1) * rpc);
-    for (int64_t r = c * rpc; r < r1; ++r) {
+// (Phi[row_map])^T by a stable radix sort: the selected rows' entries are laid out in row order as
+// (key = column, value = {position r, value bits}); a stable LSD sort by column keeps every column's
+// positions ascending -- the same CSR the chunked cursor fill gives, without its n_cols x chunks
+// count / cursor tables (1.6 GB at C4) and their random atomics.
+__global__ __launch_bounds__(256) void csr_tr_len_kernel(int64_t n_sel, const int64_t *ptr, const int32_t *row_map,
+                                                         int32_t *len) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r < n_sel) {
         const int64_t row = row_map ? row_map[r] : r;
-        for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) atomicAdd(&cnt[(int64_t)idx[e] * n_chunks + c], 1);
+        len[r] = (int32_t)(ptr[row + 1] - ptr[row]);
     }
 }
 
-__global__ void csr_tr_ptr_kernel(int64_t n_cols, int64_t n_chunks, const int64_t *off, int64_t *t_ptr) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k <= n_cols) t_ptr[k] = off[k * n_chunks];
-}
-
-// cursor[k * n_chunks + c] is touched only by chunk c's wave, one row at a time: the
-// atomic of row r has returned before the wave issues row r + 1's, so each column's
-// entries land in ascending row order.
-__global__ __launch_bounds__(256) void csr_tr_fill_kernel(int64_t n_sel, const int64_t *ptr, const int32_t *idx,
-                                                          const float *val, const int32_t *row_map, int64_t n_chunks,
-                                                          int64_t rpc, unsigned long long *cursor, int32_t *t_idx,
-                                                          float *t_val) {
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= n_chunks) return;
+__global__ __launch_bounds__(256) void csr_tr_gather_kernel(int64_t n_sel, const int64_t *ptr, const int32_t *idx,
+                                                            const float *val, const int32_t *row_map,
+                                                            const int64_t *off, uint32_t *keys, uint64_t *vals) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per selected row
+    if (r >= n_sel) return;
     const int lane = threadIdx.x & 63;
-    const int64_t r1 = min(n_sel, (c + 1) * rpc);
-    for (int64_t r = c * rpc; r < r1; ++r) {
-        const int64_t row = row_map ? row_map[r] : r;
-        for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) {
-            const unsigned long long pos = atomicAdd(&cursor[(int64_t)idx[e] * n_chunks + c], 1ull);
-            t_idx[pos] = (int32_t)r;
-            t_val[pos] = val[e];
-        }
+    const int64_t row = row_map ? row_map[r] : r, b = ptr[row], e = ptr[row + 1], o = off[r];
+    for (int64_t q = lane; q < e - b; q += 64) {
+        keys[o + q] = (uint32_t)idx[b + q];
+        vals[o + q] = ((uint64_t)(uint32_t)r << 32) | __float_as_uint(val[b + q]);
     }
 }
 
-static int64_t tr_chunks(int64_t n_sel, int64_t n_cols) {
-    // ~16 rows per wave, cursor table (12 B per column per chunk) capped at ~1.5 GB
-    int64_t c = cdiv<int64_t>(n_sel, 16);
-    const int64_t cap = std::max<int64_t>(1, (int64_t(1) << 27) / std::max<int64_t>(1, n_cols));
-    return std::max<int64_t>(1, std::min(c, std::min<int64_t>(cap, 1 << 16)));
+// sorted keys -> t_ptr (first position of every column, n_cols + 1 entries) and t_idx / t_val
+__global__ __launch_bounds__(256) void csr_tr_unpack_kernel(int64_t nnz, int64_t n_cols, const uint32_t *keys,
+                                                            const uint64_t *vals, int64_t *t_ptr, int32_t *t_idx,
+                                                            float *t_val) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i > nnz) return;
+    const int64_t k = i < nnz ? (int64_t)keys[i] : n_cols;             // (past the end: column n_cols)
+    const int64_t kp = i > 0 ? (int64_t)keys[i - 1] : -1;
+    for (int64_t c = kp + 1; c <= k; ++c) t_ptr[c] = i;                 // columns (kp, k] start at i
+    if (i < nnz) {
+        const uint64_t v = vals[i];
+        t_idx[i] = (int32_t)(v >> 32);
+        t_val[i] = __uint_as_float((uint32_t)v);
+    }
 }
+
+static unsigned key_bits(int64_t n_cols) {
+    unsigned b = 1;
+    while (b < 32 && (int64_t(1) << b) <= n_cols) ++b;
+    return b;
+}
+
+static size_t csr_tr_sort_temp_bytes(int64_t nnz, int64_t n_cols) {
+    size_t bytes = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                    (const uint64_t *)nullptr, (uint64_t *)nullptr, (size_t)std::max<int64_t>(nnz, 1),
+                                    0u, key_bits(n_cols));
+    return bytes;
+}
+
 
 // ------------------------------------------------------------------- SpMM
 // Y[r, c] = sum_e val[e] X[idx[e], c] (+ zc Z[r, c]) over row row_map[r] of A.
@@ -583,42 +593,53 @@ using namespace grf;
 extern "C" {
 #pragma GCC visibility push(default)
 
-size_t grf_csr_transpose_workspace_bytes(int64_t n_sel, int64_t n_cols) {
-    const int64_t c = tr_chunks(n_sel, n_cols), n = n_cols * c;
-    return al256((size_t)n * 4) + al256((size_t)(n + 1) * 8) + scan_ws_bytes(n);
+size_t grf_csr_transpose_workspace_bytes(int64_t n_sel, int64_t n_cols, int64_t nnz) {
+    const int64_t z = std::max<int64_t>(nnz, 1);
+    return al256((size_t)(n_sel + 1) * 4) + al256((size_t)(n_sel + 1) * 8) + scan_ws_bytes(n_sel + 1) +
+           2 * al256((size_t)z * 4) + 2 * al256((size_t)z * 8) + al256(csr_tr_sort_temp_bytes(nnz, n_cols));
 }
 
 int32_t grf_csr_transpose(int64_t n_sel, const int64_t *ptr, const int32_t *idx, const float *val,
-                          const int32_t *row_map, int64_t n_cols, int64_t *t_ptr, int32_t *t_idx, float *t_val,
-                          void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+                          const int32_t *row_map, int64_t n_cols, int64_t nnz, int64_t *t_ptr, int32_t *t_idx,
+                          float *t_val, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
     // (idx / val / t_idx / t_val may be NULL when there are no entries)
-    GRF_REQUIRE(n_sel >= 0 && n_cols > 0 && ptr && t_ptr, GRF_EINVAL, "grf_csr_transpose: bad arguments");
-    const size_t need = grf_csr_transpose_workspace_bytes(n_sel, n_cols);
+    GRF_REQUIRE(n_sel >= 0 && n_cols > 0 && nnz >= 0 && ptr && t_ptr, GRF_EINVAL, "grf_csr_transpose: bad arguments");
+    const size_t need = grf_csr_transpose_workspace_bytes(n_sel, n_cols, nnz);
     GRF_REQUIRE(workspace && workspace_bytes >= need, GRF_EINVAL, "grf_csr_transpose: workspace too small (%zu < %zu)",
                 workspace_bytes, need);
-    GRF_REQUIRE(n_sel < (1ll << 31), GRF_EUNSUPPORTED, "grf_csr_transpose: more than 2^31 rows");
+    GRF_REQUIRE(n_sel < (1ll << 31) && n_cols < (1ll << 31), GRF_EUNSUPPORTED, "grf_csr_transpose: more than 2^31 rows");
     hipStream_t st = S(stream);
-    const int64_t C = tr_chunks(n_sel, n_cols), n = n_cols * C, rpc = cdiv<int64_t>(std::max<int64_t>(n_sel, 1), C);
+    const int64_t z = std::max<int64_t>(nnz, 1);
     char *w = (char *)workspace;
-    int32_t *cnt = (int32_t *)w;
-    int64_t *off = (int64_t *)(w + al256((size_t)n * 4));
-    void *scan_ws = w + al256((size_t)n * 4) + al256((size_t)(n + 1) * 8);
-    GRF_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)n * 4, st));
-    const int64_t blocks = cdiv<int64_t>(C, 4);
+    int32_t *len = (int32_t *)w;
+    w += al256((size_t)(n_sel + 1) * 4);
+    int64_t *off = (int64_t *)w;
+    w += al256((size_t)(n_sel + 1) * 8);
+    void *scan_ws = w;
+    w += scan_ws_bytes(n_sel + 1);
+    uint32_t *k0 = (uint32_t *)w, *k1 = (uint32_t *)(w + al256((size_t)z * 4));
+    w += 2 * al256((size_t)z * 4);
+    uint64_t *v0 = (uint64_t *)w, *v1 = (uint64_t *)(w + al256((size_t)z * 8));
+    w += 2 * al256((size_t)z * 8);
+    size_t temp_bytes = csr_tr_sort_temp_bytes(nnz, n_cols);
     if (n_sel > 0) {
-        csr_tr_count_kernel<<<(unsigned)blocks, 256, 0, st>>>(n_sel, ptr, idx, row_map, C, rpc, cnt);
-        GRF_CHECK_LAUNCH("csr_tr_count_kernel");
+        csr_tr_len_kernel<<<(unsigned)cdiv<int64_t>(n_sel, 256), 256, 0, st>>>(n_sel, ptr, row_map, len);
+        GRF_CHECK_LAUNCH("csr_tr_len_kernel");
+        int32_t rc = scan_counts_i32(n_sel, len, off, scan_ws, scan_ws_bytes(n_sel + 1), st);
+        if (rc != GRF_OK) return rc;
+        GRF_REQUIRE_GRID(cdiv<int64_t>(n_sel, 4), 256, "csr_tr_gather_kernel");
+        csr_tr_gather_kernel<<<(unsigned)cdiv<int64_t>(n_sel, 4), 256, 0, st>>>(n_sel, ptr, idx, val, row_map, off, k0,
+                                                                               v0);
+        GRF_CHECK_LAUNCH("csr_tr_gather_kernel");
     }
-    int32_t rc = scan_counts_i32(n, cnt, off, scan_ws, workspace_bytes - (size_t)((char *)scan_ws - w), st);
-    if (rc != GRF_OK) return rc;
-    GRF_REQUIRE_GRID(cdiv<int64_t>(n_cols + 1, 256), 256, "csr_tr_ptr_kernel");
-    csr_tr_ptr_kernel<<<(unsigned)cdiv<int64_t>(n_cols + 1, 256), 256, 0, st>>>(n_cols, C, off, t_ptr);
-    GRF_CHECK_LAUNCH("csr_tr_ptr_kernel");
-    if (n_sel > 0) {
-        csr_tr_fill_kernel<<<(unsigned)blocks, 256, 0, st>>>(n_sel, ptr, idx, val, row_map, C, rpc,
-                                                             (unsigned long long *)off, t_idx, t_val);
-        GRF_CHECK_LAUNCH("csr_tr_fill_kernel");
+    if (nnz > 0) {
+        GRF_CHECK_HIP(rocprim::radix_sort_pairs(w, temp_bytes, (const uint32_t *)k0, k1, (const uint64_t *)v0, v1,
+                                                (size_t)nnz, 0u, key_bits(n_cols), st));
     }
+    GRF_REQUIRE_GRID(cdiv<int64_t>(nnz + 1, 256), 256, "csr_tr_unpack_kernel");
+    csr_tr_unpack_kernel<<<(unsigned)cdiv<int64_t>(nnz + 1, 256), 256, 0, st>>>(nnz, n_cols, k1, v1, t_ptr, t_idx,
+                                                                                t_val);
+    GRF_CHECK_LAUNCH("csr_tr_unpack_kernel");
     return GRF_OK;
 }
 

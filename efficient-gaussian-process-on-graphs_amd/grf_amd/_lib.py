@@ -84,8 +84,8 @@ SIGNATURES = {
     "grf_transpose_banded_fill_staged": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                                 _sz, _i64, _vp, _sz, _vp]),
     "grf_transpose_staging_bytes": (_sz, [_i64, _i64, _i64, _i64]),
-    "grf_csr_transpose_workspace_bytes": (_sz, [_i64, _i64]),
-    "grf_csr_transpose": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "grf_csr_transpose_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "grf_csr_transpose": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_spmm_csr": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
     "grf_spmm_csr_f64": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
     "grf_cg_gram_solve_f64": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _dbl, _vp, _i64, _i32, _dbl,

@@ -595,8 +595,8 @@ class GRFEngine:
         t_ptr = self._empty(phi.n_cols + 1, torch.int64)
         t_idx = self._empty(nnz, torch.int32)
         t_val = self._empty(nnz, torch.float32)
-        ws = self._ws(self.lib.grf_csr_transpose_workspace_bytes(n_sel, phi.n_cols))
-        C.check(self.lib.grf_csr_transpose(n_sel, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(rmap), phi.n_cols,
+        ws = self._ws(self.lib.grf_csr_transpose_workspace_bytes(n_sel, phi.n_cols, nnz))
+        C.check(self.lib.grf_csr_transpose(n_sel, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(rmap), phi.n_cols, nnz,
                                            _p(t_ptr), _p(t_idx), _p(t_val), _p(ws), ws.numel(), self.stream),
                 "grf_csr_transpose")
         return DeviceCSR(phi.n_cols, n_sel, t_ptr, t_idx, None, t_val, nnz)

@@ -323,12 +323,13 @@ int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, cons
  * row-major [rows x ld] with the S right-hand sides / samples as columns.
  * `row_map` (int32, optional) selects rows of Phi; NULL = rows 0..n-1. */
 
-/* (Phi[row_map])^T as CSR: t_ptr[n_cols + 1] (int64), t_idx / t_val [nnz of the selected
- * rows]; t_idx are positions in row_map; every column lists them in ascending order. */
+/* (Phi[row_map])^T as CSR: t_ptr[n_cols + 1] (int64), t_idx / t_val [nnz = the entries of the
+ * selected rows, exactly]; t_idx are positions in row_map; every column lists them in ascending
+ * order (a stable radix sort by column of the entries laid out in row order). */
 int32_t grf_csr_transpose(int64_t n_sel, const int64_t *ptr, const int32_t *idx, const float *val,
-                          const int32_t *row_map, int64_t n_cols, int64_t *t_ptr, int32_t *t_idx, float *t_val,
-                          void *workspace, size_t workspace_bytes, grf_stream_t stream);
-size_t grf_csr_transpose_workspace_bytes(int64_t n_sel, int64_t n_cols);
+                          const int32_t *row_map, int64_t n_cols, int64_t nnz, int64_t *t_ptr, int32_t *t_idx,
+                          float *t_val, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+size_t grf_csr_transpose_workspace_bytes(int64_t n_sel, int64_t n_cols, int64_t nnz);
 
 /* Y[r, :] = sum_e val[e] X[idx[e], :] over row row_map[r] (fp32, fixed summation order):
  * phi_test @ v, eps1 @ phi_train.T (sparse_grf_model.py:39-40, 45). */
