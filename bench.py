@@ -465,16 +465,18 @@ def main():
     b, e = shard_range(n, rank, world)
     ldk = eng.leading_dim(n)
     allreduce = args.mode == "allreduce"
-    # N > 1 column blocks K[:, b:e] (each rank transposes only its own rows); one GPU: row blocks
-    cols = args.mode == "cols" and world > 1 and not args.k_rows
     if args.k_rows and allreduce:
-        raise SystemExit("--k-rows applies to the row mode only")
+        raise SystemExit("--k-rows applies to the row modes only")
     kr_end = min(e, b + args.k_rows) if args.k_rows else e  # this rank's K rows [b, kr_end)
     k_rows = n if allreduce else kr_end - b
+    # column blocks K[:, b:kr_end] (= the rank's K rows, K symmetric) from a transpose of those rows
+    # alone -- N > 1, and the K-row-block workloads (C5) on any number of GPUs; one GPU whole K:
+    # the symmetric mode
+    cols = args.mode == "cols" and not allreduce and (world > 1 or bool(args.k_rows))
     if cols:
-        wl = cols_band_width(e - b)
-        cols_sym = not args.no_sym and 4 * (e - b) >= n
-        K = torch.empty((n, eng.leading_dim(e - b)), dtype=torch.float32, device=dev)  # K[:, b:e], reused
+        wl = cols_band_width(k_rows)
+        cols_sym = not args.no_sym and 4 * k_rows >= n
+        K = torch.empty((n, eng.leading_dim(k_rows)), dtype=torch.float32, device=dev)  # K[:, b:kr_end], reused
     else:
         K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
     rows_cap = max(1, min(m * L, n))  # walk_phi's padded row capacity
@@ -500,13 +502,16 @@ def main():
         # the same kernel counts this rank's buckets of the banded transpose (summed over the ranks
         # by one all-reduce in gather_phi)
         if cols:
-            # (counting the rank's own-rows transpose: no count all-reduce, and a 1/N-size transpose)
-            tws = eng.transpose_workspace(e - b, n, wl)
+            # the transpose of the block's rows alone (no count all-reduce, a 1/N-size transpose); the
+            # walk counts its buckets when the block is all of the rank's rows
+            fused = kr_end == e
+            tws = eng.transpose_workspace(k_rows, n, wl) if fused else None
             local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
-                                             band_width=wl, count_origin=b),
+                                             band_width=wl if fused else 0, count_origin=b),
                                 want64=False, want32=True, sync_free=True)
-            phi = gather_phi(eng, local)
-            tr = eng.transpose_banded(local, wl, counted_ws=tws, nnz_bound=(e - b) * rows_cap)
+            phi = gather_phi(eng, local) if world > 1 else local
+            blk = local if fused else DeviceCSR(k_rows, n, local.ptr[:k_rows + 1], local.idx, None, local.val32)
+            tr = eng.transpose_banded(blk, wl, counted_ws=tws, nnz_bound=k_rows * rows_cap)
             return phi, (tr, eng.phi_row_shifts(phi)), local
         tws = eng.transpose_workspace(n, n, bw)
         local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
@@ -686,7 +691,9 @@ def main():
         "data": wl["data"],
         "config": {"workload": f"{wl['long']}, walks_per_node={m}, max_walk_length={L}, p_halt={p}, diffusion "
                                f"modulator beta=1, Philox seed 42, dense fp32 K "
-                               + (f"rows [r0, r0+{args.k_rows}) of every rank's block" if args.k_rows else "")
+                               + ((f"columns [r0, r0+{args.k_rows}) (= those K rows: K is symmetric) of every "
+                                   f"rank's block" if cols else f"rows [r0, r0+{args.k_rows}) of every rank's block")
+                                  if args.k_rows else "")
                                + " resident in HBM",
                    "n_nodes": n, "n_edges": int(A.nnz // 2), "walks_per_node": m, "max_walk_length": L,
                    "k_rows_per_gpu": rows,

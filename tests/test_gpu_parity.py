@@ -605,6 +605,12 @@ def test_column_block_gram_from_local_transpose(eng, world):
             assert torch.equal(eng.gram_sparse_cols(phi, shift, tb, sym_row0=b), want_sym), (r, bw)
         Kp = eng.gram_sparse_cols(phi, shift, eng.transpose_banded(loc, 4096), 123, 4567)
         assert torch.equal(Kp, K[123:4567, b:e])
+        # a K-row block narrower than the rank's rows (bench --k-rows): the first k of its rows
+        from grf_amd.engine import DeviceCSR
+        k = min(1000, e - b)
+        sub = DeviceCSR(k, n, loc.ptr[:k + 1], loc.idx, None, loc.val32)
+        assert torch.equal(eng.gram_sparse_cols(phi, shift, eng.transpose_banded(sub, 1024, nnz_bound=k * 32 * 6)),
+                           K[:, b:b + k])
 
 
 @pytest.mark.parametrize("unit", [128, 12])
