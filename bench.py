@@ -474,7 +474,7 @@ def main():
     # the symmetric mode
     cols = args.mode == "cols" and not allreduce and (world > 1 or bool(args.k_rows))
     if cols:
-        wl = cols_band_width(k_rows)
+        wl = args.band_width or cols_band_width(k_rows)
         cols_sym = not args.no_sym and 4 * k_rows >= n
         K = torch.empty((n, eng.leading_dim(k_rows)), dtype=torch.float32, device=dev)  # K[:, b:kr_end], reused
     else:
