@@ -80,12 +80,18 @@ __device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const i
 }
 
 // The same walk over the "augmented" walk matrix: aug[e] = {target node, its row start (32 bits),
-// its row length, 0} for every entry e, so a step is ONE dependent round trip (the chosen entry's
-// record and weight) instead of two (the chosen entry's target, then the target's row bounds).
-// Same draws, same choices, same loads: bit-identical to philox_walk.  Needs nnz < 2^32.
+// its row length, -, the entry's weight} in 32 bytes, so a step is ONE dependent round trip that
+// touches ONE 64-byte sector (the chosen entry's record, weight included) instead of two round trips
+// (the target, then its row bounds) over three arrays.  Same draws, same choices, same loads:
+// bit-identical to philox_walk.  Needs nnz < 2^32.
+struct __attribute__((aligned(32))) AugRec {
+    int32_t v, rs, len, pad;
+    double w, pad2;
+};
+
 template <typename Visit>
-__device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, const int4 *__restrict__ aug,
-                                          const double *__restrict__ g_val, int64_t s, uint32_t w, double p,
+__device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, const AugRec *__restrict__ aug,
+                                          int64_t s, uint32_t w, double p,
                                           int32_t L, int32_t rule, uint32_t k0, uint32_t k1, Visit visit) {
     int64_t cur = s;
     double load = 1.0;
@@ -109,8 +115,9 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
             }
             k = (uint32_t)(mm >> 32);
         }
-        const int4 a = aug[rs + k];
-        const double wt = g_val[rs + k];
+        const AugRec *rec = aug + rs + k;
+        const int4 a = *reinterpret_cast<const int4 *>(rec);
+        const double wt = rec->w;
         load = load_update(rule, load, deg, wt, p);
         cur = a.x;
         rs = (int64_t)(uint32_t)a.y;

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         const int64_t *__restrict__ g_ptr,
                                                         const int32_t *__restrict__ g_idx,
                                                         const double *__restrict__ g_val,
-                                                        const int4 *__restrict__ g_aug, double p_halt, int32_t rule,
+                                                        const AugRec *__restrict__ g_aug, double p_halt, int32_t rule,
                                                         uint32_t k0, uint32_t k1, int64_t src_begin,
                                                         const double *__restrict__ f, int32_t Lf, int64_t cap,
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                 key[l * m + w] = make_key(node, l, w);
                 ld[l * m + w] = load;
             };
-            if (g_aug) philox_walk_aug(g_ptr, g_aug, g_val, src, (uint32_t)w, p_halt, L, rule, k0, k1, visit);
+            if (g_aug) philox_walk_aug(g_ptr, g_aug, src, (uint32_t)w, p_halt, L, rule, k0, k1, visit);
             else philox_walk(g_ptr, g_idx, g_val, src, (uint32_t)w, p_halt, L, rule, k0, k1, visit);
         }
     } else {
@@ -313,14 +313,22 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
 // aug[e] = {target v, row start of v (32 bits), row length of v, 0} for every entry e of the
 // walk matrix; one wave per row.
 __global__ __launch_bounds__(256) void walk_aug_kernel(int64_t n, const int64_t *__restrict__ g_ptr,
-                                                       const int32_t *__restrict__ g_idx, int4 *__restrict__ aug) {
+                                                       const int32_t *__restrict__ g_idx,
+                                                       const double *__restrict__ g_val, AugRec *__restrict__ aug) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n) return;
     const int lane = threadIdx.x & 63;
     for (int64_t e = g_ptr[row] + lane; e < g_ptr[row + 1]; e += 64) {
         const int32_t v = g_idx[e];
         const int64_t rs = g_ptr[v];
-        aug[e] = make_int4(v, (int32_t)(uint32_t)rs, (int32_t)(g_ptr[v + 1] - rs), 0);
+        AugRec r;
+        r.v = v;
+        r.rs = (int32_t)(uint32_t)rs;
+        r.len = (int32_t)(g_ptr[v + 1] - rs);
+        r.pad = 0;
+        r.w = g_val[e];
+        r.pad2 = 0.0;
+        aug[e] = r;
     }
 }
 
@@ -440,7 +448,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
 #define GRF_PHI_LAUNCH_KT(W, K, KT)                                                                               \
     phi_fused_kernel<W, K, KT><<<(unsigned)n_src, T, lds, st>>>(                                                  \
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val,                                   \
-        reinterpret_cast<const int4 *>(g_aug), p_halt, rule, (uint32_t)seed,                                      \
+        reinterpret_cast<const AugRec *>(g_aug), p_halt, rule, (uint32_t)seed,                                      \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
         n_cols, count_row0, sort_lds)
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
@@ -495,21 +503,22 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
                 GRF_EINVAL, "grf_walk_phi: counting needs band_width >= 1 and phi_cap that never truncates a row");
     GRF_REQUIRE(!t_count || (0 <= count_row0 && count_row0 <= src_begin), GRF_EINVAL,
                 "grf_walk_phi: count_row0 must be in [0, src_begin]");
-    GRF_REQUIRE(!g_aug || ((uintptr_t)g_aug & 15) == 0, GRF_EINVAL, "grf_walk_phi: g_aug must be 16-byte aligned");
+    GRF_REQUIRE(!g_aug || ((uintptr_t)g_aug & 31) == 0, GRF_EINVAL, "grf_walk_phi: g_aug must be 32-byte aligned");
     return phi_fused_launch(true, src_end - src_begin, P.walks_per_node, P.max_walk_length, norm, nullptr, nullptr,
                             g_ptr, g_idx, g_val, g_aug, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, phi_cnt,
                             phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream), count_row0);
 }
 
-size_t grf_walk_aug_bytes(int64_t nnz) { return (size_t)(nnz > 0 ? nnz : 0) * sizeof(int4); }
+size_t grf_walk_aug_bytes(int64_t nnz) { return (size_t)(nnz > 0 ? nnz : 0) * sizeof(AugRec); }
 
-int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, void *g_aug, grf_stream_t stream) {
-    GRF_REQUIRE(n >= 0 && g_ptr && g_idx && g_aug, GRF_EINVAL, "grf_walk_aug: bad arguments");
-    GRF_REQUIRE(((uintptr_t)g_aug & 15) == 0, GRF_EINVAL, "grf_walk_aug: g_aug must be 16-byte aligned");
+int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, void *g_aug,
+                     grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && g_ptr && g_idx && g_val && g_aug, GRF_EINVAL, "grf_walk_aug: bad arguments");
+    GRF_REQUIRE(((uintptr_t)g_aug & 31) == 0, GRF_EINVAL, "grf_walk_aug: g_aug must be 32-byte aligned");
     if (n == 0) return GRF_OK;
     GRF_REQUIRE_GRID(cdiv<int64_t>(n, 4), 256, "walk_aug_kernel");
-    walk_aug_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, S(stream)>>>(n, g_ptr, g_idx,
-                                                                         reinterpret_cast<int4 *>(g_aug));
+    walk_aug_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, S(stream)>>>(n, g_ptr, g_idx, g_val,
+                                                                         reinterpret_cast<AugRec *>(g_aug));
     GRF_CHECK_LAUNCH("walk_aug_kernel");
     return GRF_OK;
 }

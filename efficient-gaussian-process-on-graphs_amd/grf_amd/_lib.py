@@ -57,7 +57,7 @@ SIGNATURES = {
     "grf_steps": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "grf_steps_densify": (_i32, [_i64, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_phi": (_i32, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
-    "grf_walk_aug": (_i32, [_i64, _vp, _vp, _vp, _vp]),
+    "grf_walk_aug": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_walk_aug_bytes": (_sz, [_i64]),
     "grf_walk_phi": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32, _i64,
                              _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),

@@ -324,8 +324,8 @@ class GRFEngine:
         nnz = G.nnz_bound if getattr(G, "nnz_bound", None) is not None else G.nnz
         if nnz >= 2 ** 32:
             return None
-        aug = torch.empty(max(int(self.lib.grf_walk_aug_bytes(nnz)), 16), dtype=torch.uint8, device=self.device)
-        C.check(self.lib.grf_walk_aug(G.n_rows, _p(G.ptr), _p(G.idx), _p(aug), self.stream), "grf_walk_aug")
+        aug = torch.empty(max(int(self.lib.grf_walk_aug_bytes(nnz)), 32), dtype=torch.uint8, device=self.device)
+        C.check(self.lib.grf_walk_aug(G.n_rows, _p(G.ptr), _p(G.idx), _p(G.val), _p(aug), self.stream), "grf_walk_aug")
         G._aug = aug
         return aug
 

@@ -168,9 +168,11 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
                      float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
                      grf_stream_t stream);
 /* The augmented walk matrix of grf_walk_phi: g_aug[e] = {target v, row start of v (low 32 bits),
- * row length of v, 0} (int32 x 4) for every entry e of the CSR walk matrix (g_ptr, g_idx);
- * grf_walk_aug_bytes(nnz) bytes, 16-byte aligned. */
-int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, void *g_aug, grf_stream_t stream);
+ * row length of v, 0 (int32 x 4), weight g_val[e] (float64), 0} -- 32 bytes per entry e of the CSR
+ * walk matrix (g_ptr, g_idx, g_val): one 64-byte sector per walk step; grf_walk_aug_bytes(nnz)
+ * bytes, 32-byte aligned. */
+int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, void *g_aug,
+                     grf_stream_t stream);
 size_t grf_walk_aug_bytes(int64_t nnz);
 int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
                       const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
