@@ -46,9 +46,7 @@ __global__ __launch_bounds__(256) void steps_kernel(int64_t m, int32_t norm, int
         key[t] = k;
     }
     __syncthreads();
-#ifndef GRF_EXP_NOSORT
     block_bitonic_sort<uint64_t>(key, P);
-#endif
     // contiguous chunk per thread
     const int T = blockDim.x;
     const int per = P >= T ? P / T : 1;
@@ -202,10 +200,8 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         }
     }
     __syncthreads();
-#ifndef GRF_EXP_NOSORT
     if (sort_lds) block_bitonic_sort<KT>(key, P);
     else block_bitonic_sort_regs<KT, kPer>(key, P);  // (P == kPer * blockDim.x)
-#endif
 
     // ---- step values at (node, step) run heads, kept in registers: loads in walk order from
     //      0.0 (the run is read 8 keys / loads per LDS round trip; the source's step-0 run is m
