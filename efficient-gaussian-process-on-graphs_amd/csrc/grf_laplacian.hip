@@ -574,23 +574,28 @@ __global__ __launch_bounds__(256) void lapd_row_kernel(int64_t n, const double *
     const int lane = threadIdx.x & 63;
     int64_t out = EMIT ? l_ptr[i] : 0;
     int32_t c = 0;
-    for (int64_t j0 = 0; j0 < n; j0 += 64) {
-        const int64_t j = j0 + lane;
-        double v = 0.0;
-        bool nz = false;
-        if (j < n) {
-            v = lapd_value(mode, i, j, W[i * n + j], deg, dinv);
-            nz = (v != 0.0);
+    constexpr int kU = 4;  // 64-column chunks in flight per step (all loads issued before the ballots)
+    for (int64_t j0 = 0; j0 < n; j0 += 64 * kU) {
+        double v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t j = j0 + u * 64 + lane;
+            v[u] = j < n ? lapd_value(mode, i, j, W[i * n + j], deg, dinv) : 0.0;
         }
-        const uint64_t mask = __ballot(nz);
-        if (EMIT) {
-            if (nz) {
-                const int64_t pos = out + __popcll(mask & ((1ull << lane) - 1ull));
-                if (pos < l_cap) { l_idx[pos] = (int32_t)j; l_val[pos] = v; }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t j = j0 + u * 64 + lane;
+            const bool nz = j < n && v[u] != 0.0;
+            const uint64_t mask = __ballot(nz);
+            if (EMIT) {
+                if (nz) {
+                    const int64_t pos = out + __popcll(mask & ((1ull << lane) - 1ull));
+                    if (pos < l_cap) { l_idx[pos] = (int32_t)j; l_val[pos] = v[u]; }
+                }
+                out += __popcll(mask);
+            } else {
+                c += __popcll(mask);
             }
-            out += __popcll(mask);
-        } else {
-            c += __popcll(mask);
         }
     }
     if (!EMIT && lane == 0) cnt[i] = c;
