@@ -190,7 +190,7 @@ def main_predict(args):
     n, m, L, p, S = A.shape[0], args.walks, args.length, args.p_halt, args.samples
     f = diffusion_modulator(L, 1.0)
     G = eng.laplacian(DeviceCSR.from_scipy(A, eng.device))
-    phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42), want64=False)
+    phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, want64=False), want64=False)
     perm = np.random.default_rng(0).permutation(n)
     n_tr, n_te = int(0.6 * n), int(0.2 * n)
     tr = torch.from_numpy(perm[:n_tr]).to(eng.device)
@@ -311,7 +311,7 @@ def main_c3(args):
     def step(record):
         G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY)
         # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule
-        phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV), want64=False)
+        phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False)
         dense = eng.densify(phi)
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -507,7 +507,7 @@ def main():
             fused = kr_end == e
             tws = eng.transpose_workspace(k_rows, n, wl) if fused else None
             local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
-                                             band_width=wl if fused else 0, count_origin=b),
+                                             band_width=wl if fused else 0, count_origin=b, want64=False),
                                 want64=False, want32=True, sync_free=True)
             phi = gather_phi(eng, local) if world > 1 else local
             blk = local if fused else DeviceCSR(k_rows, n, local.ptr[:k_rows + 1], local.idx, None, local.val32)
@@ -515,7 +515,7 @@ def main():
             return phi, (tr, eng.phi_row_shifts(phi)), local
         tws = eng.transpose_workspace(n, n, bw)
         local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
-                                         band_width=bw),
+                                         band_width=bw, want64=False),
                             want64=False, want32=True, sync_free=world == 1)
         phi = gather_phi(eng, local, tws, band_width=bw) if world > 1 else local
         # sizes from bounds (n x the padded row capacity): no host round trip for the transpose

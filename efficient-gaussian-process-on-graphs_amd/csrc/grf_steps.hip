@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     for (int q = 0; q < kPer; ++q) {
         if (q < emit && rank + q < cap) {
             phi_idx[obase + rank + q] = pn_[q];
-            phi_val[obase + rank + q] = pv_[q];
+            if (phi_val) phi_val[obase + rank + q] = pv_[q];  // (NULL: the caller keeps the f32 copy only)
             if (phi_val32) phi_val32[obase + rank + q] = (float)pv_[q];
             // the banded transpose's bucket counts of this row's entries (grf_transpose_banded_plan)
             if (t_count) atomicAdd(&t_count[((src_begin + s - count_row0) / band_width) * n_cols + pn_[q]], 1);
@@ -485,7 +485,8 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
                      grf_stream_t stream) {
     GRF_REQUIRE(params != nullptr, GRF_EINVAL, "grf_walk_phi: params is NULL");
     const grf_walk_params P = *params;
-    GRF_REQUIRE(n >= 0 && g_ptr && phi_cnt && phi_idx && phi_val, GRF_EINVAL, "grf_walk_phi: bad arguments");
+    GRF_REQUIRE(n >= 0 && g_ptr && phi_cnt && phi_idx && (phi_val || phi_val32), GRF_EINVAL,
+                "grf_walk_phi: bad arguments");
     GRF_REQUIRE(P.rng == GRF_RNG_PHILOX, GRF_EUNSUPPORTED, "grf_walk_phi: Philox walks only (use grf_walk for PCG64)");
     GRF_REQUIRE(P.walks_per_node >= 1 && P.walks_per_node <= 0x7fffffff, GRF_EINVAL,
                 "grf_walk_phi: walks_per_node must be in [1, 2^31)");

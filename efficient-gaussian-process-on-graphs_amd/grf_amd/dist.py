@@ -183,7 +183,7 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
         # fused walk -> Phi, counting this rank's buckets of the banded transpose on the way
         tws = engine.transpose_workspace(n, n, bw)
         rows = engine.walk_phi(G, walks_per_node, p_halt, max_walk_length, f, seed=seed, src_begin=b, src_end=e,
-                               count_ws=tws, band_width=bw)
+                               count_ws=tws, band_width=bw, want64=False)
     else:
         rows = engine.features(engine.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed,
                                            src_begin=b, src_end=e), f)
@@ -208,7 +208,7 @@ def _cols_block(engine, G, f, m, p_halt, L, seed, rng, b, e, group, wl):
     if m * L <= 4096:
         tws = engine.transpose_workspace(e - b, n, wl)
         rows = engine.walk_phi(G, m, p_halt, L, f, seed=seed, src_begin=b, src_end=e, count_ws=tws, band_width=wl,
-                               count_origin=b)
+                               count_origin=b, want64=False)
     else:
         rows = engine.features(engine.walk(G, m, p_halt, L, rng=rng, seed=seed, src_begin=b, src_end=e), f)
     local = engine.compact(rows, want64=False, want32=True)

@@ -288,7 +288,7 @@ class GRFEngine:
                  seed: int = 42, load_rule: int = C.LOAD_CUMULATIVE, norm: int = C.NORM_MUL_RECIP,
                  src_begin: int = 0, src_end: Optional[int] = None, want32: bool = True,
                  count_ws: Optional[torch.Tensor] = None, band_width: int = 0, use_aug: bool = True,
-                 count_origin: int = 0) -> PaddedRows:
+                 count_origin: int = 0, want64: bool = True) -> PaddedRows:
         """Philox walks straight to Phi rows (one kernel; identical to walk + features).
 
         count_ws: a zeroed transpose workspace (``transpose_workspace``) in which the kernel also
@@ -304,7 +304,9 @@ class GRFEngine:
         cap = max(1, min(m * L, n))
         cnt = self._empty(ns, torch.int32)
         idx = self._empty(ns * cap, torch.int32)
-        val = self._empty(ns * cap, torch.float64)
+        if not (want64 or want32):
+            raise ValueError("walk_phi: want64 or want32")
+        val = self._empty(ns * cap, torch.float64) if want64 else None  # (want64=False: f32 values only)
         v32 = self._empty(ns * cap, torch.float32) if want32 else None
         prm = C.GrfWalkParams(m, float(p_halt), L, int(load_rule), C.RNG_PHILOX, 0, 1, int(seed) & 0xFFFFFFFFFFFFFFFF)
         aug = self.walk_aug(G) if use_aug else None

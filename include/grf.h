@@ -160,6 +160,7 @@ int32_t grf_phi(int64_t n_src, int64_t m, int32_t L, const int32_t *step_cnt, co
  * and then grf_transpose_banded_plan(..., counted = 1, ...); phi_cap must not truncate rows.
  * count_row0 (<= src_begin) is the first row of the transposed matrix: 0 for all of Phi, src_begin
  * for a transpose of these rows alone (the column-block multi-GPU Gram). 
+ * phi_val (float64) may be NULL when phi_val32 is given: only the float32 copy is written. 
  * Optional (g_aug != NULL, from grf_walk_aug on the same walk matrix, nnz < 2^32): each step of a
  * walk is one dependent memory round trip instead of two -- same draws, same Phi bits. */
 int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,

@@ -430,6 +430,12 @@ def test_walk_phi_fused_bitexact(eng, n, deg, m, L, p, rule):
         ref = eng.compact(eng.phi_fused(slots, f)).to_scipy()
         got = eng.compact(eng.walk_phi(G, m, p, L, f, seed=9, load_rule=rule, src_begin=src[0], src_end=src[1]))
         assert same_csr(got.to_scipy(), ref), src
+        # float32-only output (the bench path): the same columns and float32 values
+        g32 = eng.compact(eng.walk_phi(G, m, p, L, f, seed=9, load_rule=rule, src_begin=src[0], src_end=src[1],
+                                       want64=False), want64=False)
+        import torch
+        assert torch.equal(g32.ptr, got.ptr) and torch.equal(g32.idx[:got.nnz], got.idx[:got.nnz])
+        assert torch.equal(g32.val32[:got.nnz], got.val32[:got.nnz])
     # bucket counts from the walk kernel == the transpose's own counting (same K, bit for bit)
     bw = 256
     ws = eng.transpose_workspace(n, n, bw)
