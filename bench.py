@@ -347,7 +347,7 @@ def main_c3(args):
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "fp64 walks/Phi, fp32 MFMA Gram",
+        "dtype": "fp64 walk loads, fp32 Phi, fp32 MFMA Gram",
         "data": "real graph: Cora citation graph shipped with the reference (tests/golden/cora.npz)",
         "config": {"workload": f"C3: Cora N={n} dense adjacency resident in HBM, dense numpy-semantics Laplacian, "
                                f"walks_per_node={m}, max_walk_length={L}, p_halt={p}, diffusion modulator beta=1, "
@@ -358,8 +358,7 @@ def main_c3(args):
     }
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_dense(W, f, m, p, L,
-                                                 int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-                                                 or min(16, os.cpu_count() or 1))
+                                                 host_threads())
     print(json.dumps(out), flush=True)
 
 
@@ -429,6 +428,11 @@ def main():
     ap.add_argument("--no-overlap", dest="overlap", action="store_false", help="serial steps")
     ap.add_argument("--front-at", type=float, default=1.0,
                     help="pipelined: the next front starts after this fraction of the Gram tiles (1 = at the mirror)")
+    ap.add_argument("--balance", choices=["nodes", "phi"], default="nodes",
+                    help="N > 1 source shards: equal node ranges (default), or ranges of equal estimated step work "
+                         "from the per-source Phi row counts of one setup walk (dist.balanced_shards)")
+    ap.add_argument("--no-mfma-leg", action="store_true",
+                    help="skip the C3 dense MFMA Gram leg that adds roofline_mfma to the headline line")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
     ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
@@ -445,10 +449,9 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from grf_amd import _lib as C
+    from grf_amd import pipeline as P
     from grf_amd.dist import all_reduce as dist_all_reduce
-    from grf_amd.dist import allreduce_buckets, gather_phi, shard_range
-    from grf_amd.engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, DeviceCSR, GRFEngine, cols_band_width
+    from grf_amd.engine import DeviceCSR, GRFEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -457,111 +460,61 @@ def main():
         local_rank = init_distributed(local_rank)
     eng = GRFEngine(f"cuda:{local_rank}")
     dev = eng.device
-
     A = make_graph(args)
     n, m, L, p = A.shape[0], args.walks, args.length, args.p_halt
     f = diffusion_modulator(L, 1.0)
     A_dev = DeviceCSR.from_scipy(A, dev)
-    b, e = shard_range(n, rank, world)
-    ldk = eng.leading_dim(n)
-    allreduce = args.mode == "allreduce"
-    if args.k_rows and allreduce:
-        raise SystemExit("--k-rows applies to the row modes only")
-    kr_end = min(e, b + args.k_rows) if args.k_rows else e  # this rank's K rows [b, kr_end)
-    k_rows = n if allreduce else kr_end - b
-    # column blocks K[:, b:kr_end] (= the rank's K rows, K symmetric) from a transpose of those rows
-    # alone -- N > 1, and the K-row-block workloads (C5) on any number of GPUs; one GPU whole K:
-    # the symmetric mode
-    cols = args.mode == "cols" and not allreduce and (world > 1 or bool(args.k_rows))
-    if cols:
-        wl = args.band_width or cols_band_width(k_rows)
-        cols_sym = not args.no_sym and 4 * k_rows >= n
-        K = torch.empty((n, eng.leading_dim(k_rows)), dtype=torch.float32, device=dev)  # K[:, b:kr_end], reused
-    else:
-        K = torch.empty((k_rows, ldk), dtype=torch.float32, device=dev)  # resident output block, reused
-    rows_cap = max(1, min(m * L, n))  # walk_phi's padded row capacity
-    sym_mode = world == 1 and not args.no_sym and not args.k_rows and not allreduce
+    src = None
+    if world > 1 and args.balance != "nodes":
+        from grf_amd.dist import balanced_shards
+        src = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance)[rank]
+    pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
+                     band_width=args.band_width, no_sym=args.no_sym, src=src)
+    b, e, kr_end = pl.b, pl.e, pl.kr_end
+    K = P.alloc_k(eng, pl)  # resident output block, reused
     if args.overlap is None:
-        # one GPU, whole K: the next front beside the mirror; N > 1 row blocks: the next front's
-        # collectives beside this step's Gram (the compute of a front beside a Gram gains ~1 %:
-        # single-GPU row modes stay serial)
-        args.overlap = sym_mode or (world > 1 and not allreduce)
-    bw = DEFAULT_BAND_WIDTH if sym_mode else ROWS_BAND_WIDTH  # (engine.py: measured per mode)
-    if args.band_width:
-        bw = args.band_width
+        # one GPU, whole K: the next front beside the mirror; N > 1 row / column blocks: the next
+        # front's collectives beside this step's Gram (the compute of a front beside a Gram gains
+        # ~1 %: single-GPU row modes stay serial)
+        args.overlap = pl.mode == "sym" or (world > 1 and pl.mode != "allreduce")
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
+    walk_ev = []  # (start, end) events around walk_phi in the serial-latency steps (kernel alone)
     last = [None]
 
     side = torch.cuda.Stream(dev)  # the next step's front runs here while the Gram runs on `main`
     main = torch.cuda.current_stream(dev)
 
-    def front():
-        """Laplacian -> fused walk/Phi (+ bucket counts) -> [gather] -> banded transpose."""
-        G = eng.laplacian(A_dev)
-        # Philox walks of this rank's sources straight to Phi rows (one kernel, no slot round trip);
-        # the same kernel counts this rank's buckets of the banded transpose (summed over the ranks
-        # by one all-reduce in gather_phi)
-        if cols:
-            # the transpose of the block's rows alone (no count all-reduce, a 1/N-size transpose); the
-            # walk counts its buckets when the block is all of the rank's rows
-            fused = kr_end == e
-            tws = eng.transpose_workspace(k_rows, n, wl) if fused else None
-            local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
-                                             band_width=wl if fused else 0, count_origin=b, want64=False),
-                                want64=False, want32=True, sync_free=True)
-            phi = gather_phi(eng, local) if world > 1 else local
-            blk = local if fused else DeviceCSR(k_rows, n, local.ptr[:k_rows + 1], local.idx, None, local.val32)
-            tr = eng.transpose_banded(blk, wl, counted_ws=tws, nnz_bound=k_rows * rows_cap)
-            return phi, (tr, eng.phi_row_shifts(phi)), local
-        tws = eng.transpose_workspace(n, n, bw)
-        local = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=e, count_ws=tws,
-                                         band_width=bw, want64=False),
-                            want64=False, want32=True, sync_free=world == 1)
-        phi = gather_phi(eng, local, tws, band_width=bw) if world > 1 else local
-        # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
-        tr = eng.transpose_banded(phi, bw, counted_ws=tws, nnz_bound=n * rows_cap)
-        return phi, tr, local
+    def front(record_walk: bool = False):
+        if record_walk:
+            # the walk kernel timed alone (serial steps): events around the front's walk_phi launch
+            orig = eng.walk_phi
+
+            def timed(*a, **k):
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+                out = orig(*a, **k)
+                ev[1].record()
+                walk_ev.append(ev)
+                return out
+
+            eng.walk_phi = timed
+            try:
+                return P.front(eng, A_dev, pl)
+            finally:
+                eng.walk_phi = orig
+        return P.front(eng, A_dev, pl)
 
     def back(fr, record: bool, after_gram=None):
-        """The K assembly of one step (its front's outputs).  after_gram: called between the Gram
-        tiles and the mirror of the symmetric mode (the pipelined run issues the next front there)."""
-        phi, tr, local = fr
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if cols:
-            # K[:, b:e] = Phi Phi[b:e]^T; the square K[b:e, b:e] on and above its diagonal + mirror
-            # (the square pays from N <= 4: per-rank emulation N = 2 14.9 -> 14.1 ms, N = 4 7.95 -> 7.85 ms,
-            # N = 8 4.13 -> 4.19 ms, DESIGN.md §5)
-            eng.gram_sparse_cols(phi, tr[1], tr[0], out=K, sym_row0=b if cols_sym else None)
-        elif allreduce:
-            eng.gram_sparse_kslice(phi, tr, b, e, out=K)  # all rows, inner slice [b, e)
-        elif sym_mode:
-            # upper band tiles (the pipelined run lets the next front start at the Gram's tail) ...
-            tiles_done = None
-            if after_gram is not None and args.front_at < 1.0:
-                cut = int(round(args.front_at * 1000))
-                eng.gram_sparse_upper(phi, tr, out=K, parts=(0, cut, 1000))
-                tiles_done = torch.cuda.Event()
-                tiles_done.record(main)
-                eng.gram_sparse_upper(phi, tr, out=K, parts=(cut, 1000, 1000))
-            else:
-                eng.gram_sparse_upper(phi, tr, out=K)
-                if after_gram is not None:
-                    tiles_done = torch.cuda.Event()
-                    tiles_done.record(main)
-            # ... + mirror (= grf_gram_sparse_sym); pipelined: a 4-per-CU grid leaves slots to the next front
-            eng.gram_mirror(K, n, 1024 if after_gram is not None else 0)
-            if after_gram is not None:
-                after_gram(tiles_done)  # (issued after the mirror: the host's launch time does not delay it)
-        else:
-            eng.gram_sparse(phi, tr, b, kr_end, out=K)
+        # (pipelined: a 1024-workgroup mirror leaves CU slots to the next front)
+        P.k_assembly(eng, fr, pl, K, after_tiles=after_gram, mirror_workgroups=1024 if after_gram else 0,
+                     front_at=args.front_at)
         if record:
             ev[1].record()
             gram_ev.append(ev)
-        if allreduce:
-            allreduce_buckets(K[:, :n])
-        last[0] = (phi, local)
+        last[0] = fr
 
     def front_on_side(after=None, independent=False):
         # after: an event on `main`; default: everything issued on `main` so far.  independent: no
@@ -582,25 +535,26 @@ def main():
     def back_on_main(frd, record, after_gram=None):
         fr, done = frd
         main.wait_event(done)
-        phi, tr, local = fr
-        for obj in (phi, *(tr if isinstance(tr, tuple) else (tr,)), local):  # allocated on `side`, used on `main`
+        for obj in (fr.phi, fr.tr, fr.local, fr.row_shift):  # allocated on `side`, used on `main`
+            if obj is None:
+                continue
             for v in ([obj] if torch.is_tensor(obj) else vars(obj).values()):
                 if torch.is_tensor(v) and v.is_cuda:
                     v.record_stream(main)
         back(fr, record, after_gram)
 
-    def run(steps: int, record: bool):
+    def run(steps: int, record: bool, record_walk: bool = False):
         """`steps` whole steps.  Pipelined (--overlap): step s+1's front is issued on the side
         stream before step s's K assembly, so the two overlap on the GPU; every step still runs
         its whole path, and the first front of the call is not overlapped (no work is carried
         across the call's boundary)."""
         if not args.overlap:
             for _ in range(steps):
-                back(front(), record)
+                back(front(record_walk), record)
             return
         cur = front_on_side()
         for s_ in range(steps):
-            if sym_mode:
+            if pl.mode == "sym":
                 # the next front starts when this step's Gram tiles are done: it runs beside the
                 # HBM-bound mirror instead of the gather-bound Gram
                 nxt = [None]
@@ -612,9 +566,8 @@ def main():
                 back_on_main(cur, record, issue_next)
                 cur = nxt[0]
             else:
-                # row modes: this step's Gram is issued first, then the next front, which overlaps
-                # it (its host synchronisations -- row counts, the all-gather sizes -- then no
-                # longer hold back the Gram's launch; with N > 1 the collectives run beside it)
+                # row / column modes: this step's Gram is issued first, then the next front, which
+                # overlaps it (with N > 1 the collectives run beside it)
                 back_on_main(cur, record)
                 cur = front_on_side(independent=True) if s_ + 1 < steps else None
 
@@ -628,44 +581,49 @@ def main():
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
-    serial_ms = None
-    if args.overlap:
-        # latency of one un-pipelined step (reported beside the throughput; not part of `value`)
-        ov = args.overlap
-        args.overlap = False
-        run(1, False)  # (warm-up of the serial order)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        run(3, False)
-        torch.cuda.synchronize()
-        serial_ms = 1000.0 * (time.perf_counter() - t1) / 3
-        args.overlap = ov
+    # latency of one un-pipelined step (reported beside the throughput; not part of `value`), with
+    # the walk kernel timed alone there
+    ov = args.overlap
+    args.overlap = False
+    run(1, False)  # (warm-up of the serial order)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    run(3, False, record_walk=True)
+    torch.cuda.synchronize()
+    serial_ms = 1000.0 * (time.perf_counter() - t1) / 3
+    args.overlap = ov
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
+    walk_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in walk_ev]))
     if world > 1:
-        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        tt = torch.tensor([t, float(np.mean(gram_ms)), walk_ms], dtype=torch.float64, device=dev)
         dist_all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
-        gm = torch.tensor([float(np.mean(gram_ms))], dtype=torch.float64, device=dev)
-        dist_all_reduce(gm, op=dist.ReduceOp.MAX)
-        gram_avg = float(gm.item())
+        t, gram_avg, walk_ms = (float(x) for x in tt.tolist())
     else:
         gram_avg = float(np.mean(gram_ms))
 
     ms_per_step = 1000.0 * t / args.steps
-    nnz_phi = [last[0][0].nnz]
-    local_nnz = last[0][1].nnz
+    phi_last = last[0].phi
+    nnz_phi = phi_last.nnz
+    local_nnz = last[0].local.nnz
     # algorithmic bytes of the K assembly (gram_sparse_kernel [+ gram_mirror_kernel]): write this
     # rank's K rows once, read its Phi rows (col int32 + val fp32) and every Phi^T entry once
     rows = kr_end - b
-    alg_bytes = 4.0 * rows * n + 8.0 * local_nnz * rows / max(e - b, 1) + 8.0 * nnz_phi[0]
-    if allreduce:  # every K entry written; all of Phi scanned, the slice's share of Phi^T read
-        alg_bytes = 4.0 * n * n + 8.0 * nnz_phi[0] + 8.0 * nnz_phi[0] * rows / n
+    alg_bytes = 4.0 * rows * n + 8.0 * local_nnz * rows / max(e - b, 1) + 8.0 * nnz_phi
+    if pl.mode == "allreduce":  # every K entry written; all of Phi scanned, the slice's share of Phi^T read
+        alg_bytes = 4.0 * n * n + 8.0 * nnz_phi + 8.0 * nnz_phi * rows / n
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
-    sym = sym_mode
+    sym = pl.mode == "sym"
     kernels = ["grf::gram_sparse_kernel", "grf::gram_mirror_kernel"] if sym else ["grf::gram_sparse_kernel"]
-    traffic = None
-    if (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and args.graph == "er" and world == 1 and sym:
-        traffic = pmc_traffic(kernels)
+    headline = (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and args.graph == "er" and world == 1 and sym
+    traffic = pmc_traffic(kernels) if headline else None
+    # the walk kernel (phi_fused_kernel): per walk, E[moves] = (1-p)(1-(1-p)^(L-1))/p recorded moves,
+    # each reading the current node's row bounds + the chosen entry's column and weight (SURVEY.md
+    # §8d: 16 B per move), + the compact Phi row written (int32 column + fp32 value per entry)
+    walks = float(e - b) * m
+    moves = walks * (1.0 - p) * (1.0 - (1.0 - p) ** (L - 1)) / p
+    walk_alg = 16.0 * moves + 8.0 * local_nnz
+    walk_achieved = walk_alg / (walk_ms * 1e-3) / 1e9
+    walk_traffic = pmc_traffic(["grf::phi_fused_kernel"]) if headline else None
     wl = workload_name(args, A)
     if args.k_rows:
         metric = (f"GRF kernel rows/sec ({wl['short']}, m={m} walks: Phi of all N nodes + a {args.k_rows}-row "
@@ -676,6 +634,7 @@ def main():
         if args.graph != "er" or (n, args.edges, m, L, p) != DEFAULT_WORKLOAD:
             metric = f"GRF kernel-matrices/sec ({wl['short']}, m={m} walks; + achieved HBM GB/s of the Gram kernel)"
         unit, value, scaling = "K-matrices/s", args.steps / t, "strong"
+    cols = pl.mode == "cols"
     out = {
         "metric": metric,
         "value": value,
@@ -687,7 +646,7 @@ def main():
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
-        "dtype": "fp64 walks/Phi, fp32 K",
+        "dtype": "fp64 walk loads, fp32 Phi, exact-product int64 fixed-point Gram, fp32 K",
         "data": wl["data"],
         "config": {"workload": f"{wl['long']}, walks_per_node={m}, max_walk_length={L}, p_halt={p}, diffusion "
                                f"modulator beta=1, Philox seed 42, dense fp32 K "
@@ -696,30 +655,107 @@ def main():
                                   if args.k_rows else "")
                                + " resident in HBM",
                    "n_nodes": n, "n_edges": int(A.nnz // 2), "walks_per_node": m, "max_walk_length": L,
-                   "k_rows_per_gpu": rows,
+                   "k_rows_per_gpu": rows, "shard": [b, e], "balance": args.balance if world > 1 else None,
                    "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
-                                   f"RCCL all-reduce (K replicated)") if allreduce else
+                                   f"RCCL all-reduce (K replicated)") if pl.mode == "allreduce" else
                                   (f"source-sharded x{world}, Phi all-gather, K column blocks K[:, R_r] from each "
                                    f"rank's own-rows transpose") if cols else
-                                  f"source-sharded x{world}, Phi all-gather, K row blocks"},
+                                  f"source-sharded x{world}, Phi all-gather, K row blocks"
+                                  + (" (one GPU: symmetric tiles + mirror)" if sym else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": ("rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of the same kernels on this workload, "
-                                        "profiles/r01_pmc_summary.json (2*FETCH_SIZE + WRITE_SIZE; bytes per launch)")
+                     "traffic_source": (f"rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of the same kernels on this workload, "
+                                        f"{os.path.relpath(PMC_SUMMARY, ROOT)} (FETCH_SIZE x the calibrated factor "
+                                        f"+ WRITE_SIZE; bytes per launch)")
                      if traffic is not None else None,
                      "kernel": "+".join(k.split("::")[1] for k in kernels), "kernel_ms": gram_avg,
                      "algorithmic_bytes": alg_bytes},
-        "nnz_phi": nnz_phi[0],
-        "pipelined": bool(args.overlap),
+        "roofline_walk": {"bound": "hbm", "achieved": walk_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": walk_achieved / HBM_PEAK_GBS, "traffic": walk_traffic,
+                          "kernel": "phi_fused_kernel (fused Philox walks -> Phi rows + bucket counts)",
+                          "kernel_ms": walk_ms, "algorithmic_bytes": walk_alg,
+                          "algorithmic_note": f"16 B per expected recorded move ({moves:.4g}) + 8 B per Phi "
+                                              f"entry written ({local_nnz}); timed alone in the serial steps "
+                                              f"(pipelined it shares HBM with the mirror)"},
+        "nnz_phi": nnz_phi,
+        "pipelined": bool(ov),
         "serial_ms_per_step": serial_ms,
     }
+    if headline and not args.no_mfma_leg:
+        out["roofline_mfma"] = mfma_leg(eng, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(A, f, m, p, L, args.cpu_rows, threads, k_rows=args.k_rows)
+        out["cpu_baseline"] = cpu_baseline(A, f, m, p, L, args.cpu_rows, host_threads(), k_rows=args.k_rows)
+        out["cpu_baseline"]["host"] = host_cpu_note()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_threads() -> int:
+    """All host CPU the process is granted (the reference's pool defaults to os.cpu_count() workers):
+    the CPUs it may run on, capped by the cgroup's CPU quota.  The GPU box shows 256 logical CPUs
+    but grants a quota of 16 (cpu.max 1600000 100000, profiles/r02_host_cpu.txt); 256 threads there
+    are throttled to 16 CPUs' time and run the oracle 25 % slower than 16 threads."""
+    env = int(os.environ.get("GRF_CPU_THREADS", "0") or 0)
+    if env:
+        return env
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def host_cpu_note() -> str:
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    try:
+        quota = open("/sys/fs/cgroup/cpu.max").read().strip()
+    except OSError:
+        quota = "n/a"
+    return f"os.cpu_count()={os.cpu_count()}, affinity={aff}, cgroup cpu.max={quota}"
+
+
+def mfma_leg(eng, args, steps: int = 20):
+    """MFMA utilisation of the Phi Phi^T kernel on the dense path (C3: Cora, the reference's dense
+    graph_kernels/fast_grf_kernel_general.py:11-39; the north star puts MFMA only on the dense
+    contraction): gram_dense_kernel timed with HIP events over `steps` launches."""
+    import torch
+
+    from grf_amd import _lib as C
+
+    W = cora_adjacency()
+    n, m, L, p = W.shape[0], args.walks, args.length, args.p_halt
+    f = diffusion_modulator(L, 1.0)
+    G = eng.walk_matrix_dense(torch.from_numpy(W).to(eng.device), C.LAP_NUMPY)
+    phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False)
+    dense = eng.densify(phi)
+    for _ in range(3):
+        eng.gram_dense(dense, n)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(steps):
+        eng.gram_dense(dense, n)
+    ev[1].record()
+    ev[1].synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / steps
+    kpad = -(-n // 16) * 16
+    flops = 1.0 * n * (n + 1) * kpad
+    tfs = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "gram_dense_kernel (v_mfma_f32_32x32x2f32)",
+            "kernel_ms": ms, "algorithmic_flops": flops,
+            "workload": f"C3 dense path: Cora N={n}, m={m}, L={L}: K = Phi Phi^T of the dense fp32 Phi "
+                        f"(N (N+1) k flops: the unique entries of the symmetric product)"}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,194 @@
+"""The timed hot path of ``bench.py`` as library functions, so that the parity tests run exactly it.
+
+One step (CSR adjacency resident in HBM -> full dense fp32 K resident in HBM) is
+a *front* and a *K assembly*:
+
+* front: normalised Laplacian (a1, ``graph_utils.py:5-30``) -> fused Philox walks straight to
+  Phi rows, counting the banded transpose's buckets on the way (a7 + a9's
+  ``Phi = sum_l f_l M_l``, ``sparse_sampler.py:26-56`` and ``fast_grf_kernel_general.py:47-52``)
+  -> sync-free compaction -> [Phi all-gather, N > 1] -> banded transpose of Phi (or of this rank's
+  own rows for column blocks).
+* K assembly (a9's ``Phi @ Phi.T``, ``fast_grf_kernel_general.py:55``): one GPU, whole K: the
+  Gram tiles on and above the diagonal band + the mirror pass; row blocks; column blocks
+  ``K[:, R_r]`` (= the rank's rows: K is symmetric); or the north star's literal partial K over
+  an inner slice + all-reduce.
+
+``plan_step`` fixes every size and mode up front, so the front reads nothing back to the host.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, DeviceCSR, GRFEngine, cols_band_width
+
+
+@dataclass
+class StepPlan:
+    """Sizes and modes of one step on one rank."""
+
+    n: int
+    m: int
+    L: int
+    p_halt: float
+    f: np.ndarray
+    seed: int = 42
+    world: int = 1
+    rank: int = 0
+    src: Tuple[int, int] = (0, 0)  # this rank's walk sources [b, e) (= its K rows / columns)
+    k_rows: int = 0                # 0: all of the rank's rows; R: only [b, b + R)
+    mode: str = "sym"              # "sym" (one GPU, whole K), "rows", "cols", "allreduce"
+    band_width: int = DEFAULT_BAND_WIDTH
+    cols_sym: bool = False         # column blocks: the square K[b:e, b:e] by the symmetric enumeration
+    group: object = None           # torch.distributed group (N > 1)
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def b(self) -> int:
+        return self.src[0]
+
+    @property
+    def e(self) -> int:
+        return self.src[1]
+
+    @property
+    def kr_end(self) -> int:
+        return min(self.e, self.b + self.k_rows) if self.k_rows else self.e
+
+    @property
+    def block_rows(self) -> int:
+        """Rows of K this rank writes (all n for the all-reduce mode)."""
+        return self.n if self.mode == "allreduce" else self.kr_end - self.b
+
+    @property
+    def rows_cap(self) -> int:
+        """walk_phi's padded row capacity (the bound that sizes everything downstream)."""
+        return max(1, min(self.m * self.L, self.n))
+
+
+def plan_step(n: int, m: int, L: int, p_halt: float, f, *, seed: int = 42, world: int = 1, rank: int = 0,
+              mode: str = "cols", k_rows: int = 0, band_width: int = 0, no_sym: bool = False,
+              src: Optional[Tuple[int, int]] = None, group=None) -> StepPlan:
+    """The bench's mode rules: one GPU whole K -> symmetric mode; N > 1 or K-row workloads -> column
+    blocks (``mode="cols"``), row blocks (``"rows"``) or the all-reduce option (``"allreduce"``)."""
+    from .dist import shard_range
+
+    if mode not in ("cols", "rows", "allreduce"):
+        raise ValueError(f"mode must be 'cols', 'rows' or 'allreduce', got {mode!r}")
+    if k_rows and mode == "allreduce":
+        raise ValueError("k_rows applies to the row / column modes only")
+    b, e = src if src is not None else shard_range(n, rank, world)
+    pl = StepPlan(n, int(m), int(L), float(p_halt), np.asarray(f, np.float64), int(seed), world, rank, (b, e),
+                  int(k_rows), mode, group=group)
+    if mode == "cols" and (world > 1 or k_rows):
+        pl.mode = "cols"
+        pl.band_width = band_width or cols_band_width(pl.block_rows)
+        pl.cols_sym = not no_sym and 4 * pl.block_rows >= n
+    elif mode == "allreduce":
+        pl.band_width = band_width or ROWS_BAND_WIDTH
+    elif world == 1 and not no_sym and not k_rows:
+        pl.mode = "sym"
+        pl.band_width = band_width or DEFAULT_BAND_WIDTH
+    else:
+        pl.mode = "rows"
+        pl.band_width = band_width or ROWS_BAND_WIDTH
+    return pl
+
+
+@dataclass
+class Front:
+    phi: DeviceCSR                 # all rows of Phi (float32 values)
+    tr: object                     # Banded transpose (of all rows, or of this rank's block for "cols")
+    local: DeviceCSR               # this rank's own rows
+    row_shift: Optional[torch.Tensor] = None  # "cols": every row's fixed-point shift
+
+
+def alloc_k(eng: GRFEngine, pl: StepPlan) -> torch.Tensor:
+    """The resident K buffer of one step (reused across steps)."""
+    if pl.mode == "cols":
+        return torch.empty((pl.n, eng.leading_dim(pl.block_rows)), dtype=torch.float32, device=eng.device)
+    return torch.empty((pl.block_rows, eng.leading_dim(pl.n)), dtype=torch.float32, device=eng.device)
+
+
+def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
+    """Laplacian -> fused walk/Phi (+ bucket counts) -> compaction -> [gather] -> banded transpose."""
+    from .dist import gather_phi
+
+    n, b, e = pl.n, pl.b, pl.e
+    G = eng.laplacian(A_dev)
+    if pl.mode == "cols":
+        # the transpose of the block's rows alone (no count all-reduce, a 1/N-size transpose); the
+        # walk counts its buckets when the block is all of the rank's rows
+        fused = pl.kr_end == e
+        tws = eng.transpose_workspace(pl.block_rows, n, pl.band_width) if fused else None
+        local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
+                                         count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
+                                         want64=False),
+                            want64=False, want32=True, sync_free=True)
+        phi = gather_phi(eng, local, group=pl.group) if pl.world > 1 else local
+        blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
+                                            local.val32)
+        tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap)
+        return Front(phi, tr, local, eng.phi_row_shifts(phi))
+    tws = eng.transpose_workspace(n, n, pl.band_width)
+    local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
+                                     count_ws=tws, band_width=pl.band_width, want64=False),
+                        want64=False, want32=True, sync_free=True)
+    phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width) if pl.world > 1 else local
+    # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
+    tr = eng.transpose_banded(phi, pl.band_width, counted_ws=tws, nnz_bound=n * pl.rows_cap)
+    return Front(phi, tr, local)
+
+
+def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
+               after_tiles: Optional[Callable[[torch.cuda.Event], None]] = None, mirror_workgroups: int = 0,
+               front_at: float = 1.0) -> torch.Tensor:
+    """The K assembly of one step from its front.  Symmetric mode: ``after_tiles(event)`` is called
+    between the Gram tiles and the mirror (the pipelined bench issues the next front there, beside
+    the HBM-bound mirror; ``mirror_workgroups`` then bounds the mirror's grid, 1024 measured best)."""
+    from .dist import allreduce_buckets
+
+    if pl.mode == "cols":
+        eng.gram_sparse_cols(fr.phi, fr.row_shift, fr.tr, out=K, sym_row0=pl.b if pl.cols_sym else None)
+    elif pl.mode == "allreduce":
+        eng.gram_sparse_kslice(fr.phi, fr.tr, pl.b, pl.e, out=K)  # all rows, inner slice [b, e)
+        allreduce_buckets(K[:, :pl.n], group=pl.group)
+    elif pl.mode == "sym":
+        main = torch.cuda.current_stream(eng.device)
+        tiles_done = None
+        if after_tiles is not None and front_at < 1.0:
+            cut = int(round(front_at * 1000))
+            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(0, cut, 1000))
+            tiles_done = torch.cuda.Event()
+            tiles_done.record(main)
+            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(cut, 1000, 1000))
+        else:
+            eng.gram_sparse_upper(fr.phi, fr.tr, out=K)
+            if after_tiles is not None:
+                tiles_done = torch.cuda.Event()
+                tiles_done.record(main)
+        eng.gram_mirror(K, pl.n, mirror_workgroups)
+        if after_tiles is not None:
+            after_tiles(tiles_done)  # (issued after the mirror: the host's launch time does not delay it)
+    else:
+        eng.gram_sparse(fr.phi, fr.tr, pl.b, pl.kr_end, out=K)
+    return K
+
+
+def kernel_step(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan, K: Optional[torch.Tensor] = None,
+                mirror_workgroups: int = 0) -> Tuple[torch.Tensor, Front]:
+    """One whole un-pipelined step (front + K assembly); returns (K buffer, front)."""
+    K = alloc_k(eng, pl) if K is None else K
+    fr = front(eng, A_dev, pl)
+    k_assembly(eng, fr, pl, K, mirror_workgroups=mirror_workgroups)
+    return K, fr
+
+
+def k_view(K: torch.Tensor, pl: StepPlan) -> torch.Tensor:
+    """The logical block of the K buffer: (rows x n) for row modes, (n x block_rows) for columns."""
+    if pl.mode == "cols":
+        return K[:, :pl.block_rows]
+    return K[:, :pl.n]

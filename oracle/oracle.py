@@ -249,6 +249,54 @@ def chunk_bounds(n: int, n_chunks: int) -> np.ndarray:
     return np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
 
 
+def pstep_walk_matrix(W, p_max: int) -> np.ndarray:
+    """Exact walk tensor ``T[:, :, l] = W^l`` for l < p_max: ``compute_pstep_walk_matrix``
+    (``efficient_graph_gp/gpflow_kernels/general_kernel_pofm.py:7-42``; powers by repeated
+    right-multiplication, slice 0 the identity).  The GRF estimator is unbiased for it:
+    E[M_l] = W^l for the cumulative load rule."""
+    W = np.asarray(W, np.float64)
+    n = W.shape[0]
+    T = np.zeros((n, n, p_max), np.float64)
+    T[:, :, 0] = np.eye(n)
+    cur = np.eye(n)
+    for l in range(1, p_max):
+        cur = cur @ W
+        T[:, :, l] = cur
+    return T
+
+
+def clt_check(samples: np.ndarray, expected: np.ndarray, z: float = 6.0, rtol_exact: float = 1e-12,
+              min_nonzero: float = 0.75):
+    """Unbiasedness check of an estimator from independent replicas ``samples[r, ...]``.
+
+    * entries whose replicas all agree must equal ``expected`` to ``rtol_exact`` (deterministic parts);
+    * entries that are nonzero in at least ``min_nonzero`` of the replicas: the replica mean lies within
+      ``z`` standard errors of ``expected`` (rarer entries are dominated by a few large walks, and their
+      sample spread is no reliable standard error; the aggregate checks below cover them);
+    * the sums over the last axis-but-one (row sums of every step) and the totals per step: within
+      ``z`` standard errors as well -- these carry any systematic bias (a wrong halt probability
+      scales a whole step by ((1-p')/(1-p))^l).
+    Returns (ok, worst z-score, number of entries z-tested)."""
+    R = samples.shape[0]
+
+    def zs_of(S, E, mask=None):
+        mean = S.mean(axis=0)
+        se = S.std(axis=0, ddof=1) / np.sqrt(R)
+        scale = np.maximum(np.abs(E), 1.0)
+        spread = se > 1e-14 * scale
+        exact = bool(np.all(np.abs(mean - E)[~spread] <= rtol_exact * scale[~spread]))
+        sel = spread if mask is None else spread & mask
+        return exact, np.abs(mean - E)[sel] / se[sel]
+
+    nonzero = (samples != 0).mean(axis=0) >= min_nonzero
+    ok1, z1 = zs_of(samples, expected, nonzero)
+    ok2, z2 = zs_of(samples.sum(axis=-2), expected.sum(axis=-2))
+    ok3, z3 = zs_of(samples.sum(axis=(-3, -2)), expected.sum(axis=(-3, -2)))
+    allz = np.concatenate([z1, z2, z3])
+    worst = float(allz.max()) if allz.size else 0.0
+    return ok1 and ok2 and ok3 and worst <= z, worst, int(z1.size)
+
+
 def sparse_random_walk(adj, num_walks, p_halt, max_walk_length, n_processes, seed=None, n_threads=None):
     """``SparseRandomWalk(adj, seed).get_random_walk_matrices(..., n_processes)``."""
     ip, ix, dx = _csr_arrays(adj)

@@ -39,6 +39,62 @@ def _install_linear_operator_standin():
     sys.modules.setdefault("linear_operator.operators", ops)
 
 
+def _install_gpflow_standin():
+    """``efficient_graph_gp.gpflow_kernels`` imports gpflow and tensorflow at module level (absent here:
+    an ordinary ImportError).  These stand-ins only let the module import, so that the numpy function
+    ``compute_pstep_walk_matrix`` (general_kernel_pofm.py:7-42) can be called; no class or TF op is used."""
+    class _Meta(type):
+        def __getattr__(cls, name):  # gpflow.kernels.Kernel etc.: the placeholder class itself
+            return cls
+
+    class _Any(metaclass=_Meta):
+        def __init__(self, *a, **k):
+            pass
+
+        def __getattr__(self, name):
+            return _Any()
+
+        def __call__(self, *a, **k):
+            return _Any()
+
+    def _module_getattr(attr):  # PEP 562: every public attribute is the placeholder class
+        if attr.startswith("__"):
+            raise AttributeError(attr)
+        return _Any
+
+    for name in ("gpflow", "tensorflow"):
+        mod = types.ModuleType(name)
+        mod.__getattr__ = _module_getattr
+        sys.modules.setdefault(name, mod)
+
+
+def pstep_golden():
+    """Exact walk tensors E[M_l] = L^l for the statistical test of the Philox estimator: the
+    reference's own compute_pstep_walk_matrix on the sparse Laplacians of the small graphs (and on
+    the raw permutation matrix, walked as given)."""
+    sys.path.insert(0, REF)
+    _install_linear_operator_standin()
+    _install_gpflow_standin()
+    from efficient_graph_gp.gpflow_kernels.general_kernel_pofm import compute_pstep_walk_matrix
+    from efficient_graph_gp_sparse.utils_sparse.graph_utils import get_normalized_laplacian as lap_sparse
+
+    G = graphs()
+    d = {"names": np.array(sorted(G)), "p_max": np.array([5])}
+    for name in sorted(G):
+        Ls = lap_sparse(sp.csr_matrix(G[name])).toarray()
+        d[f"{name}_pstep"] = compute_pstep_walk_matrix(Ls, 5)
+        # row-stochastic walk matrix P = D^-1 W (isolated rows stay zero): deg * w = 1, so the
+        # estimator's loads stay bounded by (1-p)^-l and its CLT bounds are tight
+        W = np.asarray(G[name], np.float64)
+        deg = W.sum(axis=1)
+        P = np.divide(W, deg[:, None], out=np.zeros_like(W), where=deg[:, None] > 0)
+        d[f"{name}_P"] = P
+        d[f"{name}_rw_pstep"] = compute_pstep_walk_matrix(P, 5)
+    d["perm12_raw_pstep"] = compute_pstep_walk_matrix(G["perm12"], 5)
+    np.savez_compressed(os.path.join(OUT, "pstep.npz"), **d)
+    print("pstep fixtures written to", OUT)
+
+
 def graphs():
     g = {}
     A = np.zeros((4, 4))
@@ -204,4 +260,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["pstep"]:
+        pstep_golden()
+    else:
+        main()
+        pstep_golden()

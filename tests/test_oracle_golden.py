@@ -181,3 +181,64 @@ def test_snap_graphs(golden, name):
     for i, r in enumerate(rows):
         np.testing.assert_allclose(O.gram_rows(phi, int(r), int(r) + 1)[0], Kref[i], rtol=1e-12, atol=1e-15)
     np.testing.assert_allclose(np.asarray(phi.multiply(phi).sum(axis=1)).ravel(), d[f"{name}_K_diag"], rtol=1e-12)
+
+
+def test_pstep_restatement_matches_reference(golden):
+    """oracle.pstep_walk_matrix restates compute_pstep_walk_matrix (general_kernel_pofm.py:7-42);
+    the fixture is the reference function's own output (tests/golden/make_golden.py pstep)."""
+    d = golden("pstep")
+    sg = golden("small_graphs")
+    p_max = int(d["p_max"][0])
+    for name in d["names"]:
+        A = sg[f"{name}_A"]
+        L = csr(sg, f"{name}_Lsp", A.shape[0]).toarray()
+        np.testing.assert_allclose(O.pstep_walk_matrix(L, p_max), d[f"{name}_pstep"], rtol=1e-13, atol=1e-15)
+    np.testing.assert_array_equal(O.pstep_walk_matrix(sg["perm12_A"], p_max), d["perm12_raw_pstep"])
+
+
+def _estimator_replicas(W, m, p, p_max, seeds, rng=O.RNG_PHILOX):
+    ip, ix, dx = O._csr_arrays(sp.csr_matrix(W))
+    reps = []
+    for seed in seeds:
+        node, load = O.walk_slots(ip, ix, dx, m, p, p_max, rng=rng, seed=seed, n_chunks=1)
+        reps.append(np.stack([M.toarray() for M in O.reduce_steps(node, load, O.NORM_MUL_RECIP)], axis=-1))
+    return np.stack(reps)
+
+
+@pytest.mark.parametrize("name,p", [("er40", 0.1), ("wer30", 0.3), ("iso25", 0.2), ("star10", 0.5)])
+@pytest.mark.parametrize("rng", [O.RNG_PHILOX, O.RNG_PCG64])
+def test_oracle_estimator_is_unbiased(golden, name, p, rng):
+    """SURVEY.md §7 gate (iii) on the oracle's walks (both RNG streams): E[M_l] = W^l, the reference's
+    exact walk tensor (compute_pstep_walk_matrix), within CLT bounds over independent seeds.  W is the
+    row-stochastic D^-1 A (weighted, isolated rows, a star), where every load is (1-p)^-l and the
+    replica means are near-Gaussian; this pins the estimator itself (halt threshold, Lemire draw,
+    cumulative load deg*w/(1-p)), not one implementation against another."""
+    d = golden("pstep")
+    reps = _estimator_replicas(d[f"{name}_P"], 256, p, int(d["p_max"][0]), range(100, 228), rng)
+    ok, worst, k = O.clt_check(reps, d[f"{name}_rw_pstep"])
+    assert ok and k > 0, (worst, k)
+
+
+@pytest.mark.parametrize("name", ["er40", "wer30"])
+def test_oracle_estimator_on_laplacian_short_walks(golden, name):
+    """The same on the normalised Laplacian itself (signed weights, diagonal entries walked) for the
+    first three steps; later steps' loads grow like (deg/(1-p))^l and are too heavy-tailed for a
+    CLT bound at test sizes (the reference's PCG64 stream shows the same spread)."""
+    d = golden("pstep")
+    sg = golden("small_graphs")
+    A = sg[f"{name}_A"]
+    Ls = csr(sg, f"{name}_Lsp", A.shape[0])
+    reps = _estimator_replicas(Ls, 1024, 0.1, 3, range(200, 248))
+    ok, worst, k = O.clt_check(reps, d[f"{name}_pstep"][:, :, :3])
+    assert ok and k > 0, (worst, k)
+
+
+def test_oracle_degree_one_walks_are_exact(golden):
+    """Degree-1 walks with p_halt = 0 draw nothing and never halt: M_l = P^l exactly (the raw
+    permutation matrix walked as given)."""
+    d = golden("pstep")
+    P = golden("small_graphs")["perm12_A"]
+    ip, ix, dx = O._csr_arrays(sp.csr_matrix(P))
+    node, load = O.walk_slots(ip, ix, dx, 64, 0.0, 5, rng=O.RNG_PHILOX, seed=3)
+    mats = O.reduce_steps(node, load, O.NORM_MUL_RECIP)
+    np.testing.assert_array_equal(np.stack([M.toarray() for M in mats], axis=-1), d["perm12_raw_pstep"])
