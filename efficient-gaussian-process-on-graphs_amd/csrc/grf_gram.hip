@@ -422,6 +422,71 @@ __global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, int64_t nt,
     }
 }
 
+// The LDS block without bank conflicts: the 64 x 64 block is stored unpadded with its 16-byte chunks
+// XOR-swizzled by row (element (r, c) at word r * 64 + (c ^ 4 ((r >> 2) & 15))).  Loads of K rows
+// (256 B per row and wave-instruction) go in with ds_write_b128 (8 lanes per LDS cycle: 8 distinct
+// chunks); each thread then reads two adjacent source columns of four source rows with ds_read_b64
+// (64 banks; lanes {4k + c} x {y, y + 2} hit 32 distinct bank pairs) and stores two output rows of
+// 16 B (256 B per row and wave-instruction).
+__device__ __forceinline__ void gram_mirror_block_swz(int64_t n, int64_t nt, int64_t b, float *__restrict__ K,
+                                                      int64_t ldk, float *__restrict__ tile) {
+    int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
+    auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };
+    if (bi < 0) bi = 0;
+    if (bi > nt - 1) bi = nt - 1;
+    while (bi > 0 && first(bi) > b) --bi;
+    while (bi < nt - 1 && first(bi + 1) <= b) ++bi;
+    const int64_t bj = bi + (b - first(bi));
+    const int64_t i0 = bi * 64, j0 = bj * 64;
+    const int t = threadIdx.x;
+    const bool full = i0 + 64 <= n && j0 + 64 <= n && (ldk & 3) == 0 && bi != bj;
+    if (!full) {  // diagonal / ragged blocks: the padded-tile path (same LDS)
+        gram_mirror_block(n, nt, b, K, ldk, reinterpret_cast<float(*)[65]>(tile));
+        return;
+    }
+    auto swz = [](int r, int c) { return r * 64 + (c ^ (4 * ((r >> 2) & 15))); };
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
+        const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(K + (i0 + y) * ldk + j0 + x));
+        *reinterpret_cast<f32x4 *>(tile + swz(y, x)) = v;
+    }
+    __syncthreads();
+    const int k = t & 15, pr = t >> 4;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const int y = 2 * pr + 32 * it;  // output rows y, y + 1 (source columns)
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        typedef __attribute__((address_space(3))) float lds_float;
+        uint32_t a[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = (uint32_t)(uintptr_t)(lds_float *)(tile + swz(4 * k + c, y));
+        f32x2 v[4];
+        // four single ds_read_b64 (the compiler would pair them into ds_read2_b64, whose 32-bank
+        // halves conflict 2-way on this layout)
+        asm volatile(
+            "ds_read_b64 %0, %4\n\tds_read_b64 %1, %5\n\tds_read_b64 %2, %6\n\tds_read_b64 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+            : "memory");
+        f32x4 o0, o1;
+        o0[0] = v[0].x; o0[1] = v[1].x; o0[2] = v[2].x; o0[3] = v[3].x;
+        o1[0] = v[0].y; o1[1] = v[1].y; o1[2] = v[2].y; o1[3] = v[3].y;
+        __builtin_nontemporal_store(o0, reinterpret_cast<f32x4 *>(K + (j0 + y) * ldk + i0 + 4 * k));
+        __builtin_nontemporal_store(o1, reinterpret_cast<f32x4 *>(K + (j0 + y + 1) * ldk + i0 + 4 * k));
+    }
+}
+
+__global__ __launch_bounds__(256) void gram_mirror_swz_kernel(int64_t n, int64_t nt, int64_t nblocks,
+                                                              float *__restrict__ K, int64_t ldk) {
+    __shared__ __attribute__((aligned(16))) float tile[64 * 65];
+    for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        gram_mirror_block_swz(n, nt, b, K, ldk, tile);
+        __syncthreads();
+    }
+}
+
 __global__ void absmax_reset_kernel(float *m) { *m = 0.f; }
 
 // ------------------------------------------------------------------ dense MFMA
@@ -767,7 +832,12 @@ int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups
     const int64_t cap = env_cap >= 0 ? env_cap : max_workgroups;
     const int64_t grid = cap > 0 && cap < blocks ? cap : blocks;
     GRF_REQUIRE_GRID(grid, 256, "gram_mirror_kernel");
-    gram_mirror_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
+    static const int padded = [] {  // GRF_MIRROR_PADDED=1: the padded 64 x 65 tile (A/B against the swizzle)
+        const char *e = getenv("GRF_MIRROR_PADDED");
+        return e ? atoi(e) : 0;
+    }();
+    if (padded) gram_mirror_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
+    else gram_mirror_swz_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
     GRF_CHECK_LAUNCH("gram_mirror_kernel");
     return GRF_OK;
 }

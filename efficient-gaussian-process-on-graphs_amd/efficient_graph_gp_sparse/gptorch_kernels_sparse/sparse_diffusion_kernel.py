@@ -1,7 +1,11 @@
-"""Diffusion GRF kernel for GPyTorch: mirror of gptorch_kernels_sparse/sparse_diffusion_kernel.py:6-96."""
+"""Diffusion GRF kernel for GPyTorch: mirror of gptorch_kernels_sparse/sparse_diffusion_kernel.py:6-96.
+
+f_l = sigma_f (-beta)^l / (2^l l!) with learnable positive beta and sigma_f; K and its gradient
+run on the HIP kernels behind ``grf_amd.features.GRFKernelFunction`` (autograd carries dK/df to
+beta and sigma_f through the modulator formula)."""
 import torch
 
-from ._features import StepUnion, kernel_from_phi
+from grf_amd.features import StepMatrices, feature_matrix, grf_kernel
 
 try:
     import gpytorch
@@ -29,7 +33,7 @@ class SparseDiffusionKernel(_Base):
             self.register_constraint("raw_sigma_f", Positive())
         self.step_matrices = step_matrices_torch
         self.max_walk_length = max_walk_length
-        self._union = None
+        self._steps = None
 
     @property
     def beta(self):
@@ -48,16 +52,13 @@ class SparseDiffusionKernel(_Base):
         lengths = torch.arange(self.max_walk_length, dtype=self.raw_beta.dtype, device=self.raw_beta.device)
         return self.sigma_f * diffusion_modulator_torch(lengths, self.beta)
 
-    def _union_or_build(self):
-        if self._union is None:
-            self._union = StepUnion(self.step_matrices)
-        return self._union
+    def _step_set(self) -> StepMatrices:
+        if self._steps is None:
+            self._steps = StepMatrices(self.step_matrices)
+        return self._steps
 
     def forward(self, x1_idx=None, x2_idx=None, diag=False, **params):
-        u = self._union_or_build()
-        return kernel_from_phi(u, u.values(self.modulator_vector.to(u.vals[0].device)), x1_idx, x2_idx, diag)
+        return grf_kernel(self.modulator_vector, self._step_set(), x1_idx, x2_idx, diag)
 
     def _get_feature_matrix(self):
-        u = self._union_or_build()
-        return torch.sparse_coo_tensor(torch.stack([u.rows, u.cols]),
-                                       u.values(self.modulator_vector.to(u.vals[0].device)), u.shape)
+        return feature_matrix(self.modulator_vector, self._step_set())

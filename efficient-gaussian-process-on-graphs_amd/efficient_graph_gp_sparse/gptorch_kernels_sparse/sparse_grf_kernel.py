@@ -1,13 +1,14 @@
 """GRF kernel for GPyTorch: mirror of gptorch_kernels_sparse/sparse_grf_kernel.py:5-61.
 
-K[x1, x2] = Phi[x1] Phi[x2]^T with Phi = sum_l f_l M_l and a learnable modulator f.
-Subclasses ``gpytorch.kernels.Kernel`` when gpytorch is installed, else
+K[x1, x2] = Phi[x1] Phi[x2]^T with Phi = sum_l f_l M_l and a learnable modulator f.  The step
+matrices stay on the GPU; Phi, the row selections, K (the exact fixed-point sparse Gram) and the
+gradient w.r.t. f run on the HIP kernels behind ``grf_amd.features.GRFKernelFunction`` -- Phi is
+never densified.  Subclasses ``gpytorch.kernels.Kernel`` when gpytorch is installed, else
 ``torch.nn.Module`` with the same ``forward(x1_idx, x2_idx, diag)`` signature.
-Step matrices stay on the GPU; Phi is rebuilt differentiably from them.
 """
 import torch
 
-from ._features import StepUnion, kernel_from_phi
+from grf_amd.features import StepMatrices, feature_matrix, grf_kernel
 
 try:
     import gpytorch
@@ -22,27 +23,22 @@ class SparseGRFKernel(_Base):
         self.register_parameter("raw_modulator_vector",
                                 torch.nn.Parameter(torch.randn(max_walk_length)))
         self.step_matrices = step_matrices_torch
-        self._union = None
+        self._steps = None
 
     @property
     def modulator_vector(self):
         return self.raw_modulator_vector
 
-    def _phi_values(self):
-        if self._union is None:
-            self._union = StepUnion(self.step_matrices)
-        return self._union.values(self.modulator_vector.to(self._union.vals[0].device))
+    def _step_set(self) -> StepMatrices:
+        if self._steps is None:
+            self._steps = StepMatrices(self.step_matrices)
+        return self._steps
 
     def forward(self, x1_idx=None, x2_idx=None, diag=False, **params):
-        """K[x1, x2] (or its diagonal) = Phi[x1] Phi[x2]^T."""
-        return kernel_from_phi(self._union_or_build(), self._phi_values(), x1_idx, x2_idx, diag)
-
-    def _union_or_build(self):
-        if self._union is None:
-            self._union = StepUnion(self.step_matrices)
-        return self._union
+        """K[x1, x2] (or its diagonal) = Phi[x1] Phi[x2]^T (reference :24-49)."""
+        return grf_kernel(self.modulator_vector, self._step_set(), x1_idx, x2_idx, diag)
 
     def _get_feature_matrix(self):
-        """Phi as a sparse COO tensor (values differentiable w.r.t. the modulator)."""
-        u = self._union_or_build()
-        return torch.sparse_coo_tensor(torch.stack([u.rows, u.cols]), self._phi_values(), u.shape)
+        """Phi as a torch sparse CSR tensor on the device (reference :51-61; not differentiable:
+        gradients flow through ``forward``)."""
+        return feature_matrix(self.modulator_vector, self._step_set())

@@ -17,7 +17,7 @@ Subclasses ``gpytorch.models.ExactGP`` when gpytorch is installed; otherwise a
 """
 import torch
 
-from grf_amd.engine import DeviceCSR, get_engine
+from grf_amd.engine import DeviceCSR, get_engine  # noqa: F401
 
 from ..gptorch_kernels_sparse.sparse_grf_kernel import SparseGRFKernel
 
@@ -54,15 +54,11 @@ class SparseGraphGP(_Base):
 
     def _phi_csr(self, device) -> DeviceCSR:
         """Phi = sum_l f_l M_l (current modulator) as a device CSR (rows ascending, columns
-        ascending within a row, fp32 values)."""
-        u = self.covar_module._union_or_build()
-        vals = self.covar_module._phi_values().detach().to(device=device, dtype=torch.float32)
-        rows = u.rows.to(device)
-        n_rows, n_cols = u.shape
-        ptr = torch.zeros(n_rows + 1, dtype=torch.int64, device=device)
-        ptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n_rows), 0)
-        idx = u.cols.to(device=device, dtype=torch.int32)
-        return DeviceCSR(n_rows, n_cols, ptr, idx, None, vals.contiguous(), int(vals.numel()))
+        ascending within a row, fp32 values; grf_phi_steps_csr on the kernel's step matrices)."""
+        phi = self.covar_module._step_set().phi(self.covar_module.modulator_vector)
+        if phi.ptr.device != torch.device(device):
+            raise ValueError("predict: the step matrices live on another device than x_test")
+        return phi
 
     @torch.no_grad()
     def predict(self, x_test, n_samples=64, cg_dtype=torch.float64, max_iter=1000, tolerance=None):

@@ -2,8 +2,10 @@
 
 Laplacian -> walks -> per-step matrices run on the GPU; the step matrices are
 returned as ``SparseLinearOperator`` over torch CSR (float32 values, int64
-indices) that stay on the device -- the reference builds them on the host and
-the experiments copy them over (experiments/graph_bo/utils/device.py:9-14).
+indices) built from the device buffers directly -- no host round trip (the
+reference builds them on the host and the experiments copy them over,
+experiments/graph_bo/utils/device.py:9-14).  ``step_matrices_scipy`` (the
+reference's attribute, used for the cache) is copied to the host only when read.
 
 Cache format: the reference pickles a list of scipy matrices; this engine writes
 a binary ``.npz`` bundle (per step: indptr, indices, data, shape) under the same
@@ -42,6 +44,8 @@ class GraphPreprocessor:
         self.n_processes = n_processes
         self.rng = rng
         self.device = get_engine(device).device
+        self._step_device = None
+        self._step_scipy = None
         if load_from_disk:
             if os.path.exists(self.cache_filename):
                 self.step_matrices_scipy = self.load_step_matrices(self.cache_filename)
@@ -59,16 +63,31 @@ class GraphPreprocessor:
     def _to_device(self, t):
         return t.to(self.device)
 
+    @property
+    def step_matrices_scipy(self) -> List[sp.csr_matrix]:
+        """The step matrices as scipy CSR (fp64), copied from the device on first access."""
+        if self._step_scipy is None and self._step_device is not None:
+            self._step_scipy = [M.to_scipy() for M in self._step_device]
+        return self._step_scipy
+
+    @step_matrices_scipy.setter
+    def step_matrices_scipy(self, mats) -> None:
+        self._step_scipy = mats
+
     def preprocess_graph(self, save_to_disk: bool = False) -> List[SparseLinearOperator]:
-        """Laplacian -> walks -> step matrices (GPU); returns device-resident linear operators."""
-        laplacian = api.sparse_laplacian(self.adj_matrix, device=self.device)
-        self.step_matrices_scipy = api.sparse_step_matrices(
-            laplacian, self.walks_per_node, self.p_halt, self.max_walk_length, seed=self.random_walk_seed,
-            n_processes=self.n_processes, rng=self.rng, device=self.device)
+        """Laplacian -> walks -> step matrices on the GPU (reference :88-115); returns device-resident
+        linear operators over torch CSR views of the device buffers (values cast to float32)."""
+        self._step_scipy = None
+        self._step_device = api.sparse_step_matrices_device(
+            self.adj_matrix, self.walks_per_node, self.p_halt, self.max_walk_length, seed=self.random_walk_seed,
+            n_processes=self.n_processes, rng=self.rng, device=self.device, laplacian=True)
         if save_to_disk:
             self.save_step_matrices(self.step_matrices_scipy, self.cache_filename)
-        self.step_matrices_torch = [SparseLinearOperator(self._to_device(self.from_scipy_csr(m)))
-                                    for m in self.step_matrices_scipy]
+        n = self.adj_matrix.shape[0]
+        self.step_matrices_torch = [
+            SparseLinearOperator(torch.sparse_csr_tensor(M.ptr, M.idx[:M.nnz].long(), M.val[:M.nnz].float(), (n, n),
+                                                         dtype=torch.float32))
+            for M in self._step_device]
         return self.step_matrices_torch
 
     @staticmethod

@@ -97,6 +97,13 @@ SIGNATURES = {
                                       _i64, _vp, _sz, _vp]),
     "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    # the GPyTorch surface's feature algebra (step_* are host arrays of device pointers)
+    "grf_phi_steps_csr_count": (_i32, [_i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "grf_phi_steps_csr_fill": (_i32, [_i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "grf_csr_row_lengths": (_i32, [_i64, _vp, _vp, _vp, _vp]),
+    "grf_csr_gather_rows": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "grf_csr_rowdot": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "grf_csr_rows_dot_cols": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
 }
 
 _lib = None

@@ -85,11 +85,19 @@ def _sparse_walk(eng: GRFEngine, G: DeviceCSR, num_walks, p_halt, max_walk_lengt
 def sparse_step_matrices(walk_matrix, num_walks, p_halt, max_walk_length, seed=None, n_processes=None, rng=None,
                          device=None) -> list:
     """SparseRandomWalk(walk_matrix, seed).get_random_walk_matrices(...) (sparse_sampler.py:72-132)."""
+    return [M.to_scipy() for M in sparse_step_matrices_device(walk_matrix, num_walks, p_halt, max_walk_length, seed,
+                                                              n_processes, rng, device)]
+
+
+def sparse_step_matrices_device(walk_matrix, num_walks, p_halt, max_walk_length, seed=None, n_processes=None,
+                                rng=None, device=None, laplacian: bool = False) -> list:
+    """The step matrices as device CSR (fp64 values), never leaving the GPU.  laplacian=True walks
+    the normalised Laplacian of ``walk_matrix`` (GraphPreprocessor.preprocess_graph, :101-108)."""
     eng = get_engine(device)
-    G = eng.to_device(_canonical_csr(walk_matrix))
+    A = _canonical_csr(walk_matrix)
+    G = eng.laplacian(A) if laplacian else eng.to_device(A)
     slots = _sparse_walk(eng, G, num_walks, p_halt, max_walk_length, seed, n_processes, rng)
-    st = eng.steps(slots, C.NORM_MUL_RECIP)
-    return [M.to_scipy() for M in eng.step_matrices(st)]
+    return eng.step_matrices(eng.steps(slots, C.NORM_MUL_RECIP))
 
 
 def sparse_features(adj, modulator_vector, walks_per_node, p_halt, max_walk_length, *, n_processes=None, rng=None,

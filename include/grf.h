@@ -371,6 +371,48 @@ int32_t grf_cg_gram_solve_f64(int64_t n_sys, const int64_t *ptr, const int32_t *
 /* (covers both precisions) */
 size_t grf_cg_workspace_bytes(int64_t n_sys, int64_t n_cols, int32_t n_rhs);
 
+/* ------------------------------------------- the GPyTorch surface's feature algebra
+ * Device-resident step matrices (one CSR per step: int64 row pointers, sorted int32 columns,
+ * float32 values -- the preprocessor's torch CSR values) for
+ * efficient_graph_gp_sparse/gptorch_kernels_sparse/sparse_grf_kernel.py:24-61 and
+ * sparse_diffusion_kernel.py:74-96; K[x1, x2] = Phi[x1] Phi[x2]^T runs on the Gram kernels above
+ * (grf_gram_sparse_cols), the modulator gradient on grf_csr_transpose + grf_spmm_csr + these. */
+
+/* Phi = sum_l f_l M_l over L <= 64 step matrices (step_* are HOST arrays of L device pointers):
+ * `phi = sum(mod_vec * mat for ...)` (sparse_grf_kernel.py:54-60).  Per entry the terms of the
+ * steps holding it are summed in step order in fp64 (0.0 + first term, left to right), exact
+ * zeros dropped.  Two passes: _count writes the row lengths (int32 [n_rows]; scan them with
+ * grf_scan_counts), _fill writes the rows at phi_ptr (phi_val and/or phi_val32 may be NULL). */
+int32_t grf_phi_steps_csr_count(int64_t n_rows, int32_t L, const int64_t *const *step_ptr,
+                                const int32_t *const *step_idx, const float *const *step_val, const double *f,
+                                int32_t n_f, int32_t *phi_cnt, grf_stream_t stream);
+int32_t grf_phi_steps_csr_fill(int64_t n_rows, int32_t L, const int64_t *const *step_ptr,
+                               const int32_t *const *step_idx, const float *const *step_val, const double *f,
+                               int32_t n_f, const int64_t *phi_ptr, int32_t *phi_idx, double *phi_val,
+                               float *phi_val32, grf_stream_t stream);
+
+/* phi[x_idx] (sparse_grf_kernel.py:33-41): len[r] = nnz of row row_map[r] (NULL map: row r);
+ * then, with out_ptr = grf_scan_counts(len), the rows copied contiguously. */
+int32_t grf_csr_row_lengths(int64_t n_sel, const int64_t *ptr, const int32_t *row_map, int32_t *len,
+                            grf_stream_t stream);
+int32_t grf_csr_gather_rows(int64_t n_sel, const int64_t *ptr, const int32_t *idx, const float *val,
+                            const int32_t *row_map, const int64_t *out_ptr, int32_t *out_idx, float *out_val,
+                            grf_stream_t stream);
+
+/* out[r] = A[rows_a[r]] . B[rows_b[r]] (sorted CSR rows, fp64 sum of the exact products,
+ * deterministic order; NULL row maps = identity): `(phi_x1 * phi_x2).sum(dim=-1)` (:43-45), and
+ * with A = M_l the diagonal's modulator gradient. */
+int32_t grf_csr_rowdot(int64_t n_pairs, const int64_t *a_ptr, const int32_t *a_idx, const float *a_val,
+                       const int32_t *rows_a, const int64_t *b_ptr, const int32_t *b_idx, const float *b_val,
+                       const int32_t *rows_b, double *out, grf_stream_t stream);
+
+/* out[r] = sum_e val[e] Z[idx[e] * ldz + r] over the entries e of row row_map[r]: one step matrix's
+ * rows contracted with the columns of a dense Z (n_cols x ldz, fp32, ldz >= n_sel).  With
+ * Z = Phi[x2]^T G^T this is the modulator gradient of K[x1, x2] = Phi[x1] Phi[x2]^T:
+ * dL/df_l = sum_r (M_l[x1] Z)[r, r] + (the same with x1, x2 and G^T swapped). */
+int32_t grf_csr_rows_dot_cols(int64_t n_sel, const int64_t *ptr, const int32_t *idx, const float *val,
+                              const int32_t *row_map, const float *Z, int64_t ldz, double *out, grf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,153 @@
+"""The GPyTorch surface on the HIP feature algebra (grf_amd/features.py).
+
+Reference: efficient_graph_gp_sparse/gptorch_kernels_sparse/sparse_grf_kernel.py:24-61,
+sparse_diffusion_kernel.py:27-96, preprocessor/graph_preprocessor.py:88-140.  GPyTorch and
+linear_operator are absent here, so the arithmetic is pinned to a numpy fp64 restatement of the
+reference's formulas on the reference's own golden step matrices (tests/golden/small_graphs.npz,
+made by make_golden.py from SparseRandomWalk): Phi = sum_l f_l M_l, K = Phi[x1] Phi[x2]^T,
+diag = rowwise Phi[x1] . Phi[x2], and the analytic gradient
+dL/df_l = sum_{r,s} G[r,s] (M_l[x1_r] . Phi[x2_s] + Phi[x1_r] . M_l[x2_s]).
+Tolerances: K / diag |d| <= 3e-5 (|Phi||Phi|^T) + 1e-7 max|K| (fp32 Phi, exact fixed-point Gram);
+gradients rtol 1e-4 (fp32 Z = Phi^T G^T on the device).
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from golden_util import csr, same_csr
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops(mats):
+    from efficient_graph_gp_sparse.preprocessor import GraphPreprocessor
+    from efficient_graph_gp_sparse.utils_sparse.sparse_lo import SparseLinearOperator
+    return [SparseLinearOperator(GraphPreprocessor.from_scipy_csr(M).to("cuda")) for M in mats]
+
+
+def _close(got, ref, absbound):
+    err = np.abs(np.asarray(got, np.float64) - ref)
+    return bool(np.all(err <= 3e-5 * absbound + 1e-7 * max(np.abs(ref).max(), 1e-30))), float(err.max())
+
+
+def test_sparse_grf_kernel_forward_diag_and_gradient(golden):
+    from efficient_graph_gp_sparse.gptorch_kernels_sparse import SparseGRFKernel
+    d = golden("small_graphs")
+    steps = [csr(d, f"er40_sp_n3_s7_l{l}", 40) for l in range(4)]
+    dense = [M.toarray().astype(np.float32).astype(np.float64) for M in steps]  # (the torch CSR's fp32 values)
+    torch.manual_seed(0)
+    kern = SparseGRFKernel(4, _ops(steps)).cuda()
+    f = kern.modulator_vector.detach().cpu().numpy().astype(np.float64)
+    Phi = sum(fl * M for fl, M in zip(f, dense))
+    aPhi = np.abs(Phi)
+    i1, i2 = [0, 3, 5, 17, 39, 3], [1, 3, 20]
+    x1, x2 = torch.tensor(i1, device="cuda"), torch.tensor(i2, device="cuda")
+    K = kern(x1, x2)
+    assert K.is_cuda and K.shape == (6, 3)
+    ok, e = _close(K.detach().cpu().numpy(), Phi[i1] @ Phi[i2].T, aPhi[i1] @ aPhi[i2].T)
+    assert ok, e
+    Kd = kern(x1, x1, diag=True)
+    ok, e = _close(Kd.detach().cpu().numpy(), np.einsum("ij,ij->i", Phi[i1], Phi[i1]),
+                   np.einsum("ij,ij->i", aPhi[i1], aPhi[i1]))
+    assert ok, e
+    Kfull = kern()
+    ok, e = _close(Kfull.detach().cpu().numpy(), Phi @ Phi.T, aPhi @ aPhi.T)
+    assert ok, e
+    assert torch.equal(Kfull, Kfull.t())  # x1 == x2: symmetric enumeration + mirror
+    # gradient of sum(W * K[x1, x2]) w.r.t. the modulator
+    W = np.random.default_rng(1).standard_normal((6, 3))
+    (kern(x1, x2) * torch.tensor(W, device="cuda", dtype=torch.float32)).sum().backward()
+    gref = [np.sum(W * (dense[l][i1] @ Phi[i2].T + Phi[i1] @ dense[l][i2].T)) for l in range(4)]
+    np.testing.assert_allclose(kern.raw_modulator_vector.grad.cpu().numpy(), gref, rtol=1e-4, atol=1e-6)
+    kern.raw_modulator_vector.grad = None
+    w = np.random.default_rng(2).standard_normal(6)
+    (kern(x1, x1, diag=True) * torch.tensor(w, device="cuda", dtype=torch.float32)).sum().backward()
+    gref = [np.sum(w * 2 * np.einsum("ij,ij->i", dense[l][i1], Phi[i1])) for l in range(4)]
+    np.testing.assert_allclose(kern.raw_modulator_vector.grad.cpu().numpy(), gref, rtol=1e-4, atol=1e-6)
+    # the feature matrix itself
+    P = kern._get_feature_matrix()
+    assert P.is_sparse_csr and P.is_cuda
+    np.testing.assert_allclose(P.to_dense().cpu().numpy(), Phi, rtol=1e-6, atol=1e-7)
+
+
+def test_sparse_diffusion_kernel_gradients(golden):
+    """Autograd through the modulator formula to beta and sigma_f, against central finite
+    differences of the numpy restatement (fp64)."""
+    from efficient_graph_gp_sparse.gptorch_kernels_sparse import SparseDiffusionKernel
+    d = golden("small_graphs")
+    steps = [csr(d, f"wer30_sp_n3_s7_l{l}", 30) for l in range(4)]
+    dense = [M.toarray().astype(np.float32).astype(np.float64) for M in steps]
+    dk = SparseDiffusionKernel(4, _ops(steps)).cuda()
+    x = torch.tensor([0, 2, 7, 11, 29], device="cuda")
+    W = np.random.default_rng(3).standard_normal((5, 5))
+    (dk(x, x) * torch.tensor(W, device="cuda", dtype=torch.float32)).sum().backward()
+
+    def loss(rb, rs):
+        beta, sig = np.log1p(np.exp(rb)), np.log1p(np.exp(rs))
+        fm = [sig * (-beta) ** l / (2 ** l * np.prod(np.arange(1, l + 1))) for l in range(4)]
+        Phi = sum(fl * M for fl, M in zip(fm, dense))[[0, 2, 7, 11, 29]]
+        return np.sum(W * (Phi @ Phi.T))
+
+    h = 1e-5
+    gb = (loss(1.0 + h, 1.0) - loss(1.0 - h, 1.0)) / (2 * h)
+    gs = (loss(1.0, 1.0 + h) - loss(1.0, 1.0 - h)) / (2 * h)
+    np.testing.assert_allclose([dk.raw_beta.grad.item(), dk.raw_sigma_f.grad.item()], [gb, gs], rtol=2e-4)
+
+
+def test_preprocessor_device_resident_steps(golden, tmp_path):
+    """preprocess_graph keeps the step matrices on the device (no host scipy round trip); the host
+    copy is made only when step_matrices_scipy is read, and equals the reference's golden steps."""
+    from efficient_graph_gp_sparse.preprocessor import GraphPreprocessor
+    d = golden("small_graphs")
+    A = sp.csr_matrix(d["er40_A"])
+    pre = GraphPreprocessor(A, walks_per_node=20, p_halt=0.2, max_walk_length=4, random_walk_seed=7,
+                            cache_filename=str(tmp_path / "s.npz"), n_processes=3)
+    ops = pre.preprocess_graph()
+    assert pre._step_scipy is None  # nothing copied to the host yet
+    assert all(op.sparse_csr_tensor.is_cuda and op.sparse_csr_tensor.values().dtype == torch.float32 for op in ops)
+    for l, op in enumerate(ops):
+        ref = csr(d, f"er40_sp_n3_s7_l{l}", 40)
+        t = op.sparse_csr_tensor
+        assert np.array_equal(t.crow_indices().cpu().numpy(), ref.indptr)
+        assert np.array_equal(t.col_indices().cpu().numpy(), ref.indices)
+        assert np.array_equal(t.values().cpu().numpy(), ref.data.astype(np.float32))
+        assert same_csr(pre.step_matrices_scipy[l], ref)
+
+
+def test_full_graph_forward_on_enron_without_densifying(golden):
+    """Enron (36,692 nodes): the whole K from the kernel's forward, with the device's peak memory
+    within K's own bytes plus a margin (a dense Phi alone would be another 5.4 GB), sampled rows
+    against the fp64 restatement; and a 2,000-node gradient."""
+    from golden_util import snap_adjacency
+    from efficient_graph_gp_sparse.gptorch_kernels_sparse import SparseDiffusionKernel
+    from efficient_graph_gp_sparse.preprocessor import GraphPreprocessor
+    A = snap_adjacency(golden("snap"), "enron")
+    n = A.shape[0]
+    pre = GraphPreprocessor(A, walks_per_node=32, p_halt=0.1, max_walk_length=8, rng="philox")
+    ops = pre.preprocess_graph()
+    dk = SparseDiffusionKernel(8, ops).cuda()
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    K = dk()
+    torch.cuda.synchronize()
+    k_bytes = 4 * n * n
+    assert torch.cuda.max_memory_allocated() - base < 1.25 * k_bytes + (1 << 30)
+    fm = dk.modulator_vector.detach().cpu().numpy().astype(np.float64)
+    steps = [M.astype(np.float32).astype(np.float64) for M in pre.step_matrices_scipy]
+    Phi = sum(fl * M for fl, M in zip(fm, steps)).tocsr()
+    rows = np.r_[0, 1, np.argsort(-np.diff(A.indptr), kind="stable")[:3], n - 1]
+    Kr = K[torch.tensor(rows, device="cuda")].detach().cpu().numpy()
+    ok, e = _close(Kr, (Phi[rows] @ Phi.T).toarray(), (abs(Phi)[rows] @ abs(Phi).T).toarray())
+    assert ok, e
+    del K
+    x = torch.tensor(np.random.default_rng(4).choice(n, 2000, replace=False), device="cuda")
+    dk(x, x).sum().backward()
+    xs = x.cpu().numpy()
+    P = Phi[xs]
+    g_phi = [float(np.sum((steps[l][xs] @ P.T).toarray()) * 2) for l in range(8)]  # d sum(K)/d f_l
+    beta, sig = float(dk.beta), float(dk.sigma_f)
+    dfdsig = [fm[l] / sig for l in range(8)]
+    np.testing.assert_allclose(dk.raw_sigma_f.grad.item(),
+                               sum(g * df for g, df in zip(g_phi, dfdsig)) * (1 - np.exp(-sig)), rtol=1e-3)

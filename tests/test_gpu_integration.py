@@ -41,7 +41,9 @@ def test_integration_stub_walks_match_engine_and_reference_stream():
         torch.cuda.synchronize()
         eng = GRFEngine("cuda:0")
         slots = eng.walk(eng.to_device(Ls), 16, 0.1, 4, rng=0, seed=seed or 42, n_chunks=n_proc)
-        assert torch.equal(node, slots.node) and torch.equal(load, slots.load)
+        assert torch.equal(node, slots.node)
+        used = node >= 0  # (loads of empty slots are not written)
+        assert torch.equal(load[used], slots.load[used])
         on, ol = O.walk_slots(*O._csr_arrays(Ls), 16, 0.1, 4, rng=O.RNG_PCG64, n_chunks=n_proc, seed=seed or 42)
         assert np.array_equal(node.cpu().numpy(), on)
         mask = on >= 0
