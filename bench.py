@@ -464,12 +464,12 @@ def main():
     n, m, L, p = A.shape[0], args.walks, args.length, args.p_halt
     f = diffusion_modulator(L, 1.0)
     A_dev = DeviceCSR.from_scipy(A, dev)
-    src = None
+    shards = None
     if world > 1 and args.balance != "nodes":
         from grf_amd.dist import balanced_shards
-        src = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance)[rank]
+        shards = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance)  # (setup, untimed)
     pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
-                     band_width=args.band_width, no_sym=args.no_sym, src=src)
+                     band_width=args.band_width, no_sym=args.no_sym, shards=shards)
     b, e, kr_end = pl.b, pl.e, pl.kr_end
     K = P.alloc_k(eng, pl)  # resident output block, reused
     if args.overlap is None:

@@ -497,12 +497,36 @@ static int32_t tr_region_cols(int64_t n_rows, int64_t n_cols) {
     return (int32_t)cr;
 }
 
+// Segment r (src[r * stride .. r * stride + len[r])) -> dst[dst_off[r] ..]: the multi-GPU Phi
+// all-gather's compaction, with every length and offset on the device (no host round trip).
+__global__ __launch_bounds__(256) void concat_segments_kernel(int64_t stride, const uint32_t *__restrict__ src,
+                                                              const int64_t *__restrict__ len,
+                                                              const int64_t *__restrict__ dst_off,
+                                                              uint32_t *__restrict__ dst) {
+    const int64_t seg = blockIdx.y;
+    const int64_t l = len[seg], o = dst_off[seg];
+    const uint32_t *s = src + seg * stride;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < l; i += (int64_t)gridDim.x * 256) dst[o + i] = s[i];
+}
+
 }  // namespace grf
 
 using namespace grf;
 
 extern "C" {
 #pragma GCC visibility push(default)
+
+int32_t grf_concat_segments(int32_t n_seg, int64_t stride, const void *src, const int64_t *seg_len,
+                            const int64_t *dst_off, void *dst, grf_stream_t stream) {
+    GRF_REQUIRE(n_seg >= 0 && n_seg <= 65535 && stride >= 0 && (n_seg == 0 || (src && seg_len && dst_off && dst)),
+                GRF_EINVAL, "grf_concat_segments: bad arguments");
+    if (n_seg == 0 || stride == 0) return GRF_OK;
+    const int64_t bx = std::min<int64_t>(cdiv<int64_t>(stride, 256), 2048);
+    concat_segments_kernel<<<dim3((unsigned)bx, (unsigned)n_seg), 256, 0, S(stream)>>>(
+        stride, (const uint32_t *)src, seg_len, dst_off, (uint32_t *)dst);
+    GRF_CHECK_LAUNCH("concat_segments_kernel");
+    return GRF_OK;
+}
 
 size_t grf_scan_workspace_bytes(int64_t n) { return scan_ws_bytes(n); }
 

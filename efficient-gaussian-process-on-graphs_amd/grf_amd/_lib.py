@@ -64,6 +64,7 @@ SIGNATURES = {
     "grf_phi_fused": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_scan_workspace_bytes": (_sz, [_i64]),
+    "grf_concat_segments": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_compact_rows": (_i32, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "grf_transpose_banded_plan": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
     "grf_transpose_banded_fill": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz,

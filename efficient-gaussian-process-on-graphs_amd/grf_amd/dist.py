@@ -13,14 +13,17 @@ all-reduce of K would move ~70 GB per GPU through the xGMI ring).
 so both can be measured: after the same Phi all-gather, rank r computes the
 partial Gram over its slice of the inner dimension, K_r = sum over k in C_r of
 Phi[:, k] Phi[:, k]^T (all n rows), and the ranks sum the K_r with an all-reduce
-in fixed-size buckets.  Every rank ends with the whole K (replicated).
+in fixed-size buckets.  Every rank ends with the whole K (replicated).  Unlike the row and column
+modes, whose entries are the exact fixed-point sums rounded once (bit-identical for any GPU count),
+this mode adds the ranks' rounded fp32 partials in the collective's order: K depends on the rank
+count and on the reduction order, within the fp32 K tolerance (tests/test_gpu_parity.py).
 
 The reference has no distributed code; its only parallelism is a fork pool over
 source chunks (sparse_sampler.py:90-114), which this replaces.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -69,21 +72,141 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     return b, b + base + (1 if rank < extra else 0)
 
 
+def shard_bounds(weights, world: int) -> List[Tuple[int, int]]:
+    """Contiguous ranges of rows with (as nearly as row granularity allows) equal total weight:
+    rank r ends at the first row whose inclusive prefix weight reaches (r + 1) / world of the total.
+    Every rank gets at least one row when there are at least ``world`` rows."""
+    import numpy as np
+
+    w = np.asarray(weights, dtype=np.float64).ravel()
+    n = w.size
+    if world <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * (world - 1)
+    cum = np.cumsum(w)
+    total = cum[-1]
+    if total <= 0:
+        return [shard_range(n, r, world) for r in range(world)]
+    ends = []
+    prev = 0
+    for r in range(world - 1):
+        e = int(np.searchsorted(cum, total * (r + 1) / world, side="left")) + 1
+        e = max(e, prev + (1 if n - prev > world - 1 - r else 0))  # a row for everyone left, if possible
+        e = min(e, n - (world - 1 - r) if n >= world else n)
+        ends.append(e)
+        prev = e
+    ends.append(n)
+    starts = [0] + ends[:-1]
+    return list(zip(starts, ends))
+
+
+# per-row cost model of one step (C4 measurements, DESIGN.md §5): the K block row's write
+# (4 n bytes at ~6.3 TB/s) and the Gram's record gathers (g_j records of 6 B with ~1.8x line
+# amplification at ~7.3 TB/s, g_j = sum over Phi[j, k] != 0 of the column count of k)
+_K_WRITE_NS_PER_ENTRY = 4.0 / 6.3
+_GATHER_NS_PER_RECORD = 6.0 * 1.8 / 7.3
+
+
+def row_costs(engine, phi) -> torch.Tensor:
+    """Estimated step time of every row of Phi (device float64 [n]): its K row's write plus its
+    Gram tiles' record gathers.  A row's gathers are g_j = sum_{k in row j} c_k, c_k = nnz of
+    column k -- rows whose walks reach hubs cost more than their Phi nnz alone says."""
+    n_rows, n_cols = phi.n_rows, phi.n_cols
+    nnz = phi.nnz
+    idx = phi.idx[:nnz].long()
+    col_cnt = torch.bincount(idx, minlength=n_cols).to(torch.float64)
+    per_entry = col_cnt[idx]
+    csum = torch.zeros(nnz + 1, dtype=torch.float64, device=per_entry.device)
+    csum[1:] = torch.cumsum(per_entry, 0)
+    g = csum[phi.ptr[1:]] - csum[phi.ptr[:-1]]
+    return _K_WRITE_NS_PER_ENTRY * n_cols + _GATHER_NS_PER_RECORD * g
+
+
+def balanced_shards(engine, A, m: int, p_halt: float, L: int, f, world: int, *, seed: int = 42,
+                    policy: str = "phi") -> List[Tuple[int, int]]:
+    """Source shards of equal estimated step time.  policy "phi": one setup walk of ALL sources
+    (Philox is keyed by (seed, source, walk), so every rank computes the identical Phi without a
+    collective, and Phi is the same every step) gives each row's cost (``row_costs``), and the
+    ranks get contiguous ranges of equal total cost.  policy "nodes": equal node counts.
+    Run once per (graph, m, L, seed), outside the timed steps."""
+    if policy == "nodes":
+        n = A.n_rows if hasattr(A, "n_rows") else A.shape[0]
+        return [shard_range(n, r, world) for r in range(world)]
+    if policy != "phi":
+        raise ValueError(f"policy must be 'phi' or 'nodes', got {policy!r}")
+    G = engine.laplacian(A)
+    phi = engine.compact(engine.walk_phi(G, m, p_halt, L, f, seed=seed, want64=False), want64=False)
+    return shard_bounds(row_costs(engine, phi).cpu().numpy(), world)
+
+
+def allgather_csr_rows_bounded(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor,
+                               rows_per_rank: Sequence[int], entries_bound: int, group=None):
+    """All-gather of row-sharded CSR pieces with NO host round trip: every rank sends its first
+    ``entries_bound`` column / value entries (the capacity its sync-free compaction allocated,
+    rows x the padded row capacity; entries past its nnz are ignored) and its row pointers padded
+    to the largest shard; the full row pointers come from the gathered counts on the device, and
+    ``grf_concat_segments`` packs each rank's entries to its final offset.  The row counts are the
+    host-known shard sizes.  Returns (ptr, idx, val) of the concatenation (nnz = ptr[-1], read
+    lazily; idx / val are sized world x entries_bound)."""
+    from . import _lib as C
+    from .engine import _p, get_engine
+
+    world = dist.get_world_size(group)
+    dev = ptr.device
+    n_max = max(rows_per_rank)
+    B = max(int(entries_bound), 1)
+    lp = torch.empty(n_max + 1, dtype=torch.int64, device=dev)
+    n_loc = ptr.numel() - 1
+    lp[:n_loc + 1] = ptr
+    lp[n_loc + 1:] = ptr[-1]
+    g_ptr = torch.empty(world * (n_max + 1), dtype=torch.int64, device=dev)
+    _all_gather_into(g_ptr, lp, group=group)
+    g_ptr = g_ptr.view(world, n_max + 1)
+    send_i = idx[:B] if idx.numel() >= B else torch.cat([idx, idx.new_zeros(B - idx.numel())])
+    send_v = val[:B] if val.numel() >= B else torch.cat([val, val.new_zeros(B - val.numel())])
+    g_idx = torch.empty(world * B, dtype=idx.dtype, device=dev)
+    g_val = torch.empty(world * B, dtype=val.dtype, device=dev)
+    _all_gather_into(g_idx, send_i.contiguous(), group=group)
+    _all_gather_into(g_val, send_v.contiguous(), group=group)
+    counts = torch.cat([g_ptr[r, 1:n_r + 1] - g_ptr[r, :n_r] for r, n_r in enumerate(rows_per_rank)])
+    full_ptr = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=dev)
+    full_ptr[1:] = torch.cumsum(counts, 0)
+    row0 = torch.tensor([0] + list(torch.tensor(rows_per_rank).cumsum(0)[:-1].tolist()), dtype=torch.int64,
+                        device=dev)
+    seg_len = torch.stack([g_ptr[r, n_r] for r, n_r in enumerate(rows_per_rank)]).contiguous()
+    dst_off = full_ptr[row0].contiguous()
+    out_i = torch.empty(world * B, dtype=idx.dtype, device=dev)
+    out_v = torch.empty(world * B, dtype=val.dtype, device=dev)
+    if dev.type == "cuda":
+        eng = get_engine(dev)
+        for src, dst in ((g_idx, out_i), (g_val, out_v)):
+            if src.element_size() != 4:
+                raise ValueError("allgather_csr_rows_bounded: 4-byte column and value entries expected")
+            C.check(eng.lib.grf_concat_segments(world, B, _p(src), _p(seg_len), _p(dst_off), _p(dst), eng.stream),
+                    "grf_concat_segments")
+    else:  # (CPU tensors: the host-side test harness; sizes are host-readable there)
+        for r in range(world):
+            o, n_e = int(dst_off[r]), int(seg_len[r])
+            out_i[o:o + n_e] = g_idx[r * B:r * B + n_e]
+            out_v[o:o + n_e] = g_val[r * B:r * B + n_e]
+    return full_ptr, out_i, out_v
+
+
 def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, group=None):
-    """All-gather row-sharded CSR pieces (rank order) into the full CSR on every rank.
+    """All-gather row-sharded CSR pieces (rank order) into the full CSR on every rank, exactly sized.
 
     ``ptr`` is the local int64 row pointer (n_local + 1, starting at 0), ``idx``
     int32 columns, ``val`` values.  Works with RCCL (device tensors) and gloo
-    (CPU tensors).  Returns (ptr, idx, val) of the concatenation.
+    (CPU tensors).  Returns (ptr, idx, val) of the concatenation.  One host read of the
+    gathered (rows, nnz) pairs sizes the transfer; ``allgather_csr_rows_bounded`` avoids it.
     """
     world = dist.get_world_size(group)
     dev = ptr.device
     n_local = ptr.numel() - 1
-    nnz_local = int(ptr[-1].item()) if n_local >= 0 else 0
-    sizes = torch.tensor([n_local, nnz_local], dtype=torch.int64, device=dev)
+    sizes = torch.stack([torch.tensor(n_local, dtype=torch.int64, device=dev), ptr[-1].to(torch.int64)])
     all_sizes = [torch.empty_like(sizes) for _ in range(world)]
     _all_gather_list(all_sizes, sizes, group=group)
     all_sizes = torch.stack(all_sizes).cpu()
+    nnz_local = int(all_sizes[dist.get_rank(group), 1])
     n_max, nnz_max = int(all_sizes[:, 0].max()), int(all_sizes[:, 1].max())
 
     counts = torch.zeros(n_max, dtype=torch.int64, device=dev)
@@ -115,8 +238,12 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
     return full_ptr, torch.cat(parts_i), torch.cat(parts_v)
 
 
-def gather_phi(engine, local, count_ws=None, group=None, band_width=None):
+def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards=None):
     """All ranks' Phi rows (CSR, float32) from this rank's compacted rows ``local``.
+
+    shards: every rank's (begin, end) source range.  When given and ``local`` came from a
+    sync-free compaction (``nnz_bound`` = rows x row capacity), the gather reads nothing back to
+    the host (``allgather_csr_rows_bounded``); otherwise one host read sizes it exactly.
 
     count_ws: this rank's transpose workspace in which ``walk_phi`` counted the banded transpose's
     buckets for its own rows (global band ids, bands of ``band_width``).  The per-rank counts are
@@ -131,6 +258,14 @@ def gather_phi(engine, local, count_ws=None, group=None, band_width=None):
         all_reduce(count_ws[:4 * nbk].view(torch.int32), group=group)
     if dist.get_world_size(group) == 1:
         return local
+    bound = getattr(local, "nnz_bound", None)
+    if shards is not None and bound is not None and local.n_rows > 0:
+        cap = -(-bound // max(local.n_rows, 1))
+        rows = [e - b for b, e in shards]
+        ptr, idx, val32 = allgather_csr_rows_bounded(local.ptr, local.idx, local.val32, rows, max(rows) * cap, group)
+        out = DeviceCSR(n, n, ptr, idx, None, val32, None)
+        out.nnz_bound = int(idx.numel())
+        return out
     ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32, group)
     return DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))
 
@@ -149,7 +284,7 @@ def allreduce_buckets(t: torch.Tensor, bucket_bytes: int = 1 << 30, group=None) 
 
 
 def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length, *, seed=42, group=None,
-                          rng=None, mode: str = "rows"):
+                          rng=None, mode: str = "rows", shards: Optional[Sequence[Tuple[int, int]]] = None):
     """This rank's row block of K = Phi Phi^T (float32, on the engine's device), and its row range.
 
     ``mode="cols"``: this rank's column block K[:, b:e] (n x (e - b)) instead -- the same numbers
@@ -157,7 +292,9 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
     world <= 4 the square K[b:e, b:e] is computed on and above its diagonal and mirrored), from a
     transpose of the rank's own Phi rows only (no replicated transpose, no bucket-count all-reduce).
     ``mode="allreduce"``: every rank returns the whole K (row range (0, n)), assembled as the
-    all-reduced sum of per-rank partial Grams over inner-dimension slices."""
+    all-reduced sum of per-rank partial Grams over inner-dimension slices.
+    ``shards``: every rank's source range (default: equal node counts; ``balanced_shards`` for
+    equal estimated work)."""
     if mode not in ("rows", "cols", "allreduce"):
         raise ValueError(f"mode must be 'rows', 'cols' or 'allreduce', got {mode!r}")
     from . import _lib as C
@@ -172,12 +309,13 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
 
     G = engine.laplacian(A)
     n = G.n_rows
-    b, e = shard_range(n, rank, world)
+    shards = list(shards) if shards is not None else [shard_range(n, r, world) for r in range(world)]
+    b, e = shards[rank]
     bw = ROWS_BAND_WIDTH  # (row-mode Grams: the wide bands)
     if mode == "cols":
         from .engine import cols_band_width
         return _cols_block(engine, G, f, walks_per_node, p_halt, max_walk_length, seed, rng, b, e, group,
-                           cols_band_width(e - b)), (b, e)
+                           cols_band_width(e - b), shards), (b, e)
     tws = None
     if walks_per_node * max_walk_length <= 4096:
         # fused walk -> Phi, counting this rank's buckets of the banded transpose on the way
@@ -187,10 +325,9 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
     else:
         rows = engine.features(engine.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed,
                                            src_begin=b, src_end=e), f)
-    local = engine.compact(rows, want64=False, want32=True)
-    phi = gather_phi(engine, local, tws, group, band_width=bw) if world > 1 else \
-        DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
-    tr = engine.transpose_banded(phi, bw, counted_ws=tws)
+    local = engine.compact(rows, want64=False, want32=True, sync_free=True)
+    phi = gather_phi(engine, local, tws, group, band_width=bw, shards=shards) if world > 1 else local
+    tr = engine.transpose_banded(phi, bw, counted_ws=tws, nnz_bound=phi.nnz_bound)
     if mode == "allreduce":
         K = engine.gram_sparse_kslice(phi, tr, b, e)
         allreduce_buckets(K, group=group)
@@ -198,7 +335,7 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
     return engine.gram_sparse(phi, tr, b, e), (b, e)
 
 
-def _cols_block(engine, G, f, m, p_halt, L, seed, rng, b, e, group, wl):
+def _cols_block(engine, G, f, m, p_halt, L, seed, rng, b, e, group, wl, shards=None):
     """K[:, b:e] from this rank's rows: walks -> Phi rows (counting the local transpose's buckets)
     -> Phi all-gather -> transpose of the local rows -> column-block Gram with all rows' shifts."""
     from .engine import DeviceCSR
@@ -211,11 +348,10 @@ def _cols_block(engine, G, f, m, p_halt, L, seed, rng, b, e, group, wl):
                                count_origin=b, want64=False)
     else:
         rows = engine.features(engine.walk(G, m, p_halt, L, rng=rng, seed=seed, src_begin=b, src_end=e), f)
-    local = engine.compact(rows, want64=False, want32=True)
+    local = engine.compact(rows, want64=False, want32=True, sync_free=True)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    phi = gather_phi(engine, local, None, group) if world > 1 else \
-        DeviceCSR(n, n, local.ptr, local.idx, None, local.val32, local.nnz)
-    tr = engine.transpose_banded(local, wl, counted_ws=tws)
+    phi = gather_phi(engine, local, None, group, shards=shards) if world > 1 else local
+    tr = engine.transpose_banded(local, wl, counted_ws=tws, nnz_bound=local.nnz_bound)
     # the square K[b:e, b:e] on and above its diagonal, then mirrored, when it is a large enough share
     # of the block to pay for the mirror (N <= 4)
     sym = 4 * (e - b) >= n

@@ -18,7 +18,7 @@ a *front* and a *K assembly*:
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Callable, Optional, Tuple
+from typing import Callable, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -39,6 +39,7 @@ class StepPlan:
     world: int = 1
     rank: int = 0
     src: Tuple[int, int] = (0, 0)  # this rank's walk sources [b, e) (= its K rows / columns)
+    shards: Optional[List[Tuple[int, int]]] = None  # every rank's [b, e) (N > 1)
     k_rows: int = 0                # 0: all of the rank's rows; R: only [b, b + R)
     mode: str = "sym"              # "sym" (one GPU, whole K), "rows", "cols", "allreduce"
     band_width: int = DEFAULT_BAND_WIDTH
@@ -71,18 +72,24 @@ class StepPlan:
 
 def plan_step(n: int, m: int, L: int, p_halt: float, f, *, seed: int = 42, world: int = 1, rank: int = 0,
               mode: str = "cols", k_rows: int = 0, band_width: int = 0, no_sym: bool = False,
-              src: Optional[Tuple[int, int]] = None, group=None) -> StepPlan:
+              shards: Optional[List[Tuple[int, int]]] = None, group=None) -> StepPlan:
     """The bench's mode rules: one GPU whole K -> symmetric mode; N > 1 or K-row workloads -> column
-    blocks (``mode="cols"``), row blocks (``"rows"``) or the all-reduce option (``"allreduce"``)."""
+    blocks (``mode="cols"``), row blocks (``"rows"``) or the all-reduce option (``"allreduce"``).
+    shards: every rank's source range (default: equal node counts; dist.balanced_shards for equal
+    estimated work)."""
     from .dist import shard_range
 
     if mode not in ("cols", "rows", "allreduce"):
         raise ValueError(f"mode must be 'cols', 'rows' or 'allreduce', got {mode!r}")
     if k_rows and mode == "allreduce":
         raise ValueError("k_rows applies to the row / column modes only")
-    b, e = src if src is not None else shard_range(n, rank, world)
+    shards = list(shards) if shards is not None else [shard_range(n, r, world) for r in range(world)]
+    if len(shards) != world or shards[0][0] != 0 or shards[-1][1] != n or \
+            any(shards[r][1] != shards[r + 1][0] for r in range(world - 1)):
+        raise ValueError("shards must be contiguous ranges covering [0, n) in rank order")
+    b, e = shards[rank]
     pl = StepPlan(n, int(m), int(L), float(p_halt), np.asarray(f, np.float64), int(seed), world, rank, (b, e),
-                  int(k_rows), mode, group=group)
+                  shards, int(k_rows), mode, group=group)
     if mode == "cols" and (world > 1 or k_rows):
         pl.mode = "cols"
         pl.band_width = band_width or cols_band_width(pl.block_rows)
@@ -128,7 +135,7 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                                          count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
                                          want64=False),
                             want64=False, want32=True, sync_free=True)
-        phi = gather_phi(eng, local, group=pl.group) if pl.world > 1 else local
+        phi = gather_phi(eng, local, group=pl.group, shards=pl.shards) if pl.world > 1 else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
                                             local.val32)
         tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap)
@@ -137,7 +144,8 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
     local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
                                      count_ws=tws, band_width=pl.band_width, want64=False),
                         want64=False, want32=True, sync_free=True)
-    phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width) if pl.world > 1 else local
+    phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards) \
+        if pl.world > 1 else local
     # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
     tr = eng.transpose_banded(phi, pl.band_width, counted_ws=tws, nnz_bound=n * pl.rows_cap)
     return Front(phi, tr, local)

@@ -190,6 +190,12 @@ int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const 
                          const int32_t *in_idx, const double *in_val, const float *in_val32, int32_t *out_idx,
                          double *out_val, float *out_val32, grf_stream_t stream);
 
+/* dst[dst_off[r] + i] = src[r * stride + i] for i < seg_len[r], r < n_seg (4-byte elements; lengths
+ * and offsets are device arrays): the compaction of a fixed-stride all-gather of n_seg ranks'
+ * CSR segments (the multi-GPU Phi gather, grf_amd/dist.py) without reading any size back. */
+int32_t grf_concat_segments(int32_t n_seg, int64_t stride, const void *src, const int64_t *seg_len,
+                            const int64_t *dst_off, void *dst, grf_stream_t stream);
+
 /* Banded transpose for the Gram kernel: entries (j, k, v) of Phi (CSR rows j)
  * bucketed by (band = j / band_width, k):  bucket id b = band * n_cols + k.
  * A bucket is a run of 12-byte record PAIRS {u16 8 (j0 - band start), u16 8 (j1 - band start)

@@ -175,6 +175,60 @@ def _spawn(target, world):
     return sorted(res)
 
 
+def _bounded_gather_worker(rank, world, port, q):
+    """allgather_csr_rows_bounded: uneven shards, each rank's entries in a buffer padded to its
+    rows x the row capacity (as a sync-free compaction leaves them), garbage past its nnz."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import scipy.sparse as sp
+        from grf_amd.dist import allgather_csr_rows_bounded, shard_bounds
+        n, cap = 61, 20
+        full = sp.random(n, n, density=0.15, random_state=9, format="csr")
+        full.sort_indices()
+        shards = shard_bounds(np.arange(1, n + 1) ** 2, world)  # uneven on purpose
+        b, e = shards[rank]
+        part = full[b:e]
+        ptr = torch.from_numpy(part.indptr.astype(np.int64))
+        idx = torch.full(((e - b) * cap,), -7, dtype=torch.int32)
+        val = torch.full(((e - b) * cap,), 9e9, dtype=torch.float32)
+        idx[:part.nnz] = torch.from_numpy(part.indices.astype(np.int32))
+        val[:part.nnz] = torch.from_numpy(part.data.astype(np.float32))
+        rows = [s1 - s0 for s0, s1 in shards]
+        gptr, gidx, gval = allgather_csr_rows_bounded(ptr, idx, val, rows, max(rows) * cap)
+        nnz = int(gptr[-1])
+        ok = (np.array_equal(gptr.numpy(), full.indptr) and np.array_equal(gidx[:nnz].numpy(), full.indices)
+              and np.array_equal(gval[:nnz].numpy(), full.data.astype(np.float32)))
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allgather_csr_rows_bounded_gloo(world):
+    assert _spawn(_bounded_gather_worker, world) == [(r, True) for r in range(world)]
+
+
+def test_shard_bounds_equal_weight_ranges():
+    from grf_amd.dist import shard_bounds
+    rng = np.random.default_rng(0)
+    for n, w in [(100, 2), (1000, 3), (5000, 8), (7, 8), (3, 3)]:
+        wt = rng.pareto(1.5, n) + 0.1
+        sh = shard_bounds(wt, w)
+        assert len(sh) == w and sh[0][0] == 0 and sh[-1][1] == n
+        assert all(sh[i][1] == sh[i + 1][0] for i in range(w - 1))
+        if n >= w:
+            assert all(e > b for b, e in sh)
+            sums = np.array([wt[b:e].sum() for b, e in sh])
+            # every prefix boundary is within one row's weight of its target
+            for r in range(w - 1):
+                target = wt.sum() * (r + 1) / w
+                assert abs(wt[:sh[r][1]].sum() - target) <= wt.max() + 1e-9 or n < 4 * w
+            assert sums.max() <= wt.sum() / w + 2 * wt.max()
+    assert shard_bounds(np.ones(10), 1) == [(0, 10)]
+    assert shard_bounds(np.ones(12), 4) == [(0, 3), (3, 6), (6, 9), (9, 12)]
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_allreduce_buckets_gloo(world):
     assert _spawn(_allreduce_worker, world) == [(r, True) for r in range(world)]
