@@ -1,36 +1,51 @@
 """General-modulator fast GRF kernel: mirror of gpflow_kernels/general_kernel_fast_grf.py:9-77.
 
-The (N, N, L) step tensor is sampled once at construction on the GPU (Laplacian
-with safe degrees as in preprocessing/laplacian_np.py, or the raw adjacency with
-the ablation rule); ``K`` computes Phi = F f and K = Phi Phi^T on the GPU (fp32
-MFMA) and gathers rows / columns by the integer node indices in X.
+The (N, N, L) step tensor is sampled once at construction on the GPU (Laplacian with safe
+degrees as in preprocessing/laplacian_np.py, or the raw adjacency with the ablation rule) and
+stays on the device.  ``modulator_vector`` is a learnable parameter (``torch.nn.Parameter``, fp64:
+the reference's ``gpflow.Parameter(tf.float64)``, :31-41); K = (F f)(F f)^T runs on the MFMA Gram
+(fp32, ``grf_gram_dense``) once per modulator value and is cached, so ``K`` / ``K_diag`` only gather
+from it.  ``K_torch`` returns the same block as a torch tensor that is differentiable w.r.t. the
+modulator (``grf_amd.features.DenseGramFunction``).  GPflow / TensorFlow are not installed here:
+the class is a ``torch.nn.Module`` and ``K`` / ``K_diag`` return numpy arrays.
 """
 from typing import Optional
 
 import numpy as np
+import torch
 
 from grf_amd import _lib as C
 from grf_amd import api
+from grf_amd.engine import get_engine
+from grf_amd.features import DenseGramFunction, DenseSteps
 
 
-class GraphGeneralFastGRFKernel:
+def _indices(X) -> torch.Tensor:
+    if torch.is_tensor(X):
+        return X.reshape(-1).long()
+    return torch.from_numpy(np.asarray(X).reshape(-1).astype(np.int64))
+
+
+class GraphGeneralFastGRFKernel(torch.nn.Module):
     def __init__(self, adjacency_matrix, walks_per_node: int = 50, p_halt: float = 0.1, max_walk_length: int = 10,
                  random_walk_seed: int = 42, modulator_vector: np.ndarray = None, step_matrices: np.ndarray = None,
                  use_tqdm: bool = False, ablation: bool = False, *, rng: Optional[str] = None, device=None, **kwargs):
+        super().__init__()
         adjacency_matrix = np.asarray(adjacency_matrix, dtype=np.float64)
         assert adjacency_matrix.shape[0] == adjacency_matrix.shape[1], "Adjacency matrix must be square."
         self.adjacency_matrix = adjacency_matrix
         self.walks_per_node = walks_per_node
         self.p_halt = p_halt
         self.max_walk_length = max_walk_length
-        self.device = device
+        self.device = get_engine(device).device
         if modulator_vector is None:
             np.random.seed(42)
-            self.modulator_vector = np.random.randn(max_walk_length)
+            init = np.random.randn(max_walk_length)
         else:
             if len(modulator_vector) != max_walk_length:
                 raise ValueError("The length of the modulator vector must be equal to the max_walk_length.")
-            self.modulator_vector = np.asarray(modulator_vector, dtype=np.float64)
+            init = np.asarray(modulator_vector, dtype=np.float64)
+        self.modulator_vector = torch.nn.Parameter(torch.tensor(init, dtype=torch.float64, device=self.device))
         if step_matrices is not None:
             self.feature_matrices = np.asarray(step_matrices, dtype=np.float64)
         elif ablation:
@@ -41,20 +56,33 @@ class GraphGeneralFastGRFKernel:
             self.laplacian = api.dense_laplacian(adjacency_matrix, C.LAP_NUMPY_SAFE, device)
             self.feature_matrices = api.dense_step_tensor(self.laplacian, walks_per_node, p_halt, max_walk_length,
                                                           seed=random_walk_seed, rng=rng, device=device)
+        self._steps = DenseSteps(self.feature_matrices, get_engine(device))
 
     def grf_kernel(self, modulator_vector) -> np.ndarray:
-        return api.gram_from_features(self.feature_matrices, modulator_vector, self.device)
+        """The whole K (reference :74-77), fp64 numpy."""
+        f = torch.as_tensor(np.asarray(modulator_vector, dtype=np.float64) if not torch.is_tensor(modulator_vector)
+                            else modulator_vector.detach())
+        return self._steps.gram(f).cpu().numpy().astype(np.float64)
+
+    def K_torch(self, X1, X2=None) -> torch.Tensor:
+        """K[X1, X2] on the device, differentiable w.r.t. ``modulator_vector``."""
+        Kf = DenseGramFunction.apply(self.modulator_vector, self._steps)
+        i1 = _indices(X1).to(Kf.device)
+        i2 = i1 if X2 is None else _indices(X2).to(Kf.device)
+        return Kf[i1][:, i2]
 
     def K(self, X1, X2=None) -> np.ndarray:
-        X2 = X1 if X2 is None else X2
-        Kf = self.grf_kernel(self.modulator_vector)
-        i1 = np.asarray(X1).reshape(-1).astype(np.int64)
-        i2 = np.asarray(X2).reshape(-1).astype(np.int64)
-        return Kf[np.ix_(i1, i2)]
+        """K[X1, X2] (reference :61-67): a gather from the cached K of the current modulator."""
+        Kf = self._steps.gram(self.modulator_vector)
+        i1 = _indices(X1).to(Kf.device)
+        i2 = i1 if X2 is None else _indices(X2).to(Kf.device)
+        return Kf[i1][:, i2].cpu().numpy().astype(np.float64)
 
     def K_diag(self, X) -> np.ndarray:
-        Kf = self.grf_kernel(self.modulator_vector)
-        return np.diag(Kf)[np.asarray(X).reshape(-1).astype(np.int64)]
+        """diag(K)[X] (reference :69-72), from the same cached K."""
+        Kf = self._steps.gram(self.modulator_vector)
+        i = _indices(X).to(Kf.device)
+        return Kf.diagonal()[i].cpu().numpy().astype(np.float64)
 
     def __call__(self, X1, X2=None, full_cov=True):
         return self.K(X1, X2) if full_cov else self.K_diag(X1)

@@ -22,6 +22,7 @@ from __future__ import annotations
 import ctypes
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import _lib as C
@@ -205,3 +206,57 @@ def feature_matrix(f: torch.Tensor, steps: StepMatrices) -> torch.Tensor:
     phi = steps.phi(f)
     return torch.sparse_csr_tensor(phi.ptr, phi.idx[:phi.nnz].long(), phi.val32[:phi.nnz], steps.shape,
                                    dtype=torch.float32)
+
+
+# ----------------------------------------------------------------- dense step tensors (GPflow surface)
+class DenseSteps:
+    """A dense (N, N, L) step tensor F resident on the device once (the GPflow wrappers'
+    ``feature_matrices_tf``, gpflow_kernels/general_kernel_fast_grf.py:44-59), with K = (F f)(F f)^T
+    on the MFMA Gram (grf_gram_dense) cached per modulator value."""
+
+    def __init__(self, F, engine: Optional[GRFEngine] = None):
+        self.engine = engine or get_engine()
+        Ft = F if torch.is_tensor(F) else torch.from_numpy(np.ascontiguousarray(F, dtype=np.float64))
+        self.F = Ft.to(self.engine.device, torch.float64).contiguous()
+        if self.F.dim() != 3 or self.F.shape[0] != self.F.shape[1]:
+            raise ValueError("step tensor must be (N, N, L)")
+        self.n, self.L = self.F.shape[0], self.F.shape[2]
+        self._key = None
+        self._K = None
+
+    def phi(self, f: torch.Tensor) -> torch.Tensor:
+        """Phi = F f (N x N, fp64 on the device): ``tf.linalg.matmul(F, f[:, None])`` (:76)."""
+        return self.F @ f.detach().to(self.engine.device, torch.float64).reshape(-1)
+
+    def gram(self, f: torch.Tensor) -> torch.Tensor:
+        """K = Phi Phi^T (fp32, N x N) on the MFMA Gram, cached for the last modulator value."""
+        key = f.detach().to("cpu", torch.float64).reshape(-1).numpy().tobytes()
+        if key != self._key:
+            n = self.n
+            lda = max(16, -(-n // 16) * 16)
+            A = torch.zeros((n, lda), dtype=torch.float32, device=self.engine.device)
+            A[:, :n] = self.phi(f).to(torch.float32)
+            self._K = self.engine.gram_dense(A, n)
+            self._key = key
+        return self._K
+
+
+class DenseGramFunction(torch.autograd.Function):
+    """K = (F f)(F f)^T with dK/df_l = F_l Phi^T + Phi F_l^T: the backward contracts the upstream
+    G with it, dL/df_l = <F_l, (G + G^T) Phi> (one plain N x N GEMM + a reduction over F)."""
+
+    @staticmethod
+    def forward(ctx, f: torch.Tensor, steps: DenseSteps):
+        ctx.steps = steps
+        ctx.save_for_backward(f)
+        return steps.gram(f).to(f.dtype)
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor):
+        (f,) = ctx.saved_tensors
+        steps = ctx.steps
+        phi = steps.phi(f)
+        G = g.to(steps.engine.device, torch.float64)
+        H = (G + G.t()) @ phi
+        grad = torch.einsum("ijl,ij->l", steps.F, H)
+        return grad.to(f.dtype), None

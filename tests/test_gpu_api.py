@@ -157,7 +157,11 @@ def test_graph_preprocessor_and_sparse_kernels(golden, tmp_path):
     assert SparseDiffusionKernel(4, ops).cuda()().shape == (40, 40)
 
 
-def test_gpflow_style_kernels():
+def test_gpflow_style_kernels(golden):
+    """GPflow-surface wrappers (gpflow_kernels/general_kernel_fast_grf.py:9-77,
+    diffusion_kernel_fast_grf.py:8-60; GPflow/TF absent: parity unpinned by the reference, pinned to
+    the numpy restatement K = (F f)(F f)^T on the reference's own golden step tensors)."""
+    import torch
     from efficient_graph_gp.gpflow_kernels import GraphDiffusionFastGRFKernel, GraphGeneralFastGRFKernel
     r = np.random.default_rng(8)
     U = np.triu((r.random((30, 30)) < 0.2).astype(float), 1)
@@ -168,15 +172,45 @@ def test_gpflow_style_kernels():
         GraphGeneralFastGRFKernel(A, max_walk_length=4, modulator_vector=[1.0, 2.0])
     k = GraphGeneralFastGRFKernel(A, walks_per_node=16, p_halt=0.2, max_walk_length=4)
     np.random.seed(42)
-    np.testing.assert_array_equal(k.modulator_vector, np.random.randn(4))
-    Phi = k.feature_matrices @ k.modulator_vector
+    np.testing.assert_array_equal(k.modulator_vector.detach().cpu().numpy(), np.random.randn(4))
+    assert isinstance(k.modulator_vector, torch.nn.Parameter) and k.modulator_vector.requires_grad
+    Phi = k.feature_matrices @ k.modulator_vector.detach().cpu().numpy()
     X = np.array([[0], [4], [29]])
     np.testing.assert_allclose(k.K(X), (Phi @ Phi.T)[np.ix_([0, 4, 29], [0, 4, 29])], rtol=3e-5, atol=1e-6)
+    Kc = k._steps._K
     np.testing.assert_allclose(k.K_diag(X), np.diag(Phi @ Phi.T)[[0, 4, 29]], rtol=3e-5, atol=1e-6)
+    assert k._steps._K is Kc  # K / K_diag gather from one cached Gram per modulator value
+    # the golden step tensor of the reference's own dense sampler (step_matrices=)
+    F = golden("small_graphs")["er40_dpar_n3"]
+    f = np.array([0.9, -0.4, 0.2, 0.05])
+    kg = GraphGeneralFastGRFKernel(golden("small_graphs")["er40_A"], max_walk_length=4, modulator_vector=f,
+                                   step_matrices=F)
+    P = F @ f
+    np.testing.assert_allclose(kg.K(np.arange(40)), P @ P.T, rtol=3e-5, atol=1e-6 * np.abs(P @ P.T).max())
+    # learnable: d sum(W * K[X, Y]) / d f against the analytic gradient
+    W = r.standard_normal((3, 5))
+    Y = np.array([1, 2, 3, 4, 39])
+    (kg.K_torch(X, Y) * torch.tensor(W, device=kg.device)).sum().backward()
+    xs = [0, 4, 29]
+    gref = [np.sum(W * (F[xs, :, l] @ P[Y].T + P[xs] @ F[Y, :, l].T)) for l in range(4)]
+    np.testing.assert_allclose(kg.modulator_vector.grad.cpu().numpy(), gref, rtol=1e-4, atol=1e-6)
     kd = GraphDiffusionFastGRFKernel(A, walks_per_node=16, p_halt=0.2, max_walk_length=4, beta=2.0, sigma_f=1.5)
+    np.testing.assert_allclose([float(kd.beta), float(kd.sigma_f)], [2.0, 1.5], rtol=1e-12)
     fm = np.array([(-2.0) ** l / (2 ** l * np.prod(np.arange(1, l + 1))) for l in range(4)])
     Phi = kd.feature_matrices @ fm
     np.testing.assert_allclose(kd.K(np.arange(30)), 2.25 * Phi @ Phi.T, rtol=3e-5, atol=1e-6)
+    # gradients w.r.t. beta and sigma_f: central differences of the numpy restatement
+    (kd.K_torch(np.arange(30)) * torch.tensor(np.eye(30), device=kd.device)).sum().backward()
+
+    def trace(beta, sig):
+        f_ = np.array([(-beta) ** l / (2 ** l * np.prod(np.arange(1, l + 1))) for l in range(4)])
+        P_ = kd.feature_matrices @ f_
+        return sig ** 2 * np.trace(P_ @ P_.T)
+
+    h = 1e-6
+    gb = (trace(2.0 + h, 1.5) - trace(2.0 - h, 1.5)) / (2 * h) * (1 - np.exp(-2.0))  # d softplus = sigmoid
+    gs = (trace(2.0, 1.5 + h) - trace(2.0, 1.5 - h)) / (2 * h) * (1 - np.exp(-1.5))
+    np.testing.assert_allclose([kd.raw_beta.grad.item(), kd.raw_sigma_f.grad.item()], [gb, gs], rtol=1e-4)
 
 
 def test_philox_mode_through_api_matches_oracle():
