@@ -36,7 +36,7 @@ from grf_amd.graphs import er_graph_exact_edges, powerlaw_graph, snap_graph  # n
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh -> tools/pmc_summary.py), committed
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
 DEFAULT_WORKLOAD = (100_000, 1_000_000, 128, 8, 0.1)
 
 
@@ -476,7 +476,10 @@ def main():
         # one GPU, whole K: the next front beside the mirror; N > 1 row / column blocks: the next
         # front's collectives beside this step's Gram (the compute of a front beside a Gram gains
         # ~1 %: single-GPU row modes stay serial)
-        args.overlap = pl.mode == "sym" or (world > 1 and pl.mode != "allreduce")
+        # K-row-block workloads (C5) on one GPU: the next front beside this step's column-block Gram
+        # (22.3 vs 22.9 ms per step, profiles/r02_c5_overlap.txt)
+        args.overlap = pl.mode == "sym" or (world > 1 and pl.mode != "allreduce") or \
+            (pl.mode == "cols" and bool(args.k_rows))
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     walk_ev = []  # (start, end) events around walk_phi in the serial-latency steps (kernel alone)
     last = [None]

@@ -851,13 +851,24 @@ int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, fl
     if (n == 0) return GRF_OK;
     // tile: 128 when the upper triangle of 128-tiles gives >= 2 workgroups per CU (n >= ~4.5 k), else 64
     const int64_t nt128 = cdiv<int64_t>(n, 128);
-    const bool big = nt128 * (nt128 + 1) / 2 >= 512;
-    const int bk = (!big && lda % 32 == 0) ? 32 : 16;  // (zero padding up to lda covers the last k-tile)
+    static const int env_tile = [] {  // GRF_DENSE_TILE=64/128, GRF_DENSE_BK=16/32: A/B knobs
+        const char *e = getenv("GRF_DENSE_TILE");
+        return e ? atoi(e) : 0;
+    }();
+    static const int env_bk = [] {
+        const char *e = getenv("GRF_DENSE_BK");
+        return e ? atoi(e) : 0;
+    }();
+    const bool big = env_tile ? env_tile == 128 : nt128 * (nt128 + 1) / 2 >= 512;
+    int bk = (!big && lda % 32 == 0) ? 32 : 16;  // (zero padding up to lda covers the last k-tile)
+    if (env_bk == 32 && lda % 32 == 0) bk = 32;
+    if (env_bk == 16) bk = 16;
     const int64_t kpad = cdiv<int64_t>(k_dim, bk) * bk;
     GRF_REQUIRE(kpad <= lda, GRF_EINVAL, "grf_gram_dense: lda must cover k_dim rounded up to %d", bk);
     const int64_t nt = cdiv<int64_t>(n, big ? 128 : 64), tiles = nt * (nt + 1) / 2;
     GRF_REQUIRE_GRID(tiles, 256, "gram_dense_kernel");
-    if (big) gram_dense_kernel<128, 16><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
+    if (big && bk == 32) gram_dense_kernel<128, 32><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
+    else if (big) gram_dense_kernel<128, 16><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
     else if (bk == 32) gram_dense_kernel<64, 32><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
     else gram_dense_kernel<64, 16><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
     GRF_CHECK_LAUNCH("gram_dense_kernel");

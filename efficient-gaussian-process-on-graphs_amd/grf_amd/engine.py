@@ -551,7 +551,7 @@ class GRFEngine:
         return K[:, :n]
 
     def densify(self, phi: DeviceCSR) -> torch.Tensor:
-        lda = max(16, -(-phi.n_cols // 16) * 16)
+        lda = max(64, -(-phi.n_cols // 64) * 64)  # (zero-padded k: every k-tile width of the MFMA Gram divides it)
         out = torch.empty((phi.n_rows, lda), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_densify(phi.n_rows, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(out), lda, self.stream),
                 "grf_densify")

@@ -1,7 +1,9 @@
 """Summarise tools/pmc_passes.sh output: per-kernel mean counters + HBM traffic per launch.
 
 traffic (bytes) = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024: FETCH_SIZE / WRITE_SIZE are in KiB and
-on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read (MI355X_MICROARCH.md, HBM).
+on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read (MI355X_MICROARCH.md, HBM); the same
+factor 2 holds for 12-B buffer_load_dwordx3 streams and line-aligned 12-B gathers (tools/fetch_calib.hip,
+profiles/r02_fetch_calib.json).
 usage: python tools/pmc_summary.py <outdir> [kernel-substring] > summary.json
 """
 import csv
