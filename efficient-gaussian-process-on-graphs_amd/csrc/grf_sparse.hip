@@ -485,6 +485,139 @@ __global__ __launch_bounds__(256) void tr_place_kernel(int64_t n_rows, int64_t n
     }
 }
 
+// ---- the plan-free (self-counting) staged transpose: no bucket counts from the walk, no scan over
+// every bucket.  After tr_bin, (1) tr_region_units bounds each (band, region)'s record units from
+// its entry count E and bucket count nb (units of its buckets <= 6 (E + nb) / unit + nb + 1, packed:
+// (E + nb + 1) / 2), (2) one scan over the regions gives every region a slab of that size, and
+// (3) tr_place_self counts the region's buckets in LDS, lays them out inside the slab (the unused
+// tail of a slab is never read: the Gram reads through the descriptors), writes their descriptors
+// and places the records as tr_place does.
+__global__ __launch_bounds__(256) void tr_region_units_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, int32_t cr,
+                                                              int32_t nreg, int64_t n_regions, const int32_t *tab,
+                                                              int32_t unit, int64_t *region_units) {
+    const int64_t rg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (rg >= n_regions) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t band = rg / nreg, g = rg - band * nreg;
+    const int64_t w0 = band * bw / kBinRows, w1 = cdiv<int64_t>(min<int64_t>(n_rows, (band + 1) * bw), kBinRows);
+    int64_t E = 0;
+    for (int64_t w = w0 + lane; w < w1; w += 64) {
+        const int32_t *trow = tab + w * (nreg + 1);
+        E += trow[g + 1] - trow[g];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) E += __shfl_xor(E, off, 64);
+    const int64_t nb = min<int64_t>(n_cols, (g + 1) * (int64_t)cr) - g * (int64_t)cr;
+    if (lane == 0)
+        region_units[rg] = E == 0 ? 0 : unit == kPairBytes ? (E + nb + 1) / 2 : (6 * (E + nb)) / unit + nb + 1;
+}
+
+struct RegionBaseOut {  // region_base[i] = first unit of region i; the total also as desc[nbk] (lo, hi)
+    int64_t *base;
+    uint2 *desc_total;
+    __device__ void operator()(int64_t i, int64_t prefix) const { base[i] = prefix; }
+    __device__ void total(int64_t n, int64_t t) const {
+        base[n] = t;
+        *desc_total = make_uint2((uint32_t)t, (uint32_t)(t >> 32));
+    }
+};
+
+__global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, int32_t cr,
+                                                            int32_t nreg, const int64_t *ptr,
+                                                            const int64_t *region_base, const uint2 *staging,
+                                                            const int32_t *tab, int32_t *gcur, uint2 *desc,
+                                                            unsigned char *t_rec, int32_t unit) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char tps_smem[];
+    const int tid = threadIdx.x;
+    const int64_t rg = blockIdx.x, band = rg / nreg, g = rg - band * nreg;
+    const int64_t c0 = g * cr, c1 = min<int64_t>(n_cols, c0 + cr);
+    const int nbk_r = (int)(c1 - c0);
+    const int64_t b0 = band * n_cols + c0;
+    const int64_t U0 = region_base[rg];
+    uint32_t *lcur = reinterpret_cast<uint32_t *>(tps_smem);   // [cr] counts, then cursors
+    uint32_t *lline = lcur + cr;                                // [cr] first byte of each bucket in the image
+    int32_t *scratch = reinterpret_cast<int32_t *>(lline + cr); // [8]
+    unsigned char *image = reinterpret_cast<unsigned char *>(scratch + 8);
+    const int64_t w0 = band * bw / kBinRows, w1 = cdiv<int64_t>(min<int64_t>(n_rows, (band + 1) * bw), kBinRows);
+    for (int i = tid; i < nbk_r; i += 256) lcur[i] = 0u;
+    __syncthreads();
+    // pass 1: the region's bucket counts
+    for (int64_t w = w0 + tid; w < w1; w += 256) {
+        const int32_t *trow = tab + w * (nreg + 1);
+        const int32_t o0 = trow[g], o1 = trow[g + 1];
+        const uint2 *run = staging + ptr[w * kBinRows];
+        for (int32_t o = o0; o < o1; ++o) atomicAdd(&lcur[run[o].x >> 16], 1u);
+    }
+    __syncthreads();
+    // bucket units -> local offsets (thread t owns buckets [t * per, (t + 1) * per)), descriptors
+    const int per = (nbk_r + 255) / 256;
+    int32_t sum = 0;
+    for (int q = 0; q < per; ++q) {
+        const int i = tid * per + q;
+        if (i < nbk_r) sum += (int32_t)((kPairBytes * ((lcur[i] + 1) >> 1) + unit - 1) / unit);
+    }
+    int32_t total;
+    int32_t run_u = block_exclusive_scan<int32_t>(sum, scratch, &total);
+    for (int q = 0; q < per; ++q) {
+        const int i = tid * per + q;
+        if (i < nbk_r) {
+            const uint32_t c = lcur[i];
+            desc[b0 + i] = make_uint2((uint32_t)(U0 + run_u), (c + 1) >> 1);
+            lline[i] = (uint32_t)run_u * (uint32_t)unit;
+            run_u += (int32_t)((kPairBytes * ((c + 1) >> 1) + unit - 1) / unit);
+        }
+    }
+    __syncthreads();
+    const int64_t img = (int64_t)total * unit;
+    if (img == 0) return;
+    const bool lds = (img + 15) / 16 * 16 <= kPlaceCap;
+    if (lds) {
+        for (int64_t i = tid; i < (img + 15) / 16; i += 256) reinterpret_cast<uint4 *>(image)[i] = make_uint4(0u, 0u, 0u, 0u);
+    } else {  // oversized region: global cursors of its own buckets, odd buckets padded below
+        for (int i = tid; i < nbk_r; i += 256) {
+            gcur[b0 + i] = 0;
+            const uint32_t c = lcur[i];
+            if (c & 1) {
+                unsigned char *pair = t_rec + (U0 * unit + lline[i]) + (int64_t)kPairBytes * (c >> 1);
+                reinterpret_cast<uint16_t *>(pair)[1] = 0;
+                reinterpret_cast<float *>(pair + 4)[1] = 0.f;
+            }
+        }
+    }
+    for (int i = tid; i < nbk_r; i += 256) lcur[i] = 0u;
+    __syncthreads();
+    // pass 2: place the records (the region's entries come from L2: pass 1 just read them)
+    for (int64_t w = w0 + tid; w < w1; w += 256) {
+        const int32_t *trow = tab + w * (nreg + 1);
+        const int32_t o0 = trow[g], o1 = trow[g + 1];
+        const uint2 *run = staging + ptr[w * kBinRows];
+        for (int32_t o = o0; o < o1; ++o) {
+            const uint2 x = run[o];
+            const uint32_t kk = x.x >> 16;
+            if (lds) {
+                const uint32_t s = atomicAdd(&lcur[kk], 1u);
+                unsigned char *pair = image + lline[kk] + kPairBytes * (s >> 1);
+                reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(x.x & 0xffffu);
+                reinterpret_cast<uint32_t *>(pair + 4)[s & 1] = x.y;
+            } else {
+                const int32_t s = atomicAdd(&gcur[b0 + kk], 1);
+                unsigned char *pair = t_rec + (U0 * unit + lline[kk]) + (int64_t)kPairBytes * (s >> 1);
+                reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(x.x & 0xffffu);
+                reinterpret_cast<uint32_t *>(pair + 4)[s & 1] = x.y;
+            }
+        }
+    }
+    if (!lds) return;
+    __syncthreads();
+    if ((U0 * unit) % 16 == 0 && img % 16 == 0) {
+        uint4 *dst = reinterpret_cast<uint4 *>(t_rec + U0 * unit);
+        for (int64_t i = tid; i < img / 16; i += 256) dst[i] = reinterpret_cast<const uint4 *>(image)[i];
+    } else {
+        uint32_t *dst = reinterpret_cast<uint32_t *>(t_rec + U0 * unit);
+        for (int64_t i = tid; i < img / 4; i += 256) dst[i] = reinterpret_cast<const uint32_t *>(image)[i];
+    }
+}
+
 // Region width: at most 4096 regions per band, and every placing workgroup reads one table
 // entry per binning workgroup of its band, n_rows * n_cols / (16 cr) scattered reads in all --
 // kept <= 32 M (C4: cr = 128, 4.9 M; C5, N = 1M: cr = 2048 instead of 256, where 244 M reads
@@ -692,6 +825,97 @@ int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t
     tr_place_kernel<<<(unsigned)n_regions, 256, lds2, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr, desc, ent_off,
                                                             ent, tab, cnt, (unsigned char *)t_rec, rec_unit);
     GRF_CHECK_LAUNCH("tr_place_kernel");
+    return GRF_OK;
+}
+
+size_t grf_transpose_self_workspace_bytes(int64_t n_rows, int64_t n_cols, int64_t band_width) {
+    if (n_cols <= 0 || band_width <= 0) return 16;
+    const int64_t nb = cdiv<int64_t>(std::max<int64_t>(n_rows, 1), band_width);
+    const int64_t n_regions = nb * cdiv<int64_t>(n_cols, tr_region_cols(n_rows, n_cols));
+    return tr_align((size_t)std::max<int64_t>(n_rows, 1) * 4) + 2 * tr_align((size_t)(n_regions + 1) * 8) +
+           tr_align((size_t)nb * n_cols * 4) + scan_ws_bytes(n_regions);
+}
+
+int64_t grf_transpose_self_units_bound(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                       int64_t nnz) {
+    if (n_cols <= 0 || band_width <= 0) return 1;
+    const int64_t nb = cdiv<int64_t>(std::max<int64_t>(n_rows, 1), band_width), nbk = nb * n_cols;
+    const int64_t n_regions = nb * cdiv<int64_t>(n_cols, tr_region_cols(n_rows, n_cols));
+    // the sum of tr_region_units over the regions, for any split of nnz entries
+    if (rec_unit == GRF_REC_PACKED) return (nnz + nbk) / 2 + n_regions + 1;
+    return (6 * (nnz + nbk)) / rec_unit + nbk + 2 * n_regions + 1;
+}
+
+int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                  const int64_t *ptr, const int32_t *idx, const float *val, uint32_t *t_desc,
+                                  void *t_rec, int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
+                                  void *workspace, size_t workspace_bytes, int64_t nnz, void *staging,
+                                  size_t staging_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && val && t_desc &&
+                    t_rec && t_maxabs && t_rowshift && t_rec_bytes >= 0 && staging && workspace,
+                GRF_EINVAL, "grf_transpose_banded_self: bad arguments");
+    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED, GRF_EINVAL,
+                "grf_transpose_banded_self: rec_unit must be GRF_REC_LINE or GRF_REC_PACKED");
+    GRF_REQUIRE(band_width % 64 == 0, GRF_EUNSUPPORTED, "grf_transpose_banded_self: band_width must be a multiple of 64");
+    GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_transpose_banded_self: t_rec must be 128-byte aligned");
+    const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
+    const int32_t cr = tr_region_cols(n_rows, n_cols);
+    GRF_REQUIRE(cr <= 65536, GRF_EUNSUPPORTED, "grf_transpose_banded_self: too many columns");
+    const int32_t nreg = (int32_t)cdiv<int64_t>(n_cols, cr);
+    GRF_REQUIRE(workspace_bytes >= grf_transpose_self_workspace_bytes(n_rows, n_cols, band_width), GRF_EINVAL,
+                "grf_transpose_banded_self: workspace too small");
+    GRF_REQUIRE(nnz >= 0 && staging_bytes >= grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz), GRF_EINVAL,
+                "grf_transpose_banded_self: staging too small");
+    GRF_REQUIRE(t_rec_bytes >= grf_transpose_self_units_bound(n_rows, n_cols, band_width, rec_unit, nnz) * rec_unit,
+                GRF_ECAPACITY, "grf_transpose_banded_self: t_rec too small for the region slabs");
+    hipStream_t st = S(stream);
+    const int64_t n_regions = nb * nreg;
+    char *w = (char *)workspace;
+    float *row_max = (float *)w;
+    w += tr_align((size_t)std::max<int64_t>(n_rows, 1) * 4);
+    int64_t *region_units = (int64_t *)w;
+    w += tr_align((size_t)(n_regions + 1) * 8);
+    int64_t *region_base = (int64_t *)w;
+    w += tr_align((size_t)(n_regions + 1) * 8);
+    int32_t *gcur = (int32_t *)w;  // (fallback cursors of oversized regions; zeroed by their owners)
+    w += tr_align((size_t)nbk * 4);
+    void *scan_ws = w;
+    char *sg = (char *)staging;
+    uint2 *ent = (uint2 *)sg;
+    double *row_sum = (double *)(sg + tr_align((size_t)nnz * 8));
+    int32_t *tab = (int32_t *)(sg + tr_align((size_t)nnz * 8) + tr_align((size_t)std::max<int64_t>(n_rows, 1) * 8));
+    const int64_t nwg = cdiv<int64_t>(n_rows, kBinRows);
+    float *wg_max = (float *)((char *)tab + tr_align((size_t)std::max<int64_t>(nwg, 1) * (nreg + 1) * 4));
+    uint2 *desc = reinterpret_cast<uint2 *>(t_desc);
+    GRF_CHECK_HIP(hipMemsetAsync(t_maxabs, 0, sizeof(float), st));
+    if (n_rows == 0) {
+        GRF_CHECK_HIP(hipMemsetAsync(t_desc, 0, (size_t)(nbk + 1) * 8, st));
+        return GRF_OK;
+    }
+    const size_t lds1 = (size_t)kBinCap * 8 + (size_t)nreg * 4 + (kBinRows + 1 + 8) * 4;
+    GRF_REQUIRE_GRID(nwg, 256, "tr_bin_kernel");
+    tr_bin_kernel<<<(unsigned)nwg, 256, lds1, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr, idx, val, ent, tab,
+                                                    wg_max, row_max, row_sum);
+    GRF_CHECK_LAUNCH("tr_bin_kernel");
+    tr_maxabs_kernel<<<1, 1024, 0, st>>>(nwg, wg_max, t_maxabs);
+    GRF_CHECK_LAUNCH("tr_maxabs_kernel");
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 256), 256, "tr_rowshift_kernel");
+    tr_rowshift_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 256), 256, 0, st>>>(n_rows, row_max, row_sum, t_maxabs,
+                                                                            t_rowshift);
+    GRF_CHECK_LAUNCH("tr_rowshift_kernel");
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_regions, 4), 256, "tr_region_units_kernel");
+    tr_region_units_kernel<<<(unsigned)cdiv<int64_t>(n_regions, 4), 256, 0, st>>>(n_rows, n_cols, band_width, cr, nreg,
+                                                                                 n_regions, tab, rec_unit, region_units);
+    GRF_CHECK_LAUNCH("tr_region_units_kernel");
+    int32_t rc = scan_exclusive<int64_t>(n_regions, region_units, ScanIdentity{},
+                                         RegionBaseOut{region_base, desc + nbk}, (int64_t *)scan_ws, st);
+    if (rc != GRF_OK) return rc;
+    const size_t lds2 = (size_t)8 * cr + 32 + kPlaceCap;
+    GRF_REQUIRE_GRID(n_regions, 256, "tr_place_self_kernel");
+    tr_place_self_kernel<<<(unsigned)n_regions, 256, lds2, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr,
+                                                                 region_base, ent, tab, gcur, desc,
+                                                                 (unsigned char *)t_rec, rec_unit);
+    GRF_CHECK_LAUNCH("tr_place_self_kernel");
     return GRF_OK;
 }
 

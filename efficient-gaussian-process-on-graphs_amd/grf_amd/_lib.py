@@ -85,6 +85,10 @@ SIGNATURES = {
     "grf_transpose_banded_fill_staged": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                                 _sz, _i64, _vp, _sz, _vp]),
     "grf_transpose_staging_bytes": (_sz, [_i64, _i64, _i64, _i64]),
+    "grf_transpose_banded_self": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz,
+                                         _i64, _vp, _sz, _vp]),
+    "grf_transpose_self_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "grf_transpose_self_units_bound": (_i64, [_i64, _i64, _i64, _i32, _i64]),
     "grf_csr_transpose_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "grf_csr_transpose": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_spmm_csr": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),

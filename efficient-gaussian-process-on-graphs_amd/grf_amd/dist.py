@@ -298,7 +298,7 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
     if mode not in ("rows", "cols", "allreduce"):
         raise ValueError(f"mode must be 'rows', 'cols' or 'allreduce', got {mode!r}")
     from . import _lib as C
-    from .engine import DeviceCSR
+    from .engine import SELF_COUNT_TRANSPOSE, DeviceCSR  # noqa: F401
 
     rng = C.RNG_PHILOX if rng is None else rng
     if rng != C.RNG_PHILOX:
@@ -318,10 +318,11 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
                            cols_band_width(e - b), shards), (b, e)
     tws = None
     if walks_per_node * max_walk_length <= 4096:
-        # fused walk -> Phi, counting this rank's buckets of the banded transpose on the way
-        tws = engine.transpose_workspace(n, n, bw)
+        # fused walk -> Phi (counting this rank's buckets of the banded transpose on the way when the
+        # transpose does not count them itself, GRF_TRANSPOSE_SELF=0)
+        tws = None if SELF_COUNT_TRANSPOSE else engine.transpose_workspace(n, n, bw)
         rows = engine.walk_phi(G, walks_per_node, p_halt, max_walk_length, f, seed=seed, src_begin=b, src_end=e,
-                               count_ws=tws, band_width=bw, want64=False)
+                               count_ws=tws, band_width=bw if tws is not None else 0, want64=False)
     else:
         rows = engine.features(engine.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed,
                                            src_begin=b, src_end=e), f)
@@ -336,16 +337,16 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
 
 
 def _cols_block(engine, G, f, m, p_halt, L, seed, rng, b, e, group, wl, shards=None):
-    """K[:, b:e] from this rank's rows: walks -> Phi rows (counting the local transpose's buckets)
-    -> Phi all-gather -> transpose of the local rows -> column-block Gram with all rows' shifts."""
-    from .engine import DeviceCSR
+    """K[:, b:e] from this rank's rows: walks -> Phi rows -> Phi all-gather -> transpose of the local
+    rows -> column-block Gram with all rows' shifts."""
+    from .engine import SELF_COUNT_TRANSPOSE
 
     n = G.n_rows
     tws = None
     if m * L <= 4096:
-        tws = engine.transpose_workspace(e - b, n, wl)
-        rows = engine.walk_phi(G, m, p_halt, L, f, seed=seed, src_begin=b, src_end=e, count_ws=tws, band_width=wl,
-                               count_origin=b, want64=False)
+        tws = None if SELF_COUNT_TRANSPOSE else engine.transpose_workspace(e - b, n, wl)
+        rows = engine.walk_phi(G, m, p_halt, L, f, seed=seed, src_begin=b, src_end=e, count_ws=tws,
+                               band_width=wl if tws is not None else 0, count_origin=b, want64=False)
     else:
         rows = engine.features(engine.walk(G, m, p_halt, L, rng=rng, seed=seed, src_begin=b, src_end=e), f)
     local = engine.compact(rows, want64=False, want32=True, sync_free=True)

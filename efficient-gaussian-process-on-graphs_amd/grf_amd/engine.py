@@ -31,6 +31,9 @@ DEFAULT_BAND_WIDTH = 4096  # transpose band = one Gram tile (32 KB int64 LDS acc
 # tiles (C4: 25.9 vs 27.5 ms); the symmetric whole-K mode stays at 4096 (21.9 vs 22.7 ms: with 13
 # bands the diagonal band tiles' lower halves cost more than the wider buckets save)
 ROWS_BAND_WIDTH = 8192
+# the banded transpose counts its buckets itself (grf_transpose_banded_self: no count atomics in the
+# walk, no scan over every bucket); GRF_TRANSPOSE_SELF=0 restores the walk-counted plan (A/B)
+SELF_COUNT_TRANSPOSE = os.environ.get("GRF_TRANSPOSE_SELF", "1") != "0"
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -384,9 +387,12 @@ class GRFEngine:
 
     def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH,
                          counted_ws: Optional[torch.Tensor] = None, staged: Optional[bool] = None,
-                         nnz_bound: Optional[int] = None, rec_unit: Optional[int] = None) -> Banded:
+                         nnz_bound: Optional[int] = None, rec_unit: Optional[int] = None,
+                         self_count: Optional[bool] = None) -> Banded:
         """Banded transpose of Phi.  counted_ws: workspace whose bucket counts ``walk_phi`` filled.
         staged: two-pass binned fill (default when band_width % 64 == 0) or the atomic fill.
+        self_count: the staged fill without a plan (grf_transpose_banded_self; default unless
+        counted_ws is given or GRF_TRANSPOSE_SELF=0): buckets in per-region slabs.
         nnz_bound: an upper bound of nnz(Phi) (e.g. ``compact(..., sync_free=True)``'s): the record
         buffer is then sized from bounds and no size is read back (no host synchronisation)."""
         n_rows, n_cols = phi.n_rows, phi.n_cols
@@ -395,6 +401,14 @@ class GRFEngine:
         t_desc = self._empty(2 * (nbk + 1), torch.int32)
         t_max = self._empty(1, torch.float32)
         t_shift = self._empty(max(n_rows, 1), torch.int32)
+        if staged is None:
+            staged = band_width % 64 == 0 and os.environ.get("GRF_TRANSPOSE_STAGED", "1") != "0"
+        if self_count is None:
+            self_count = SELF_COUNT_TRANSPOSE and counted_ws is None and staged
+        if self_count:
+            if counted_ws is not None or not staged:
+                raise ValueError("self_count: the staged transpose counts its own buckets (no counted_ws)")
+            return self._transpose_self(phi, band_width, nnz_bound, rec_unit, t_desc, t_max, t_shift)
         ws = counted_ws if counted_ws is not None else self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
         if rec_unit is None:
             rec_unit = choose_rec_unit(phi.nnz if phi._nnz is not None or nnz_bound is None else nnz_bound,
@@ -424,8 +438,6 @@ class GRFEngine:
                 raise NotImplementedError("a transpose band holds >= 2 GiB of records; use a smaller band_width")
         # (+128 B: a masked Gram lane reads the first pair of an empty last band)
         t_rec = self._empty(max(units, 1) * u + 128, torch.uint8)  # torch allocations are 256-B aligned
-        if staged is None:
-            staged = band_width % 64 == 0 and os.environ.get("GRF_TRANSPOSE_STAGED", "1") != "0"
         if staged:
             nnz = nnz_bound if nnz_bound is not None else phi.nnz
             sg = self._ws(self.lib.grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz))
@@ -438,6 +450,32 @@ class GRFEngine:
                                                        _p(phi.val32), _p(t_desc), _p(t_rec), t_rec.numel(),
                                                        _p(t_max), _p(t_shift), _p(ws), ws.numel(), self.stream),
                     "grf_transpose_banded_fill")
+        return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols, u)
+
+    def _transpose_self(self, phi: DeviceCSR, band_width: int, nnz_bound: Optional[int], rec_unit: Optional[int],
+                        t_desc, t_max, t_shift) -> Banded:
+        """The plan-free staged transpose (grf_transpose_banded_self): buckets counted by the placing
+        workgroups themselves, no counts from the walk and no scan over every bucket."""
+        n_rows, n_cols = phi.n_rows, phi.n_cols
+        nnz = int(nnz_bound) if nnz_bound is not None else phi.nnz
+        if rec_unit is None:
+            rec_unit = choose_rec_unit(phi.nnz if phi._nnz is not None or nnz_bound is None else nnz_bound,
+                                       n_rows, n_cols, band_width)
+        u = int(rec_unit)
+        # the Gram addresses a band's records with 32-bit byte offsets: bound one band's slabs
+        row_cap = min(n_cols, max(1, -(-nnz // max(n_rows, 1))))
+        band_units = self.lib.grf_transpose_self_units_bound(min(band_width, n_rows), n_cols, band_width, u,
+                                                             min(nnz, band_width * row_cap))
+        if n_rows and band_units * u >= 2 ** 31:
+            raise NotImplementedError("a transpose band holds >= 2 GiB of records; use a smaller band_width")
+        units = self.lib.grf_transpose_self_units_bound(n_rows, n_cols, band_width, u, nnz)
+        t_rec = self._empty(max(units, 1) * u + 128, torch.uint8)
+        ws = self._ws(self.lib.grf_transpose_self_workspace_bytes(n_rows, n_cols, band_width))
+        sg = self._ws(self.lib.grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz))
+        C.check(self.lib.grf_transpose_banded_self(n_rows, n_cols, band_width, u, _p(phi.ptr), _p(phi.idx),
+                                                   _p(phi.val32), _p(t_desc), _p(t_rec), t_rec.numel(), _p(t_max),
+                                                   _p(t_shift), _p(ws), ws.numel(), nnz, _p(sg), sg.numel(),
+                                                   self.stream), "grf_transpose_banded_self")
         return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols, u)
 
     # ----------------------------------------------------------------- Gram

@@ -23,7 +23,7 @@ from typing import Callable, List, Optional, Tuple
 import numpy as np
 import torch
 
-from .engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, DeviceCSR, GRFEngine, cols_band_width
+from .engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, SELF_COUNT_TRANSPOSE, DeviceCSR, GRFEngine, cols_band_width
 
 
 @dataclass
@@ -129,7 +129,7 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
     if pl.mode == "cols":
         # the transpose of the block's rows alone (no count all-reduce, a 1/N-size transpose); the
         # walk counts its buckets when the block is all of the rank's rows
-        fused = pl.kr_end == e
+        fused = pl.kr_end == e and not SELF_COUNT_TRANSPOSE
         tws = eng.transpose_workspace(pl.block_rows, n, pl.band_width) if fused else None
         local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
                                          count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
@@ -140,9 +140,11 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                                             local.val32)
         tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap)
         return Front(phi, tr, local, eng.phi_row_shifts(phi))
-    tws = eng.transpose_workspace(n, n, pl.band_width)
+    # (the transpose counts its own buckets unless GRF_TRANSPOSE_SELF=0: then the walk counts them)
+    tws = None if SELF_COUNT_TRANSPOSE else eng.transpose_workspace(n, n, pl.band_width)
     local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
-                                     count_ws=tws, band_width=pl.band_width, want64=False),
+                                     count_ws=tws, band_width=pl.band_width if tws is not None else 0,
+                                     want64=False),
                         want64=False, want32=True, sync_free=True)
     phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards) \
         if pl.world > 1 else local

@@ -229,6 +229,23 @@ int32_t grf_transpose_banded_fill_staged(int64_t n_rows, int64_t n_cols, int64_t
                                          void *staging, size_t staging_bytes, grf_stream_t stream);
 size_t grf_transpose_staging_bytes(int64_t n_rows, int64_t n_cols, int64_t band_width, int64_t nnz);
 
+/* The staged transpose without a plan: no bucket counts from the walk (grf_walk_phi's t_count may
+ * then be NULL) and no scan over every bucket.  Each (band, region) of the binning gets a slab of
+ * record units bounded by its entry and bucket counts (one scan over the regions); its placing
+ * workgroup counts its buckets in LDS, lays them out in the slab and writes their descriptors
+ * t_desc (same meaning as the plan's: {first unit, pairs}; t_desc[nbk] = the slabs' total, an
+ * upper bound of the units written).  Buckets stay in (band, column) order; unused slab tails are
+ * never read.  t_rec >= grf_transpose_self_units_bound(...) * rec_unit bytes; workspace >=
+ * grf_transpose_self_workspace_bytes; staging as for grf_transpose_banded_fill_staged. */
+int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                  const int64_t *ptr, const int32_t *idx, const float *val, uint32_t *t_desc,
+                                  void *t_rec, int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
+                                  void *workspace, size_t workspace_bytes, int64_t nnz, void *staging,
+                                  size_t staging_bytes, grf_stream_t stream);
+size_t grf_transpose_self_workspace_bytes(int64_t n_rows, int64_t n_cols, int64_t band_width);
+int64_t grf_transpose_self_units_bound(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
+                                       int64_t nnz);
+
 /* ---------------------------------------------------------------------- Gram
  * Replaces `Phi @ Phi.T` of fast_grf_kernel_general.py:55 (sparse) and :39 (dense).
  * Sparse path: K[r, :] for rows r in [row_begin, row_end) of Phi (compact CSR,

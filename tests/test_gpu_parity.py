@@ -304,28 +304,36 @@ def test_transpose_staged_fill_matches_atomic_fill(eng, n, deg, m, L, bw, unit):
     G = eng.laplacian(A)
     phi = eng.compact(eng.walk_phi(G, m, 0.15, L, [1.0, -0.5, 0.25, -0.125, 0.1, -0.05, 0.02, -0.01][:L], seed=4))
     ta = eng.transpose_banded(phi, bw, staged=False, rec_unit=unit)
-    ts = eng.transpose_banded(phi, bw, staged=True, rec_unit=unit)
-    assert ta.rec_unit == ts.rec_unit == unit
+    ts = eng.transpose_banded(phi, bw, staged=True, rec_unit=unit, self_count=False)
+    tself = eng.transpose_banded(phi, bw, rec_unit=unit, self_count=True) if bw % 64 == 0 else ts
+    assert ta.rec_unit == ts.rec_unit == tself.rec_unit == unit
     assert np.array_equal(ta.t_desc.cpu().numpy(), ts.t_desc.cpu().numpy())
-    assert np.array_equal(ta.t_rowshift.cpu().numpy(), ts.t_rowshift.cpu().numpy())
-    assert ta.t_maxabs.item() == ts.t_maxabs.item()
+    for t in (ts, tself):
+        assert np.array_equal(ta.t_rowshift.cpu().numpy(), t.t_rowshift.cpu().numpy())
+        assert ta.t_maxabs.item() == t.t_maxabs.item()
     desc = ta.t_desc.cpu().numpy().view(np.uint32).reshape(-1, 2)
-    ra, rs = ta.t_rec.cpu().numpy(), ts.t_rec.cpu().numpy()
+    dself = tself.t_desc.cpu().numpy().view(np.uint32).reshape(-1, 2)
     nb = -(-n // bw)
+    assert np.array_equal(desc[:nb * n, 1], dself[:nb * n, 1])  # same pairs per bucket
+    # the slabs keep (band, column) order: first units never decrease within a band
+    assert all(np.all(np.diff(dself[J * n:(J + 1) * n, 0].astype(np.int64)) >= 0) for J in range(nb))
+    ra, rs, rself = ta.t_rec.cpu().numpy(), ts.t_rec.cpu().numpy(), tself.t_rec.cpu().numpy()
     rng = np.random.default_rng(0)
     for b in rng.choice(nb * n, size=min(nb * n, 3000), replace=False):
-        line, pairs = int(desc[b, 0]), int(desc[b, 1])
+        pairs = int(desc[b, 1])
         if pairs == 0:
             continue
-        def recs(buf):
+
+        def recs(buf, line):
             seg = buf[line * unit: line * unit + 12 * pairs].reshape(pairs, 12)
             cols = seg[:, :4].copy().view(np.uint16).reshape(pairs, 2)
             vals = seg[:, 4:].copy().view(np.float32).reshape(pairs, 2)
             return sorted(zip(cols.ravel().tolist(), vals.ravel().tolist()))
-        assert recs(ra) == recs(rs), b
+        assert recs(ra, int(desc[b, 0])) == recs(rs, int(desc[b, 0])) == recs(rself, int(dself[b, 0])), b
     Ka = eng.gram_sparse(phi, ta, 0, 300).cpu().numpy()
     Ks = eng.gram_sparse(phi, ts, 0, 300).cpu().numpy()
     assert np.array_equal(Ka, Ks)
+    assert np.array_equal(eng.gram_sparse(phi, tself, 0, 300).cpu().numpy(), Ka)
     other = eng.transpose_banded(phi, bw, rec_unit=140 - unit)  # the other layout
     assert np.array_equal(eng.gram_sparse(phi, other, 0, 300).cpu().numpy(), Ka)
     if bw % 64 == 0:
@@ -628,12 +636,15 @@ def test_transpose_wide_regions(eng, unit):
     G = eng.laplacian(A)
     phi = eng.compact(eng.walk_phi(G, 4, 0.2, 3, [1.0, -0.5, 0.25], seed=8))
     ta = eng.transpose_banded(phi, 8192, staged=False, rec_unit=unit)
-    ts = eng.transpose_banded(phi, 8192, staged=True, rec_unit=unit)
+    ts = eng.transpose_banded(phi, 8192, staged=True, rec_unit=unit, self_count=False)
+    tself = eng.transpose_banded(phi, 8192, rec_unit=unit, self_count=True)
     assert np.array_equal(ta.t_desc.cpu().numpy(), ts.t_desc.cpu().numpy())
     assert np.array_equal(ta.t_rowshift.cpu().numpy(), ts.t_rowshift.cpu().numpy())
+    assert np.array_equal(ta.t_rowshift.cpu().numpy(), tself.t_rowshift.cpu().numpy())
     for r0 in (0, n - 200):
         Ka = eng.gram_sparse(phi, ta, r0, r0 + 200).cpu().numpy()
         assert np.array_equal(Ka, eng.gram_sparse(phi, ts, r0, r0 + 200).cpu().numpy())
+        assert np.array_equal(Ka, eng.gram_sparse(phi, tself, r0, r0 + 200).cpu().numpy())
     ok, fro = gram_close(eng.gram_sparse(phi, ts, 0, 50).cpu().numpy(), phi.to_scipy(), (0, 50))
     assert ok, fro
 
