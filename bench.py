@@ -608,7 +608,7 @@ def main():
     phi_last = last[0].phi
     nnz_phi = phi_last.nnz
     local_nnz = last[0].local.nnz
-    # algorithmic bytes of the K assembly (gram_sparse_kernel [+ gram_mirror_kernel]): write this
+    # algorithmic bytes of the K assembly (gram_sparse_kernel [+ the mirror kernel]): write this
     # rank's K rows once, read its Phi rows (col int32 + val fp32) and every Phi^T entry once
     rows = kr_end - b
     alg_bytes = 4.0 * rows * n + 8.0 * local_nnz * rows / max(e - b, 1) + 8.0 * nnz_phi
@@ -616,7 +616,8 @@ def main():
         alg_bytes = 4.0 * n * n + 8.0 * nnz_phi + 8.0 * nnz_phi * rows / n
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
     sym = pl.mode == "sym"
-    kernels = ["grf::gram_sparse_kernel", "grf::gram_mirror_kernel"] if sym else ["grf::gram_sparse_kernel"]
+    mirror = "grf::gram_mirror_kernel" if os.environ.get("GRF_MIRROR_PADDED", "0") == "1" else "grf::gram_mirror_swz_kernel"
+    kernels = ["grf::gram_sparse_kernel", mirror] if sym else ["grf::gram_sparse_kernel"]
     headline = (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and args.graph == "er" and world == 1 and sym
     traffic = pmc_traffic(kernels) if headline else None
     # the walk kernel (phi_fused_kernel): per walk, E[moves] = (1-p)(1-(1-p)^(L-1))/p recorded moves,
@@ -675,7 +676,7 @@ def main():
                      "algorithmic_bytes": alg_bytes},
         "roofline_walk": {"bound": "hbm", "achieved": walk_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": walk_achieved / HBM_PEAK_GBS, "traffic": walk_traffic,
-                          "kernel": "phi_fused_kernel (fused Philox walks -> Phi rows + bucket counts)",
+                          "kernel": "phi_fused_kernel (fused Philox walks -> Phi rows)",
                           "kernel_ms": walk_ms, "algorithmic_bytes": walk_alg,
                           "algorithmic_note": f"16 B per expected recorded move ({moves:.4g}) + 8 B per Phi "
                                               f"entry written ({local_nnz}); timed alone in the serial steps "
