@@ -428,6 +428,10 @@ def main():
     ap.add_argument("--no-overlap", dest="overlap", action="store_false", help="serial steps")
     ap.add_argument("--front-at", type=float, default=1.0,
                     help="pipelined: the next front starts after this fraction of the Gram tiles (1 = at the mirror)")
+    ap.add_argument("--fused", dest="fused", action="store_true", default=None,
+                    help="one GPU, whole K: the symmetric completion inside the Gram tiles (the last tile of every "
+                         "32-row group writes the group's block transposed; no mirror pass)")
+    ap.add_argument("--no-fused", dest="fused", action="store_false", help="Gram tiles + a separate mirror pass")
     ap.add_argument("--balance", choices=["nodes", "phi"], default="nodes",
                     help="N > 1 source shards: equal node ranges (default), or ranges of equal estimated step work "
                          "from the per-source Phi row counts of one setup walk (dist.balanced_shards)")
@@ -469,7 +473,7 @@ def main():
         from grf_amd.dist import balanced_shards
         shards = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance)  # (setup, untimed)
     pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
-                     band_width=args.band_width, no_sym=args.no_sym, shards=shards)
+                     band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused)
     b, e, kr_end = pl.b, pl.e, pl.kr_end
     K = P.alloc_k(eng, pl)  # resident output block, reused
     if args.overlap is None:
@@ -617,7 +621,7 @@ def main():
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
     sym = pl.mode == "sym"
     mirror = "grf::gram_mirror_kernel" if os.environ.get("GRF_MIRROR_PADDED", "0") == "1" else "grf::gram_mirror_swz_kernel"
-    kernels = ["grf::gram_sparse_kernel", mirror] if sym else ["grf::gram_sparse_kernel"]
+    kernels = ["grf::gram_sparse_kernel", mirror] if sym and not pl.fused else ["grf::gram_sparse_kernel"]
     headline = (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and args.graph == "er" and world == 1 and sym
     traffic = pmc_traffic(kernels) if headline else None
     # the walk kernel (phi_fused_kernel): per walk, E[moves] = (1-p)(1-(1-p)^(L-1))/p recorded moves,
@@ -665,7 +669,8 @@ def main():
                                   (f"source-sharded x{world}, Phi all-gather, K column blocks K[:, R_r] from each "
                                    f"rank's own-rows transpose") if cols else
                                   f"source-sharded x{world}, Phi all-gather, K row blocks"
-                                  + (" (one GPU: symmetric tiles + mirror)" if sym else "")},
+                                  + ((" (one GPU: symmetric tiles completing K by their last arrivers)" if pl.fused
+                                      else " (one GPU: symmetric tiles + mirror)") if sym else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": (f"rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of the same kernels on this workload, "

@@ -4,18 +4,18 @@
 //   efficient_graph_gp_sparse/graph_kernels_sparse/fast_grf_kernel_general.py:55 (scipy SpGEMM)
 //   efficient_graph_gp/graph_kernels/fast_grf_kernel_general.py:39 (dense BLAS)
 //
-// Sparse path (Gustavson, output-stationary in LDS): one wave owns the
-// tile K[row, j0 : j0 + W] (W = one band of the banded transpose, ~1k columns =
-// 8 KB of int64 accumulator; bands pinned to XCDs so each band's Phi^T slice
-// stays in that XCD's L2).  For every nonzero
-// Phi[row, k] it streams bucket (band, k) -- the entries Phi[j, k] with j in the
-// band, stored as (uint16 j - j0, float32 value) -- and adds the exact product
-// Phi[row,k]*Phi[j,k] in int64 fixed point with ds_add_u64.  Measured on gfx950
-// (tools/lds_bench.hip): ds_add_f32 serialises per lane (~170 cycles per wave
-// instruction per CU) while ds_add_u64 takes ~12, so fixed point is both ~14x
-// cheaper and exactly order-independent (bit-reproducible K).  The finished tile is
-// written once, coalesced, with non-temporal stores (K is write-once; keep L2
-// for the transpose).  Bound: HBM write of K (4 N^2 bytes).
+// Sparse path (Gustavson, output-stationary in LDS): a workgroup of 4 waves owns the tile
+// K[row, j0 : j0 + W] (W = one band of the banded transpose, 4096 columns = 32 KB of int64
+// accumulators; 4 tiles per CU).  For every nonzero Phi[row, k] it streams bucket (band, k) --
+// the entries Phi[j, k] with j in the band, stored as 12-byte record pairs (2 x u16 j - j0,
+// 2 x f32 value) -- and adds the exact product Phi[row,k]*Phi[j,k] in int64 fixed point with
+// ds_add_u64.  Measured on gfx950 (tools/lds_bench.hip): ds_add_f32 serialises per lane (~170
+// cycles per wave instruction per CU) while ds_add_u64 takes ~12, so fixed point is both ~14x
+// cheaper and exactly order-independent (bit-reproducible K).  Tiles are dispatched band-major,
+// so the tiles in flight share one band's records in L2 / the Infinity Cache.  The finished tile
+// is written once, coalesced, with non-temporal stores.  Bound: the gathers of bucket records
+// that miss L2; the symmetric mode computes the tiles on and above the diagonal
+// band and a mirror pass copies the upper triangle down.
 //
 // Dense path: LDS-tiled fp32 MFMA (v_mfma_f32_32x32x2f32, exact f32 FMA chain),
 // 128x128 tile per 256-thread workgroup, 2x2 waves of 64x64.
@@ -225,6 +225,126 @@ struct GramTiles {
     }
 };
 
+// ---------------------------------------------------------------- fused symmetric completion
+// grf_gram_sparse_sym_fused: the Gram tiles of the symmetric mode complete K themselves (no
+// separate mirror pass re-reading the upper triangle from HBM).  The tiles of one band are
+// dispatched row after row, so the 64 tiles of a row group g = rows [gs, gs + 64) of band J run
+// together; each writes its row K[i, band J] write-through (sc1: visible to every XCD without a
+// release fence), drains its stores and takes a ticket on the group's counter.  The last arriver
+// (no waiting: the others exit) acquires and transposes the group's 64 x W block into
+// K[band J, gs : gs + 64] (256-byte row segments, 4 x 4 register transposes).  Ownership keeps
+// every lower entry single-writer and ordered after the upper one: on the diagonal band a tile
+// writes only the columns >= its group's first row (the columns before it are lower entries that
+// the earlier groups' last arrivers write), and inside the group's own diagonal block the last
+// arriver overwrites the entries below the diagonal after all rows have been stored.  K is
+// bit-identical to grf_gram_sparse_sym's.
+// MEASURED SLOWER (profiles/r02_fused_ab.txt): 100-150 ms per K against 22.6 for tiles + mirror.
+// The tiles with their tickets cost +0.8 ms and the block loads +5 ms, but the last arrivers'
+// transposed stores (20 GB, one workgroup per 1 MB block) add ~100 ms: one workgroup cannot keep
+// enough stores in flight, where the mirror pass spreads the same bytes over every CU.  Kept as a
+// tested option (bench --fused); the default stays tiles + mirror.
+#ifndef GRF_FUSE_GROUP
+#define GRF_FUSE_GROUP 64
+#endif
+constexpr int kFuseGroup = GRF_FUSE_GROUP;         // rows per ticket group (64: 256-byte K row segments)
+
+// The completion's edge cases, element by element: K[j, i] = K[i, j] for the K rows j = j0 + col
+// .. j0 + col + 3 (< j0 + wlen) and i = gs + 4q .. gs + 4q + 3 (< ge, < j: the group's diagonal block)
+__device__ __attribute__((noinline)) void gram_fused_edge(float *__restrict__ K, int64_t ldk, int64_t gs, int64_t ge,
+                                                          int64_t j0, int64_t col, int64_t wlen, int q) {
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = gs + 4 * q + u;
+        if (i >= ge) break;
+        for (int e = 0; e < 4 && col + e < wlen; ++e) {
+            const int64_t j = j0 + col + e;
+            if (i < j) K[j * ldk + i] = __hip_atomic_load(K + i * ldk + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <int kWaves>
+__device__ __forceinline__ void gram_fused_completion(const GramTiles &tl, int64_t J, int64_t r, int64_t j0,
+                                                      int64_t wlen, int sh, unsigned long long *acc,
+                                                      float *__restrict__ K, int64_t ldk,
+                                                      int32_t *__restrict__ tickets, int32_t exp) {
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int kT = 64 * kWaves;
+    const int tid = threadIdx.x;
+    const int64_t gs = r & ~(int64_t)(kFuseGroup - 1);
+    const int64_t rows_J = tl.count(J);
+    const int64_t ge = (gs + kFuseGroup) < rows_J ? gs + kFuseGroup : rows_J;
+    const int gn = (int)(ge - gs);
+    const bool diag = gs >= j0;  // the group's rows lie in this band (j0 <= gs < j0 + W)
+    // 1. the tile's row, write-through: on the diagonal band from the group's first row on
+    const u64x2 *acc2 = reinterpret_cast<const u64x2 *>(acc);
+    float *krow = K + r * ldk + j0;
+    const int64_t c_lo = diag ? gs - j0 : 0;  // a multiple of 32
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(krow, (short)0, 0x7fffffff, 0x00020000);
+    const int64_t n4 = wlen / 4;
+    for (int64_t i = c_lo / 4 + tid; i < n4; i += kT) {
+        const u64x2 a = acc2[2 * i], b = acc2[2 * i + 1];
+        u32x4 o;
+        o[0] = __float_as_uint(fx_to_float(a[0], sh));
+        o[1] = __float_as_uint(fx_to_float(a[1], sh));
+        o[2] = __float_as_uint(fx_to_float(b[0], sh));
+        o[3] = __float_as_uint(fx_to_float(b[1], sh));
+        __builtin_amdgcn_raw_buffer_store_b128(o, rs, (int)(i * 16), 0, 16);  // aux 16: sc1 (write-through)
+    }
+    for (int64_t i = n4 * 4 + tid; i < wlen; i += kT)
+        __hip_atomic_store(krow + i, fx_to_float(acc[i], sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // 2. every storing wave drains, then one ticket for the workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *flag = reinterpret_cast<int *>(acc);
+    if (tid == 0) {
+        const int64_t ngroups = (tl.rows + kFuseGroup - 1) / kFuseGroup;
+        const int old = __hip_atomic_fetch_add(tickets + J * ngroups + (r / kFuseGroup), 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = old == gn - 1;
+    }
+    __syncthreads();
+    if (!flag[0] || (exp & 2)) return;  // (uniform) not the last of the group
+    if (tid < 64) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // 3. the last arriver: K[j, gs : ge] = K[gs : ge, j] for the band's columns j (j > i), in 4 x 4
+    // register transposes (no LDS, no barrier: the tiles still running on this CU keep the LDS
+    // pipe).  Lane (q, g) = (lane % 8, lane / 8) of a wave loads rows 4q .. 4q + 3 of the group at
+    // columns c + 4g .. c + 4g + 3 (8 lanes = one 128-byte segment of a row) and stores them as
+    // rows c + 4g .. c + 4g + 3 of K at columns gs + 4q .. gs + 4q + 3 (8 lanes = one 128-byte
+    // row segment); a wave covers 32 columns, kFuseUnroll column blocks in flight.
+    constexpr int kQ = kFuseGroup / 4, kCols = 4 * (64 / kQ);  // lanes per row segment, columns per wave
+    const int lane = tid & 63, wave = tid >> 6, q = lane % kQ, g = lane / kQ;
+    const auto grs = __builtin_amdgcn_make_buffer_rsrc(K + gs * ldk + j0, (short)0, 0x7fffffff, 0x00020000);
+    const int64_t cb0 = diag ? gs - j0 : 0;
+    // compact code on purpose: this path runs once per 32 tiles, and its instructions share the
+    // instruction cache with the tiles' loop (edge columns / rows go to a separate function)
+    const int32_t row_off = (int32_t)(4 * q * ldk * 4);
+    for (int64_t cb = cb0 + wave * kCols; cb < wlen; cb += kWaves * kCols) {
+        const int64_t col = cb + 4 * g;
+        const int64_t j = j0 + col;  // K rows j .. j + 3 are written
+        if (gn == kFuseGroup && col + 4 <= wlen && j >= ge) {
+            f32x4 x[4];
+            const int32_t off = row_off + (int32_t)(col * 4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const auto y = __builtin_amdgcn_raw_buffer_load_b128(grs, off + (int32_t)(u * ldk * 4), 0, 16);
+                x[u] = f32x4{__uint_as_float(y[0]), __uint_as_float(y[1]), __uint_as_float(y[2]), __uint_as_float(y[3])};
+            }
+            if (exp & 8) continue;
+            float *dst = K + j * ldk + gs + 4 * q;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                __builtin_nontemporal_store(f32x4{x[0][e], x[1][e], x[2][e], x[3][e]}, reinterpret_cast<f32x4 *>(dst + e * ldk));
+        } else {
+            gram_fused_edge(K, ldk, gs, ge, j0, col, wlen, q);
+        }
+    }
+}
+
 // One workgroup of kWaves waves = one tile K[row, j0 : j0 + W] (W = a band of the banded
 // transpose), accumulated in LDS in exact int64 fixed point with the per-row power-of-two
 // scale S = 2^rowshift[row] (from the transpose) such that every term |Phi[row,k] Phi[j,k]| S
@@ -237,12 +357,12 @@ struct GramTiles {
 // id (bucket-start markers propagated by a running maximum, one LDS read); the gathers of kGramUnroll
 // windows of 64 pairs are in flight together.  Tiles are dispatched band-major, so the
 // tiles in flight share one band's records (L2 / Infinity Cache).
-template <int kWaves, int kHalves, int kGramUnroll, bool kTailExact>
+template <int kWaves, int kHalves, int kGramUnroll, bool kTailExact, bool kFuse>
 __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
     const unsigned char *__restrict__ t_rec, int32_t unit, const int32_t *__restrict__ rowshift,
-    float *__restrict__ K, int64_t ldk) {
+    float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets, int32_t fuse_exp) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t W = tl.W;
@@ -254,6 +374,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
 
     int64_t J, r;
     tl.locate(t_begin + (int64_t)blockIdx.x, J, r);
+    const int64_t J_local = J;
     J += tl.J_off;  // global band
     const int64_t row = row_begin + r;
     const int64_t j0 = J * W;
@@ -341,6 +462,10 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     if (kWaves > 1) __syncthreads();
     else __builtin_amdgcn_wave_barrier();
 
+    if constexpr (kFuse) {
+        gram_fused_completion<kWaves>(tl, J_local, r, j0, wlen, sh, acc, K, ldk, tickets, fuse_exp);
+        return;
+    }
     // write the tile once (non-temporal: K is write-once)
     float *krow = K + r * ldk + j0;
     if ((ldk & 3) == 0 && (j0 & 3) == 0) {
@@ -608,7 +733,7 @@ size_t grf_gram_workspace_bytes(void) { return 256; }
 static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramTiles &tl, int64_t t_first,
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
                                  const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
-                                 float *K, int64_t ldk, hipStream_t st) {
+                                 float *K, int64_t ldk, hipStream_t st, int32_t *tickets = nullptr) {
     // tuning knobs (defaults = measured best on MI355X): gathers in flight per wave, waves per tile
     static const int knobs = [] {
         const char *e = getenv("GRF_GRAM_UNROLL"), *w = getenv("GRF_GRAM_WAVES"), *t = getenv("GRF_GRAM_TAIL");
@@ -625,21 +750,30 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
         return e ? (size_t)atoll(e) : (size_t)0;
     }();
     const size_t lds = gram_lds_bytes(tl.W, waves, halves) + lds_pad;
+    static const int fuse_exp = [] {  // GRF_FUSE_EXP: timing-only decomposition of the fused completion (wrong
+                                      // K): 2 = no completion, 8 = the block's loads without its stores
+        const char *e = getenv("GRF_FUSE_EXP");
+        return e ? atoi(e) : 0;
+    }();
     // one launch covers at most 2^32 - 1 work-items: split the tile range
     const int64_t max_tiles = ((1ll << 32) - 1) / (64 * waves);
     for (int64_t t0 = t_first; t0 < t_last; t0 += max_tiles) {
         const int64_t nt = (t_last - t0) < max_tiles ? (t_last - t0) : max_tiles;
-#define GRF_GRAM_LAUNCH_T(WV, H, U, T)                                                                            \
-    gram_sparse_kernel<WV, H, U, T><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx, val,\
-                                                                     reinterpret_cast<const uint2 *>(t_desc),     \
-                                                                     reinterpret_cast<const unsigned char *>(t_rec), \
-                                                                     unit, t_rowshift, K, ldk)
+#define GRF_GRAM_LAUNCH_F(WV, H, U, T, F)                                                                         \
+    gram_sparse_kernel<WV, H, U, T, F><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx,   \
+                                                                        val, reinterpret_cast<const uint2 *>(t_desc), \
+                                                                        reinterpret_cast<const unsigned char *>(t_rec), \
+                                                                        unit, t_rowshift, K, ldk, tickets, fuse_exp)
+#define GRF_GRAM_LAUNCH_T(WV, H, U, T) GRF_GRAM_LAUNCH_F(WV, H, U, T, false)
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     do {                                                                                                          \
         if (tail_exact) GRF_GRAM_LAUNCH_T(WV, H, U, true);                                                        \
         else GRF_GRAM_LAUNCH_T(WV, H, U, false);                                                                  \
     } while (0)
-        if (waves == 8) {
+        if (tickets) {  // fused symmetric completion: the default unroll and exact tails only
+            if (waves == 8) GRF_GRAM_LAUNCH_F(8, 1, 8, true, true);
+            else GRF_GRAM_LAUNCH_F(4, 2, 8, true, true);
+        } else if (waves == 8) {
             if (unroll == 4) GRF_GRAM_LAUNCH(8, 1, 4);
             else GRF_GRAM_LAUNCH(8, 1, 8);
         } else {
@@ -649,6 +783,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
         }
 #undef GRF_GRAM_LAUNCH
 #undef GRF_GRAM_LAUNCH_T
+#undef GRF_GRAM_LAUNCH_F
         GRF_CHECK_LAUNCH("gram_sparse_kernel");
     }
     return GRF_OK;
@@ -722,6 +857,39 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
     if (t1 <= t0) return GRF_OK;
     return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
                              S(stream));
+}
+
+size_t grf_gram_sym_fused_workspace_bytes(int64_t n_total, int64_t band_width) {
+    if (n_total <= 0 || band_width <= 0) return 16;
+    const int64_t nb = cdiv<int64_t>(n_total, band_width), ng = cdiv<int64_t>(n_total, kFuseGroup);
+    return (size_t)cdiv<int64_t>(nb * ng * 4, 16) * 16;
+}
+
+int32_t grf_gram_sparse_sym_fused(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                                  int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                                  const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                                  int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
+                                  grf_stream_t stream) {
+    int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
+    if (rc != GRF_OK) return rc;
+    GRF_REQUIRE(n_parts >= 1 && 0 <= part_begin && part_begin <= part_end && part_end <= n_parts, GRF_EINVAL,
+                "grf_gram_sparse_sym_fused: bad tile parts [%d, %d) of %d", part_begin, part_end, n_parts);
+    GRF_REQUIRE(ldk % 4 == 0 && ((uintptr_t)K & 15) == 0, GRF_EINVAL,
+                "grf_gram_sparse_sym_fused: K must be 16-byte aligned with ldk a multiple of 4");
+    const size_t need = grf_gram_sym_fused_workspace_bytes(n_total, band_width);
+    GRF_REQUIRE(workspace && workspace_bytes >= need && ((uintptr_t)workspace & 15) == 0, GRF_EINVAL,
+                "grf_gram_sparse_sym_fused: workspace needs %zu bytes (16-byte aligned), got %zu", need,
+                workspace_bytes);
+    if (n_total == 0 || part_begin == part_end) return GRF_OK;
+    hipStream_t st = S(stream);
+    // the group tickets are zeroed by the call that issues the first part
+    if (part_begin == 0) GRF_CHECK_HIP(hipMemsetAsync(workspace, 0, need, st));
+    const GramTiles tl{n_total, band_width, cdiv<int64_t>(n_total, band_width), true, 0, (int32_t)n_total};
+    const int64_t total = tl.total();
+    const int64_t t0 = total * part_begin / n_parts, t1 = total * part_end / n_parts;
+    if (t1 <= t0) return GRF_OK;
+    return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk, st,
+                             reinterpret_cast<int32_t *>(workspace));
 }
 
 // Column block: K[r - row_begin, 0 : t_rows] = sum_k Phi[r, k] Phi_B[:, k] for the rows r of Phi

@@ -582,6 +582,25 @@ class GRFEngine:
                 "grf_gram_sparse_upper")
         return out[:, :n]
 
+    def gram_sparse_sym_fused(self, phi: DeviceCSR, tr: Banded, out: Optional[torch.Tensor] = None,
+                              parts=(0, 1, 1)) -> torch.Tensor:
+        """Whole K as ``gram_sparse_sym`` (bit-identical) with the symmetric completion fused into the
+        Gram tiles (no mirror pass).  parts = (begin, end, n): those parts of the tile sequence; the
+        parts of one K must be issued in order on this engine's stream."""
+        n = tr.n_rows
+        if out is None:
+            out = torch.empty((n, self.leading_dim(n)), dtype=torch.float32, device=self.device)
+        need = int(self.lib.grf_gram_sym_fused_workspace_bytes(n, tr.band_width))
+        ws = getattr(self, "_fused_ws", None)
+        if ws is None or ws.numel() < need:
+            ws = self._fused_ws = self._ws(need)
+        C.check(self.lib.grf_gram_sparse_sym_fused(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
+                                                   tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift),
+                                                   _p(out), out.stride(0), int(parts[0]), int(parts[1]),
+                                                   int(parts[2]), _p(ws), ws.numel(), self.stream),
+                "grf_gram_sparse_sym_fused")
+        return out[:, :n]
+
     def gram_mirror(self, K: torch.Tensor, n: int, max_workgroups: int = 0) -> torch.Tensor:
         """K[j, i] = K[i, j] for every j > i (the second half of ``gram_sparse_sym``).
         max_workgroups > 0 bounds the grid (leaves CU slots to work on another stream)."""

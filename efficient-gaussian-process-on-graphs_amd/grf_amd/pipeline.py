@@ -17,6 +17,7 @@ a *front* and a *K assembly*:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Tuple
 
@@ -24,6 +25,8 @@ import numpy as np
 import torch
 
 from .engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, SELF_COUNT_TRANSPOSE, DeviceCSR, GRFEngine, cols_band_width
+
+FUSED_DEFAULT = os.environ.get("GRF_GRAM_FUSED", "0") == "1"
 
 
 @dataclass
@@ -44,6 +47,7 @@ class StepPlan:
     mode: str = "sym"              # "sym" (one GPU, whole K), "rows", "cols", "allreduce"
     band_width: int = DEFAULT_BAND_WIDTH
     cols_sym: bool = False         # column blocks: the square K[b:e, b:e] by the symmetric enumeration
+    fused: bool = False            # "sym": symmetric completion fused into the Gram tiles (no mirror pass)
     group: object = None           # torch.distributed group (N > 1)
     extra: dict = field(default_factory=dict)
 
@@ -72,11 +76,12 @@ class StepPlan:
 
 def plan_step(n: int, m: int, L: int, p_halt: float, f, *, seed: int = 42, world: int = 1, rank: int = 0,
               mode: str = "cols", k_rows: int = 0, band_width: int = 0, no_sym: bool = False,
-              shards: Optional[List[Tuple[int, int]]] = None, group=None) -> StepPlan:
+              shards: Optional[List[Tuple[int, int]]] = None, group=None, fused: Optional[bool] = None) -> StepPlan:
     """The bench's mode rules: one GPU whole K -> symmetric mode; N > 1 or K-row workloads -> column
     blocks (``mode="cols"``), row blocks (``"rows"``) or the all-reduce option (``"allreduce"``).
     shards: every rank's source range (default: equal node counts; dist.balanced_shards for equal
-    estimated work)."""
+    estimated work).  fused: the symmetric mode's completion inside the Gram tiles (default: env
+    GRF_GRAM_FUSED, off)."""
     from .dist import shard_range
 
     if mode not in ("cols", "rows", "allreduce"):
@@ -99,6 +104,7 @@ def plan_step(n: int, m: int, L: int, p_halt: float, f, *, seed: int = 42, world
     elif world == 1 and not no_sym and not k_rows:
         pl.mode = "sym"
         pl.band_width = band_width or DEFAULT_BAND_WIDTH
+        pl.fused = FUSED_DEFAULT if fused is None else bool(fused)
     else:
         pl.mode = "rows"
         pl.band_width = band_width or ROWS_BAND_WIDTH
@@ -166,6 +172,24 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
     elif pl.mode == "allreduce":
         eng.gram_sparse_kslice(fr.phi, fr.tr, pl.b, pl.e, out=K)  # all rows, inner slice [b, e)
         allreduce_buckets(K[:, :pl.n], group=pl.group)
+    elif pl.mode == "sym" and pl.fused:
+        # one launch completes K (the tiles' last arrivers write the lower triangle); pipelined, the
+        # next front starts after front_at of the tiles and overlaps the rest
+        main = torch.cuda.current_stream(eng.device)
+        tiles_done = None
+        if after_tiles is not None and front_at < 1.0:
+            cut = int(round(front_at * 1000))
+            eng.gram_sparse_sym_fused(fr.phi, fr.tr, out=K, parts=(0, cut, 1000))
+            tiles_done = torch.cuda.Event()
+            tiles_done.record(main)
+            eng.gram_sparse_sym_fused(fr.phi, fr.tr, out=K, parts=(cut, 1000, 1000))
+        else:
+            eng.gram_sparse_sym_fused(fr.phi, fr.tr, out=K)
+            if after_tiles is not None:
+                tiles_done = torch.cuda.Event()
+                tiles_done.record(main)
+        if after_tiles is not None:
+            after_tiles(tiles_done)
     elif pl.mode == "sym":
         main = torch.cuda.current_stream(eng.device)
         tiles_done = None

@@ -285,6 +285,22 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
                               int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                               grf_stream_t stream);
 
+/* Whole K as grf_gram_sparse_sym, with the symmetric completion fused into the Gram tiles: the
+ * tiles of 64 consecutive rows of a band take tickets on a group counter and the last one writes
+ * the group's block transposed below the diagonal (from the Infinity Cache: no separate mirror
+ * pass re-reads the upper triangle from HBM).  K is bit-identical to grf_gram_sparse_sym's.
+ * Parts as grf_gram_sparse_upper (all parts of one K on one stream, in order; the call that
+ * issues part 0 zeroes the tickets).  workspace: grf_gram_sym_fused_workspace_bytes bytes,
+ * 16-byte aligned; K 16-byte aligned, ldk a multiple of 4.  Measured slower than
+ * grf_gram_sparse_sym on MI355X (the last arrivers' transposed stores serialise:
+ * profiles/r02_fused_ab.txt); an option, not the bench default. */
+size_t grf_gram_sym_fused_workspace_bytes(int64_t n_total, int64_t band_width);
+int32_t grf_gram_sparse_sym_fused(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                                  int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                                  const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                                  int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
+                                  grf_stream_t stream);
+
 /* Column block of K against another row set: K[r - row_begin, 0 : t_rows] = sum_k Phi[r, k] Phi_B[:, k]
  * for the rows r in [row_begin, row_end) of Phi (CSR ptr/idx/val, n_cols columns), where Phi_B
  * (t_rows rows, the same n_cols columns) is given by its banded transpose (grf_transpose_banded_*

@@ -156,7 +156,15 @@ def test_c4_headline_path(eng):
         ok, worst = _matvec_close(_k_matvec(Kv, u), ref, u, parts=parts)
         assert ok, worst
     print(f"[c4] symmetry, diag, K 1, K v ok {time.time() - t0:.1f} s", flush=True)
-    del K, Kv
+    # the completion fused into the Gram tiles (bench --fused): the whole 40 GB K bit for bit
+    pl.fused = True
+    Kf = P.alloc_k(eng, pl)
+    P.k_assembly(eng, fr, pl, Kf)
+    Kfv = P.k_view(Kf, pl)
+    for r0 in range(0, n, 8192):
+        assert torch.equal(Kfv[r0:r0 + 8192], Kv[r0:r0 + 8192]), r0
+    print(f"[c4] fused completion bit-identical {time.time() - t0:.1f} s", flush=True)
+    del K, Kv, Kf, Kfv
 
 
 def test_c5_column_block_path(eng):

@@ -243,6 +243,14 @@ def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
         eng.gram_sparse_upper(phi, tr, Ku, parts=(0, 7, 10))
         eng.gram_sparse_upper(phi, tr, Ku, parts=(7, 10, 10))
         assert np.array_equal(eng.gram_mirror(Ku, n, max_workgroups=37).cpu().numpy(), Ks)  # (grid-stride)
+        # the completion fused into the tiles (last arriver of every 32-row group): the same bits,
+        # whole and issued in parts (the tickets of a group straddling the cut carry over)
+        Kf = torch.full((n, eng.leading_dim(n)), float("nan"), dtype=torch.float32, device=eng.device)
+        assert np.array_equal(eng.gram_sparse_sym_fused(phi, tr, Kf).cpu().numpy(), Ks)
+        Kf.fill_(float("nan"))
+        for part in [(0, 3, 10), (3, 4, 10), (4, 10, 10)]:
+            eng.gram_sparse_sym_fused(phi, tr, Kf, parts=part)
+        assert np.array_equal(Kf[:, :n].cpu().numpy(), Ks)
     upper = np.triu(np.ones((n, n), bool))
     assert np.array_equal(Ks[upper], K[upper])
     ok, fro = gram_close(Ks, phi.to_scipy())
@@ -782,6 +790,8 @@ def test_bench_path_on_degenerate_graphs(eng, name):
     assert ok, fro
     Ks = eng.gram_sparse_sym(phi, tr)
     assert torch.equal(Ks, Ks.T) and torch.equal(torch.triu(Ks), torch.triu(K))
+    assert torch.equal(eng.gram_sparse_sym_fused(phi, tr), Ks)
+    assert torch.equal(eng.gram_sparse_sym_fused(phi, eng.transpose_banded(phi, 64)), Ks)
     b, e = n // 3, n - n // 4
     if e > b:
         loc = eng.compact(eng.walk_phi(G, 16, 0.2, 4, f, seed=4, src_begin=b, src_end=e), want64=False)
