@@ -289,8 +289,23 @@ def cora_adjacency() -> np.ndarray:
     return sp.csr_matrix((d["A_data"], d["A_indices"], d["A_indptr"]), shape=(n, n)).toarray()
 
 
+C2_DENSE = (10_000, 49_995)  # G(10k, 0.001) (E[M] = 49,995), run through the dense path
+
+
+def dense_workload(name: str):
+    """(dense adjacency, description, data) of a dense-path workload: C3 = Cora, C2 = ER N = 10k with
+    49,995 edges (graph seed 0), both as the reference's dense path takes them (an ndarray)."""
+    if name == "c2":
+        n, edges = C2_DENSE
+        W = er_graph_exact_edges(n, edges, seed=0).toarray()
+        return W, f"C2: ER N={n}, {edges} undirected edges, dense adjacency", \
+            "synthetic Erdos-Renyi graph (seed 0), unit weights"
+    return cora_adjacency(), "C3: Cora N=2708 dense adjacency", \
+        "real graph: Cora citation graph shipped with the reference (tests/golden/cora.npz)"
+
+
 def main_c3(args):
-    """C3: the reference's DENSE path on Cora (graph_kernels/fast_grf_kernel_general.py:11-39) --
+    """C3 (C2 with --workload c2): the reference's DENSE path on Cora (graph_kernels/fast_grf_kernel_general.py:11-39) --
     numpy-semantics dense Laplacian of the dense adjacency (resident in HBM) -> Philox walks
     (m = 128, L = 8) -> step rows (dense sampler's divide-by-m rule) -> Phi = F f -> dense
     float32 Phi -> K = Phi Phi^T on the MFMA (gram_dense_kernel, v_mfma_f32_32x32x2_f32).
@@ -302,7 +317,7 @@ def main_c3(args):
     from grf_amd.engine import GRFEngine
 
     eng = GRFEngine("cuda:0")
-    W = cora_adjacency()
+    W, wdesc, wdata = dense_workload(args.workload)
     n, m, L, p = W.shape[0], args.walks, args.length, args.p_halt
     f = diffusion_modulator(L, 1.0)
     Wt = torch.from_numpy(W).to(eng.device)
@@ -331,13 +346,14 @@ def main_c3(args):
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
     gram_ms = float(np.mean([a.elapsed_time(b) for a, b in gram_ev]))
-    kpad = -(-n // 16) * 16
     # the symmetric product's unique entries, 2 k flops each (the kernel computes the tiles on and
-    # above the diagonal and mirrors them; counting 2 n^2 k would credit work it does not do)
-    flops = 1.0 * n * (n + 1) * kpad
+    # above the diagonal and mirrors them; counting 2 n^2 k would credit work it does not do; k = n,
+    # the zero padding of the k range is not counted either)
+    flops = 1.0 * n * (n + 1) * n
     tfs = flops / (gram_ms * 1e-3) / 1e12
     out = {
-        "metric": "GRF kernel-matrices/sec (Cora N=2708, dense path, m=128 walks; MFMA utilisation of the Gram)",
+        "metric": (f"GRF kernel-matrices/sec ({'Cora N=2708' if args.workload == 'c3' else f'ER N={n}'}, dense path, "
+                   f"m={m} walks; MFMA utilisation of the Gram)"),
         "value": args.steps / t,
         "unit": "K-matrices/s",
         "n_gpus": 1,
@@ -348,8 +364,8 @@ def main_c3(args):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp64 walk loads, fp32 Phi, fp32 MFMA Gram",
-        "data": "real graph: Cora citation graph shipped with the reference (tests/golden/cora.npz)",
-        "config": {"workload": f"C3: Cora N={n} dense adjacency resident in HBM, dense numpy-semantics Laplacian, "
+        "data": wdata,
+        "config": {"workload": f"{wdesc} resident in HBM, dense numpy-semantics Laplacian, "
                                f"walks_per_node={m}, max_walk_length={L}, p_halt={p}, diffusion modulator beta=1, "
                                f"Philox seed 42, dense fp32 Phi and K", "n_nodes": n},
         "roofline": {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
@@ -405,10 +421,10 @@ def main():
                          "transpose of all of Phi (one GPU always runs rows / symmetric); allreduce: the north star's literal "
                          "option -- per-rank partial K over an inner-dimension slice + bucketed RCCL all-reduce, "
                          "K replicated on every rank (SURVEY.md §8e)")
-    ap.add_argument("--workload", choices=["kernel", "predict", "c5", "c3"], default="kernel",
+    ap.add_argument("--workload", choices=["kernel", "predict", "c5", "c3", "c2"], default="kernel",
                     help="kernel: K = Phi Phi^T (headline); predict: pathwise-conditioning posterior samples; "
                          "c5: SURVEY.md C5 -- N=1M power-law graph, m=64, Phi + a K row block per GPU; "
-                         "c3: Cora dense path with the MFMA Gram")
+                         "c3: Cora dense path with the MFMA Gram; c2: ER N=10k through the dense path (MFMA Gram)")
     ap.add_argument("--graph", choices=["er", "powerlaw", "facebook", "enron"], default="er",
                     help="er: Erdos-Renyi with --edges edges (C4); powerlaw: Chung-Lu, exponent 2.5, mean degree "
                          "--avg-degree (C5); facebook / enron: the reference's shipped social graphs")
@@ -447,7 +463,7 @@ def main():
         args.n = None
     if args.workload == "predict":
         return main_predict(args)
-    if args.workload == "c3":
+    if args.workload in ("c3", "c2"):
         return main_c3(args)
 
     import torch
@@ -691,7 +707,8 @@ def main():
         "serial_ms_per_step": serial_ms,
     }
     if headline and not args.no_mfma_leg:
-        out["roofline_mfma"] = mfma_leg(eng, args)
+        out["roofline_mfma"] = mfma_leg(eng, args)                      # C3 (Cora)
+        out["roofline_mfma_c2"] = mfma_leg(eng, args, workload="c2")    # C2 (ER N = 10k) through the dense path
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(A, f, m, p, L, args.cpu_rows, host_threads(), k_rows=args.k_rows)
         out["cpu_baseline"]["host"] = host_cpu_note()
@@ -734,20 +751,22 @@ def host_cpu_note() -> str:
     return f"os.cpu_count()={os.cpu_count()}, affinity={aff}, cgroup cpu.max={quota}"
 
 
-def mfma_leg(eng, args, steps: int = 20):
-    """MFMA utilisation of the Phi Phi^T kernel on the dense path (C3: Cora, the reference's dense
-    graph_kernels/fast_grf_kernel_general.py:11-39; the north star puts MFMA only on the dense
-    contraction): gram_dense_kernel timed with HIP events over `steps` launches."""
+def mfma_leg(eng, args, steps: int = 20, workload: str = "c3"):
+    """MFMA utilisation of the Phi Phi^T kernel on the dense path (C3: Cora; C2: ER N = 10k; the
+    reference's dense graph_kernels/fast_grf_kernel_general.py:11-39; the north star puts MFMA only
+    on the dense contraction): grf_gram_dense (tiles + split-K combine / mirror) timed with HIP
+    events over `steps` launches."""
     import torch
 
     from grf_amd import _lib as C
 
-    W = cora_adjacency()
+    W, wdesc, _ = dense_workload(workload)
     n, m, L, p = W.shape[0], args.walks, args.length, args.p_halt
     f = diffusion_modulator(L, 1.0)
     G = eng.walk_matrix_dense(torch.from_numpy(W).to(eng.device), C.LAP_NUMPY)
     phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False)
     dense = eng.densify(phi)
+    del G, W
     for _ in range(3):
         eng.gram_dense(dense, n)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -757,14 +776,13 @@ def mfma_leg(eng, args, steps: int = 20):
     ev[1].record()
     ev[1].synchronize()
     ms = ev[0].elapsed_time(ev[1]) / steps
-    kpad = -(-n // 16) * 16
-    flops = 1.0 * n * (n + 1) * kpad
+    flops = 1.0 * n * (n + 1) * n
     tfs = flops / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "gram_dense_kernel (v_mfma_f32_32x32x2f32)",
+            "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "gram_dense_kernel (v_mfma_f32_32x32x2f32) + its combine/mirror",
             "kernel_ms": ms, "algorithmic_flops": flops,
-            "workload": f"C3 dense path: Cora N={n}, m={m}, L={L}: K = Phi Phi^T of the dense fp32 Phi "
-                        f"(N (N+1) k flops: the unique entries of the symmetric product)"}
+            "workload": f"{wdesc} dense path, m={m}, L={L}: K = Phi Phi^T of the dense fp32 Phi "
+                        f"(N (N+1) N flops: the unique entries of the symmetric product)"}
 
 
 if __name__ == "__main__":

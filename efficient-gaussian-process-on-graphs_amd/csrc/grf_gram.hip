@@ -629,10 +629,14 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kDensePad = 32;
 __device__ __forceinline__ int dense_swz(int k) { return ((k >> 2) & 7) << 3; }
 
+// Split-K (gridDim.y = S > 1, small n: too few tiles to fill the CUs): slice s of the k range,
+// k_split wide, goes to the partial buffer K + s * part_stride; gram_dense_combine_kernel sums the
+// S partials in slice order and writes both triangles.
 template <int BM, int BK>
 __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, int64_t k_dim,
                                                          const float *__restrict__ A, int64_t lda,
-                                                         float *__restrict__ K, int64_t ldk) {
+                                                         float *__restrict__ K, int64_t ldk, int64_t k_split,
+                                                         int64_t part_stride) {
     constexpr int NB = BM / 64;          // 32 x 32 MFMA blocks per wave and dimension
     constexpr int F4 = BM * BK / 4 / 256;  // float4 loads per thread and operand per k-tile
     __shared__ __attribute__((aligned(16))) float As[BK][BM + kDensePad];
@@ -658,6 +662,9 @@ __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, 
 #pragma unroll
             for (int q = 0; q < 16; ++q) c[x][y][q] = 0.f;
 
+    const int64_t kb = (int64_t)blockIdx.y * k_split;
+    const int64_t ke = (kb + k_split) < k_dim ? kb + k_split : k_dim;
+    K += (int64_t)blockIdx.y * part_stride;
     float4 ra[F4], rb[F4];
     auto load = [&](int64_t k0) {
 #pragma unroll
@@ -670,8 +677,8 @@ __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, 
             if (n0 + row < n) rb[it] = *reinterpret_cast<const float4 *>(A + (n0 + row) * lda + k0 + kq);
         }
     };
-    load(0);
-    for (int64_t k0 = 0; k0 < k_dim; k0 += BK) {
+    load(kb);
+    for (int64_t k0 = kb; k0 < ke; k0 += BK) {
         __syncthreads();  // (the previous tile's MFMA reads are done)
 #pragma unroll
         for (int it = 0; it < F4; ++it) {
@@ -682,7 +689,7 @@ __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, 
             Bs[kq + 0][sr] = rb[it].x; Bs[kq + 1][sr] = rb[it].y; Bs[kq + 2][sr] = rb[it].z; Bs[kq + 3][sr] = rb[it].w;
         }
         __syncthreads();
-        if (k0 + BK < k_dim) load(k0 + BK);  // in flight during the MFMAs below
+        if (k0 + BK < ke) load(k0 + BK);  // in flight during the MFMAs below
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 2) {
             const int kr = kk + (lane >> 5), rc = lane & 31, sw = dense_swz(kr);
@@ -709,6 +716,68 @@ __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, 
                 const int64_t col = n0 + wn * (BM / 2) + y * 32 + (lane & 31);
                 if (row < n && col < n) K[row * ldk + col] = c[x][y][q];
             }
+}
+
+// Split-K epilogue: K[i, j] = sum_s P_s[i, j] (slices in order: deterministic) for the 64 x 64 blocks
+// on and above the diagonal, written to the upper block and, transposed through LDS, to the lower one
+// (the diagonal block: its upper half, mirrored), so K comes out exactly symmetric.
+__global__ __launch_bounds__(256) void gram_dense_combine_kernel(int64_t n, int64_t nt, int n_parts,
+                                                                 const float *__restrict__ P, int64_t ldp,
+                                                                 int64_t part_stride, float *__restrict__ K,
+                                                                 int64_t ldk) {
+    __shared__ float tile[64][65];
+    const int64_t b = blockIdx.x;
+    int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
+    auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };
+    if (bi < 0) bi = 0;
+    if (bi > nt - 1) bi = nt - 1;
+    while (bi > 0 && first(bi) > b) --bi;
+    while (bi < nt - 1 && first(bi + 1) <= b) ++bi;
+    const int64_t bj = bi + (b - first(bi));
+    const int64_t i0 = bi * 64, j0 = bj * 64;
+    const int t = threadIdx.x;
+    const bool full = i0 + 64 <= n && j0 + 64 <= n && (ldk & 3) == 0 && (ldp & 3) == 0 && (part_stride & 3) == 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
+        const int64_t i = i0 + y;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (full) {
+            for (int sl = 0; sl < n_parts; ++sl)
+                acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(P + sl * part_stride + i * ldp + j0 + x));
+        } else {
+            for (int sl = 0; sl < n_parts; ++sl)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (i < n && j0 + x + c < n) acc[c] += P[sl * part_stride + i * ldp + j0 + x + c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) tile[y][x + c] = acc[c];
+        if (full && bi != bj) {
+            __builtin_nontemporal_store(acc, reinterpret_cast<f32x4 *>(K + i * ldk + j0 + x));
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (i < n && j0 + x + c < n && j0 + x + c >= i) K[i * ldk + j0 + x + c] = acc[c];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
+        const int64_t j = j0 + y;
+        if (full && bi != bj) {
+            f32x4 v;
+            v[0] = tile[x][y]; v[1] = tile[x + 1][y]; v[2] = tile[x + 2][y]; v[3] = tile[x + 3][y];
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(K + j * ldk + i0 + x));
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int64_t i = i0 + x + c;
+                if (j < n && i < n && j > i) K[j * ldk + i] = tile[x + c][y];
+            }
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void densify_kernel(int64_t n_rows, const int64_t *__restrict__ ptr,
@@ -1010,14 +1079,36 @@ int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups
     return GRF_OK;
 }
 
-int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
-                       grf_stream_t stream) {
+// split-K slices for a dense Gram of n rows (128-row tiles on and above the diagonal): measured on
+// MI355X (tools/dense_sweep.py, profiles/r02_dense_splitk.txt) 4 slices below 1024 tiles (n < 5.8 k),
+// 2 below 4096 (n < 11.6 k), none above; every slice at least 256 deep
+static int dense_splits(int64_t n, int64_t k_dim) {
+    static const int env_split = [] {  // GRF_DENSE_SPLIT: A/B knob (1 = never split)
+        const char *e = getenv("GRF_DENSE_SPLIT");
+        return e ? atoi(e) : 0;
+    }();
+    if (env_split > 0) return env_split;
+    const int64_t nt = cdiv<int64_t>(n, 128), tiles = nt * (nt + 1) / 2;
+    const int64_t S = tiles < 1024 ? 4 : tiles < 4096 ? 2 : 1;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(S, k_dim / 256));
+}
+
+size_t grf_gram_dense_workspace_bytes(int64_t n, int64_t k_dim) {
+    const int S = n > 0 ? dense_splits(n, k_dim) : 1;
+    if (S <= 1) return 16;
+    const int64_t ldp = cdiv<int64_t>(n, 64) * 64;
+    return (size_t)S * (size_t)n * (size_t)ldp * sizeof(float);
+}
+
+int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                          void *workspace, size_t workspace_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n >= 0 && k_dim >= 0 && A && K && ldk >= n && lda >= k_dim, GRF_EINVAL,
                 "grf_gram_dense: bad arguments");
     GRF_REQUIRE(lda % 16 == 0 && ((uintptr_t)A & 15) == 0, GRF_EINVAL,
                 "grf_gram_dense: lda must be a multiple of 16 and A 16-byte aligned");
     if (n == 0) return GRF_OK;
-    // tile: 128 when the upper triangle of 128-tiles gives >= 2 workgroups per CU (n >= ~4.5 k), else 64
+    // tile: 128 when the upper triangle of 128-tiles gives >= 2 workgroups per CU (n >= ~4.5 k), else
+    // 64 -- or 128 with split-K slices when a workspace for the partials is given (small n)
     const int64_t nt128 = cdiv<int64_t>(n, 128);
     static const int env_tile = [] {  // GRF_DENSE_TILE=64/128, GRF_DENSE_BK=16/32: A/B knobs
         const char *e = getenv("GRF_DENSE_TILE");
@@ -1027,7 +1118,10 @@ int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, fl
         const char *e = getenv("GRF_DENSE_BK");
         return e ? atoi(e) : 0;
     }();
-    const bool big = env_tile ? env_tile == 128 : nt128 * (nt128 + 1) / 2 >= 512;
+    int ns = workspace ? dense_splits(n, k_dim) : 1;
+    const int64_t ldp = cdiv<int64_t>(n, 64) * 64;
+    if (ns > 1 && workspace_bytes < (size_t)ns * (size_t)n * (size_t)ldp * sizeof(float)) ns = 1;
+    const bool big = ns > 1 || (env_tile ? env_tile == 128 : nt128 * (nt128 + 1) / 2 >= 512);
     int bk = (!big && lda % 32 == 0) ? 32 : 16;  // (zero padding up to lda covers the last k-tile)
     if (env_bk == 32 && lda % 32 == 0) bk = 32;
     if (env_bk == 16) bk = 16;
@@ -1035,12 +1129,27 @@ int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, fl
     GRF_REQUIRE(kpad <= lda, GRF_EINVAL, "grf_gram_dense: lda must cover k_dim rounded up to %d", bk);
     const int64_t nt = cdiv<int64_t>(n, big ? 128 : 64), tiles = nt * (nt + 1) / 2;
     GRF_REQUIRE_GRID(tiles, 256, "gram_dense_kernel");
-    if (big && bk == 32) gram_dense_kernel<128, 32><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
-    else if (big) gram_dense_kernel<128, 16><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
-    else if (bk == 32) gram_dense_kernel<64, 32><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
-    else gram_dense_kernel<64, 16><<<(unsigned)tiles, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, K, ldk);
+    const int64_t k_split = ns > 1 ? cdiv<int64_t>(cdiv<int64_t>(kpad, ns), bk) * bk : kpad;
+    if (ns > 1) ns = (int)cdiv<int64_t>(kpad, k_split);
+    float *out = ns > 1 ? reinterpret_cast<float *>(workspace) : K;
+    const int64_t ldo = ns > 1 ? ldp : ldk, pstride = ns > 1 ? n * ldp : 0;
+    const dim3 grid((unsigned)tiles, (unsigned)ns);
+    if (big && bk == 32) gram_dense_kernel<128, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride);
+    else if (big) gram_dense_kernel<128, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride);
+    else if (bk == 32) gram_dense_kernel<64, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride);
+    else gram_dense_kernel<64, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride);
     GRF_CHECK_LAUNCH("gram_dense_kernel");
-    return grf_gram_mirror(n, K, ldk, 0, stream);  // the lower triangle
+    if (ns == 1) return grf_gram_mirror(n, K, ldk, 0, stream);  // the lower triangle
+    const int64_t nt64 = cdiv<int64_t>(n, 64), blocks = nt64 * (nt64 + 1) / 2;
+    GRF_REQUIRE_GRID(blocks, 256, "gram_dense_combine_kernel");
+    gram_dense_combine_kernel<<<(unsigned)blocks, 256, 0, S(stream)>>>(n, nt64, ns, out, ldp, pstride, K, ldk);
+    GRF_CHECK_LAUNCH("gram_dense_combine_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                       grf_stream_t stream) {
+    return grf_gram_dense_ws(n, k_dim, A, lda, K, ldk, nullptr, 0, stream);
 }
 
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,

@@ -104,6 +104,8 @@ SIGNATURES = {
     "grf_gram_sparse_kslice": (_i32, [_i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp,
                                       _i64, _vp, _sz, _vp]),
     "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "grf_gram_dense_workspace_bytes": (_sz, [_i64, _i64]),
+    "grf_gram_dense_ws": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
     "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     # the GPyTorch surface's feature algebra (step_* are host arrays of device pointers)
     "grf_phi_steps_csr_count": (_i32, [_i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),

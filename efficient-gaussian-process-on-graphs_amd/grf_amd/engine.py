@@ -618,8 +618,13 @@ class GRFEngine:
         n = dense_phi.shape[0]
         ldk = self.leading_dim(n)
         out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
-        C.check(self.lib.grf_gram_dense(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, self.stream),
-                "grf_gram_dense")
+        # split-K partials for small n (too few tiles to fill the GPU): a cached workspace
+        need = int(self.lib.grf_gram_dense_workspace_bytes(n, k_dim))
+        ws = getattr(self, "_dense_ws", None)
+        if ws is None or ws.numel() < need:
+            ws = self._dense_ws = self._ws(need)
+        C.check(self.lib.grf_gram_dense_ws(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, _p(ws),
+                                           ws.numel(), self.stream), "grf_gram_dense_ws")
         return out[:, :n]
 
     def gram(self, phi: DeviceCSR, method: str = "auto") -> torch.Tensor:

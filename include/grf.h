@@ -352,6 +352,14 @@ int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups
  * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */
 int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                        grf_stream_t stream);
+/* As grf_gram_dense, with a device workspace for split-K partials: when n is too small for the
+ * tiles on and above the diagonal to fill the GPU, the k range is cut into S slices whose partial
+ * Grams are summed in slice order (deterministic) by the pass that also writes the lower triangle.
+ * workspace: grf_gram_dense_workspace_bytes(n, k_dim) bytes (16 when no split is used); NULL or a
+ * smaller workspace runs unsplit. */
+size_t grf_gram_dense_workspace_bytes(int64_t n, int64_t k_dim);
+int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                          void *workspace, size_t workspace_bytes, grf_stream_t stream);
 
 /* CSR (float32) -> dense float32 [n_rows x lda], zero filled. */
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,

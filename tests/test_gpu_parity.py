@@ -405,6 +405,31 @@ def test_gram_dense_asymmetric_layout(eng):
     np.testing.assert_allclose(K, ref, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("n,k", [(300, 900), (2708, 2708), (1500, 4000)])
+def test_gram_dense_split_k(eng, n, k):
+    """Split-K dense Gram (small n: slices of k summed in order by the combine pass that writes both
+    triangles) against fp64 and against the unsplit kernel; exactly symmetric, run-to-run identical."""
+    import torch
+    from grf_amd import _lib as C
+    lda = -(-k // 64) * 64
+    Ad = np.zeros((n, lda), np.float32)
+    r = np.random.default_rng(n)
+    Ad[:, :k] = (r.standard_normal((n, k)) * (r.random((n, k)) < 0.1)).astype(np.float32)
+    At = torch.from_numpy(Ad).to(eng.device)
+    assert eng.lib.grf_gram_dense_workspace_bytes(n, k) > 16  # (the split path is taken)
+    Ks = eng.gram_dense(At, k)
+    K1 = torch.empty((n, eng.leading_dim(n)), dtype=torch.float32, device=eng.device)
+    C.check(eng.lib.grf_gram_dense(n, k, At.data_ptr(), lda, K1.data_ptr(), K1.stride(0), eng.stream),
+            "grf_gram_dense")
+    ref = Ad.astype(np.float64) @ Ad.astype(np.float64).T
+    bound = np.abs(Ad).astype(np.float64) @ np.abs(Ad).astype(np.float64).T
+    for K in (Ks.cpu().numpy(), K1[:, :n].cpu().numpy()):
+        assert np.all(np.abs(K - ref) <= 1e-5 * bound + 1e-30)
+    Ksn = Ks.cpu().numpy()
+    assert np.array_equal(Ksn, Ksn.T)
+    assert np.array_equal(eng.gram_dense(At, k).cpu().numpy(), Ksn)
+
+
 def test_full_pipeline_c2_scale(eng):
     """ER N=10k (C2-like) -- Philox walks vs oracle on a source sample, K rows vs oracle, symmetry."""
     n = 10000
