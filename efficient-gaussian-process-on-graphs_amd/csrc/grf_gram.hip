@@ -612,6 +612,103 @@ __global__ __launch_bounds__(256) void gram_mirror_swz_kernel(int64_t n, int64_t
     }
 }
 
+// The bounded grid (grid-stride over the blocks: the pipelined bench gives the mirror 1024
+// workgroups beside the next step's front), GRF_MIRROR_PIPE=1: a workgroup's loads of its next block
+// are issued before the stores of the current one.  On gfx950 one vmcnt counter covers loads and stores, so a wait for
+// loads issued after stores also waits for those stores' acknowledgements; issued before them, the
+// next block's loads are in flight while the current block is written (profiles/r02_fused_ab.txt,
+// where one workgroup per 1 MB block lost ~100 ms to that serialisation).  Measured beside the next
+// front (profiles/r02_mirror_pipe_ab.txt): the K assembly ends at the same time but the front beside
+// it is slowed (24.9 vs 24.0 ms per step, same box), so it is off by default.
+// Strictly-upper full blocks only (the diagonal blocks and, for n % 64 != 0, the ragged last block
+// column go to gram_mirror_edge_kernel): nf = nt - 1 (n % 64 == 0) or nt - 2 block columns are full,
+// and the strictly-upper blocks of that nf x nf grid are enumerated row-major (bi < bj < nf).
+__device__ __forceinline__ void gram_mirror_upper_coords(int64_t nf, int64_t b, int64_t &i0, int64_t &j0) {
+    // row bi holds nf - 1 - bi blocks; first(bi) = bi (2 nf - bi - 1) / 2
+    const double m = (double)(2 * nf - 1);
+    int64_t bi = (int64_t)((m - sqrt(m * m - 8.0 * (double)b)) * 0.5);
+    auto first = [nf](int64_t i) { return i * (2 * nf - i - 1) / 2; };
+    if (bi < 0) bi = 0;
+    if (bi > nf - 2) bi = nf - 2;
+    while (bi > 0 && first(bi) > b) --bi;
+    while (bi < nf - 2 && first(bi + 1) <= b) ++bi;
+    i0 = bi * 64;
+    j0 = (bi + 1 + (b - first(bi))) * 64;
+}
+
+__global__ __launch_bounds__(256) void gram_mirror_pipe_kernel(int64_t nf, int64_t nblocks, float *__restrict__ K,
+                                                               int64_t ldk) {
+    __shared__ __attribute__((aligned(16))) float tile[64 * 64];
+    const int t = threadIdx.x;
+    auto swz = [](int r, int c) { return r * 64 + (c ^ (4 * ((r >> 2) & 15))); };
+    f32x4 v[4];
+    int64_t i0 = 0, j0 = 0;
+    auto load = [&](int64_t b) {
+        gram_mirror_upper_coords(nf, b, i0, j0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
+            v[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(K + (i0 + y) * ldk + j0 + x));
+        }
+    };
+    auto to_lds = [&]() {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
+            *reinterpret_cast<f32x4 *>(tile + swz(y, x)) = v[q];
+        }
+    };
+    int64_t b = blockIdx.x;
+    if (b >= nblocks) return;
+    load(b);
+    to_lds();
+    __syncthreads();
+    for (; b < nblocks; b += gridDim.x) {
+        const int64_t ci0 = i0, cj0 = j0;
+        // the next block's loads, issued before this block's stores (unconditional, clamped: the wait
+        // for them below is then vmcnt(4), the 4 stores behind them, on every path)
+        load(b + gridDim.x < nblocks ? b + gridDim.x : nblocks - 1);
+        const int k = t & 15, pr = t >> 4;
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            const int y = 2 * pr + 32 * it;
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            typedef __attribute__((address_space(3))) float lds_float;
+            uint32_t a[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a[c] = (uint32_t)(uintptr_t)(lds_float *)(tile + swz(4 * k + c, y));
+            f32x2 w[4];
+            asm volatile(
+                "ds_read_b64 %0, %4\n\tds_read_b64 %1, %5\n\tds_read_b64 %2, %6\n\tds_read_b64 %3, %7\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
+                : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+                : "memory");
+            f32x4 o0, o1;
+            o0[0] = w[0].x; o0[1] = w[1].x; o0[2] = w[2].x; o0[3] = w[3].x;
+            o1[0] = w[0].y; o1[1] = w[1].y; o1[2] = w[2].y; o1[3] = w[3].y;
+            __builtin_nontemporal_store(o0, reinterpret_cast<f32x4 *>(K + (cj0 + y) * ldk + ci0 + 4 * k));
+            __builtin_nontemporal_store(o1, reinterpret_cast<f32x4 *>(K + (cj0 + y + 1) * ldk + ci0 + 4 * k));
+        }
+        __syncthreads();  // (this block's LDS reads are done)
+        to_lds();
+        __syncthreads();
+    }
+}
+
+// The blocks gram_mirror_pipe_kernel leaves: the nt diagonal blocks, then the blocks of the last
+// (ragged) block column when n % 64 != 0, then the strictly-upper blocks of full block columns beyond
+// the pipelined grid's enumeration (none: every full strictly-upper block is in it).
+__global__ __launch_bounds__(256) void gram_mirror_edge_kernel(int64_t n, int64_t nt, float *__restrict__ K,
+                                                               int64_t ldk) {
+    __shared__ float tile[64][65];
+    const int64_t e = blockIdx.x;
+    // express the edge block as its index in the triangular enumeration of gram_mirror_block
+    const int64_t bi = e < nt ? e : e - nt, bj = e < nt ? e : nt - 1;
+    const int64_t b = bi * nt - bi * (bi - 1) / 2 + (bj - bi);
+    gram_mirror_block(n, nt, b, K, ldk, tile);
+}
+
 __global__ void absmax_reset_kernel(float *m) { *m = 0.f; }
 
 // ------------------------------------------------------------------ dense MFMA
@@ -1073,8 +1170,19 @@ int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups
         const char *e = getenv("GRF_MIRROR_PADDED");
         return e ? atoi(e) : 0;
     }();
+    static const int pipe = [] {  // GRF_MIRROR_PIPE=1: the bounded grid with the next block's loads in flight
+        const char *e = getenv("GRF_MIRROR_PIPE");  // (measured slower beside the next front: off by default)
+        return e ? atoi(e) : 0;
+    }();
     if (padded) gram_mirror_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
-    else gram_mirror_swz_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
+    else if (pipe && grid < blocks && (ldk & 3) == 0 && nt >= 3) {
+        // the full strictly-upper blocks, with the next block's loads in flight, then the edges
+        const int64_t nf = n % 64 == 0 ? nt : nt - 1, nfull = nf * (nf - 1) / 2;
+        const int64_t g = grid < nfull ? grid : nfull;
+        if (nfull > 0) gram_mirror_pipe_kernel<<<(unsigned)g, 256, 0, S(stream)>>>(nf, nfull, K, ldk);
+        const int64_t nedge = nt + (n % 64 == 0 ? 0 : nt - 1);
+        gram_mirror_edge_kernel<<<(unsigned)nedge, 256, 0, S(stream)>>>(n, nt, K, ldk);
+    } else gram_mirror_swz_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
     GRF_CHECK_LAUNCH("gram_mirror_kernel");
     return GRF_OK;
 }
