@@ -412,6 +412,10 @@ def main():
     ap.add_argument("--length", type=int, default=8)
     ap.add_argument("--p-halt", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--transfers", action="store_true",
+                    help="also time the host hand-over of the drop-in boundary (SURVEY.md §8d: H2D of the CSR "
+                         "adjacency, D2H of the K block into pinned host memory) and report the PCIe-inclusive "
+                         "rate beside the device-resident value (never as `value`)")
     ap.add_argument("--cpu-rows", type=int, default=2048)
     ap.add_argument("--no-sym", action="store_true", help="compute every K tile (one GPU: no symmetric mode; N > 1 "
                     "column blocks: no symmetric square K[b:e, b:e])")
@@ -709,6 +713,10 @@ def main():
     if headline and not args.no_mfma_leg:
         out["roofline_mfma"] = mfma_leg(eng, args)                      # C3 (Cora)
         out["roofline_mfma_c2"] = mfma_leg(eng, args, workload="c2")    # C2 (ER N = 10k) through the dense path
+    if args.transfers:
+        out["transfers"] = time_transfers(A, K, pl, dev, ms_per_step)
+        out["transfers"]["pcie_inclusive_value"] = value * ms_per_step / out["transfers"]["pcie_inclusive_ms_per_step"]
+        out["transfers"]["pcie_inclusive_unit"] = unit
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(A, f, m, p, L, args.cpu_rows, host_threads(), k_rows=args.k_rows)
         out["cpu_baseline"]["host"] = host_cpu_note()
@@ -716,6 +724,48 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def time_transfers(A, K, pl, dev, ms_per_step: float, reps: int = 3) -> dict:
+    """The drop-in boundary's host hand-over, timed apart from the device-resident step (SURVEY.md
+    §8d): H2D of the CSR adjacency (DeviceCSR.from_scipy: indptr, indices, data) and D2H of this
+    rank's K block into pinned host memory (one async copy on a side stream, HIP events)."""
+    import torch
+
+    from grf_amd import pipeline as P
+    from grf_amd.engine import DeviceCSR
+
+    h2d = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        DeviceCSR.from_scipy(A, dev)
+        torch.cuda.synchronize()
+        h2d.append(1000.0 * (time.perf_counter() - t0))
+    Kv = P.k_view(K, pl)
+    nbytes = Kv.numel() * Kv.element_size()
+    try:
+        host = torch.empty(K.shape, dtype=K.dtype, pin_memory=True)
+        pinned = True
+    except RuntimeError:
+        host = torch.empty(K.shape, dtype=K.dtype)
+        pinned = False
+    d2h = []
+    for _ in range(2):
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        host.copy_(K, non_blocking=pinned)
+        ev[1].record()
+        ev[1].synchronize()
+        d2h.append(ev[0].elapsed_time(ev[1]))
+    h2d_ms, d2h_ms = min(h2d), min(d2h)
+    total = ms_per_step + h2d_ms + d2h_ms
+    return {"h2d_adjacency_ms": h2d_ms, "h2d_adjacency_bytes": int(A.indptr.nbytes + A.indices.nbytes + A.data.nbytes),
+            "d2h_k_ms": d2h_ms, "d2h_k_bytes": int(K.numel() * K.element_size()), "d2h_k_logical_bytes": int(nbytes),
+            "d2h_GBps": K.numel() * K.element_size() / (d2h_ms * 1e-3) / 1e9, "pinned": pinned,
+            "pcie_inclusive_ms_per_step": total,
+            "note": "serial sum: device-resident step + H2D of A + D2H of the whole K buffer (ldk-padded rows); "
+                    "reported beside `value`, never as it"}
 
 
 def host_threads() -> int:
