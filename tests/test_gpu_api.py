@@ -230,6 +230,28 @@ def test_philox_mode_through_api_matches_oracle():
         assert same_csr(a, b)
 
 
+def test_sparse_entry_point_many_walks():
+    """The drop-in sparse entry point with walks_per_node * max_walk_length > 4096 (the walk matrix
+    goes through the step kernels instead of the fused Phi kernel), reference stream: step matrices
+    bit-exact against the oracle, K within the K tolerance of the oracle's fp64 Gram."""
+    from efficient_graph_gp_sparse.graph_kernels_sparse.fast_grf_kernel_general import fast_general_grf_kernel
+    from oracle import oracle as O
+    from test_gpu_parity import gram_close
+    U = sp.random(300, 300, density=0.03, random_state=5, format="csr")
+    A = ((U + U.T) > 0).astype(np.float64).tocsr()
+    A.setdiag(0)
+    A.eliminate_zeros()
+    A.sort_indices()
+    f = [1.0, -0.5, 0.25, -0.125, 0.0625, -0.03125, 0.015625, -0.0078125]
+    K = fast_general_grf_kernel(A, f, walks_per_node=600, p_halt=0.2, max_walk_length=8, n_processes=3)
+    L, _ = O.laplacian_sparse(A)
+    ip, ix, dx = O._csr_arrays(L)
+    node, load = O.walk_slots(ip, ix, dx, 600, 0.2, 8, rng=O.RNG_PCG64, seed=42, n_chunks=3)
+    phi = O.phi_sparse(O.reduce_steps(node, load, O.NORM_MUL_RECIP), np.asarray(f))
+    ok, fro = gram_close(K.toarray(), phi)
+    assert ok, fro
+
+
 def _degenerate_graphs():
     """Edge cases the path has to survive: one node, no edges, a star (one hub of degree n - 1),
     disjoint components with isolated nodes, a path, a weighted pair."""

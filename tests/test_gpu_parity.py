@@ -184,7 +184,8 @@ def test_cora_m128_reference_digests(eng, golden):
 
 
 # -------------------------------------------------------------- steps / Phi
-@pytest.mark.parametrize("m,L,p", [(16, 8, 0.1), (128, 8, 0.1), (50, 3, 0.1), (300, 4, 0.05), (7, 20, 0.02)])
+@pytest.mark.parametrize("m,L,p", [(16, 8, 0.1), (128, 8, 0.1), (50, 3, 0.1), (300, 4, 0.05), (7, 20, 0.02),
+                                   (600, 8, 0.2)])  # (m L = 4800 > 4096: steps + phi, no fused kernel)
 def test_steps_and_phi_bitexact(eng, m, L, p):
     A = er_graph(600, 7, m + L)
     Ls, _ = O.laplacian_sparse(A)
