@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         const int64_t *__restrict__ g_ptr,
                                                         const int32_t *__restrict__ g_idx,
                                                         const double *__restrict__ g_val,
-                                                        const AugRec *__restrict__ g_aug, double p_halt, int32_t rule,
+                                                        const unsigned char *__restrict__ g_aug, double p_halt, int32_t rule,
                                                         uint32_t k0, uint32_t k1, int64_t src_begin,
                                                         const double *__restrict__ f, int32_t Lf, int64_t cap,
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
@@ -306,29 +306,45 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
 }
 
 // ---------------------------------------------- augmented walk matrix (philox_walk_aug)
-// aug[e] = {target v, row start of v (32 bits), row length of v, 0} for every entry e of the
-// walk matrix; one wave per row.
-__global__ __launch_bounds__(256) void walk_aug_kernel(int64_t n, const int64_t *__restrict__ g_ptr,
+// The header and one record per entry e of the walk matrix (grf_philox.h); one wave per row.  The
+// compact 16-byte format when tb + rb + lb <= 64 (tb: bits of the largest node id, lb: bits of a
+// row length <= n, rb: bits of a row start <= nnz); every thread derives the same choice from
+// nnz = g_ptr[n].
+__global__ __launch_bounds__(256) void walk_aug_kernel(int64_t n, int32_t tb, int32_t lb, int32_t allow16,
+                                                       const int64_t *__restrict__ g_ptr,
                                                        const int32_t *__restrict__ g_idx,
-                                                       const double *__restrict__ g_val, AugRec *__restrict__ aug) {
+                                                       const double *__restrict__ g_val, unsigned char *__restrict__ aug) {
+    const int64_t nnz = g_ptr[n];
+    const int rb = ceil_log2((uint64_t)nnz + 1) > 0 ? ceil_log2((uint64_t)nnz + 1) : 1;
+    const bool compact = allow16 && tb + rb + lb <= 64;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        *reinterpret_cast<int4 *>(aug) = make_int4(compact ? 1 : 0, tb, rb, 0);
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n) return;
     const int lane = threadIdx.x & 63;
+    unsigned char *recs = aug + kAugHeader;
     for (int64_t e = g_ptr[row] + lane; e < g_ptr[row + 1]; e += 64) {
         const int32_t v = g_idx[e];
         const int64_t rs = g_ptr[v];
-        AugRec r;
-        r.v = v;
-        r.rs = (int32_t)(uint32_t)rs;
-        r.len = (int32_t)(g_ptr[v + 1] - rs);
-        r.pad = 0;
-        r.w = g_val[e];
-        r.pad2 = 0.0;
-        aug[e] = r;
+        const int64_t len = g_ptr[v + 1] - rs;
+        if (compact) {
+            AugRec16 r;
+            r.packed = (uint64_t)(uint32_t)v | ((uint64_t)rs << tb) | ((uint64_t)len << (tb + rb));
+            r.w = g_val[e];
+            reinterpret_cast<AugRec16 *>(recs)[e] = r;
+        } else {
+            AugRec r;
+            r.v = v;
+            r.rs = (int32_t)(uint32_t)rs;
+            r.len = (int32_t)len;
+            r.pad = 0;
+            r.w = g_val[e];
+            r.pad2 = 0.0;
+            reinterpret_cast<AugRec *>(recs)[e] = r;
+        }
     }
 }
 
-// ------------------------------------------------------- dense (N, N, L) out
 __global__ __launch_bounds__(256) void steps_densify_kernel(int64_t n_src, int64_t m, int32_t L, int64_t n_cols,
                                                             const int32_t *__restrict__ step_cnt,
                                                             const int32_t *__restrict__ step_idx,
@@ -444,7 +460,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
 #define GRF_PHI_LAUNCH_KT(W, K, KT)                                                                               \
     phi_fused_kernel<W, K, KT><<<(unsigned)n_src, T, lds, st>>>(                                                  \
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val,                                   \
-        reinterpret_cast<const AugRec *>(g_aug), p_halt, rule, (uint32_t)seed,                                      \
+        reinterpret_cast<const unsigned char *>(g_aug), p_halt, rule, (uint32_t)seed,                               \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
         n_cols, count_row0, sort_lds)
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
@@ -506,7 +522,7 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
                             phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream), count_row0);
 }
 
-size_t grf_walk_aug_bytes(int64_t nnz) { return (size_t)(nnz > 0 ? nnz : 0) * sizeof(AugRec); }
+size_t grf_walk_aug_bytes(int64_t nnz) { return kAugHeader + (size_t)(nnz > 0 ? nnz : 0) * sizeof(AugRec); }
 
 int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, void *g_aug,
                      grf_stream_t stream) {
@@ -514,8 +530,13 @@ int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
     GRF_REQUIRE(((uintptr_t)g_aug & 31) == 0, GRF_EINVAL, "grf_walk_aug: g_aug must be 32-byte aligned");
     if (n == 0) return GRF_OK;
     GRF_REQUIRE_GRID(cdiv<int64_t>(n, 4), 256, "walk_aug_kernel");
-    walk_aug_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, S(stream)>>>(n, g_ptr, g_idx, g_val,
-                                                                         reinterpret_cast<AugRec *>(g_aug));
+    // GRF_WALK_AUG16=0: always the 32-byte records (A/B; read per call so tests can cover both formats)
+    const char *e16 = getenv("GRF_WALK_AUG16");
+    const int allow16 = e16 ? atoi(e16) : 1;
+    const int32_t tb = ceil_log2((uint64_t)n) > 0 ? ceil_log2((uint64_t)n) : 1;  // node ids < n
+    const int32_t lb = ceil_log2((uint64_t)n + 1);                               // row lengths <= n
+    walk_aug_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, S(stream)>>>(n, tb, lb, allow16, g_ptr, g_idx, g_val,
+                                                                         reinterpret_cast<unsigned char *>(g_aug));
     GRF_CHECK_LAUNCH("walk_aug_kernel");
     return GRF_OK;
 }

@@ -168,10 +168,12 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
                      int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
                      float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
                      grf_stream_t stream);
-/* The augmented walk matrix of grf_walk_phi: g_aug[e] = {target v, row start of v (low 32 bits),
- * row length of v, 0 (int32 x 4), weight g_val[e] (float64), 0} -- 32 bytes per entry e of the CSR
- * walk matrix (g_ptr, g_idx, g_val): one 64-byte sector per walk step; grf_walk_aug_bytes(nnz)
- * bytes, 32-byte aligned. */
+/* The augmented walk matrix of grf_walk_phi (opaque to the caller): a 32-byte header, then one
+ * record per entry e of the CSR walk matrix (g_ptr, g_idx, g_val) holding the target v, the row
+ * start and row length of v and the weight g_val[e] -- 16 bytes ({v, row start, length} packed
+ * into 64 bits, float64 weight) when the node ids, row starts and lengths fit 64 bits together,
+ * else 32 bytes; one record per walk step either way.  grf_walk_aug_bytes(nnz) bytes (enough for
+ * both), 32-byte aligned. */
 int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, void *g_aug,
                      grf_stream_t stream);
 size_t grf_walk_aug_bytes(int64_t nnz);

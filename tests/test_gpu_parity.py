@@ -702,6 +702,21 @@ def test_walk_phi_augmented_matrix_bitexact(eng, rule):
     mask = torch.arange(a.cap, device=a.cnt.device)[None, :] < a.cnt[:, None]
     assert torch.equal(a.idx.view(-1, a.cap)[mask], b.idx.view(-1, b.cap)[mask])
     assert torch.equal(a.val.view(-1, a.cap)[mask], b.val.view(-1, b.cap)[mask])
+    # the 16-byte records (the default here: the ids, starts and lengths fit 64 bits) and the 32-byte
+    # ones (GRF_WALK_AUG16=0) take the same walks
+    hdr = eng.walk_aug(G)[:16].view(torch.int32).cpu().numpy()
+    assert hdr[0] == 1, hdr
+    import os
+    os.environ["GRF_WALK_AUG16"] = "0"
+    try:
+        G32 = eng.laplacian(A)
+        assert eng.walk_aug(G32)[:16].view(torch.int32).cpu().numpy()[0] == 0
+        c = eng.walk_phi(G32, 40, 0.15, 5, f, seed=11, load_rule=rule, use_aug=True)
+    finally:
+        del os.environ["GRF_WALK_AUG16"]
+    assert torch.equal(c.cnt, a.cnt)
+    assert torch.equal(c.idx.view(-1, c.cap)[mask], a.idx.view(-1, a.cap)[mask])
+    assert torch.equal(c.val.view(-1, c.cap)[mask], a.val.view(-1, a.cap)[mask])
     Ls, _ = O.laplacian_sparse(A)
     ip, ix, dx = O._csr_arrays(Ls)
     node, load = O.walk_slots(ip, ix, dx, 40, 0.15, 5, rng=O.RNG_PHILOX, load_rule=rule, seed=11)
