@@ -10,8 +10,11 @@ __device__ inline void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint
                                      uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        // one 32 x 32 -> 64-bit product per multiplier (v_mad_u64_u32: both halves from one
+        // instruction instead of a v_mul_lo_u32 + v_mul_hi_u32 pair)
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
