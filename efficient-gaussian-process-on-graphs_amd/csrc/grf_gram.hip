@@ -239,9 +239,10 @@ struct GramTiles {
 // arriver overwrites the entries below the diagonal after all rows have been stored.  K is
 // bit-identical to grf_gram_sparse_sym's.
 // MEASURED SLOWER (profiles/r02_fused_ab.txt): 100-150 ms per K against 22.6 for tiles + mirror.
-// The tiles with their tickets cost +0.8 ms and the block loads +5 ms, but the last arrivers'
-// transposed stores (20 GB, one workgroup per 1 MB block) add ~100 ms: one workgroup cannot keep
-// enough stores in flight, where the mirror pass spreads the same bytes over every CU.  Kept as a
+// The tiles with their tickets cost +0.8 ms and the block loads +5 ms (a timing-only decomposition,
+// since removed), but the last arrivers' transposed stores (20 GB, one workgroup per 1 MB block)
+// add ~100 ms: one workgroup cannot keep enough stores in flight, where the mirror pass spreads the
+// same bytes over every CU.  Kept as a
 // tested option (bench --fused); the default stays tiles + mirror.
 #ifndef GRF_FUSE_GROUP
 #define GRF_FUSE_GROUP 64
@@ -266,7 +267,7 @@ template <int kWaves>
 __device__ __forceinline__ void gram_fused_completion(const GramTiles &tl, int64_t J, int64_t r, int64_t j0,
                                                       int64_t wlen, int sh, unsigned long long *acc,
                                                       float *__restrict__ K, int64_t ldk,
-                                                      int32_t *__restrict__ tickets, int32_t exp) {
+                                                      int32_t *__restrict__ tickets) {
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     constexpr int kT = 64 * kWaves;
@@ -304,7 +305,7 @@ __device__ __forceinline__ void gram_fused_completion(const GramTiles &tl, int64
         flag[0] = old == gn - 1;
     }
     __syncthreads();
-    if (!flag[0] || (exp & 2)) return;  // (uniform) not the last of the group
+    if (!flag[0]) return;  // (uniform) not the last of the group
     if (tid < 64) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -334,7 +335,6 @@ __device__ __forceinline__ void gram_fused_completion(const GramTiles &tl, int64
                 const auto y = __builtin_amdgcn_raw_buffer_load_b128(grs, off + (int32_t)(u * ldk * 4), 0, 16);
                 x[u] = f32x4{__uint_as_float(y[0]), __uint_as_float(y[1]), __uint_as_float(y[2]), __uint_as_float(y[3])};
             }
-            if (exp & 8) continue;
             float *dst = K + j * ldk + gs + 4 * q;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
     const unsigned char *__restrict__ t_rec, int32_t unit, const int32_t *__restrict__ rowshift,
-    float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets, int32_t fuse_exp) {
+    float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t W = tl.W;
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     else __builtin_amdgcn_wave_barrier();
 
     if constexpr (kFuse) {
-        gram_fused_completion<kWaves>(tl, J_local, r, j0, wlen, sh, acc, K, ldk, tickets, fuse_exp);
+        gram_fused_completion<kWaves>(tl, J_local, r, j0, wlen, sh, acc, K, ldk, tickets);
         return;
     }
     // write the tile once (non-temporal: K is write-once)
@@ -916,11 +916,6 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
         return e ? (size_t)atoll(e) : (size_t)0;
     }();
     const size_t lds = gram_lds_bytes(tl.W, waves, halves) + lds_pad;
-    static const int fuse_exp = [] {  // GRF_FUSE_EXP: timing-only decomposition of the fused completion (wrong
-                                      // K): 2 = no completion, 8 = the block's loads without its stores
-        const char *e = getenv("GRF_FUSE_EXP");
-        return e ? atoi(e) : 0;
-    }();
     // one launch covers at most 2^32 - 1 work-items: split the tile range
     const int64_t max_tiles = ((1ll << 32) - 1) / (64 * waves);
     for (int64_t t0 = t_first; t0 < t_last; t0 += max_tiles) {
@@ -929,7 +924,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
     gram_sparse_kernel<WV, H, U, T, F><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx,   \
                                                                         val, reinterpret_cast<const uint2 *>(t_desc), \
                                                                         reinterpret_cast<const unsigned char *>(t_rec), \
-                                                                        unit, t_rowshift, K, ldk, tickets, fuse_exp)
+                                                                        unit, t_rowshift, K, ldk, tickets)
 #define GRF_GRAM_LAUNCH_T(WV, H, U, T) GRF_GRAM_LAUNCH_F(WV, H, U, T, false)
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     do {                                                                                                          \
