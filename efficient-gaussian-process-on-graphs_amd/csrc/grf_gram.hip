@@ -733,15 +733,19 @@ template <int BM, int BK>
 __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, int64_t k_dim,
                                                          const float *__restrict__ A, int64_t lda,
                                                          float *__restrict__ K, int64_t ldk, int64_t k_split,
-                                                         int64_t part_stride) {
+                                                         int64_t part_stride, int32_t n_split) {
     constexpr int NB = BM / 64;          // 32 x 32 MFMA blocks per wave and dimension
     constexpr int F4 = BM * BK / 4 / 256;  // float4 loads per thread and operand per k-tile
     __shared__ __attribute__((aligned(16))) float As[BK][BM + kDensePad];
     __shared__ __attribute__((aligned(16))) float Bs[BK][BM + kDensePad];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    // block -> (bi, bj), bj >= bi, row-major over the upper triangle of the nt x nt tile grid
-    const int64_t b = blockIdx.x;
+    // workgroup -> (tile b, k slice): the slice is the fastest index, so with round-robin workgroup
+    // placement over the 8 XCDs all tiles of one slice share an XCD (8 slices: one XCD's L2 holds its
+    // slice of the operand; speed only, never correctness); tile b -> (bi, bj), bj >= bi, row-major
+    // over the upper triangle of the nt x nt tile grid
+    const int64_t b = (int64_t)blockIdx.x / n_split;
+    const int32_t slice = (int32_t)((int64_t)blockIdx.x - b * n_split);
     int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
     auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };
     if (bi < 0) bi = 0;
@@ -759,9 +763,9 @@ __global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, 
 #pragma unroll
             for (int q = 0; q < 16; ++q) c[x][y][q] = 0.f;
 
-    const int64_t kb = (int64_t)blockIdx.y * k_split;
+    const int64_t kb = (int64_t)slice * k_split;
     const int64_t ke = (kb + k_split) < k_dim ? kb + k_split : k_dim;
-    K += (int64_t)blockIdx.y * part_stride;
+    K += (int64_t)slice * part_stride;
     float4 ra[F4], rb[F4];
     auto load = [&](int64_t k0) {
 #pragma unroll
@@ -1236,11 +1240,12 @@ int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda,
     if (ns > 1) ns = (int)cdiv<int64_t>(kpad, k_split);
     float *out = ns > 1 ? reinterpret_cast<float *>(workspace) : K;
     const int64_t ldo = ns > 1 ? ldp : ldk, pstride = ns > 1 ? n * ldp : 0;
-    const dim3 grid((unsigned)tiles, (unsigned)ns);
-    if (big && bk == 32) gram_dense_kernel<128, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride);
-    else if (big) gram_dense_kernel<128, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride);
-    else if (bk == 32) gram_dense_kernel<64, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride);
-    else gram_dense_kernel<64, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride);
+    GRF_REQUIRE_GRID(tiles * ns, 256, "gram_dense_kernel");
+    const unsigned grid = (unsigned)(tiles * ns);
+    if (big && bk == 32) gram_dense_kernel<128, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
+    else if (big) gram_dense_kernel<128, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
+    else if (bk == 32) gram_dense_kernel<64, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
+    else gram_dense_kernel<64, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
     GRF_CHECK_LAUNCH("gram_dense_kernel");
     if (ns == 1) return grf_gram_mirror(n, K, ldk, 0, stream);  // the lower triangle
     const int64_t nt64 = cdiv<int64_t>(n, 64), blocks = nt64 * (nt64 + 1) / 2;
