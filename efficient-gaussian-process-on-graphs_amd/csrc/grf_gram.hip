@@ -125,15 +125,17 @@ struct __attribute__((aligned(4))) RecPair {
 };
 
 // NW windows of 64 pairs starting at stream position w0 (chunk base c0, chunk end cend).
-// TAIL: positions >= cend are masked: they read pair 0 of the band and add exactly 0 to
-// distinct entries.
-template <int NW, bool TAIL>
+// TAIL: positions >= cend are masked (they read pair 0 of the band and add exactly 0 to distinct
+// entries) -- 0: no window, 1: the last window only (an exact tail group: NW = ceil((cend - w0) / 64),
+// so every other window is full), 2: every window.
+template <int NW, int TAIL>
 __device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, int32_t c0, int32_t cend, int lane) {
     int m[NW];
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
         const int32_t p = w0 + u * 64 + lane;
-        m[u] = (!TAIL || p < cend) ? (int)g.bid[p - c0] - 1 : 0;
+        const bool mk = TAIL == 2 || (TAIL == 1 && u == NW - 1);  // (compile-time per window)
+        m[u] = (!mk || p < cend) ? (int)g.bid[p - c0] - 1 : 0;
     }
     int32_t pos[NW];
     double sc[NW];
@@ -145,6 +147,7 @@ __device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, in
     if (TAIL) {
 #pragma unroll
         for (int u = 0; u < NW; ++u) {
+            if (TAIL == 1 && u != NW - 1) continue;
             const bool ok = w0 + u * 64 + lane < cend;
             pos[u] = ok ? pos[u] : 0;  // the band's first pair: valid and finite
             sc[u] = ok ? sc[u] : 0.0;
@@ -166,7 +169,7 @@ __device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, in
         const long long q0 = fx_fma_round(sc[u], (double)rec[u].v0);
         const long long q1 = fx_fma_round(sc[u], (double)rec[u].v1);
         uint32_t c0 = rec[u].cols & 0xffffu, c1 = rec[u].cols >> 16;
-        if (TAIL) {
+        if (TAIL == 2 || (TAIL == 1 && u == NW - 1)) {
             const bool ok = w0 + u * 64 + lane < cend;
             c0 = ok ? c0 : (uint32_t)(lane & 15) * 8u;
             c1 = ok ? c1 : (uint32_t)(lane & 15) * 8u;
@@ -437,23 +440,24 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             __builtin_amdgcn_wave_barrier();
             int32_t w0 = c0;
             for (; w0 + 64 * kGramUnroll <= cend; w0 += 64 * kGramUnroll)
-                gram_windows<kGramUnroll, false>(gs, w0, c0, cend, lane);
+                gram_windows<kGramUnroll, 0>(gs, w0, c0, cend, lane);
             if (w0 < cend) {
                 // last group: exactly the windows left (a group of kGramUnroll would issue up to
                 // kGramUnroll - 1 all-masked windows of loads and LDS adds per batch)
                 if (kTailExact) {
                     switch ((cend - w0 + 63) >> 6) {
-                        case 1: gram_windows<1, true>(gs, w0, c0, cend, lane); break;
-                        case 2: gram_windows<2, true>(gs, w0, c0, cend, lane); break;
-                        case 3: gram_windows<3, true>(gs, w0, c0, cend, lane); break;
-                        case 4: gram_windows<4, true>(gs, w0, c0, cend, lane); break;
-                        case 5: gram_windows<kGramUnroll < 5 ? kGramUnroll : 5, true>(gs, w0, c0, cend, lane); break;
-                        case 6: gram_windows<kGramUnroll < 6 ? kGramUnroll : 6, true>(gs, w0, c0, cend, lane); break;
-                        case 7: gram_windows<kGramUnroll < 7 ? kGramUnroll : 7, true>(gs, w0, c0, cend, lane); break;
-                        default: gram_windows<kGramUnroll, true>(gs, w0, c0, cend, lane); break;
+                        case 1: gram_windows<1, 1>(gs, w0, c0, cend, lane); break;
+                        case 2: gram_windows<2, 1>(gs, w0, c0, cend, lane); break;
+                        case 3: gram_windows<3, 1>(gs, w0, c0, cend, lane); break;
+                        case 4: gram_windows<4, 1>(gs, w0, c0, cend, lane); break;
+                        case 5: gram_windows<kGramUnroll < 5 ? kGramUnroll : 5, 1>(gs, w0, c0, cend, lane); break;
+                        case 6: gram_windows<kGramUnroll < 6 ? kGramUnroll : 6, 1>(gs, w0, c0, cend, lane); break;
+                        case 7: gram_windows<kGramUnroll < 7 ? kGramUnroll : 7, 1>(gs, w0, c0, cend, lane); break;
+                        // (unroll <= 8: exactly kGramUnroll windows are left here; 16: 8 .. 16 are, so every window is masked)
+                        default: gram_windows<kGramUnroll, (kGramUnroll <= 8 ? 1 : 2)>(gs, w0, c0, cend, lane); break;
                     }
                 } else {
-                    gram_windows<kGramUnroll, true>(gs, w0, c0, cend, lane);  // masked last group
+                    gram_windows<kGramUnroll, 2>(gs, w0, c0, cend, lane);  // masked last group
                 }
             }
             __builtin_amdgcn_wave_barrier();

@@ -16,6 +16,8 @@ import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libgrf_amd.so")
+if os.environ.get("GRF_AMD_LIB"):  # (same-box A/B of two builds of the library: tools/gpu_*.sh)
+    LIB_PATH = os.path.abspath(os.environ["GRF_AMD_LIB"])
 CSRC = os.path.join(os.path.dirname(_PKG), "csrc")
 
 GRF_OK, GRF_EINVAL, GRF_EHIP, GRF_ECAPACITY, GRF_EUNSUPPORTED = 0, -1, -2, -3, -4
