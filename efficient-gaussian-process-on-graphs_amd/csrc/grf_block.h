@@ -16,6 +16,19 @@ __device__ inline T wave_inclusive_scan(T v) {
     return v;
 }
 
+// int32: the same scan in DPP steps (row shifts within 16-lane rows, then the row broadcasts of
+// lanes 15 and 31): no ds_bpermute round trips through the LDS pipe; identical sums
+template <>
+__device__ inline int32_t wave_inclusive_scan<int32_t>(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
 template <typename T>
 __device__ inline T wave_sum(T v) {
 #pragma unroll

@@ -66,18 +66,6 @@ __device__ inline int wave_incl_max(int v) {
     return v;
 }
 
-// inclusive sum-scan of ints over the 64 lanes in DPP steps (no ds_bpermute round trips through the
-// LDS pipe, whose latency the batch set-up of every tile would otherwise pay 6 times per scan)
-__device__ inline int32_t wave_incl_add(int32_t v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
-
 // Bucket ids of a chunk of 1024 stream positions from bucket-start markers: bid[p] holds
 // (bucket + 1) at the first position of every non-empty bucket and 0 elsewhere; since the
 // ids increase along the stream, the id of a position is the running maximum.  Lane l owns
@@ -428,7 +416,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
         int32_t total = 0;
 #pragma unroll
         for (int h = 0; h < kHalves; ++h) {
-            const int32_t inc = wave_incl_add(cnt[h]) + total;
+            const int32_t inc = wave_inclusive_scan<int32_t>(cnt[h]) + total;  // (DPP: grf_block.h)
             excl[h] = inc - cnt[h];
             total = __builtin_amdgcn_readlane(inc, 63);
         }
