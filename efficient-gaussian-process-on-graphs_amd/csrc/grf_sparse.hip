@@ -529,7 +529,11 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
                                                             unsigned char *t_rec, int32_t unit) {
     extern __shared__ __attribute__((aligned(16))) unsigned char tps_smem[];
     const int tid = threadIdx.x;
-    const int64_t rg = blockIdx.x, band = rg / nreg, g = rg - band * nreg;
+    // dispatch group x = blockIdx % 8 (one XCD) takes a contiguous run of regions: neighbouring
+    // regions read neighbouring words of the same table lines, which then come from one L2
+    const int64_t nblk = gridDim.x, per8 = nblk / 8, rem8 = nblk % 8;
+    const int64_t x8 = blockIdx.x % 8, k8 = blockIdx.x / 8;
+    const int64_t rg = x8 * per8 + (x8 < rem8 ? x8 : rem8) + k8, band = rg / nreg, g = rg - band * nreg;
     const int64_t c0 = g * cr, c1 = min<int64_t>(n_cols, c0 + cr);
     const int nbk_r = (int)(c1 - c0);
     const int64_t b0 = band * n_cols + c0;
