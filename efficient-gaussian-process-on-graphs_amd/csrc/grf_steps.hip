@@ -177,6 +177,16 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         const int64_t src = src_begin + s;
         for (int64_t w = tid; w < m; w += T) {
             auto visit = [&](int32_t l, int32_t node, double load) {
+                if (l == 0) {
+                    // every walk records (source, step 0) with load 1.0, a run of m equal slots whose
+                    // sum is exactly m: one slot carries it (the same bits as the m-term sum) and the
+                    // head thread no longer walks an m-long run
+                    if (w == 0) {
+                        key[0] = make_key(node, 0, 0);
+                        ld[0] = (double)m;
+                    }
+                    return;
+                }
                 key[l * m + w] = make_key(node, l, w);
                 ld[l * m + w] = load;
             };
