@@ -214,16 +214,18 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     else block_bitonic_sort_regs<KT, kPer>(key, P);  // (P == kPer * blockDim.x)
 
     // ---- step values at (node, step) run heads, kept in registers: loads in walk order from
-    //      0.0 (the run is read 8 keys / loads per LDS round trip; the source's step-0 run is m
-    //      long); thread t owns the sorted positions [t kPer, (t + 1) kPer)
+    //      0.0 (the run is read 8 keys / loads per LDS round trip; the source's step-0 run is one
+    //      slot of load m, see the walk above); thread t owns the sorted positions [t kPer, (t + 1) kPer)
     const int i0 = tid * kPer;
-    KT hk_[kPer];
+    KT hk_[kPer];  // position q's head key (kNone: not a head), its step value
     double hv_[kPer];
     int c = 0;
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
         const int i = i0 + q;
         const KT k = key[i];
+        hk_[q] = kNone;
+        hv_[q] = 0.0;
         if (k == kNone || (i > 0 && (key[i - 1] >> wbits) == (k >> wbits))) continue;
         const KT hk = k >> wbits;
         const KT k1 = i + 1 < P ? key[i + 1] : kNone;
@@ -247,23 +249,20 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                 if (!more) break;
             }
         }
-        const double v = normalise(acc, norm, m);
-#pragma unroll
-        for (int e = 0; e < kPer; ++e)  // static register indexing
-            if (e == c) {
-                hk_[e] = k;
-                hv_[e] = v;
-            }
+        hk_[q] = k;  // (static register indexing: q is the unrolled position)
+        hv_[q] = normalise(acc, norm, m);
         ++c;
     }
     // ---- compact the step heads (sorted order): key -> key[rank], value -> ld[rank]
     int32_t n_heads;
     const int32_t rank0 = block_exclusive_scan_fast<int32_t>(c, scratch, &n_heads);  // (barrier: reads done)
+    int32_t r0 = rank0;
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
-        if (q < c) {
-            key[rank0 + q] = hk_[q];
-            ld[rank0 + q] = hv_[q];
+        if (hk_[q] != kNone) {
+            key[r0] = hk_[q];
+            ld[r0] = hv_[q];
+            ++r0;
         }
     }
     __syncthreads();
@@ -272,11 +271,14 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     const int per2 = (n_heads + T - 1) / T;  // <= kPer
     const int q0 = tid * per2;
     int emit = 0;
-    double pv_[kPer];
+    double pv_[kPer];   // position qq's Phi value, its node (-1: no entry)
     int32_t pn_[kPer];
-    for (int qq = 0; qq < per2; ++qq) {
+#pragma unroll
+    for (int qq = 0; qq < kPer; ++qq) {
+        pn_[qq] = -1;
+        pv_[qq] = 0.0;
         const int q = q0 + qq;
-        if (q >= n_heads) break;
+        if (qq >= per2 || q >= n_heads) continue;
         const KT k = key[q];
         if (q > 0 && (key[q - 1] >> sh) == (k >> sh)) continue;  // not a node head
         double acc = 0.0;
@@ -290,12 +292,8 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
             }
         }
         if (present && acc != 0.0) {
-#pragma unroll
-            for (int e = 0; e < kPer; ++e)  // static register indexing: pv_[emit] without a dynamic index
-                if (e == emit) {
-                    pv_[e] = acc;
-                    pn_[e] = (int32_t)(k >> sh);
-                }
+            pv_[qq] = acc;  // (static register indexing)
+            pn_[qq] = (int32_t)(k >> sh);
             ++emit;
         }
     }
@@ -303,13 +301,16 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     int32_t rank = block_exclusive_scan_fast<int32_t>(emit, scratch + 16, &total);
     const int64_t obase = s * cap;
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        if (q < emit && rank + q < cap) {
-            phi_idx[obase + rank + q] = pn_[q];
-            if (phi_val) phi_val[obase + rank + q] = pv_[q];  // (NULL: the caller keeps the f32 copy only)
-            if (phi_val32) phi_val32[obase + rank + q] = (float)pv_[q];
-            // the banded transpose's bucket counts of this row's entries (grf_transpose_banded_plan)
-            if (t_count) atomicAdd(&t_count[((src_begin + s - count_row0) / band_width) * n_cols + pn_[q]], 1);
+    for (int qq = 0; qq < kPer; ++qq) {
+        if (pn_[qq] >= 0) {
+            if (rank < cap) {
+                phi_idx[obase + rank] = pn_[qq];
+                if (phi_val) phi_val[obase + rank] = pv_[qq];  // (NULL: the caller keeps the f32 copy only)
+                if (phi_val32) phi_val32[obase + rank] = (float)pv_[qq];
+                // the banded transpose's bucket counts of this row's entries (grf_transpose_banded_plan)
+                if (t_count) atomicAdd(&t_count[((src_begin + s - count_row0) / band_width) * n_cols + pn_[qq]], 1);
+            }
+            ++rank;
         }
     }
     if (tid == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
