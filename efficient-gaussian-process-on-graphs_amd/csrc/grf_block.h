@@ -122,57 +122,65 @@ __device__ __forceinline__ KT lane_xor(KT v) {
     }
 }
 
+// the compare-exchange of one key with its partner's: the minimum when take_min, else the maximum
+// (u32 keys: v_min_u32 / v_max_u32 + one select)
+template <typename KT>
+__device__ __forceinline__ KT bitonic_keep(KT a, KT o, bool take_min) {
+    const KT mn = o < a ? o : a, mx = o < a ? a : o;
+    return take_min ? mn : mx;
+}
+
 template <int TJ, typename KT, int R>
 __device__ __forceinline__ void bitonic_lane_stage(KT (&v)[R], int tid, int k) {
     if (TJ * R < k) {
-        const bool lo = (tid & TJ) == 0;
+        // k > TJ R >= R: bit k of the position tid R + r is bit k of tid R for every r (r < R), so
+        // the direction is the thread's, computed once per stage
+        const bool take_min = ((tid & TJ) == 0) == (((tid * R) & k) == 0);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const KT o = lane_xor<TJ>(v[r]);
-            const bool asc = ((tid * R + r) & k) == 0;
-            v[r] = (lo == asc) ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
-        }
+        for (int r = 0; r < R; ++r) v[r] = bitonic_keep(v[r], lane_xor<TJ>(v[r]), take_min);
     }
 }
 
-// Bitonic sort (ascending) of P = R * blockDim.x keys with each thread holding the R consecutive
-// keys [tid R, (tid + 1) R) in registers: the stages whose partner is in the same thread (j < R)
-// run in registers, the ones whose partner thread is in the same wave through lane shuffles, and
-// only partners in another wave go through LDS -- against two LDS reads, up to two writes and a
-// barrier per pair and stage for block_bitonic_sort.  Same result (a sorting network; keys equal
-// only when interchangeable).  Reads its keys from key[] and writes the sorted keys back; the
-// caller must __syncthreads() before (keys written); the sorted key[] is visible on return.
+// One merge level k of block_bitonic_sort_regs (inlined with a compile-time k when the size is a
+// template argument, so every stage's condition folds and the network is straight-line code: no
+// register copies at the merge points of runtime-conditional stages).
 template <typename KT, int R>
-__device__ inline void block_bitonic_sort_regs(KT *key, int P) {
-    const int tid = threadIdx.x;
-    KT v[R];
+__device__ __forceinline__ void bitonic_regs_level(KT (&v)[R], KT *key, int tid, int k) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = key[tid * R + r];
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j >= 64 * R; j >>= 1) {  // partner thread tid ^ (j / R) in another wave
-            const int tj = j / R;
-            const bool lo = (tid & tj) == 0;
-            __syncthreads();  // (key[] may still be read by a previous cross-wave stage)
+    for (int j = k >> 1; j >= 64 * R; j >>= 1) {  // partner thread tid ^ (j / R) in another wave
+        const int tj = j / R;
+        const bool lo = (tid & tj) == 0;
+        __syncthreads();  // (key[] may still be read by a previous cross-wave stage)
 #pragma unroll
-            for (int r = 0; r < R; ++r) key[tid * R + r] = v[r];
-            __syncthreads();
+        for (int r = 0; r < R; ++r) key[tid * R + r] = v[r];
+        __syncthreads();
+        const bool take_min = lo == (((tid * R) & k) == 0);  // (k > R: the thread's direction)
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const KT o = key[(tid ^ tj) * R + r];
-                const bool asc = ((tid * R + r) & k) == 0;
-                v[r] = (lo == asc) ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
-            }
-        }
-        // partner lane tid ^ tj in this wave
-        bitonic_lane_stage<32>(v, tid, k);
-        bitonic_lane_stage<16>(v, tid, k);
-        bitonic_lane_stage<8>(v, tid, k);
-        bitonic_lane_stage<4>(v, tid, k);
-        bitonic_lane_stage<2>(v, tid, k);
-        bitonic_lane_stage<1>(v, tid, k);
+        for (int r = 0; r < R; ++r) v[r] = bitonic_keep(v[r], key[(tid ^ tj) * R + r], take_min);
+    }
+    // partner lane tid ^ tj in this wave
+    bitonic_lane_stage<32>(v, tid, k);
+    bitonic_lane_stage<16>(v, tid, k);
+    bitonic_lane_stage<8>(v, tid, k);
+    bitonic_lane_stage<4>(v, tid, k);
+    bitonic_lane_stage<2>(v, tid, k);
+    bitonic_lane_stage<1>(v, tid, k);
 #pragma unroll
-        for (int jj = R / 2; jj >= 1; jj >>= 1) {  // partner in this thread's registers (static indices)
-            if (jj < k) {
+    for (int jj = R / 2; jj >= 1; jj >>= 1) {  // partner in this thread's registers (static indices)
+        if (jj < k) {
+            if (k >= R) {  // one direction for the whole thread (bit k of tid R + r is tid R's)
+                const bool asc = ((tid * R) & k) == 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int p = r ^ jj;
+                    if (p > r) {
+                        const KT a = v[r], b = v[p];
+                        const KT mn = b < a ? b : a, mx = b < a ? a : b;
+                        v[r] = asc ? mn : mx;
+                        v[p] = asc ? mx : mn;
+                    }
+                }
+            } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const int p = r ^ jj;
@@ -186,6 +194,29 @@ __device__ inline void block_bitonic_sort_regs(KT *key, int P) {
                 }
             }
         }
+    }
+}
+
+// Bitonic sort (ascending) of P = R * blockDim.x keys with each thread holding the R consecutive
+// keys [tid R, (tid + 1) R) in registers: the stages whose partner is in the same thread (j < R)
+// run in registers, the ones whose partner thread is in the same wave through lane shuffles, and
+// only partners in another wave go through LDS -- against two LDS reads, up to two writes and a
+// barrier per pair and stage for block_bitonic_sort.  Same result (a sorting network; keys equal
+// only when interchangeable).  Reads its keys from key[] and writes the sorted keys back; the
+// caller must __syncthreads() before (keys written); the sorted key[] is visible on return.
+// kP > 0: the size P = kP is a compile-time constant (the network fully unrolled); kP = 0: P at
+// run time (P == R * blockDim.x either way).
+template <typename KT, int R, int kP = 0>
+__device__ inline void block_bitonic_sort_regs(KT *key, int P) {
+    const int tid = threadIdx.x;
+    KT v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = key[tid * R + r];
+    if constexpr (kP > 0) {
+#pragma unroll
+        for (int k = 2; k <= kP; k <<= 1) bitonic_regs_level<KT, R>(v, key, tid, k);
+    } else {
+        for (int k = 2; k <= P; k <<= 1) bitonic_regs_level<KT, R>(v, key, tid, k);
     }
     __syncthreads();  // (cross-wave stages: every read of key[] done)
 #pragma unroll

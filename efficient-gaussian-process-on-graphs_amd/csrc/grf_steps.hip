@@ -137,7 +137,9 @@ __global__ __launch_bounds__(256) void phi_merge_kernel(int64_t n_src, int64_t m
 // workgroup (kWalk = true, grf_walk_phi: no slot round trip through HBM).
 constexpr int kPhiMaxPer = 16;  // sorted positions per thread (P <= 4096, 256 threads)
 
-template <bool kWalk, int kPer, typename KT>  // kPer = P / blockDim.x sorted positions per thread
+// kPer = P / blockDim.x sorted positions per thread; kT > 0: blockDim.x == kT, known at compile time
+// (the sort network then unrolls into straight-line code)
+template <bool kWalk, int kPer, typename KT, int kT = 0>
 __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, int32_t norm, int32_t P, int32_t wbits,
                                                         int32_t lbits, const int32_t *__restrict__ slot_node,
                                                         const double *__restrict__ slot_load,
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     // keys when (node, step, walk) fits 32 bits (C4 / C5): half the sort's LDS traffic and a
     // third of the footprint of the 64-bit layout with its separate head-value array.
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    const int E = (int)(m * L), T = (int)blockDim.x, tid = (int)threadIdx.x;
+    const int E = (int)(m * L), T = kT > 0 ? kT : (int)blockDim.x, tid = (int)threadIdx.x;
     double *ld = reinterpret_cast<double *>(smem);             // [E]
     double *fl = ld + E;                                        // [Lf rounded up to even]
     int32_t *scratch = reinterpret_cast<int32_t *>(fl + ((Lf + 1) & ~1));  // [32]
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     }
     __syncthreads();
     if (sort_lds) block_bitonic_sort<KT>(key, P);
-    else block_bitonic_sort_regs<KT, kPer>(key, P);  // (P == kPer * blockDim.x)
+    else block_bitonic_sort_regs<KT, kPer, kT * kPer>(key, P);  // (P == kPer * blockDim.x)
 
     // ---- step values at (node, step) run heads, kept in registers: loads in walk order from
     //      0.0 (the run is read 8 keys / loads per LDS round trip; the source's step-0 run is one
@@ -468,12 +470,13 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     GRF_REQUIRE(P / T <= kPhiMaxPer, GRF_EUNSUPPORTED, "grf_phi_fused: too many positions per thread");
     const int32_t Lf = n_f < L ? n_f : L;
     GRF_REQUIRE_GRID(n_src, T, "phi_fused_kernel");
-#define GRF_PHI_LAUNCH_KT(W, K, KT)                                                                               \
-    phi_fused_kernel<W, K, KT><<<(unsigned)n_src, T, lds, st>>>(                                                  \
+#define GRF_PHI_LAUNCH_KTT(W, K, KT, TT)                                                                           \
+    phi_fused_kernel<W, K, KT, TT><<<(unsigned)n_src, T, lds, st>>>(                                              \
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val,                                   \
         reinterpret_cast<const unsigned char *>(g_aug), p_halt, rule, (uint32_t)seed,                               \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
         n_cols, count_row0, sort_lds)
+#define GRF_PHI_LAUNCH_KT(W, K, KT) GRF_PHI_LAUNCH_KTT(W, K, KT, 0)
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
     do {                                                                                                          \
         if (key32) GRF_PHI_LAUNCH_KT(W, K, uint32_t);                                                             \
@@ -487,10 +490,15 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
         case 8: GRF_PHI_LAUNCH(W, 8); break;                                                                      \
         default: GRF_PHI_LAUNCH(W, 16); break;                                                                    \
     }
-    if (walk) { GRF_PHI_PER(true) } else { GRF_PHI_PER(false) }
+    // the walking configurations of C4 (m = 128, L = 8: 128 threads) and C5 (m = 64: 64 threads),
+    // 8 positions per thread, 32-bit keys: the sort fully unrolled
+    if (walk && key32 && P / T == 8 && T == 128) GRF_PHI_LAUNCH_KTT(true, 8, uint32_t, 128);
+    else if (walk && key32 && P / T == 8 && T == 64) GRF_PHI_LAUNCH_KTT(true, 8, uint32_t, 64);
+    else if (walk) { GRF_PHI_PER(true) } else { GRF_PHI_PER(false) }
 #undef GRF_PHI_PER
 #undef GRF_PHI_LAUNCH
 #undef GRF_PHI_LAUNCH_KT
+#undef GRF_PHI_LAUNCH_KTT
     GRF_CHECK_LAUNCH("phi_fused_kernel");
     return GRF_OK;
 }
