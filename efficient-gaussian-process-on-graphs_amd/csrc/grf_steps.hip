@@ -170,6 +170,11 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     auto make_key = [&](int32_t node, int l, int64_t w) {
         return (KT)(((KT)(uint32_t)node << sh) | ((KT)l << wbits) | (KT)w);
     };
+    // the load slot l m + w of a key, in 32-bit arithmetic (m L <= 4096)
+    const uint32_t mu = (uint32_t)m;
+    auto slot_of = [&](KT k) -> uint32_t {
+        return __umul24((uint32_t)((k >> wbits) & lmask), mu) + (uint32_t)(k & wmask);
+    };
 
     for (int l = tid; l < Lf; l += T) fl[l] = f[l];
     // ---- slots -> keys
@@ -189,8 +194,9 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                     }
                     return;
                 }
-                key[l * m + w] = make_key(node, l, w);
-                ld[l * m + w] = load;
+                const uint32_t t = __umul24((uint32_t)l, mu) + (uint32_t)w;
+                key[t] = make_key(node, l, w);
+                ld[t] = load;
             };
             if (g_aug) philox_walk_aug(g_ptr, g_aug, src, (uint32_t)w, p_halt, L, rule, k0, k1, visit);
             else philox_walk(g_ptr, g_idx, g_val, src, (uint32_t)w, p_halt, L, rule, k0, k1, visit);
@@ -231,9 +237,9 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         if (k == kNone || (i > 0 && (key[i - 1] >> wbits) == (k >> wbits))) continue;
         const KT hk = k >> wbits;
         const KT k1 = i + 1 < P ? key[i + 1] : kNone;
-        double acc = 0.0 + ld[((k >> wbits) & lmask) * m + (k & wmask)];
+        double acc = 0.0 + ld[slot_of(k)];
         if ((k1 >> wbits) == hk) {  // a run of more than one visit: 8 keys / loads per round trip
-            acc += ld[((k1 >> wbits) & lmask) * m + (k1 & wmask)];
+            acc += ld[slot_of(k1)];
             for (int j = i + 2;; j += 8) {
                 KT kk[8];
                 double lv[8];
@@ -241,7 +247,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                 for (int r = 0; r < 8; ++r) kk[r] = j + r < P ? key[j + r] : kNone;
 #pragma unroll
                 for (int r = 0; r < 8; ++r)
-                    lv[r] = (kk[r] >> wbits) == hk ? ld[((kk[r] >> wbits) & lmask) * m + (kk[r] & wmask)] : 0.0;
+                    lv[r] = (kk[r] >> wbits) == hk ? ld[slot_of(kk[r])] : 0.0;
                 bool more = true;
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
