@@ -146,8 +146,7 @@ __device__ __forceinline__ void bitonic_lane_stage(KT (&v)[R], int tid, int k) {
 // register copies at the merge points of runtime-conditional stages).
 template <typename KT, int R>
 __device__ __forceinline__ void bitonic_regs_level(KT (&v)[R], KT *key, int tid, int k) {
-#pragma unroll
-    for (int j = k >> 1; j >= 64 * R; j >>= 1) {  // partner thread tid ^ (j / R) in another wave
+    for (int j = k >> 1; j >= 64 * R; j >>= 1) {  // (a constant trip count of 0-2 when k is: unrolled by itself)  // partner thread tid ^ (j / R) in another wave
         const int tj = j / R;
         const bool lo = (tid & tj) == 0;
         __syncthreads();  // (key[] may still be read by a previous cross-wave stage)
