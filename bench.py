@@ -57,6 +57,22 @@ def pmc_traffic(kernels):
     return total
 
 
+def pmc_counter(kernel, counter):
+    """One counter's per-launch value of the named kernel from the committed PMC summary (None if absent)."""
+    import json as _json
+    try:
+        d = _json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None
+    hits = [v for name, v in d.items() if name.split("<")[0].replace("void ", "") == kernel]
+    return hits[0].get(counter) if hits else None
+
+
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 4 cycles at the 2.4 GHz
+# peak engine clock (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 4
+
+
 def init_distributed(local_rank: int) -> int:
     """One process per GPU over RCCL (backend "nccl").  GRF_DIST_BACKEND=gloo rehearses the same
     multi-process path with several ranks on one GPU (device tensors staged through host memory
@@ -652,6 +668,9 @@ def main():
     walk_alg = 16.0 * moves + 8.0 * local_nnz
     walk_achieved = walk_alg / (walk_ms * 1e-3) / 1e9
     walk_traffic = pmc_traffic(["grf::phi_fused_kernel"]) if headline else None
+    # the walk is VALU-issue-bound: its wave-instructions per launch over its live time
+    walk_valu = pmc_counter("grf::phi_fused_kernel", "SQ_INSTS_VALU") if headline else None
+    walk_valu_rate = walk_valu / (walk_ms * 1e-3) / 1e9 if walk_valu and walk_ms else None
     wl = workload_name(args, A)
     if args.k_rows:
         metric = (f"GRF kernel rows/sec ({wl['short']}, m={m} walks: Phi of all N nodes + a {args.k_rows}-row "
@@ -699,8 +718,17 @@ def main():
                      if traffic is not None else None,
                      "kernel": "+".join(k.split("::")[1] for k in kernels), "kernel_ms": gram_avg,
                      "algorithmic_bytes": alg_bytes},
-        "roofline_walk": {"bound": "hbm", "achieved": walk_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": walk_achieved / HBM_PEAK_GBS, "traffic": walk_traffic,
+        "roofline_walk": {"bound": "valu" if walk_valu_rate is not None else "hbm",
+                          "achieved": walk_valu_rate if walk_valu_rate is not None else walk_achieved,
+                          "peak": VALU_PEAK_GINST if walk_valu_rate is not None else HBM_PEAK_GBS,
+                          "unit": "G VALU wave-instructions/s" if walk_valu_rate is not None else "GB/s",
+                          "frac": (walk_valu_rate / VALU_PEAK_GINST) if walk_valu_rate is not None
+                          else walk_achieved / HBM_PEAK_GBS,
+                          "valu_insts_per_launch": walk_valu,
+                          "valu_source": (f"rocprofv3 --pmc SQ_INSTS_VALU of the same kernel on this workload, "
+                                          f"{os.path.relpath(PMC_SUMMARY, ROOT)}") if walk_valu is not None else None,
+                          "hbm": {"achieved": walk_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": walk_achieved / HBM_PEAK_GBS, "traffic": walk_traffic},
                           "kernel": "phi_fused_kernel (fused Philox walks -> Phi rows)",
                           "kernel_ms": walk_ms, "algorithmic_bytes": walk_alg,
                           "algorithmic_note": f"16 B per expected recorded move ({moves:.4g}) + 8 B per Phi "
