@@ -221,33 +221,55 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     if (sort_lds) block_bitonic_sort<KT>(key, P);
     else block_bitonic_sort_regs<KT, kPer, kT * kPer>(key, P);  // (P == kPer * blockDim.x)
 
-    // ---- step values at (node, step) run heads, kept in registers: loads in walk order from
-    //      0.0 (the run is read 8 keys / loads per LDS round trip; the source's step-0 run is one
-    //      slot of load m, see the walk above); thread t owns the sorted positions [t kPer, (t + 1) kPer)
+    // ---- step values of the (node, step) runs, kept in registers: loads in walk order from 0.0.
+    //      Thread t owns the sorted positions [t kPer, (t + 1) kPer) and the runs whose first visit
+    //      is among them; it scans its positions once, left to right, and records each run's value
+    //      at the run's last position in the block (so the runs stay in sorted order).  Only a run
+    //      still open at the block's end reads on into the next threads' positions (8 keys / loads
+    //      per LDS round trip) -- one such loop per thread instead of one per head: the wave no
+    //      longer runs the loop body once per position whenever any lane has a longer run there.
+    //      (The source's step-0 run is one slot of load m, see the walk above.)
     const int i0 = tid * kPer;
-    KT hk_[kPer];  // position q's head key (kNone: not a head), its step value
+    KT kq[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) kq[q] = key[i0 + q];
+    const KT kprev = i0 > 0 ? key[i0 - 1] : kNone;
+    KT hk_[kPer];  // the key of the run recorded at position q (kNone: none), its step value
     double hv_[kPer];
     int c = 0;
+    KT run_k = kNone;
+    double acc = 0.0;
+    bool owned = false;  // the open run started in this block
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
-        const int i = i0 + q;
-        const KT k = key[i];
+        const KT k = kq[q];
+        const KT before = q == 0 ? kprev : kq[q - 1];
         hk_[q] = kNone;
         hv_[q] = 0.0;
-        if (k == kNone || (i > 0 && (key[i - 1] >> wbits) == (k >> wbits))) continue;
-        const KT hk = k >> wbits;
-        const KT k1 = i + 1 < P ? key[i + 1] : kNone;
-        double acc = 0.0 + ld[slot_of(k)];
-        if ((k1 >> wbits) == hk) {  // a run of more than one visit: 8 keys / loads per round trip
-            acc += ld[slot_of(k1)];
-            for (int j = i + 2;; j += 8) {
+        if (k == kNone) {
+            owned = false;  // (sorted: only sentinels from here on)
+            continue;
+        }
+        if ((before >> wbits) != (k >> wbits)) {  // a run's first visit: this thread owns it
+            run_k = k;
+            acc = 0.0 + ld[slot_of(k)];
+            owned = true;
+        } else if (owned) {
+            acc += ld[slot_of(k)];
+        }
+        if (!owned) continue;  // (a run owned by an earlier thread)
+        if (q < kPer - 1) {
+            if ((kq[q + 1] >> wbits) == (k >> wbits)) continue;  // the run goes on in this block
+        } else {
+            // the block's last position: read on while the run continues
+            const KT hk = k >> wbits;
+            for (int j = i0 + kPer;; j += 8) {
                 KT kk[8];
                 double lv[8];
 #pragma unroll
                 for (int r = 0; r < 8; ++r) kk[r] = j + r < P ? key[j + r] : kNone;
 #pragma unroll
-                for (int r = 0; r < 8; ++r)
-                    lv[r] = (kk[r] >> wbits) == hk ? ld[slot_of(kk[r])] : 0.0;
+                for (int r = 0; r < 8; ++r) lv[r] = (kk[r] >> wbits) == hk ? ld[slot_of(kk[r])] : 0.0;
                 bool more = true;
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
@@ -257,8 +279,9 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                 if (!more) break;
             }
         }
-        hk_[q] = k;  // (static register indexing: q is the unrolled position)
+        hk_[q] = run_k;  // (static register indexing: q is the unrolled position)
         hv_[q] = normalise(acc, norm, m);
+        owned = false;
         ++c;
     }
     // ---- compact the step heads (sorted order): key -> key[rank], value -> ld[rank]
