@@ -471,6 +471,10 @@ def main():
     ap.add_argument("--balance", choices=["nodes", "phi"], default="nodes",
                     help="N > 1 source shards: equal node ranges (default), or ranges of equal estimated step work "
                          "from the per-source Phi row counts of one setup walk (dist.balanced_shards)")
+    ap.add_argument("--gather-bound", choices=["exact", "cap"], default="exact",
+                    help="N > 1 Phi all-gather size per rank: the rank's Phi entries from the setup walk "
+                         "(default; checked on the device, a larger step raises after the loop) or its rows x "
+                         "the padded row capacity")
     ap.add_argument("--no-mfma-leg", action="store_true",
                     help="skip the C3 dense MFMA Gram leg that adds roofline_mfma to the headline line")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
@@ -505,11 +509,21 @@ def main():
     f = diffusion_modulator(L, 1.0)
     A_dev = DeviceCSR.from_scipy(A, dev)
     shards = None
-    if world > 1 and args.balance != "nodes":
-        from grf_amd.dist import balanced_shards
-        shards = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance)  # (setup, untimed)
+    phi0 = None
+    if world > 1:
+        from grf_amd.dist import balanced_shards, setup_phi
+        phi0 = setup_phi(eng, A_dev, m, p, L, f, seed=42)  # (setup, untimed: the Phi every step makes)
+        if args.balance != "nodes":
+            shards = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance, phi=phi0)
     pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
                      band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused)
+    if phi0 is not None:
+        if args.gather_bound == "exact":
+            # the Phi all-gather moves each rank's actual entries (C4: 435 per row) instead of its rows x
+            # the padded row capacity (1024); a step whose Phi outgrew it would raise after the loop
+            from grf_amd.dist import shard_entries
+            pl.gather_bound = max(shard_entries(phi0, pl.shards))
+        del phi0
     b, e, kr_end = pl.b, pl.e, pl.kr_end
     K = P.alloc_k(eng, pl)  # resident output block, reused
     if args.overlap is None:
@@ -635,6 +649,9 @@ def main():
     torch.cuda.synchronize()
     serial_ms = 1000.0 * (time.perf_counter() - t1) / 3
     args.overlap = ov
+    if world > 1:
+        from grf_amd.dist import check_gather_overflow
+        check_gather_overflow(dev)  # (raises if a bounded all-gather truncated a rank's Phi)
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
     walk_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in walk_ev]))
     if world > 1:
@@ -703,6 +720,7 @@ def main():
                                + " resident in HBM",
                    "n_nodes": n, "n_edges": int(A.nnz // 2), "walks_per_node": m, "max_walk_length": L,
                    "k_rows_per_gpu": rows, "shard": [b, e], "balance": args.balance if world > 1 else None,
+                   "gather_entries_per_rank": pl.gather_bound or None,
                    "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
                                    f"RCCL all-reduce (K replicated)") if pl.mode == "allreduce" else
                                   (f"source-sharded x{world}, Phi all-gather, K column blocks K[:, R_r] from each "

@@ -121,21 +121,50 @@ def row_costs(engine, phi) -> torch.Tensor:
     return _K_WRITE_NS_PER_ENTRY * n_cols + _GATHER_NS_PER_RECORD * g
 
 
+def setup_phi(engine, A, m: int, p_halt: float, L: int, f, *, seed: int = 42):
+    """Phi of ALL sources from one setup walk (float32 CSR on the engine's device).  Philox is keyed
+    by (seed, source, walk), so every rank computes the identical Phi without a collective, and it
+    is the Phi every step with this seed produces.  Run once, outside the timed steps."""
+    G = engine.laplacian(A)
+    return engine.compact(engine.walk_phi(G, m, p_halt, L, f, seed=seed, want64=False), want64=False)
+
+
 def balanced_shards(engine, A, m: int, p_halt: float, L: int, f, world: int, *, seed: int = 42,
-                    policy: str = "phi") -> List[Tuple[int, int]]:
-    """Source shards of equal estimated step time.  policy "phi": one setup walk of ALL sources
-    (Philox is keyed by (seed, source, walk), so every rank computes the identical Phi without a
-    collective, and Phi is the same every step) gives each row's cost (``row_costs``), and the
-    ranks get contiguous ranges of equal total cost.  policy "nodes": equal node counts.
+                    policy: str = "phi", phi=None) -> List[Tuple[int, int]]:
+    """Source shards of equal estimated step time.  policy "phi": the setup walk's Phi (``setup_phi``,
+    or ``phi`` when the caller already has it) gives each row's cost (``row_costs``), and the ranks
+    get contiguous ranges of equal total cost.  policy "nodes": equal node counts.
     Run once per (graph, m, L, seed), outside the timed steps."""
     if policy == "nodes":
         n = A.n_rows if hasattr(A, "n_rows") else A.shape[0]
         return [shard_range(n, r, world) for r in range(world)]
     if policy != "phi":
         raise ValueError(f"policy must be 'phi' or 'nodes', got {policy!r}")
-    G = engine.laplacian(A)
-    phi = engine.compact(engine.walk_phi(G, m, p_halt, L, f, seed=seed, want64=False), want64=False)
+    if phi is None:
+        phi = setup_phi(engine, A, m, p_halt, L, f, seed=seed)
     return shard_bounds(row_costs(engine, phi).cpu().numpy(), world)
+
+
+def shard_entries(phi, shards: Sequence[Tuple[int, int]]) -> List[int]:
+    """Phi entries of every shard's rows (one host read of the row pointer; setup only).  With the
+    step's seed these are exactly the entries each rank's compaction produces every step, so their
+    maximum is a tight ``entries_bound`` for the sync-free Phi all-gather (``gather_phi``)."""
+    ptr = phi.ptr.cpu()
+    return [int(ptr[e] - ptr[b]) for b, e in shards]
+
+
+_GATHER_OVERFLOW = {}  # device -> int32 flag: a bounded all-gather met a rank with more entries than its bound
+
+
+def check_gather_overflow(device) -> None:
+    """Raise if any bounded Phi all-gather on ``device`` since the last check met a rank whose
+    entries exceeded the bound (that rank's rows were gathered empty, so K is wrong).  One host read;
+    call it after the timed steps."""
+    flag = _GATHER_OVERFLOW.get(torch.device(device))
+    if flag is not None and int(flag.item()):
+        flag.zero_()
+        raise RuntimeError("bounded Phi all-gather: a rank's Phi entries exceeded entries_bound "
+                           "(the gathered Phi is incomplete; size the bound from this step's seed)")
 
 
 def allgather_csr_rows_bounded(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor,
@@ -145,7 +174,9 @@ def allgather_csr_rows_bounded(ptr: torch.Tensor, idx: torch.Tensor, val: torch.
     rows x the padded row capacity; entries past its nnz are ignored) and its row pointers padded
     to the largest shard; the full row pointers come from the gathered counts on the device, and
     ``grf_concat_segments`` packs each rank's entries to its final offset.  The row counts are the
-    host-known shard sizes.  Returns (ptr, idx, val) of the concatenation (nnz = ptr[-1], read
+    host-known shard sizes.  A tighter ``entries_bound`` (``shard_entries`` of the setup walk) moves
+    only the entries that exist; a rank above it is gathered empty and flagged
+    (``check_gather_overflow``).  Returns (ptr, idx, val) of the concatenation (nnz = ptr[-1], read
     lazily; idx / val are sized world x entries_bound)."""
     from . import _lib as C
     from .engine import _p, get_engine
@@ -167,12 +198,18 @@ def allgather_csr_rows_bounded(ptr: torch.Tensor, idx: torch.Tensor, val: torch.
     g_val = torch.empty(world * B, dtype=val.dtype, device=dev)
     _all_gather_into(g_idx, send_i.contiguous(), group=group)
     _all_gather_into(g_val, send_v.contiguous(), group=group)
-    counts = torch.cat([g_ptr[r, 1:n_r + 1] - g_ptr[r, :n_r] for r, n_r in enumerate(rows_per_rank)])
+    # a rank whose entries exceed the bound sent a truncated segment: its rows are gathered empty
+    # (every read and write stays inside the buffers) and the overflow flag is raised on the device
+    seg_len = torch.stack([g_ptr[r, n_r] for r, n_r in enumerate(rows_per_rank)]).contiguous()
+    fits = seg_len <= B
+    flag = _GATHER_OVERFLOW.setdefault(dev, torch.zeros((), dtype=torch.int32, device=dev))
+    flag.bitwise_or_((~fits.all()).to(torch.int32))
+    seg_len = seg_len * fits
+    counts = torch.cat([(g_ptr[r, 1:n_r + 1] - g_ptr[r, :n_r]) * fits[r] for r, n_r in enumerate(rows_per_rank)])
     full_ptr = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=dev)
     full_ptr[1:] = torch.cumsum(counts, 0)
     row0 = torch.tensor([0] + list(torch.tensor(rows_per_rank).cumsum(0)[:-1].tolist()), dtype=torch.int64,
                         device=dev)
-    seg_len = torch.stack([g_ptr[r, n_r] for r, n_r in enumerate(rows_per_rank)]).contiguous()
     dst_off = full_ptr[row0].contiguous()
     out_i = torch.empty(world * B, dtype=idx.dtype, device=dev)
     out_v = torch.empty(world * B, dtype=val.dtype, device=dev)
@@ -238,12 +275,14 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
     return full_ptr, torch.cat(parts_i), torch.cat(parts_v)
 
 
-def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards=None):
+def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards=None, entries_bound=None):
     """All ranks' Phi rows (CSR, float32) from this rank's compacted rows ``local``.
 
     shards: every rank's (begin, end) source range.  When given and ``local`` came from a
     sync-free compaction (``nnz_bound`` = rows x row capacity), the gather reads nothing back to
     the host (``allgather_csr_rows_bounded``); otherwise one host read sizes it exactly.
+    entries_bound: the per-rank entry bound of that gather (default: rows x the row capacity, which
+    no rank can exceed; ``shard_entries`` of the setup walk gives the exact, ~2.4x smaller one at C4).
 
     count_ws: this rank's transpose workspace in which ``walk_phi`` counted the banded transpose's
     buckets for its own rows (global band ids, bands of ``band_width``).  The per-rank counts are
@@ -262,7 +301,8 @@ def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards
     if shards is not None and bound is not None and local.n_rows > 0:
         cap = -(-bound // max(local.n_rows, 1))
         rows = [e - b for b, e in shards]
-        ptr, idx, val32 = allgather_csr_rows_bounded(local.ptr, local.idx, local.val32, rows, max(rows) * cap, group)
+        B = int(entries_bound) if entries_bound else max(rows) * cap
+        ptr, idx, val32 = allgather_csr_rows_bounded(local.ptr, local.idx, local.val32, rows, B, group)
         out = DeviceCSR(n, n, ptr, idx, None, val32, None)
         out.nnz_bound = int(idx.numel())
         return out

@@ -49,6 +49,8 @@ class StepPlan:
     cols_sym: bool = False         # column blocks: the square K[b:e, b:e] by the symmetric enumeration
     fused: bool = False            # "sym": symmetric completion fused into the Gram tiles (no mirror pass)
     group: object = None           # torch.distributed group (N > 1)
+    gather_bound: int = 0          # N > 1: per-rank Phi entries moved by the all-gather (0: rows x rows_cap;
+    #                                dist.shard_entries of the setup walk: exact, checked by check_gather_overflow)
     extra: dict = field(default_factory=dict)
 
     @property
@@ -141,7 +143,8 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                                          count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
                                          want64=False),
                             want64=False, want32=True, sync_free=True)
-        phi = gather_phi(eng, local, group=pl.group, shards=pl.shards) if pl.world > 1 else local
+        phi = gather_phi(eng, local, group=pl.group, shards=pl.shards, entries_bound=pl.gather_bound or None) \
+            if pl.world > 1 else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
                                             local.val32)
         tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap)
@@ -152,8 +155,8 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                                      count_ws=tws, band_width=pl.band_width if tws is not None else 0,
                                      want64=False),
                         want64=False, want32=True, sync_free=True)
-    phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards) \
-        if pl.world > 1 else local
+    phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards,
+                     entries_bound=pl.gather_bound or None) if pl.world > 1 else local
     # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
     tr = eng.transpose_banded(phi, pl.band_width, counted_ws=tws, nnz_bound=n * pl.rows_cap)
     return Front(phi, tr, local)

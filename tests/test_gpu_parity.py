@@ -811,6 +811,67 @@ def test_sharded_allreduce_mode_within_tolerance_gloo():
     assert _run_sharded(2, "allreduce") == [(0, True), (1, True)]
 
 
+def _bench_front_worker(rank, world, port, mode, q):
+    """One gloo rank of the bench's own N > 1 step (grf_amd.pipeline, cuda:0): the setup walk's exact
+    per-rank entries bound the sync-free Phi all-gather (bench.py --gather-bound exact)."""
+    import os
+
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from grf_amd import pipeline as P
+        from grf_amd.dist import check_gather_overflow, setup_phi, shard_entries
+        from grf_amd.engine import DeviceCSR, GRFEngine
+        from grf_amd.graphs import powerlaw_graph
+        eng = GRFEngine("cuda:0")
+        n = 12000
+        A = DeviceCSR.from_scipy(powerlaw_graph(n, 10.0, 2.5, seed=6), eng.device)
+        f = [1.0, -0.5, 0.125, -0.02, 0.003]
+        m, p, L = 32, 0.15, 5
+        phi0 = setup_phi(eng, A, m, p, L, f, seed=42)
+        pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=mode)
+        pl.gather_bound = max(shard_entries(phi0, pl.shards))
+        Kb, fr = P.kernel_step(eng, A, pl)
+        Kb = P.k_view(Kb, pl)
+        check_gather_overflow(eng.device)
+        K = eng.gram_sparse(phi0, eng.transpose_banded(phi0, 8192))
+        b, e = pl.src
+        if mode == "cols":
+            want = _sym_square(K[:, b:e], b, e) if pl.cols_sym else K[:, b:e]
+        else:
+            want = K[b:e]
+        ok = bool(torch.equal(Kb, want)) and fr.phi.ptr.numel() == n + 1 and \
+            int(fr.phi.ptr[-1]) == int(phi0.ptr[-1]) and fr.phi.idx.numel() == world * pl.gather_bound
+        q.put((rank, ok))
+    except Exception as exc:
+        q.put((rank, repr(exc)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode", [(2, "cols"), (3, "cols"), (2, "rows")])
+def test_bench_step_exact_gather_bound_gloo(world, mode):
+    """The bench's N > 1 step with the Phi all-gather sized by the setup walk's exact per-rank entries
+    (not rows x the padded row capacity): every rank's K block bit-identical to the single-GPU K's."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_front_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+    assert res == [(r, True) for r in range(world)]
+
+
 @pytest.mark.parametrize("name", ["single", "empty", "star", "components", "path", "pair", "er_sparse"])
 def test_bench_path_on_degenerate_graphs(eng, name):
     """The bench's device path (fused Philox walks -> Phi -> banded transpose -> symmetric Gram +

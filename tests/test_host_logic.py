@@ -209,6 +209,57 @@ def test_allgather_csr_rows_bounded_gloo(world):
     assert _spawn(_bounded_gather_worker, world) == [(r, True) for r in range(world)]
 
 
+def _tight_gather_worker(rank, world, port, q):
+    """The exact bound (dist.shard_entries: the largest shard's entries) gathers the same CSR; one
+    entry less flags the overflow (raised by check_gather_overflow on every rank) and gathers the
+    overflowing rank's rows empty, with every offset inside the buffers."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import scipy.sparse as sp
+        from grf_amd.dist import allgather_csr_rows_bounded, check_gather_overflow, shard_bounds
+        n, cap = 61, 20
+        full = sp.random(n, n, density=0.15, random_state=11, format="csr")
+        full.sort_indices()
+        shards = shard_bounds(np.arange(1, n + 1) ** 2, world)
+        b, e = shards[rank]
+        part = full[b:e]
+        ptr = torch.from_numpy(part.indptr.astype(np.int64))
+        idx = torch.full(((e - b) * cap,), -7, dtype=torch.int32)
+        val = torch.full(((e - b) * cap,), 9e9, dtype=torch.float32)
+        idx[:part.nnz] = torch.from_numpy(part.indices.astype(np.int32))
+        val[:part.nnz] = torch.from_numpy(part.data.astype(np.float32))
+        rows = [s1 - s0 for s0, s1 in shards]
+        ents = [int(full.indptr[s1] - full.indptr[s0]) for s0, s1 in shards]
+        exact = max(ents)
+        gptr, gidx, gval = allgather_csr_rows_bounded(ptr, idx, val, rows, exact)
+        nnz = int(gptr[-1])
+        ok = (np.array_equal(gptr.numpy(), full.indptr) and np.array_equal(gidx[:nnz].numpy(), full.indices)
+              and np.array_equal(gval[:nnz].numpy(), full.data.astype(np.float32)) and gidx.numel() == world * exact)
+        check_gather_overflow("cpu")  # (no overflow: must not raise)
+        gptr, gidx, _ = allgather_csr_rows_bounded(ptr, idx, val, rows, exact - 1)
+        over = [r for r in range(world) if ents[r] > exact - 1]
+        cnt = np.diff(gptr.numpy())
+        for r, (s0, s1) in enumerate(shards):
+            want = 0 if r in over else np.diff(full.indptr[s0:s1 + 1])
+            ok = ok and np.array_equal(cnt[s0:s1], np.broadcast_to(want, (s1 - s0,)))
+        ok = ok and int(gptr[-1]) <= gidx.numel()
+        try:
+            check_gather_overflow("cpu")
+            ok = False
+        except RuntimeError:
+            pass
+        check_gather_overflow("cpu")  # (the flag is cleared by the raise)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allgather_csr_rows_tight_bound_and_overflow_gloo(world):
+    assert _spawn(_tight_gather_worker, world) == [(r, True) for r in range(world)]
+
+
 def test_shard_bounds_equal_weight_ranges():
     from grf_amd.dist import shard_bounds
     rng = np.random.default_rng(0)
