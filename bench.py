@@ -471,6 +471,9 @@ def main():
     ap.add_argument("--balance", choices=["nodes", "phi"], default="nodes",
                     help="N > 1 source shards: equal node ranges (default), or ranges of equal estimated step work "
                          "from the per-source Phi row counts of one setup walk (dist.balanced_shards)")
+    ap.add_argument("--hubs", type=int, default=0,
+                    help="one GPU, whole K: split Phi's densest HUBS columns off into a dense panel whose MFMA Gram "
+                         "the sparse Gram adds to (hub-heavy graphs: enron, facebook; 0 = no split)")
     ap.add_argument("--gather-bound", choices=["exact", "cap"], default="exact",
                     help="N > 1 Phi all-gather size per rank: the rank's Phi entries from the setup walk "
                          "(default; checked on the device, a larger step raises after the loop) or its rows x "
@@ -517,6 +520,8 @@ def main():
             shards = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance, phi=phi0)
     pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
                      band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused)
+    if args.hubs and pl.mode == "sym" and not pl.fused:
+        pl.hubs = int(args.hubs)
     if phi0 is not None:
         if args.gather_bound == "exact":
             # the Phi all-gather moves each rank's actual entries (C4: 435 per row) instead of its rows x
@@ -721,6 +726,7 @@ def main():
                    "n_nodes": n, "n_edges": int(A.nnz // 2), "walks_per_node": m, "max_walk_length": L,
                    "k_rows_per_gpu": rows, "shard": [b, e], "balance": args.balance if world > 1 else None,
                    "gather_entries_per_rank": pl.gather_bound or None,
+                   "hub_columns": pl.hubs or None,
                    "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
                                    f"RCCL all-reduce (K replicated)") if pl.mode == "allreduce" else
                                   (f"source-sharded x{world}, Phi all-gather, K column blocks K[:, R_r] from each "

@@ -202,6 +202,7 @@ struct GramTiles {
     int32_t k_begin, k_end;  // only the nonzeros Phi[i, k] with k in [k_begin, k_end) contribute
     int64_t J_off = 0;       // the launch's bands are the global bands J_off .. J_off + nb - 1
     int64_t t_rows = -1;     // rows of the transposed matrix (< 0: n_total, the square case)
+    bool add_k = false;      // write-out adds to K (which holds the dense hub-column part: grf_gram_sparse_upper_add)
     __host__ __device__ int64_t count(int64_t J) const {
         if (!sym) return rows;
         const int64_t c = (J + 1) * W;
@@ -470,8 +471,10 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
         gram_fused_completion<kWaves>(tl, J_local, r, j0, wlen, sh, acc, K, ldk, tickets);
         return;
     }
-    // write the tile once (non-temporal: K is write-once)
+    // write the tile once (non-temporal: K is write-once); add_k: K already holds the dense
+    // hub-column part of these entries, and the fixed-point sum is rounded once and added to it
     float *krow = K + r * ldk + j0;
+    const bool addk = tl.add_k;
     if ((ldk & 3) == 0 && (j0 & 3) == 0) {
         const int64_t n4 = wlen / 4;
         f32x4 *k4 = reinterpret_cast<f32x4 *>(krow);
@@ -482,12 +485,42 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             o[1] = fx_to_float(a[1], sh);
             o[2] = fx_to_float(b[0], sh);
             o[3] = fx_to_float(b[1], sh);
+            if (addk) o += __builtin_nontemporal_load(&k4[i]);
             __builtin_nontemporal_store(o, &k4[i]);
         }
-        for (int64_t i = n4 * 4 + tid; i < wlen; i += 64 * kWaves) krow[i] = fx_to_float(acc[i], sh);
+        for (int64_t i = n4 * 4 + tid; i < wlen; i += 64 * kWaves)
+            krow[i] = addk ? fx_to_float(acc[i], sh) + krow[i] : fx_to_float(acc[i], sh);
     } else {
-        for (int64_t i = tid; i < wlen; i += 64 * kWaves) krow[i] = fx_to_float(acc[i], sh);
+        for (int64_t i = tid; i < wlen; i += 64 * kWaves)
+            krow[i] = addk ? fx_to_float(acc[i], sh) + krow[i] : fx_to_float(acc[i], sh);
     }
+}
+
+// Hub columns (the densest columns of Phi): their entries as a dense fp32 panel
+// P[r, hub_pos[k]] = Phi[r, k] (P zeroed by the caller; hub_pos[k] = -1 for the other columns),
+// one wave per row.  The MFMA Gram of P carries those columns' share of K.
+__global__ __launch_bounds__(256) void hub_panel_kernel(int64_t n_rows, const int64_t *__restrict__ ptr,
+                                                        const int32_t *__restrict__ idx, const float *__restrict__ val,
+                                                        const int32_t *__restrict__ hub_pos, float *__restrict__ P,
+                                                        int64_t ldp) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t e1 = ptr[row + 1];
+    for (int64_t e = ptr[row] + lane; e < e1; e += 64) {
+        const int32_t q = hub_pos[idx[e]];
+        if (q >= 0) P[row * ldp + q] = val[e];
+    }
+}
+
+// the hub columns' buckets emptied in every band of a banded transpose (descriptor pair counts
+// set to 0), so the sparse Gram skips the entries the panel carries
+__global__ __launch_bounds__(256) void transpose_drop_kernel(int64_t n_bands, int64_t n_cols, uint2 *__restrict__ t_desc,
+                                                             const int32_t *__restrict__ cols, int32_t n_drop) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n_bands * n_drop) return;
+    const int64_t J = t / n_drop;
+    t_desc[J * n_cols + cols[t - J * n_drop]].y = 0u;
 }
 
 __device__ __forceinline__ void gram_mirror_block(int64_t n, int64_t nt, int64_t b, float *__restrict__ K, int64_t ldk,
@@ -1010,22 +1043,65 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
     return grf_gram_mirror(n_total, K, ldk, 0, stream);
 }
 
-int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
-                              int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                              const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
-                              int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
-                              grf_stream_t stream) {
+static int32_t gram_sparse_upper_impl(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                                      int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                                      const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                                      int32_t part_end, int32_t n_parts, bool add_k, grf_stream_t stream) {
     int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
     if (rc != GRF_OK) return rc;
     GRF_REQUIRE(n_parts >= 1 && 0 <= part_begin && part_begin <= part_end && part_end <= n_parts, GRF_EINVAL,
                 "grf_gram_sparse_upper: bad tile parts [%d, %d) of %d", part_begin, part_end, n_parts);
     if (n_total == 0 || part_begin == part_end) return GRF_OK;
-    const GramTiles tl{n_total, band_width, cdiv<int64_t>(n_total, band_width), true, 0, (int32_t)n_total};
+    GramTiles tl{n_total, band_width, cdiv<int64_t>(n_total, band_width), true, 0, (int32_t)n_total};
+    tl.add_k = add_k;
     const int64_t total = tl.total();
     const int64_t t0 = total * part_begin / n_parts, t1 = total * part_end / n_parts;
     if (t1 <= t0) return GRF_OK;
     return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
                              S(stream));
+}
+
+int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                              int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                              const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                              int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
+                              grf_stream_t stream) {
+    return gram_sparse_upper_impl(n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk,
+                                  part_begin, part_end, n_parts, false, stream);
+}
+
+int32_t grf_gram_sparse_upper_add(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                                  int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                                  const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                                  int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
+                                  grf_stream_t stream) {
+    return gram_sparse_upper_impl(n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk,
+                                  part_begin, part_end, n_parts, true, stream);
+}
+
+int32_t grf_hub_panel(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val,
+                      const int32_t *hub_pos, float *P, int64_t ldp, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && ldp >= 0 && (n_rows == 0 || (ptr && idx && val && hub_pos && P)), GRF_EINVAL,
+                "grf_hub_panel: bad arguments");
+    if (n_rows == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "hub_panel_kernel");
+    hub_panel_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, S(stream)>>>(n_rows, ptr, idx, val, hub_pos, P,
+                                                                                 ldp);
+    GRF_CHECK_LAUNCH("hub_panel_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_transpose_drop_columns(int64_t n_bands, int64_t n_cols, uint32_t *t_desc, const int32_t *cols,
+                                   int32_t n_drop, grf_stream_t stream) {
+    GRF_REQUIRE(n_bands >= 0 && n_cols >= 0 && n_drop >= 0 && (n_drop == 0 || (t_desc && cols)), GRF_EINVAL,
+                "grf_transpose_drop_columns: bad arguments");
+    const int64_t work = n_bands * (int64_t)n_drop;
+    if (work == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(work, 256), 256, "transpose_drop_kernel");
+    transpose_drop_kernel<<<(unsigned)cdiv<int64_t>(work, 256), 256, 0, S(stream)>>>(
+        n_bands, n_cols, reinterpret_cast<uint2 *>(t_desc), cols, n_drop);
+    GRF_CHECK_LAUNCH("transpose_drop_kernel");
+    return GRF_OK;
 }
 
 size_t grf_gram_sym_fused_workspace_bytes(int64_t n_total, int64_t band_width) {
@@ -1211,8 +1287,8 @@ size_t grf_gram_dense_workspace_bytes(int64_t n, int64_t k_dim) {
     return (size_t)S * (size_t)n * (size_t)ldp * sizeof(float);
 }
 
-int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
-                          void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+static int32_t gram_dense_impl(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                               void *workspace, size_t workspace_bytes, bool upper_only, grf_stream_t stream) {
     GRF_REQUIRE(n >= 0 && k_dim >= 0 && A && K && ldk >= n && lda >= k_dim, GRF_EINVAL,
                 "grf_gram_dense: bad arguments");
     GRF_REQUIRE(lda % 16 == 0 && ((uintptr_t)A & 15) == 0, GRF_EINVAL,
@@ -1229,7 +1305,7 @@ int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda,
         const char *e = getenv("GRF_DENSE_BK");
         return e ? atoi(e) : 0;
     }();
-    int ns = workspace ? dense_splits(n, k_dim) : 1;
+    int ns = (workspace && !upper_only) ? dense_splits(n, k_dim) : 1;
     const int64_t ldp = cdiv<int64_t>(n, 64) * 64;
     if (ns > 1 && workspace_bytes < (size_t)ns * (size_t)n * (size_t)ldp * sizeof(float)) ns = 1;
     const bool big = ns > 1 || (env_tile ? env_tile == 128 : nt128 * (nt128 + 1) / 2 >= 512);
@@ -1251,12 +1327,22 @@ int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda,
     else if (bk == 32) gram_dense_kernel<64, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
     else gram_dense_kernel<64, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
     GRF_CHECK_LAUNCH("gram_dense_kernel");
-    if (ns == 1) return grf_gram_mirror(n, K, ldk, 0, stream);  // the lower triangle
+    if (ns == 1) return upper_only ? GRF_OK : grf_gram_mirror(n, K, ldk, 0, stream);  // the lower triangle
     const int64_t nt64 = cdiv<int64_t>(n, 64), blocks = nt64 * (nt64 + 1) / 2;
     GRF_REQUIRE_GRID(blocks, 256, "gram_dense_combine_kernel");
     gram_dense_combine_kernel<<<(unsigned)blocks, 256, 0, S(stream)>>>(n, nt64, ns, out, ldp, pstride, K, ldk);
     GRF_CHECK_LAUNCH("gram_dense_combine_kernel");
     return GRF_OK;
+}
+
+int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                          void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    return gram_dense_impl(n, k_dim, A, lda, K, ldk, workspace, workspace_bytes, false, stream);
+}
+
+int32_t grf_gram_dense_upper(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                             grf_stream_t stream) {
+    return gram_dense_impl(n, k_dim, A, lda, K, ldk, nullptr, 0, true, stream);
 }
 
 int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,

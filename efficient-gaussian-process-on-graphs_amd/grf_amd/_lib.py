@@ -87,6 +87,11 @@ SIGNATURES = {
                                          _vp, _sz, _vp]),
     "grf_gram_sparse_upper": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32,
                                      _vp, _sz, _vp]),
+    "grf_gram_sparse_upper_add": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
+                                         _i32, _vp, _sz, _vp]),
+    "grf_hub_panel": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "grf_transpose_drop_columns": (_i32, [_i64, _i64, _vp, _vp, _i32, _vp]),
+    "grf_gram_dense_upper": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_transpose_banded_fill_staged": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                                 _sz, _i64, _vp, _sz, _vp]),
     "grf_transpose_staging_bytes": (_sz, [_i64, _i64, _i64, _i64]),

@@ -18,7 +18,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 import scipy.sparse as sp
@@ -580,6 +580,66 @@ class GRFEngine:
                                                out.stride(0), int(parts[0]), int(parts[1]), int(parts[2]),
                                                _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_upper")
+        return out[:, :n]
+
+    def hub_split(self, phi: DeviceCSR, tr: Banded, hubs: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Split Phi's ``hubs`` densest columns off the banded transpose ``tr`` of Phi (modified in place:
+        their buckets emptied in every band) into a dense fp32 panel P (n_rows x ldp, ldp a multiple of 32).
+        The columns are ranked by their record pairs over all bands (the descriptors the transpose left:
+        no host read), ties by column id; the panel holds them in ascending column order.
+        Returns (P, cols).  Hub-heavy graphs: a column in a large share of the rows costs the sparse
+        Gram one gathered record per multiply-add, the MFMA Gram of the panel ~60x less."""
+        n_rows, n = phi.n_rows, tr.n_cols
+        h = max(0, min(int(hubs), n))
+        nb = -(-tr.n_rows // tr.band_width)
+        pairs = tr.t_desc[:2 * nb * n].view(nb, n, 2)[:, :, 1].sum(0, dtype=torch.int64)
+        top = torch.sort(pairs, descending=True, stable=True).indices[:h]
+        cols = torch.sort(top).values.to(torch.int32).contiguous()
+        pos = torch.full((n,), -1, dtype=torch.int32, device=self.device)
+        pos[cols.long()] = torch.arange(h, dtype=torch.int32, device=self.device)
+        ldp = max(32, -(-h // 32) * 32)
+        P = torch.zeros((n_rows, ldp), dtype=torch.float32, device=self.device)
+        C.check(self.lib.grf_hub_panel(n_rows, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(pos), _p(P), ldp,
+                                       self.stream), "grf_hub_panel")
+        C.check(self.lib.grf_transpose_drop_columns(nb, n, _p(tr.t_desc), _p(cols), h, self.stream),
+                "grf_transpose_drop_columns")
+        return P, cols
+
+    def gram_sparse_sym_hubs(self, phi: DeviceCSR, tr: Banded, hubs: int, out: Optional[torch.Tensor] = None,
+                             mirror_workgroups: int = 0, after_tiles=None) -> torch.Tensor:
+        """Whole K with the hub-column split: the panel of Phi's ``hubs`` densest columns through the
+        MFMA Gram (tiles on and above the diagonal), the rest through the sparse Gram tiles adding to
+        it, then the mirror.  ``tr`` is consumed (its hub buckets emptied).  Within the fp32 K
+        tolerance of ``gram_sparse_sym`` (the hub part is an fp32 MFMA sum), exactly symmetric.
+        ``after_tiles(event)``: called between the tiles and the mirror (the pipelined bench)."""
+        n = tr.n_rows
+        if out is None:
+            out = torch.empty((n, self.leading_dim(n)), dtype=torch.float32, device=self.device)
+        if int(hubs) <= 0:  # (no split: the plain symmetric Gram)
+            self.gram_sparse_upper(phi, tr, out)
+            ev = None
+            if after_tiles is not None:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
+            self.gram_mirror(out, n, mirror_workgroups)
+            if after_tiles is not None:
+                after_tiles(ev)
+            return out[:, :n]
+        P, cols = self.hub_split(phi, tr, hubs)
+        h = int(cols.numel())
+        C.check(self.lib.grf_gram_dense_upper(n, h, _p(P), P.stride(0), _p(out), out.stride(0), self.stream),
+                "grf_gram_dense_upper")
+        C.check(self.lib.grf_gram_sparse_upper_add(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
+                                                   tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift),
+                                                   _p(out), out.stride(0), 0, 1, 1, _p(self._gram_ws),
+                                                   self._gram_ws.numel(), self.stream), "grf_gram_sparse_upper_add")
+        ev = None
+        if after_tiles is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        self.gram_mirror(out, n, mirror_workgroups)
+        if after_tiles is not None:
+            after_tiles(ev)
         return out[:, :n]
 
     def gram_sparse_sym_fused(self, phi: DeviceCSR, tr: Banded, out: Optional[torch.Tensor] = None,

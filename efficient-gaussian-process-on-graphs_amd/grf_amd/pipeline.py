@@ -48,6 +48,7 @@ class StepPlan:
     band_width: int = DEFAULT_BAND_WIDTH
     cols_sym: bool = False         # column blocks: the square K[b:e, b:e] by the symmetric enumeration
     fused: bool = False            # "sym": symmetric completion fused into the Gram tiles (no mirror pass)
+    hubs: int = 0                  # "sym": Phi's densest columns as a dense MFMA panel (hub-column split)
     group: object = None           # torch.distributed group (N > 1)
     gather_bound: int = 0          # N > 1: per-rank Phi entries moved by the all-gather (0: rows x rows_cap;
     #                                dist.shard_entries of the setup walk: exact, checked by check_gather_overflow)
@@ -193,6 +194,9 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
                 tiles_done.record(main)
         if after_tiles is not None:
             after_tiles(tiles_done)
+    elif pl.mode == "sym" and pl.hubs > 0:
+        eng.gram_sparse_sym_hubs(fr.phi, fr.tr, pl.hubs, out=K, mirror_workgroups=mirror_workgroups,
+                                 after_tiles=after_tiles)
     elif pl.mode == "sym":
         main = torch.cuda.current_stream(eng.device)
         tiles_done = None

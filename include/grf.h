@@ -287,6 +287,28 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
                               int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                               grf_stream_t stream);
 
+/* grf_gram_sparse_upper whose tile write-out ADDS the rounded fixed-point sums to K instead of
+ * storing them: K's entries on and above the diagonal must hold the dense part first (the hub
+ * columns' MFMA Gram, grf_gram_dense_upper).  With the hub columns' buckets emptied from the
+ * transpose (grf_transpose_drop_columns) and their entries in the dense panel (grf_hub_panel),
+ * dense upper + this + grf_gram_mirror is K = Phi Phi^T within the fp32 K tolerance (the hub part is
+ * an fp32 MFMA sum instead of the exact fixed-point one).  Same arguments as grf_gram_sparse_upper. */
+int32_t grf_gram_sparse_upper_add(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                                  int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                                  const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                                  int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
+                                  grf_stream_t stream);
+
+/* Hub-column split (hub-heavy graphs: Enron, Facebook, power-law).  grf_hub_panel writes the entries
+ * Phi[r, k] of the columns with hub_pos[k] >= 0 into the dense fp32 panel P[r, hub_pos[k]] (row-major,
+ * n_rows x ldp, zeroed by the caller; int32 hub_pos[n_cols], -1 elsewhere).  grf_transpose_drop_columns
+ * empties the buckets of the n_drop columns cols[] in all n_bands bands of a banded transpose
+ * (t_desc as returned by grf_transpose_banded_*, n_cols = the transposed matrix's columns). */
+int32_t grf_hub_panel(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val,
+                      const int32_t *hub_pos, float *P, int64_t ldp, grf_stream_t stream);
+int32_t grf_transpose_drop_columns(int64_t n_bands, int64_t n_cols, uint32_t *t_desc, const int32_t *cols,
+                                   int32_t n_drop, grf_stream_t stream);
+
 /* Whole K as grf_gram_sparse_sym, with the symmetric completion fused into the Gram tiles: the
  * tiles of 64 consecutive rows of a band take tickets on a group counter and the last one writes
  * the group's block transposed below the diagonal (from the Infinity Cache: no separate mirror
@@ -354,6 +376,11 @@ int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups
  * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */
 int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                        grf_stream_t stream);
+/* grf_gram_dense's tiles on and above the diagonal only (128 x 128 tiles J >= I, or 64 x 64 for small
+ * n; no split-K, no lower triangle): every K[i, j >= i] is written, entries below the diagonal only
+ * where a diagonal tile covers them.  The hub part of the hub-column split (grf_gram_sparse_upper_add). */
+int32_t grf_gram_dense_upper(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                             grf_stream_t stream);
 /* As grf_gram_dense, with a device workspace for split-K partials: when n is too small for the
  * tiles on and above the diagonal to fill the GPU, the k range is cut into S slices whose partial
  * Grams are summed in slice order (deterministic) by the pass that also writes the lower triangle.

@@ -571,6 +571,62 @@ def test_bench_path_heavy_tailed_graphs(eng, golden, name):
     del K, Kr
 
 
+@pytest.mark.parametrize("name,hubs", [("enron", 64), ("enron", 256), ("powerlaw", 100), ("er", 32)])
+def test_hub_column_split(eng, golden, name, hubs):
+    """Hub-column split (grf_hub_panel + grf_transpose_drop_columns + grf_gram_dense_upper +
+    grf_gram_sparse_upper_add + mirror): the panel holds exactly Phi's chosen columns, their buckets
+    are emptied, K is exactly symmetric and within the K tolerance of the fp64 oracle product (and of
+    the all-sparse K) on sampled rows, hubs included; hubs = 0 is the all-sparse K bit for bit."""
+    import torch
+    from golden_util import snap_adjacency
+    from grf_amd import pipeline as P
+    from grf_amd.graphs import powerlaw_graph
+    if name == "enron":
+        A = snap_adjacency(golden("snap"), name)
+    elif name == "powerlaw":
+        A = powerlaw_graph(20_000, 10.0, 2.5, seed=5)
+    else:
+        A = er_graph(9000, 6, 13)
+    n = A.shape[0]
+    m, p, L = 32, 0.1, 8
+    f = _diffusion(L)
+    G = eng.laplacian(A)
+    phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42), want64=True, want32=True)
+    phi64 = phi.to_scipy()
+    K0 = eng.gram_sparse_sym(phi, eng.transpose_banded(phi))
+    tr = eng.transpose_banded(phi)
+    Pn, cols = eng.hub_split(phi, tr, hubs)
+    c = cols.cpu().numpy().astype(np.int64)
+    assert c.size == hubs and np.all(np.diff(c) > 0)
+    cnt = np.bincount(phi64.indices, minlength=n)
+    # the chosen columns are the densest by record pairs: no unchosen column has more entries than
+    # twice the sparsest chosen one plus a band's rounding (pairs ~ entries / 2 per band)
+    nb = -(-n // tr.band_width)
+    assert cnt[np.setdiff1d(np.arange(n), c)].max(initial=0) <= 2 * cnt[c].min() + 2 * nb
+    panel = Pn[:, :hubs].cpu().numpy()
+    want = phi64.astype(np.float32)[:, c].toarray()
+    assert np.array_equal(panel, want) and not Pn[:, hubs:].any()
+    d = tr.t_desc[:2 * nb * n].view(nb, n, 2)[:, :, 1]
+    assert int(d[:, cols.long()].abs().sum()) == 0
+    tr = eng.transpose_banded(phi)
+    Kh = eng.gram_sparse_sym_hubs(phi, tr, hubs)
+    assert torch.equal(Kh, Kh.t())
+    sample = np.r_[0, 1, np.argsort(-np.diff(A.indptr), kind="stable")[:4], c[:2], n - 1].astype(np.int64)
+    si = torch.from_numpy(sample).to(Kh.device)
+    ref = (phi64[sample] @ phi64.T).toarray()
+    ok, e = _k_bound_close(Kh[si].cpu().numpy(), phi64, sample, ref)
+    assert ok, e
+    ok, e = _k_bound_close(Kh[si].cpu().numpy(), phi64, sample, K0[si].cpu().numpy().astype(np.float64))
+    assert ok, e
+    # the bench's pipeline with the split (pl.hubs): the same K
+    pl = P.plan_step(n, m, L, p, f, seed=42)
+    pl.hubs = hubs
+    Kb = P.k_view(P.k_assembly(eng, P.Front(phi, eng.transpose_banded(phi), phi), pl, P.alloc_k(eng, pl)), pl)
+    assert torch.equal(Kb, Kh)
+    assert torch.equal(eng.gram_sparse_sym_hubs(phi, eng.transpose_banded(phi), 0), K0)
+    del K0, Kh, Kb
+
+
 def test_sharded_counts_and_phi_equal_single_gpu(eng):
     """The multi-GPU assembly, emulated in one process: per-shard fused walk -> Phi with bucket
     counting, counts summed (the all-reduce of dist.gather_phi) and rows concatenated (the
