@@ -1267,8 +1267,9 @@ int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups
 }
 
 // split-K slices for a dense Gram of n rows (128-row tiles on and above the diagonal): measured on
-// MI355X (tools/dense_sweep.py, profiles/r02_dense_splitk.txt) 4 slices below 1024 tiles (n < 5.8 k),
-// 2 below 4096 (n < 11.6 k), none above; every slice at least 256 deep
+// MI355X (tools/dense_sweep.py, profiles/r02_dense_splitk.txt) 2 slices below 384 tiles (n < 3.5 k:
+// C3's 253 tiles, 0.209-0.214 ms vs 0.221 with 4), 4 below 1024 tiles (n < 5.8 k), 2 below 4096
+// (n < 11.6 k), none above; every slice at least 256 deep
 static int dense_splits(int64_t n, int64_t k_dim) {
     static const int env_split = [] {  // GRF_DENSE_SPLIT: A/B knob (1 = never split)
         const char *e = getenv("GRF_DENSE_SPLIT");
@@ -1276,7 +1277,7 @@ static int dense_splits(int64_t n, int64_t k_dim) {
     }();
     if (env_split > 0) return env_split;
     const int64_t nt = cdiv<int64_t>(n, 128), tiles = nt * (nt + 1) / 2;
-    const int64_t S = tiles < 1024 ? 4 : tiles < 4096 ? 2 : 1;
+    const int64_t S = tiles < 384 ? 2 : tiles < 1024 ? 4 : tiles < 4096 ? 2 : 1;
     return (int)std::max<int64_t>(1, std::min<int64_t>(S, k_dim / 256));
 }
 
