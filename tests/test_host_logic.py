@@ -344,3 +344,16 @@ def test_snap_graphs_load():
     assert (fb != fb.T).nnz == 0 and (en != en.T).nnz == 0
     with pytest.raises(ValueError):
         snap_graph("youtube")
+
+
+def test_shard_entries_from_row_pointer():
+    """dist.shard_entries: every shard's Phi entries from the row pointer (the exact gather bound)."""
+    from types import SimpleNamespace
+    from grf_amd.dist import shard_entries, shard_range
+    rng = np.random.default_rng(3)
+    cnt = rng.integers(0, 40, size=57)
+    ptr = torch.from_numpy(np.r_[0, np.cumsum(cnt)].astype(np.int64))
+    for world in (1, 2, 3, 8):
+        shards = [shard_range(57, r, world) for r in range(world)]
+        got = shard_entries(SimpleNamespace(ptr=ptr), shards)
+        assert got == [int(cnt[b:e].sum()) for b, e in shards] and sum(got) == int(cnt.sum())
