@@ -73,6 +73,20 @@ def pmc_counter(kernel, counter):
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 4
 
 
+def auto_hubs(eng, A_dev, m, p, L, f, share: float = 0.13) -> int:
+    """Hub columns worth a dense panel (setup, untimed): a column in c of the n rows saves ~c^2 / 2 gathered
+    records and costs n^2 / 2 MFMA multiply-adds, ~60x cheaper each, so it pays from c / n ~ 1 / sqrt(60) = 0.13
+    (measured: Enron's best split is 128 columns, whose c reaches 13 % of n; Facebook's 64th column is in 9 % of
+    the rows and the split loses there, profiles/r02_hubs_sweep.txt).  Multiples of 32 (the panel's width)."""
+    import torch
+
+    from grf_amd.dist import setup_phi
+    phi = setup_phi(eng, A_dev, m, p, L, f, seed=42)
+    n = phi.n_cols
+    c = torch.bincount(phi.idx[:phi.nnz].long(), minlength=n)
+    return int((c >= share * n).sum().item()) // 32 * 32
+
+
 def init_distributed(local_rank: int) -> int:
     """One process per GPU over RCCL (backend "nccl").  GRF_DIST_BACKEND=gloo rehearses the same
     multi-process path with several ranks on one GPU (device tensors staged through host memory
@@ -471,9 +485,10 @@ def main():
     ap.add_argument("--balance", choices=["nodes", "phi"], default="nodes",
                     help="N > 1 source shards: equal node ranges (default), or ranges of equal estimated step work "
                          "from the per-source Phi row counts of one setup walk (dist.balanced_shards)")
-    ap.add_argument("--hubs", type=int, default=0,
+    ap.add_argument("--hubs", type=lambda v: -1 if v == "auto" else int(v), default=-1,
                     help="one GPU, whole K: split Phi's densest HUBS columns off into a dense panel whose MFMA Gram "
-                         "the sparse Gram adds to (hub-heavy graphs: enron, facebook; 0 = no split)")
+                         "the sparse Gram adds to (hub-heavy graphs: enron; 0 = no split; auto, the default = the columns "
+                         "in at least 13%% of the rows, from a setup walk, in multiples of 32: C4 / Facebook 0, Enron 96)")
     ap.add_argument("--gather-bound", choices=["exact", "cap"], default="exact",
                     help="N > 1 Phi all-gather size per rank: the rank's Phi entries from the setup walk "
                          "(default; checked on the device, a larger step raises after the loop) or its rows x "
@@ -521,7 +536,7 @@ def main():
     pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
                      band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused)
     if args.hubs and pl.mode == "sym" and not pl.fused:
-        pl.hubs = int(args.hubs)
+        pl.hubs = int(args.hubs) if args.hubs > 0 else auto_hubs(eng, A_dev, m, p, L, f)
     if phi0 is not None:
         if args.gather_bound == "exact":
             # the Phi all-gather moves each rank's actual entries (C4: 435 per row) instead of its rows x
