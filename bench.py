@@ -511,6 +511,7 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from grf_amd import dist as D
     from grf_amd import pipeline as P
     from grf_amd.dist import all_reduce as dist_all_reduce
     from grf_amd.engine import DeviceCSR, GRFEngine
@@ -652,12 +653,15 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+        D.GATHER_STATS = []  # HIP events around every Phi all-gather of the timed steps
     t0 = time.perf_counter()
     run(args.steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
+    gather_stats = D.GATHER_STATS or []
+    D.GATHER_STATS = None
     # latency of one un-pipelined step (reported beside the throughput; not part of `value`), with
     # the walk kernel timed alone there
     ov = args.overlap
@@ -672,14 +676,38 @@ def main():
     if world > 1:
         from grf_amd.dist import check_gather_overflow
         check_gather_overflow(dev)  # (raises if a bounded all-gather truncated a rank's Phi)
+    # in-run parity of the last step's K block against the Phi that step gathered (every rank)
+    parity = P.k_block_check(eng, last[0], pl, K)
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
     walk_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in walk_ev]))
+    coll_ms = float(np.mean([a.elapsed_time(b_) for a, b_, _, _ in gather_stats])) if gather_stats else 0.0
+    coll_sent = float(np.mean([x for _, _, x, _ in gather_stats])) if gather_stats else 0.0
+    coll_recv = float(np.mean([x for _, _, _, x in gather_stats])) if gather_stats else 0.0
     if world > 1:
         tt = torch.tensor([t, float(np.mean(gram_ms)), walk_ms], dtype=torch.float64, device=dev)
         dist_all_reduce(tt, op=dist.ReduceOp.MAX)
         t, gram_avg, walk_ms = (float(x) for x in tt.tolist())
+        # every rank's Gram time, collective time and volume, and parity ratio (rank order)
+        mine = torch.tensor([float(np.mean(gram_ms)), coll_ms, coll_sent, coll_recv, parity["max_ratio"],
+                             float(pl.e - pl.b)], dtype=torch.float64, device=dev)
+        allr = torch.zeros(world * mine.numel(), dtype=torch.float64, device=dev)
+        allr[rank * mine.numel():(rank + 1) * mine.numel()] = mine
+        dist_all_reduce(allr)
+        per_rank = allr.view(world, -1).cpu().numpy()
+        parity = dict(parity, max_ratio=float(per_rank[:, 4].max()), ok=bool(per_rank[:, 4].max() <= 1.0),
+                      per_rank=[float(x) for x in per_rank[:, 4]])
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "rank_rows": [int(x) for x in per_rank[:, 5]],
+                     "gram_ms_per_rank": [float(x) for x in per_rank[:, 0]],
+                     "gram_balance": float(per_rank[:, 0].min() / max(per_rank[:, 0].max(), 1e-9)),
+                     "gather_ms_per_rank": [float(x) for x in per_rank[:, 1]],
+                     "gather_bytes_sent_per_rank": [int(x) for x in per_rank[:, 2]],
+                     "gather_bytes_received_per_rank": [int(x) for x in per_rank[:, 3]],
+                     "gather_note": "HIP events on the issuing stream around each step's Phi all-gather "
+                                    "(the transfer + the wait for the slowest rank), mean over the timed steps"}
     else:
         gram_avg = float(np.mean(gram_ms))
+        dist_info = None
 
     ms_per_step = 1000.0 * t / args.steps
     phi_last = last[0].phi
@@ -774,9 +802,12 @@ def main():
                                               f"entry written ({local_nnz}); timed alone in the serial steps "
                                               f"(pipelined it shares HBM with the mirror)"},
         "nnz_phi": nnz_phi,
+        "parity": parity,
         "pipelined": bool(ov),
         "serial_ms_per_step": serial_ms,
     }
+    if dist_info is not None:
+        out["distributed"] = dist_info
     if headline and not args.no_mfma_leg:
         # (side legs: a failure there is reported in the line and never costs the headline number)
         for key, wl in (("roofline_mfma", "c3"), ("roofline_mfma_c2", "c2")):  # C3 (Cora); C2 (ER N = 10k) dense path

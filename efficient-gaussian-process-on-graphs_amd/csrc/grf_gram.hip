@@ -31,6 +31,8 @@ namespace grf {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kChunk = 1024;  // stream positions covered by one bucket-id chunk (16 per lane)
+constexpr int kSub = 8;       // sub-bands of the transpose's split (grf_transpose_banded_self, t_split)
+constexpr int kPairBytesG = 12;  // one record pair
 // per wave: ids [kChunk], then tbase and aval for a batch of 64 * halves nonzeros
 constexpr int wave_state_bytes(int halves) { return kChunk + halves * 64 * 8; }
 
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
     const unsigned char *__restrict__ t_rec, int32_t unit, const int32_t *__restrict__ rowshift,
-    float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets) {
+    float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets, const uint16_t *__restrict__ t_split) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t W = tl.W;
@@ -389,6 +391,11 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     const int sh = rowshift[row];
     const int32_t line0 = (int32_t)t_desc[boff].x;                  // the band's first unit
     const unsigned char *brec = t_rec + (int64_t)line0 * unit;  // the band's records
+    // symmetric mode on the row's own band (a diagonal tile): only the columns j >= row are kept (the
+    // mirror overwrites the rest), so with sub-band ordered buckets (t_split) every bucket stream starts
+    // at the row's sub-band -- the pairs of the earlier sub-bands are never fetched -- and the write-out
+    // starts at that sub-band's first column
+    const int dsub = (t_split && tl.sym && r >= J_local * W) ? (int)(((r - J_local * W) * kSub) / W) : 0;
 
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     u64x2 *acc2 = reinterpret_cast<u64x2 *>(acc);
@@ -411,8 +418,10 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             if (k < tl.k_begin || k >= tl.k_end) k = -1;  // (k-slice mode)
             av[h] = k >= 0 ? val[e] : 0.f;
             const uint2 d = k >= 0 ? t_desc[boff + k] : make_uint2((uint32_t)line0, 0u);
-            t0[h] = ((int32_t)d.x - line0) * unit;  // bucket byte offset within the band
-            cnt[h] = (int32_t)d.y;                 // pairs
+            // pairs of the sub-bands before the row's (diagonal tiles; capped: a dropped hub bucket has 0)
+            const int32_t skip = (dsub > 0 && k >= 0) ? min((int32_t)(t_split[(boff + k) * kSub + dsub] >> 1), (int32_t)d.y) : 0;
+            t0[h] = ((int32_t)d.x - line0) * unit + kPairBytesG * skip;  // first fetched byte within the band
+            cnt[h] = (int32_t)d.y - skip;                                   // pairs
         }
         int32_t total = 0;
 #pragma unroll
@@ -475,10 +484,11 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     // hub-column part of these entries, and the fixed-point sum is rounded once and added to it
     float *krow = K + r * ldk + j0;
     const bool addk = tl.add_k;
+    const int64_t c_lo = (int64_t)dsub * (W / kSub);  // (a multiple of 8: W % 64 == 0)
     if ((ldk & 3) == 0 && (j0 & 3) == 0) {
         const int64_t n4 = wlen / 4;
         f32x4 *k4 = reinterpret_cast<f32x4 *>(krow);
-        for (int64_t i = tid; i < n4; i += 64 * kWaves) {
+        for (int64_t i = c_lo / 4 + tid; i < n4; i += 64 * kWaves) {
             const u64x2 a = acc2[2 * i], b = acc2[2 * i + 1];
             f32x4 o;
             o[0] = fx_to_float(a[0], sh);
@@ -940,7 +950,14 @@ size_t grf_gram_workspace_bytes(void) { return 256; }
 static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramTiles &tl, int64_t t_first,
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
                                  const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
-                                 float *K, int64_t ldk, hipStream_t st, int32_t *tickets = nullptr) {
+                                 float *K, int64_t ldk, hipStream_t st, int32_t *tickets = nullptr,
+                                 const void *t_split = nullptr) {
+    // GRF_GRAM_SPLIT=0: ignore the sub-band split (A/B of the diagonal tiles' skip)
+    static const bool use_split = [] {
+        const char *e = getenv("GRF_GRAM_SPLIT");
+        return !e || atoi(e) != 0;
+    }();
+    const uint16_t *split = (use_split && tl.sym && !tickets) ? (const uint16_t *)t_split : nullptr;
     // tuning knobs (defaults = measured best on MI355X): gathers in flight per wave, waves per tile
     static const int knobs = [] {
         const char *e = getenv("GRF_GRAM_UNROLL"), *w = getenv("GRF_GRAM_WAVES"), *t = getenv("GRF_GRAM_TAIL");
@@ -965,7 +982,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
     gram_sparse_kernel<WV, H, U, T, F><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx,   \
                                                                         val, reinterpret_cast<const uint2 *>(t_desc), \
                                                                         reinterpret_cast<const unsigned char *>(t_rec), \
-                                                                        unit, t_rowshift, K, ldk, tickets)
+                                                                        unit, t_rowshift, K, ldk, tickets, split)
 #define GRF_GRAM_LAUNCH_T(WV, H, U, T) GRF_GRAM_LAUNCH_F(WV, H, U, T, false)
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     do {                                                                                                          \
@@ -994,13 +1011,14 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
 static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t rows, bool sym, int64_t k_begin,
                                   int64_t k_end, const int64_t *ptr, const int32_t *idx, const float *val,
                                   int64_t band_width, int32_t unit, const uint32_t *t_desc, const void *t_rec,
-                                  const int32_t *t_rowshift, float *K, int64_t ldk, hipStream_t st) {
+                                  const int32_t *t_rowshift, float *K, int64_t ldk, hipStream_t st,
+                                  const void *t_split = nullptr) {
     const int64_t nb = cdiv<int64_t>(n_total, band_width);
     const GramTiles tl{rows, band_width, nb, sym, (int32_t)k_begin, (int32_t)k_end};
     const int64_t n_tiles = tl.total();
     if (n_tiles == 0) return GRF_OK;
     return gram_tiles_launch(n_total, row_begin, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, unit, t_rowshift, K,
-                             ldk, st);
+                             ldk, st, nullptr, t_split);
 }
 
 static int32_t gram_sparse_check(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
@@ -1032,20 +1050,20 @@ int32_t grf_gram_sparse(int64_t n_total, int64_t row_begin, int64_t row_end, con
 
 int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                             int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                            const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
+                            const void *t_split, const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
                             grf_stream_t stream) {
     int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
     if (rc != GRF_OK) return rc;
     if (n_total == 0) return GRF_OK;
     rc = gram_sparse_launch(n_total, 0, n_total, true, 0, n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec,
-                            t_rowshift, K, ldk, S(stream));
+                            t_rowshift, K, ldk, S(stream), t_split);
     if (rc != GRF_OK) return rc;
     return grf_gram_mirror(n_total, K, ldk, 0, stream);
 }
 
 static int32_t gram_sparse_upper_impl(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                                       int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                                      const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                                      const void *t_split, const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
                                       int32_t part_end, int32_t n_parts, bool add_k, grf_stream_t stream) {
     int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
     if (rc != GRF_OK) return rc;
@@ -1058,25 +1076,26 @@ static int32_t gram_sparse_upper_impl(int64_t n_total, const int64_t *ptr, const
     const int64_t t0 = total * part_begin / n_parts, t1 = total * part_end / n_parts;
     if (t1 <= t0) return GRF_OK;
     return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
-                             S(stream));
+                             S(stream), nullptr, t_split);
 }
 
 int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                               int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                              const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                              const void *t_split, const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
                               int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                               grf_stream_t stream) {
-    return gram_sparse_upper_impl(n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk,
-                                  part_begin, part_end, n_parts, false, stream);
+    return gram_sparse_upper_impl(n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec, t_split, t_rowshift,
+                                  K, ldk, part_begin, part_end, n_parts, false, stream);
 }
 
 int32_t grf_gram_sparse_upper_add(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                                   int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                                  const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                                  const void *t_split, const int32_t *t_rowshift, float *K, int64_t ldk,
+                                  int32_t part_begin,
                                   int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                                   grf_stream_t stream) {
-    return gram_sparse_upper_impl(n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk,
-                                  part_begin, part_end, n_parts, true, stream);
+    return gram_sparse_upper_impl(n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec, t_split, t_rowshift,
+                                  K, ldk, part_begin, part_end, n_parts, true, stream);
 }
 
 int32_t grf_hub_panel(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val,
@@ -1144,8 +1163,8 @@ int32_t grf_gram_sparse_sym_fused(int64_t n_total, const int64_t *ptr, const int
 int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
                              const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
                              int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
-                             const void *t_rec, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
-                             grf_stream_t stream) {
+                             const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
+                             size_t workspace_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n_cols > 0 && 0 <= row_begin && row_begin <= row_end && ptr && idx && val && row_shift &&
                     t_rows >= 0 && t_desc && t_rec && K && ldk >= t_rows,
                 GRF_EINVAL, "grf_gram_sparse_cols: bad arguments");
@@ -1167,7 +1186,7 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
         GramTiles tl{r1 - r0, band_width, nb, sym, 0, (int32_t)n_cols};
         tl.t_rows = t_rows;
         return gram_tiles_launch(n_cols, r0, tl, 0, tl.total(), ptr, idx, val, t_desc, t_rec, rec_unit, row_shift,
-                                 K + (r0 - row_begin) * ldk, ldk, st);
+                                 K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr);
     };
     if (sym_row0 < 0) return launch(row_begin, row_end, false);
     // Phi_B = Phi[sym_row0, sym_row0 + t_rows): the square K[B, B] is symmetric and its bands start at
@@ -1184,7 +1203,8 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
 // diagonal for the block's interior rows and mirrored; everything else is the row mode.
 int32_t grf_gram_sparse_block(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
                               const int32_t *idx, const float *val, int64_t band_width, int32_t rec_unit,
-                              const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
+                              const uint32_t *t_desc, const void *t_rec, const void *t_split,
+                              const int32_t *t_rowshift, float *K,
                               int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
     int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift,
                                    K, ldk);
@@ -1205,7 +1225,7 @@ int32_t grf_gram_sparse_block(int64_t n_total, int64_t row_begin, int64_t row_en
         tl.J_off = ja;
         const int64_t n_tiles = tl.total();
         return gram_tiles_launch(n_total, r0, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift,
-                                 K + (r0 - row_begin) * ldk, ldk, st);
+                                 K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr);
     };
     if ((rc = launch(B0, B1, J0, J1, true)) != GRF_OK) return rc;            // interior, symmetric
     if ((rc = launch(row_begin, row_end, 0, J0, false)) != GRF_OK) return rc;  // bands before

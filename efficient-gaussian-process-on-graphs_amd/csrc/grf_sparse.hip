@@ -522,12 +522,21 @@ struct RegionBaseOut {  // region_base[i] = first unit of region i; the total al
     }
 };
 
+// kSplit: every bucket's entries are laid out by sub-band -- the eight row ranges of W / 8 rows
+// of the band, in order -- and t_split[b] holds 8 u16 entry offsets, the entries of bucket b before
+// each sub-band.  A symmetric-mode Gram tile on its own (diagonal) band needs only the columns j >= its
+// row, i.e. the sub-bands from its row's on: it starts its bucket streams there.
+// Oversized regions (global cursors) keep arbitrary order and report no split (all offsets 0).
+constexpr int kSub = 8;
+
+template <bool kSplit>
 __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, int32_t cr,
                                                             int32_t nreg, const int64_t *ptr,
                                                             const int64_t *region_base, const uint2 *staging,
                                                             const int32_t *tab, int32_t *gcur, uint2 *desc,
-                                                            unsigned char *t_rec, int32_t unit) {
+                                                            uint4 *t_split, unsigned char *t_rec, int32_t unit) {
     extern __shared__ __attribute__((aligned(16))) unsigned char tps_smem[];
+    constexpr int kS = kSplit ? kSub : 1;  // counters per bucket
     const int tid = threadIdx.x;
     // dispatch group x = blockIdx % 8 (one XCD) takes a contiguous run of regions: neighbouring
     // regions read neighbouring words of the same table lines, which then come from one L2
@@ -538,49 +547,71 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
     const int nbk_r = (int)(c1 - c0);
     const int64_t b0 = band * n_cols + c0;
     const int64_t U0 = region_base[rg];
-    uint32_t *lcur = reinterpret_cast<uint32_t *>(tps_smem);   // [cr] counts, then cursors
-    uint32_t *lline = lcur + cr;                                // [cr] first byte of each bucket in the image
+    uint32_t *lcur = reinterpret_cast<uint32_t *>(tps_smem);   // [cr * kS] counts, then cursors
+    uint32_t *lline = lcur + cr * kS;                           // [cr] first byte of each bucket in the image
     int32_t *scratch = reinterpret_cast<int32_t *>(lline + cr); // [8]
     unsigned char *image = reinterpret_cast<unsigned char *>(scratch + 8);
     const int64_t w0 = band * bw / kBinRows, w1 = cdiv<int64_t>(min<int64_t>(n_rows, (band + 1) * bw), kBinRows);
-    for (int i = tid; i < nbk_r; i += 256) lcur[i] = 0u;
+    // (the staged entry's low half is 8 * its row in the band: 8 sub-bands of bw / 8 rows -> x / bw)
+    auto slot = [&](uint32_t x) -> uint32_t {
+        return kSplit ? (x >> 16) * kSub + (x & 0xffffu) / (uint32_t)bw : (x >> 16);
+    };
+    for (int i = tid; i < nbk_r * kS; i += 256) lcur[i] = 0u;
     __syncthreads();
-    // pass 1: the region's bucket counts
+    // pass 1: the region's bucket (and sub-band) counts
     for (int64_t w = w0 + tid; w < w1; w += 256) {
         const int32_t *trow = tab + w * (nreg + 1);
         const int32_t o0 = trow[g], o1 = trow[g + 1];
         const uint2 *run = staging + ptr[w * kBinRows];
-        for (int32_t o = o0; o < o1; ++o) atomicAdd(&lcur[run[o].x >> 16], 1u);
+        for (int32_t o = o0; o < o1; ++o) atomicAdd(&lcur[slot(run[o].x)], 1u);
     }
     __syncthreads();
+    auto bucket_count = [&](int i) -> uint32_t {
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < kS; ++q) c += lcur[i * kS + q];
+        return c;
+    };
     // bucket units -> local offsets (thread t owns buckets [t * per, (t + 1) * per)), descriptors
     const int per = (nbk_r + 255) / 256;
     int32_t sum = 0;
     for (int q = 0; q < per; ++q) {
         const int i = tid * per + q;
-        if (i < nbk_r) sum += (int32_t)((kPairBytes * ((lcur[i] + 1) >> 1) + unit - 1) / unit);
+        if (i < nbk_r) sum += (int32_t)((kPairBytes * ((bucket_count(i) + 1) >> 1) + unit - 1) / unit);
     }
     int32_t total;
     int32_t run_u = block_exclusive_scan<int32_t>(sum, scratch, &total);
+    const bool lds = ((int64_t)total * unit + 15) / 16 * 16 <= kPlaceCap;
     for (int q = 0; q < per; ++q) {
         const int i = tid * per + q;
         if (i < nbk_r) {
-            const uint32_t c = lcur[i];
+            const uint32_t c = bucket_count(i);
             desc[b0 + i] = make_uint2((uint32_t)(U0 + run_u), (c + 1) >> 1);
             lline[i] = (uint32_t)run_u * (uint32_t)unit;
             run_u += (int32_t)((kPairBytes * ((c + 1) >> 1) + unit - 1) / unit);
+            if (kSplit) {
+                // entry offsets of the sub-bands; the counters become the sub-band cursors
+                uint32_t off[kSub], o = 0;
+#pragma unroll
+                for (int sb = 0; sb < kSub; ++sb) {
+                    off[sb] = lds ? o : 0u;
+                    o += lcur[i * kSub + sb];
+                    lcur[i * kSub + sb] = off[sb];
+                }
+                t_split[b0 + i] = make_uint4(off[0] | (off[1] << 16), off[2] | (off[3] << 16), off[4] | (off[5] << 16),
+                                             off[6] | (off[7] << 16));
+            }
         }
     }
     __syncthreads();
     const int64_t img = (int64_t)total * unit;
     if (img == 0) return;
-    const bool lds = (img + 15) / 16 * 16 <= kPlaceCap;
     if (lds) {
         for (int64_t i = tid; i < (img + 15) / 16; i += 256) reinterpret_cast<uint4 *>(image)[i] = make_uint4(0u, 0u, 0u, 0u);
     } else {  // oversized region: global cursors of its own buckets, odd buckets padded below
         for (int i = tid; i < nbk_r; i += 256) {
             gcur[b0 + i] = 0;
-            const uint32_t c = lcur[i];
+            const uint32_t c = bucket_count(i);
             if (c & 1) {
                 unsigned char *pair = t_rec + (U0 * unit + lline[i]) + (int64_t)kPairBytes * (c >> 1);
                 reinterpret_cast<uint16_t *>(pair)[1] = 0;
@@ -588,7 +619,9 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
             }
         }
     }
-    for (int i = tid; i < nbk_r; i += 256) lcur[i] = 0u;
+    if (!kSplit) {
+        for (int i = tid; i < nbk_r; i += 256) lcur[i] = 0u;
+    }
     __syncthreads();
     // pass 2: place the records (the region's entries come from L2: pass 1 just read them)
     for (int64_t w = w0 + tid; w < w1; w += 256) {
@@ -599,7 +632,7 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
             const uint2 x = run[o];
             const uint32_t kk = x.x >> 16;
             if (lds) {
-                const uint32_t s = atomicAdd(&lcur[kk], 1u);
+                const uint32_t s = atomicAdd(&lcur[slot(x.x)], 1u);
                 unsigned char *pair = image + lline[kk] + kPairBytes * (s >> 1);
                 reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(x.x & 0xffffu);
                 reinterpret_cast<uint32_t *>(pair + 4)[s & 1] = x.y;
@@ -852,7 +885,7 @@ int64_t grf_transpose_self_units_bound(int64_t n_rows, int64_t n_cols, int64_t b
 
 int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
                                   const int64_t *ptr, const int32_t *idx, const float *val, uint32_t *t_desc,
-                                  void *t_rec, int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
+                                  void *t_split, void *t_rec, int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
                                   void *workspace, size_t workspace_bytes, int64_t nnz, void *staging,
                                   size_t staging_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && val && t_desc &&
@@ -896,6 +929,9 @@ int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_w
         GRF_CHECK_HIP(hipMemsetAsync(t_desc, 0, (size_t)(nbk + 1) * 8, st));
         return GRF_OK;
     }
+    GRF_REQUIRE(!t_split || band_width <= 8192, GRF_EUNSUPPORTED,
+                "grf_transpose_banded_self: the sub-band split needs band_width <= 8192 (u16 offsets)");
+    GRF_REQUIRE(((uintptr_t)t_split & 15) == 0, GRF_EINVAL, "grf_transpose_banded_self: t_split must be 16-byte aligned");
     const size_t lds1 = (size_t)kBinCap * 8 + (size_t)nreg * 4 + (kBinRows + 1 + 8) * 4;
     GRF_REQUIRE_GRID(nwg, 256, "tr_bin_kernel");
     tr_bin_kernel<<<(unsigned)nwg, 256, lds1, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr, idx, val, ent, tab,
@@ -914,11 +950,18 @@ int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_w
     int32_t rc = scan_exclusive<int64_t>(n_regions, region_units, ScanIdentity{},
                                          RegionBaseOut{region_base, desc + nbk}, (int64_t *)scan_ws, st);
     if (rc != GRF_OK) return rc;
-    const size_t lds2 = (size_t)8 * cr + 32 + kPlaceCap;
     GRF_REQUIRE_GRID(n_regions, 256, "tr_place_self_kernel");
-    tr_place_self_kernel<<<(unsigned)n_regions, 256, lds2, st>>>(n_rows, n_cols, band_width, cr, nreg, ptr,
-                                                                 region_base, ent, tab, gcur, desc,
-                                                                 (unsigned char *)t_rec, rec_unit);
+    if (t_split) {
+        const size_t lds2 = (size_t)4 * cr * (kSub + 1) + 32 + kPlaceCap;
+        tr_place_self_kernel<true><<<(unsigned)n_regions, 256, lds2, st>>>(
+            n_rows, n_cols, band_width, cr, nreg, ptr, region_base, ent, tab, gcur, desc, (uint4 *)t_split,
+            (unsigned char *)t_rec, rec_unit);
+    } else {
+        const size_t lds2 = (size_t)8 * cr + 32 + kPlaceCap;
+        tr_place_self_kernel<false><<<(unsigned)n_regions, 256, lds2, st>>>(
+            n_rows, n_cols, band_width, cr, nreg, ptr, region_base, ent, tab, gcur, desc, nullptr,
+            (unsigned char *)t_rec, rec_unit);
+    }
     GRF_CHECK_LAUNCH("tr_place_self_kernel");
     return GRF_OK;
 }

@@ -42,11 +42,26 @@ class GraphDiffusionFastGRFKernel(torch.nn.Module):
                                                         device=self.device))
         self.raw_sigma_f = torch.nn.Parameter(torch.tensor(_softplus_inverse(float(sigma_f)), dtype=torch.float64,
                                                            device=self.device))
-        mode = C.LAP_NUMPY_SAFE if normalize_laplacian else C.LAP_COMBINATORIAL
-        self.laplacian = api.dense_laplacian(adjacency_matrix, mode, device)
-        self.feature_matrices = api.dense_step_tensor(self.laplacian, walks_per_node, p_halt, max_walk_length,
-                                                      seed=random_walk_seed, rng=rng, device=device)
-        self._steps = DenseSteps(self.feature_matrices, get_engine(device))
+        self._lap_mode = C.LAP_NUMPY_SAFE if normalize_laplacian else C.LAP_COMBINATORIAL
+        # the walks run on that Laplacian, built and walked on the device (no host round trip)
+        F = api.dense_step_tensor_device(adjacency_matrix, walks_per_node, p_halt, max_walk_length,
+                                         seed=random_walk_seed, rng=rng, device=device, laplacian_mode=self._lap_mode)
+        self._steps = DenseSteps(F, get_engine(device))
+
+    @property
+    def feature_matrices_device(self) -> torch.Tensor:
+        """The (N, N, L) step tensor (the reference's ``feature_matrices_tf``), resident on the device."""
+        return self._steps.F
+
+    @property
+    def feature_matrices(self) -> np.ndarray:
+        """Host copy of the step tensor (made on access only; the kernel never reads it)."""
+        return self._steps.F.cpu().numpy()
+
+    @property
+    def laplacian(self) -> np.ndarray:
+        """The Laplacian the walks ran on (reference attribute; computed on access)."""
+        return api.dense_laplacian(self.adjacency_matrix, self._lap_mode, self.device)
 
     @property
     def beta(self) -> torch.Tensor:

@@ -46,17 +46,36 @@ class GraphGeneralFastGRFKernel(torch.nn.Module):
                 raise ValueError("The length of the modulator vector must be equal to the max_walk_length.")
             init = np.asarray(modulator_vector, dtype=np.float64)
         self.modulator_vector = torch.nn.Parameter(torch.tensor(init, dtype=torch.float64, device=self.device))
+        self._lap_mode = None
         if step_matrices is not None:
-            self.feature_matrices = np.asarray(step_matrices, dtype=np.float64)
+            F = torch.as_tensor(np.asarray(step_matrices, dtype=np.float64))
         elif ablation:
-            self.feature_matrices = api.dense_step_tensor(adjacency_matrix, walks_per_node, p_halt, max_walk_length,
-                                                          seed=random_walk_seed, ablation=True, rng=rng,
-                                                          device=device)
+            F = api.dense_step_tensor_device(adjacency_matrix, walks_per_node, p_halt, max_walk_length,
+                                             seed=random_walk_seed, ablation=True, rng=rng, device=device)
         else:
-            self.laplacian = api.dense_laplacian(adjacency_matrix, C.LAP_NUMPY_SAFE, device)
-            self.feature_matrices = api.dense_step_tensor(self.laplacian, walks_per_node, p_halt, max_walk_length,
-                                                          seed=random_walk_seed, rng=rng, device=device)
-        self._steps = DenseSteps(self.feature_matrices, get_engine(device))
+            # walks on the safe-degree normalised Laplacian, built and walked on the device
+            self._lap_mode = C.LAP_NUMPY_SAFE
+            F = api.dense_step_tensor_device(adjacency_matrix, walks_per_node, p_halt, max_walk_length,
+                                             seed=random_walk_seed, rng=rng, device=device,
+                                             laplacian_mode=C.LAP_NUMPY_SAFE)
+        self._steps = DenseSteps(F, get_engine(device))
+
+    @property
+    def feature_matrices_device(self) -> torch.Tensor:
+        """The (N, N, L) step tensor (the reference's ``feature_matrices_tf``), resident on the device."""
+        return self._steps.F
+
+    @property
+    def feature_matrices(self) -> np.ndarray:
+        """Host copy of the step tensor (made on access only; the kernel never reads it)."""
+        return self._steps.F.cpu().numpy()
+
+    @property
+    def laplacian(self) -> np.ndarray:
+        """The normalised Laplacian the walks ran on (reference attribute; computed on access)."""
+        if self._lap_mode is None:
+            raise AttributeError("laplacian: this kernel was built from given step matrices or the ablation walk")
+        return api.dense_laplacian(self.adjacency_matrix, self._lap_mode, self.device)
 
     def grf_kernel(self, modulator_vector) -> np.ndarray:
         """The whole K (reference :74-77), fp64 numpy."""

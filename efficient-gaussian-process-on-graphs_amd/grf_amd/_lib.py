@@ -73,30 +73,30 @@ SIGNATURES = {
                                          _vp]),
     "grf_transpose_workspace_bytes": (_sz, [_i64]),
     "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
-    "grf_gram_sparse_block": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz,
-                                     _vp]),
+    "grf_gram_sparse_block": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                     _sz, _vp]),
     "grf_gram_workspace_bytes": (_sz, []),
-    "grf_gram_sparse_cols": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _i64,
-                                    _vp, _sz, _vp]),
+    "grf_gram_sparse_cols": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp,
+                                    _i64, _vp, _sz, _vp]),
     "grf_phi_row_shifts_workspace_bytes": (_sz, [_i64]),
     "grf_phi_row_shifts": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
-    "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
+    "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _i64, _vp]),
     "grf_gram_sym_fused_workspace_bytes": (_sz, [_i64, _i64]),
     "grf_gram_sparse_sym_fused": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32,
                                          _vp, _sz, _vp]),
-    "grf_gram_sparse_upper": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32,
-                                     _vp, _sz, _vp]),
-    "grf_gram_sparse_upper_add": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
-                                         _i32, _vp, _sz, _vp]),
+    "grf_gram_sparse_upper": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
+                                     _i32, _vp, _sz, _vp]),
+    "grf_gram_sparse_upper_add": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32,
+                                         _i32, _i32, _vp, _sz, _vp]),
     "grf_hub_panel": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "grf_transpose_drop_columns": (_i32, [_i64, _i64, _vp, _vp, _i32, _vp]),
     "grf_gram_dense_upper": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_transpose_banded_fill_staged": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                                 _sz, _i64, _vp, _sz, _vp]),
     "grf_transpose_staging_bytes": (_sz, [_i64, _i64, _i64, _i64]),
-    "grf_transpose_banded_self": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz,
-                                         _i64, _vp, _sz, _vp]),
+    "grf_transpose_banded_self": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                         _sz, _i64, _vp, _sz, _vp]),
     "grf_transpose_self_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "grf_transpose_self_units_bound": (_i64, [_i64, _i64, _i64, _i32, _i64]),
     "grf_csr_transpose_workspace_bytes": (_sz, [_i64, _i64, _i64]),
@@ -121,6 +121,10 @@ SIGNATURES = {
     "grf_csr_gather_rows": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "grf_csr_rowdot": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "grf_csr_rows_dot_cols": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    # the GPflow surface's algebra on a dense (N, N, L) step tensor
+    "grf_dense_steps_phi": (_i32, [_i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "grf_dense_steps_grad_workspace_bytes": (_sz, [_i64, _i32]),
+    "grf_dense_steps_grad": (_i32, [_i64, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _sz, _vp]),
 }
 
 _lib = None

@@ -171,14 +171,24 @@ def _dense_slots(eng, G, num_walks, p_halt, max_walk_length, seed, n_processes, 
     return eng.walk(G, num_walks, p_halt, max_walk_length, rng=C.RNG_PHILOX, seed=base)
 
 
-def dense_step_tensor(walk_matrix, num_walks, p_halt, max_walk_length, seed=None, n_processes=None, ablation=False,
-                      rng=None, device=None) -> np.ndarray:
-    """RandomWalk(Graph(walk_matrix), seed).get_random_walk_matrices(...) -> (N, N, L) float64."""
+def dense_step_tensor_device(walk_matrix, num_walks, p_halt, max_walk_length, seed=None, n_processes=None,
+                             ablation=False, rng=None, device=None, laplacian_mode=C.LAP_NONE) -> torch.Tensor:
+    """RandomWalk(Graph(W), seed).get_random_walk_matrices(...) as an (N, N, L) float64 tensor that
+    stays on the device (the GPflow wrappers keep it there: no host round trip).  W is
+    ``walk_matrix`` itself (LAP_NONE) or its Laplacian of the given mode, built on the device
+    (``Graph(get_normalized_laplacian(adj))``, gpflow_kernels/general_kernel_fast_grf.py:53-55)."""
     eng = get_engine(device)
-    G = dense_walk_matrix(walk_matrix, C.LAP_NONE, device)
+    G = dense_walk_matrix(walk_matrix, laplacian_mode, device)
     slots = _dense_slots(eng, G, num_walks, p_halt, max_walk_length, seed, n_processes, ablation, rng)
     st = eng.steps(slots, C.NORM_DIV)
-    return eng.steps_dense(st).cpu().numpy()
+    return eng.steps_dense(st)
+
+
+def dense_step_tensor(walk_matrix, num_walks, p_halt, max_walk_length, seed=None, n_processes=None, ablation=False,
+                      rng=None, device=None) -> np.ndarray:
+    """RandomWalk(Graph(walk_matrix), seed).get_random_walk_matrices(...) -> (N, N, L) float64 numpy."""
+    return dense_step_tensor_device(walk_matrix, num_walks, p_halt, max_walk_length, seed, n_processes, ablation,
+                                    rng, device).cpu().numpy()
 
 
 def dense_kernel(adj, modulator_vector, walks_per_node=50, p_halt=0.1, max_walk_length=10, *, seed=42,
@@ -205,10 +215,5 @@ def gram_from_features(F: np.ndarray, f: Sequence[float], device=None) -> np.nda
     f = np.asarray(f, dtype=np.float64).reshape(-1)
     if F.shape[2] != f.shape[0]:
         raise ValueError("modulator length must equal the step tensor's last dimension")
-    Ft = torch.from_numpy(np.ascontiguousarray(F)).to(eng.device)
-    phi = (Ft @ torch.from_numpy(f).to(eng.device))  # (N, N) float64 on the device
-    n = phi.shape[0]
-    lda = max(16, -(-n // 16) * 16)
-    A = torch.zeros((n, lda), dtype=torch.float32, device=eng.device)
-    A[:, :n] = phi.to(torch.float32)
-    return eng.gram_dense(A, n).cpu().numpy().astype(np.float64)
+    from .features import DenseSteps
+    return DenseSteps(F, eng).gram(torch.from_numpy(f)).cpu().numpy().astype(np.float64)

@@ -154,6 +154,42 @@ def shard_entries(phi, shards: Sequence[Tuple[int, int]]) -> List[int]:
 
 
 _GATHER_OVERFLOW = {}  # device -> int32 flag: a bounded all-gather met a rank with more entries than its bound
+_ROW0 = {}             # (device, rows per rank) -> int64 first global row of every rank, on the device
+
+# Collective instrumentation (bench.py --gpus N): when a list, every Phi all-gather appends
+# (start event, end event, bytes sent by this rank, bytes received) -- HIP events on the issuing stream around
+# the collectives (RCCL runs them on its own stream, which the issuing stream then waits for: the
+# interval covers the transfer and the wait for the slowest rank).  None: no events recorded.
+GATHER_STATS: Optional[list] = None
+
+
+def _gather_timer():
+    if GATHER_STATS is None or not torch.cuda.is_available():
+        return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    return ev
+
+
+def _gather_record(start, sent: int, received: int):
+    if start is None:
+        return
+    end = torch.cuda.Event(enable_timing=True)
+    end.record()
+    GATHER_STATS.append((start, end, int(sent), int(received)))
+
+
+def _row0(rows_per_rank: Sequence[int], dev) -> torch.Tensor:
+    """First global row of every rank as a device tensor, made once per shard layout (a pageable
+    host-to-device copy per step would synchronise the issuing stream inside the pipelined front)."""
+    key = (str(dev), tuple(int(r) for r in rows_per_rank))
+    t = _ROW0.get(key)
+    if t is None:
+        starts = [0]
+        for r in rows_per_rank[:-1]:
+            starts.append(starts[-1] + int(r))
+        t = _ROW0[key] = torch.tensor(starts, dtype=torch.int64, device=dev)
+    return t
 
 
 def check_gather_overflow(device) -> None:
@@ -185,6 +221,7 @@ def allgather_csr_rows_bounded(ptr: torch.Tensor, idx: torch.Tensor, val: torch.
     dev = ptr.device
     n_max = max(rows_per_rank)
     B = max(int(entries_bound), 1)
+    t0 = _gather_timer()
     lp = torch.empty(n_max + 1, dtype=torch.int64, device=dev)
     n_loc = ptr.numel() - 1
     lp[:n_loc + 1] = ptr
@@ -208,9 +245,7 @@ def allgather_csr_rows_bounded(ptr: torch.Tensor, idx: torch.Tensor, val: torch.
     counts = torch.cat([(g_ptr[r, 1:n_r + 1] - g_ptr[r, :n_r]) * fits[r] for r, n_r in enumerate(rows_per_rank)])
     full_ptr = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=dev)
     full_ptr[1:] = torch.cumsum(counts, 0)
-    row0 = torch.tensor([0] + list(torch.tensor(rows_per_rank).cumsum(0)[:-1].tolist()), dtype=torch.int64,
-                        device=dev)
-    dst_off = full_ptr[row0].contiguous()
+    dst_off = full_ptr[_row0(rows_per_rank, dev)].contiguous()
     out_i = torch.empty(world * B, dtype=idx.dtype, device=dev)
     out_v = torch.empty(world * B, dtype=val.dtype, device=dev)
     if dev.type == "cuda":
@@ -225,6 +260,8 @@ def allgather_csr_rows_bounded(ptr: torch.Tensor, idx: torch.Tensor, val: torch.
             o, n_e = int(dst_off[r]), int(seg_len[r])
             out_i[o:o + n_e] = g_idx[r * B:r * B + n_e]
             out_v[o:o + n_e] = g_val[r * B:r * B + n_e]
+    sent = (n_max + 1) * 8 + B * (idx.element_size() + val.element_size())
+    _gather_record(t0, sent, world * sent)
     return full_ptr, out_i, out_v
 
 
@@ -275,7 +312,8 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
     return full_ptr, torch.cat(parts_i), torch.cat(parts_v)
 
 
-def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards=None, entries_bound=None):
+def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards=None, entries_bound=None,
+               row_cap=None):
     """All ranks' Phi rows (CSR, float32) from this rank's compacted rows ``local``.
 
     shards: every rank's (begin, end) source range.  When given and ``local`` came from a
@@ -283,6 +321,9 @@ def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards
     the host (``allgather_csr_rows_bounded``); otherwise one host read sizes it exactly.
     entries_bound: the per-rank entry bound of that gather (default: rows x the row capacity, which
     no rank can exceed; ``shard_entries`` of the setup walk gives the exact, ~2.4x smaller one at C4).
+    row_cap: the padded row capacity of every rank's compaction (global: min(m L, n)); default: this
+    rank's nnz_bound / rows.  The bounded / exact choice depends on global information only, so every
+    rank issues the same collectives (an empty shard included).
 
     count_ws: this rank's transpose workspace in which ``walk_phi`` counted the banded transpose's
     buckets for its own rows (global band ids, bands of ``band_width``).  The per-rank counts are
@@ -298,15 +339,18 @@ def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards
     if dist.get_world_size(group) == 1:
         return local
     bound = getattr(local, "nnz_bound", None)
-    if shards is not None and bound is not None and local.n_rows > 0:
-        cap = -(-bound // max(local.n_rows, 1))
+    if shards is not None and (bound is not None or row_cap is not None) and (row_cap or entries_bound
+                                                                          or local.n_rows > 0):
+        cap = int(row_cap) if row_cap else -(-bound // max(local.n_rows, 1))
         rows = [e - b for b, e in shards]
         B = int(entries_bound) if entries_bound else max(rows) * cap
         ptr, idx, val32 = allgather_csr_rows_bounded(local.ptr, local.idx, local.val32, rows, B, group)
         out = DeviceCSR(n, n, ptr, idx, None, val32, None)
         out.nnz_bound = int(idx.numel())
         return out
+    t0 = _gather_timer()
     ptr, idx, val32 = allgather_csr_rows(local.ptr, local.idx, local.val32, group)
+    _gather_record(t0, (local.n_rows + 1) * 8 + 8 * local.nnz, 8 * int(idx.numel()) + 8 * (n + 1))
     return DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))
 
 
@@ -367,7 +411,8 @@ def sharded_kernel_matrix(engine, A, f, walks_per_node, p_halt, max_walk_length,
         rows = engine.features(engine.walk(G, walks_per_node, p_halt, max_walk_length, rng=rng, seed=seed,
                                            src_begin=b, src_end=e), f)
     local = engine.compact(rows, want64=False, want32=True, sync_free=True)
-    phi = gather_phi(engine, local, tws, group, band_width=bw, shards=shards) if world > 1 else local
+    phi = gather_phi(engine, local, tws, group, band_width=bw, shards=shards,
+                     row_cap=max(1, min(walks_per_node * max_walk_length, n))) if world > 1 else local
     tr = engine.transpose_banded(phi, bw, counted_ws=tws, nnz_bound=phi.nnz_bound)
     if mode == "allreduce":
         K = engine.gram_sparse_kslice(phi, tr, b, e)
@@ -391,7 +436,7 @@ def _cols_block(engine, G, f, m, p_halt, L, seed, rng, b, e, group, wl, shards=N
         rows = engine.features(engine.walk(G, m, p_halt, L, rng=rng, seed=seed, src_begin=b, src_end=e), f)
     local = engine.compact(rows, want64=False, want32=True, sync_free=True)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    phi = gather_phi(engine, local, None, group, shards=shards) if world > 1 else local
+    phi = gather_phi(engine, local, None, group, shards=shards, row_cap=max(1, min(m * L, n))) if world > 1 else local
     tr = engine.transpose_banded(local, wl, counted_ws=tws, nnz_bound=local.nnz_bound)
     # the square K[b:e, b:e] on and above its diagonal, then mirrored, when it is a large enough share
     # of the block to pay for the mirror (N <= 4)

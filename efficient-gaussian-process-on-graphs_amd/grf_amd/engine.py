@@ -133,6 +133,9 @@ class Banded:
     n_rows: int
     n_cols: int
     rec_unit: int = C.REC_LINE  # bucket alignment: 128-byte lines or packed 12-byte pairs
+    # per bucket 8 uint16 entry offsets of its sub-bands (buckets laid out by sub-band; the symmetric
+    # Gram's diagonal tiles start there), or None (records in arbitrary order within a bucket)
+    t_split: Optional[torch.Tensor] = None
 
 
 def cols_band_width(rows: int, max_width: int = ROWS_BAND_WIDTH) -> int:
@@ -388,7 +391,7 @@ class GRFEngine:
     def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH,
                          counted_ws: Optional[torch.Tensor] = None, staged: Optional[bool] = None,
                          nnz_bound: Optional[int] = None, rec_unit: Optional[int] = None,
-                         self_count: Optional[bool] = None) -> Banded:
+                         self_count: Optional[bool] = None, split: bool = True) -> Banded:
         """Banded transpose of Phi.  counted_ws: workspace whose bucket counts ``walk_phi`` filled.
         staged: two-pass binned fill (default when band_width % 64 == 0) or the atomic fill.
         self_count: the staged fill without a plan (grf_transpose_banded_self; default unless
@@ -408,7 +411,7 @@ class GRFEngine:
         if self_count:
             if counted_ws is not None or not staged:
                 raise ValueError("self_count: the staged transpose counts its own buckets (no counted_ws)")
-            return self._transpose_self(phi, band_width, nnz_bound, rec_unit, t_desc, t_max, t_shift)
+            return self._transpose_self(phi, band_width, nnz_bound, rec_unit, t_desc, t_max, t_shift, split)
         ws = counted_ws if counted_ws is not None else self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
         if rec_unit is None:
             rec_unit = choose_rec_unit(phi.nnz if phi._nnz is not None or nnz_bound is None else nnz_bound,
@@ -453,7 +456,7 @@ class GRFEngine:
         return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols, u)
 
     def _transpose_self(self, phi: DeviceCSR, band_width: int, nnz_bound: Optional[int], rec_unit: Optional[int],
-                        t_desc, t_max, t_shift) -> Banded:
+                        t_desc, t_max, t_shift, split: bool = True) -> Banded:
         """The plan-free staged transpose (grf_transpose_banded_self): buckets counted by the placing
         workgroups themselves, no counts from the walk and no scan over every bucket."""
         n_rows, n_cols = phi.n_rows, phi.n_cols
@@ -472,11 +475,13 @@ class GRFEngine:
         t_rec = self._empty(max(units, 1) * u + 128, torch.uint8)
         ws = self._ws(self.lib.grf_transpose_self_workspace_bytes(n_rows, n_cols, band_width))
         sg = self._ws(self.lib.grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz))
+        nbk = -(-n_rows // band_width) * n_cols
+        t_split = self._empty(8 * nbk, torch.int16) if split and band_width <= 8192 else None
         C.check(self.lib.grf_transpose_banded_self(n_rows, n_cols, band_width, u, _p(phi.ptr), _p(phi.idx),
-                                                   _p(phi.val32), _p(t_desc), _p(t_rec), t_rec.numel(), _p(t_max),
-                                                   _p(t_shift), _p(ws), ws.numel(), nnz, _p(sg), sg.numel(),
-                                                   self.stream), "grf_transpose_banded_self")
-        return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols, u)
+                                                   _p(phi.val32), _p(t_desc), _p(t_split), _p(t_rec), t_rec.numel(),
+                                                   _p(t_max), _p(t_shift), _p(ws), ws.numel(), nnz, _p(sg),
+                                                   sg.numel(), self.stream), "grf_transpose_banded_self")
+        return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols, u, t_split)
 
     # ----------------------------------------------------------------- Gram
     @staticmethod
@@ -507,8 +512,9 @@ class GRFEngine:
             out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_gram_sparse_block(n, row_begin, row_end, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
                                                tr.band_width, tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec),
-                                               _p(tr.t_rowshift), _p(out), out.stride(0), _p(self._gram_ws),
-                                               self._gram_ws.numel(), self.stream), "grf_gram_sparse_block")
+                                               _p(tr.t_split), _p(tr.t_rowshift), _p(out), out.stride(0),
+                                               _p(self._gram_ws), self._gram_ws.numel(), self.stream),
+                "grf_gram_sparse_block")
         return out[:, :n]
 
     def phi_row_shifts(self, phi: DeviceCSR) -> torch.Tensor:
@@ -539,7 +545,7 @@ class GRFEngine:
         C.check(self.lib.grf_gram_sparse_cols(phi.n_cols, row_begin, row_end, _p(phi.ptr), _p(phi.idx),
                                               _p(phi.val32), _p(row_shift), t_rows,
                                               -1 if sym_row0 is None else int(sym_row0), tr_b.band_width, tr_b.rec_unit,
-                                              _p(tr_b.t_desc), _p(tr_b.t_rec), _p(out), out.stride(0),
+                                              _p(tr_b.t_desc), _p(tr_b.t_rec), _p(tr_b.t_split), _p(out), out.stride(0),
                                               _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_cols")
         return out[:, :t_rows]
@@ -566,7 +572,8 @@ class GRFEngine:
         if out is None:
             out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_gram_sparse_sym(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
-                                             tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out), out.stride(0),
+                                             tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_split), _p(tr.t_rowshift),
+                                             _p(out), out.stride(0),
                                              _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_sym")
         return out[:, :n]
@@ -576,7 +583,8 @@ class GRFEngine:
         parts = (begin, end, n): only those parts of the band-major tile sequence cut into n."""
         n = tr.n_rows
         C.check(self.lib.grf_gram_sparse_upper(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
-                                               tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift), _p(out),
+                                               tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_split),
+                                               _p(tr.t_rowshift), _p(out),
                                                out.stride(0), int(parts[0]), int(parts[1]), int(parts[2]),
                                                _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_upper")
@@ -630,7 +638,8 @@ class GRFEngine:
         C.check(self.lib.grf_gram_dense_upper(n, h, _p(P), P.stride(0), _p(out), out.stride(0), self.stream),
                 "grf_gram_dense_upper")
         C.check(self.lib.grf_gram_sparse_upper_add(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
-                                                   tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift),
+                                                   tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_split),
+                                                   _p(tr.t_rowshift),
                                                    _p(out), out.stride(0), 0, 1, 1, _p(self._gram_ws),
                                                    self._gram_ws.numel(), self.stream), "grf_gram_sparse_upper_add")
         ev = None

@@ -36,6 +36,20 @@ def _torch_csr(mat) -> torch.Tensor:
     return t
 
 
+def _rows_sorted_unique(t: torch.Tensor) -> bool:
+    """Every row's column indices strictly increasing (one device pass, one host read)."""
+    col = t.col_indices()
+    nnz = col.numel()
+    if nnz < 2:
+        return True
+    crow = t.crow_indices().long()
+    starts = torch.zeros(nnz, dtype=torch.bool, device=col.device)
+    first = crow[:-1]
+    starts[first[first < nnz]] = True  # entry e opens a row: no order constraint against e - 1
+    bad = (col[1:] <= col[:-1]) & ~starts[1:]
+    return not bool(bad.any().item())
+
+
 class StepMatrices:
     """The L step matrices of one graph on one device: int64 row pointers, int32 columns and the
     preprocessor's float32 values (views of the torch CSR tensors where the dtypes already match)."""
@@ -51,6 +65,10 @@ class StepMatrices:
         for t in ts:
             if tuple(t.shape) != self.shape:
                 raise ValueError("step matrices differ in shape")
+            if not _rows_sorted_unique(t):
+                # grf_phi_steps_csr's L-way merge needs sorted, duplicate-free columns in every row;
+                # torch's own sparse ops accept any order and sum duplicates, so coalesce to that meaning
+                t = t.to_sparse_coo().coalesce().to_sparse_csr()
             ptr = t.crow_indices().to(dev, torch.int64).contiguous()
             idx = t.col_indices().to(dev, torch.int32).contiguous()
             val = t.values().to(dev, torch.float32).contiguous()
@@ -137,7 +155,12 @@ def kernel_block(eng: GRFEngine, phi: DeviceCSR, x1: Optional[torch.Tensor], x2:
     if n1 == 0 or n2 == 0:
         return torch.zeros((n1, n2), dtype=torch.float32, device=eng.device)
     tr = eng.transpose_banded(P2, cols_band_width(n2))
-    return eng.gram_sparse_cols(P1, eng.phi_row_shifts(P1), tr, 0, n1, sym_row0=0 if same else None)
+    # the fixed-point shift of row r bounds |Phi[r, k] Phi[j, k]| with max|Phi| over the OTHER operand's
+    # rows j too: take it over all of Phi (a superset of Phi[x1] and Phi[x2]) and pick the x1 rows
+    shifts = eng.phi_row_shifts(phi)
+    if x1 is not None:
+        shifts = shifts[x1.to(eng.device).long()].contiguous()
+    return eng.gram_sparse_cols(P1, shifts, tr, 0, n1, sym_row0=0 if same else None)
 
 
 def _index(x: Optional[torch.Tensor], dev) -> Optional[torch.Tensor]:
@@ -166,7 +189,7 @@ class GRFKernelFunction(torch.autograd.Function):
             out = kernel_block(eng, phi, i1, i2, same)
             out = out.to(f.dtype) if out.dtype != f.dtype else out
         ctx.steps, ctx.phi, ctx.i1, ctx.i2, ctx.diag, ctx.n_f = steps, phi, i1, i2, diag, f.numel()
-        ctx.f_dtype = f.dtype
+        ctx.f_dtype, ctx.f_device = f.dtype, f.device
         return out
 
     @staticmethod
@@ -193,7 +216,8 @@ class GRFKernelFunction(torch.autograd.Function):
                 for l in range(L):
                     M = steps.steps[l]
                     grad[l] = rows_dot_cols(eng, M, i1, Z1).sum() + rows_dot_cols(eng, M, i2, Z2).sum()
-        return grad.to(ctx.f_dtype), None, None, None, None
+        # (on f's own device: a modulator parameter left on the CPU still gets its gradient)
+        return grad.to(device=ctx.f_device, dtype=ctx.f_dtype), None, None, None, None
 
 
 def grf_kernel(f: torch.Tensor, steps: StepMatrices, x1=None, x2=None, diag: bool = False) -> torch.Tensor:
@@ -211,8 +235,9 @@ def feature_matrix(f: torch.Tensor, steps: StepMatrices) -> torch.Tensor:
 # ----------------------------------------------------------------- dense step tensors (GPflow surface)
 class DenseSteps:
     """A dense (N, N, L) step tensor F resident on the device once (the GPflow wrappers'
-    ``feature_matrices_tf``, gpflow_kernels/general_kernel_fast_grf.py:44-59), with K = (F f)(F f)^T
-    on the MFMA Gram (grf_gram_dense) cached per modulator value."""
+    ``feature_matrices_tf``, gpflow_kernels/general_kernel_fast_grf.py:44-59).  Per modulator value:
+    Phi = F f on ``grf_dense_steps_phi`` (fp64, plus the fp32 image of the Gram), K = Phi Phi^T on the
+    MFMA Gram (``grf_gram_dense_ws``), cached; the modulator gradient on ``grf_dense_steps_grad``."""
 
     def __init__(self, F, engine: Optional[GRFEngine] = None):
         self.engine = engine or get_engine()
@@ -221,29 +246,57 @@ class DenseSteps:
         if self.F.dim() != 3 or self.F.shape[0] != self.F.shape[1]:
             raise ValueError("step tensor must be (N, N, L)")
         self.n, self.L = self.F.shape[0], self.F.shape[2]
+        self.lda = max(64, -(-self.n // 64) * 64)  # (zero-padded k range of the MFMA Gram)
         self._key = None
         self._K = None
+        self._phi64 = None
+
+    def _modulator(self, f: torch.Tensor) -> torch.Tensor:
+        ft = f.detach().to(self.engine.device, torch.float64).reshape(-1).contiguous()
+        if ft.numel() != self.L:
+            raise ValueError(f"modulator length {ft.numel()} != the step tensor's L = {self.L}")
+        return ft
+
+    def _phi_both(self, f: torch.Tensor):
+        eng, n = self.engine, self.n
+        ft = self._modulator(f)
+        phi64 = torch.empty((n, n), dtype=torch.float64, device=eng.device)
+        phi32 = torch.empty((n, self.lda), dtype=torch.float32, device=eng.device)
+        C.check(eng.lib.grf_dense_steps_phi(n, self.L, _p(self.F), _p(ft), _p(phi64), _p(phi32), self.lda,
+                                            eng.stream), "grf_dense_steps_phi")
+        return phi64, phi32
 
     def phi(self, f: torch.Tensor) -> torch.Tensor:
         """Phi = F f (N x N, fp64 on the device): ``tf.linalg.matmul(F, f[:, None])`` (:76)."""
-        return self.F @ f.detach().to(self.engine.device, torch.float64).reshape(-1)
+        return self._phi_both(f)[0]
 
     def gram(self, f: torch.Tensor) -> torch.Tensor:
         """K = Phi Phi^T (fp32, N x N) on the MFMA Gram, cached for the last modulator value."""
         key = f.detach().to("cpu", torch.float64).reshape(-1).numpy().tobytes()
         if key != self._key:
-            n = self.n
-            lda = max(16, -(-n // 16) * 16)
-            A = torch.zeros((n, lda), dtype=torch.float32, device=self.engine.device)
-            A[:, :n] = self.phi(f).to(torch.float32)
-            self._K = self.engine.gram_dense(A, n)
+            self._phi64, phi32 = self._phi_both(f)
+            self._K = self.engine.gram_dense(phi32, self.n)
             self._key = key
         return self._K
+
+    def grad(self, f: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
+        """dL/df_l = <F_l, (G + G^T) Phi> for the upstream gradient G of K (fp64, length L)."""
+        eng, n = self.engine, self.n
+        self.gram(f)  # (Phi of this modulator value)
+        Gd = G.to(eng.device, torch.float64).contiguous()
+        out = torch.empty(self.L, dtype=torch.float64, device=eng.device)
+        need = int(eng.lib.grf_dense_steps_grad_workspace_bytes(n, self.L))
+        ws = getattr(self, "_grad_ws", None)
+        if ws is None or ws.numel() < need:
+            ws = self._grad_ws = eng._ws(need)
+        C.check(eng.lib.grf_dense_steps_grad(n, self.L, _p(self.F), _p(self._phi64), _p(Gd), Gd.stride(0), _p(out),
+                                             _p(ws), ws.numel(), eng.stream), "grf_dense_steps_grad")
+        return out
 
 
 class DenseGramFunction(torch.autograd.Function):
     """K = (F f)(F f)^T with dK/df_l = F_l Phi^T + Phi F_l^T: the backward contracts the upstream
-    G with it, dL/df_l = <F_l, (G + G^T) Phi> (one plain N x N GEMM + a reduction over F)."""
+    G with it, dL/df_l = <F_l, (G + G^T) Phi> (grf_dense_steps_grad: fp64 MFMA GEMM + fused reduction)."""
 
     @staticmethod
     def forward(ctx, f: torch.Tensor, steps: DenseSteps):
@@ -254,9 +307,5 @@ class DenseGramFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         (f,) = ctx.saved_tensors
-        steps = ctx.steps
-        phi = steps.phi(f)
-        G = g.to(steps.engine.device, torch.float64)
-        H = (G + G.t()) @ phi
-        grad = torch.einsum("ijl,ij->l", steps.F, H)
-        return grad.to(f.dtype), None
+        grad = ctx.steps.grad(f, g)
+        return grad.to(device=f.device, dtype=f.dtype), None

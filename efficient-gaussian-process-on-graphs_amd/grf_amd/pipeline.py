@@ -144,11 +144,12 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                                          count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
                                          want64=False),
                             want64=False, want32=True, sync_free=True)
-        phi = gather_phi(eng, local, group=pl.group, shards=pl.shards, entries_bound=pl.gather_bound or None) \
-            if pl.world > 1 else local
+        phi = gather_phi(eng, local, group=pl.group, shards=pl.shards, entries_bound=pl.gather_bound or None,
+                         row_cap=pl.rows_cap) if pl.world > 1 else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
                                             local.val32)
-        tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap)
+        tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap,
+                                  split=pl.cols_sym)
         return Front(phi, tr, local, eng.phi_row_shifts(phi))
     # (the transpose counts its own buckets unless GRF_TRANSPOSE_SELF=0: then the walk counts them)
     tws = None if SELF_COUNT_TRANSPOSE else eng.transpose_workspace(n, n, pl.band_width)
@@ -157,9 +158,10 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                                      want64=False),
                         want64=False, want32=True, sync_free=True)
     phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards,
-                     entries_bound=pl.gather_bound or None) if pl.world > 1 else local
+                     entries_bound=pl.gather_bound or None, row_cap=pl.rows_cap) if pl.world > 1 else local
     # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
-    tr = eng.transpose_banded(phi, pl.band_width, counted_ws=tws, nnz_bound=n * pl.rows_cap)
+    # (the sub-band split serves the symmetric mode's diagonal tiles only)
+    tr = eng.transpose_banded(phi, pl.band_width, counted_ws=tws, nnz_bound=n * pl.rows_cap, split=pl.mode == "sym")
     return Front(phi, tr, local)
 
 
@@ -233,3 +235,56 @@ def k_view(K: torch.Tensor, pl: StepPlan) -> torch.Tensor:
     if pl.mode == "cols":
         return K[:, :pl.block_rows]
     return K[:, :pl.n]
+
+
+def _abs_csr(A: DeviceCSR) -> DeviceCSR:
+    return DeviceCSR(A.n_rows, A.n_cols, A.ptr, A.idx, None, A.val32.abs(), A._nnz)
+
+
+def k_block_check(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, seed: int = 7,
+                  chunk: int = 2048) -> dict:
+    """Size-independent check of this rank's K block against the Phi the step gathered (the bench's
+    in-run parity, on the device; tests/test_gpu_headline.py's matvec checks).  With the block
+    K_blk = Phi_A Phi_B^T (rows A, columns B of K) and random +-1 vectors u (over B) and v (over A):
+        K_blk u   against  Phi_A (Phi_B^T u)      and      K_blk^T v  against  Phi_B (Phi_A^T v),
+    both sides summed in fp64, each entry within the summed elementwise K tolerance
+        3e-5 |Phi_A| (|Phi_B|^T |u|) + 1e-12 max|Phi| max_i max_k |Phi_ik| sum|u| + 1e-7 |want|.
+    Returns {"max_ratio": max |got - want| / bound (<= 1 passes), ...}.  Reads K once (chunked)."""
+    n = pl.n
+    phi = fr.phi
+    if pl.mode == "cols":
+        A_rows, B_rows = None, torch.arange(pl.b, pl.kr_end, device=eng.device)
+        Kv = K[:, :pl.block_rows]                      # n x |B|
+    elif pl.mode == "allreduce":
+        A_rows, B_rows = None, None
+        Kv = K[:, :n]
+    else:  # sym (all rows) / rows (this rank's rows)
+        A_rows = None if (pl.b, pl.kr_end) == (0, n) else torch.arange(pl.b, pl.kr_end, device=eng.device)
+        B_rows = None
+        Kv = K[:, :n][:pl.block_rows]
+    gen = torch.Generator(device=eng.device).manual_seed(seed)
+    u = (torch.randint(0, 2, (Kv.shape[1],), generator=gen, device=eng.device) * 2 - 1).to(torch.float64)
+    v = (torch.randint(0, 2, (Kv.shape[0],), generator=gen, device=eng.device) * 2 - 1).to(torch.float64)
+    Ku = torch.empty(Kv.shape[0], dtype=torch.float64, device=eng.device)
+    Ktv = torch.zeros(Kv.shape[1], dtype=torch.float64, device=eng.device)
+    for r0 in range(0, Kv.shape[0], chunk):
+        blk = Kv[r0:r0 + chunk].double()
+        Ku[r0:r0 + chunk] = blk @ u
+        Ktv += blk.t() @ v[r0:r0 + chunk]
+    aphi = _abs_csr(phi)
+
+    def prod(P, rows_out, rows_in, w):
+        """P[rows_out] (P[rows_in]^T w) in fp64 on the device (two CSR SpMMs)."""
+        Pt = eng.csr_transpose(P, rows_in)
+        return eng.spmm(P, eng.spmm(Pt, w[:, None].contiguous()), rows_out)[:, 0]
+
+    amax = float(phi.val32[:phi.nnz].abs().max().item()) if phi.nnz else 0.0
+    ratios = []
+    for got, w, out_rows, in_rows in ((Ku, u, A_rows, B_rows), (Ktv, v, B_rows, A_rows)):
+        want = prod(phi, out_rows, in_rows, w)
+        bound = 3e-5 * prod(aphi, out_rows, in_rows, w.abs()) + 1e-12 * amax * amax * float(w.abs().sum()) \
+            + 1e-7 * want.abs() + 1e-300
+        ratios.append(float(((got - want).abs() / bound).max().item()))
+    return {"max_ratio": max(ratios), "ok": max(ratios) <= 1.0,
+            "checks": "K_blk u and K_blk^T v (fp64, random +-1 vectors) vs Phi_A (Phi_B^T u) and Phi_B (Phi_A^T v) "
+                      "from this step's gathered Phi, elementwise-summed K tolerance"}

@@ -238,10 +238,15 @@ size_t grf_transpose_staging_bytes(int64_t n_rows, int64_t n_cols, int64_t band_
  * t_desc (same meaning as the plan's: {first unit, pairs}; t_desc[nbk] = the slabs' total, an
  * upper bound of the units written).  Buckets stay in (band, column) order; unused slab tails are
  * never read.  t_rec >= grf_transpose_self_units_bound(...) * rec_unit bytes; workspace >=
- * grf_transpose_self_workspace_bytes; staging as for grf_transpose_banded_fill_staged. */
+ * grf_transpose_self_workspace_bytes; staging as for grf_transpose_banded_fill_staged.
+ * t_split (NULL: none; else 16 bytes per bucket, 16-byte aligned, band_width <= 8192): every
+ * bucket's entries are laid out by sub-band (the 8 row ranges of band_width / 8 rows, in order)
+ * and t_split[b] holds 8 uint16 entry offsets, the entries of bucket b before each sub-band
+ * (all 0 for a region too large for the LDS image: order unspecified there).  The symmetric
+ * Gram entry points take it to start a diagonal tile's buckets at its row's sub-band. */
 int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_width, int32_t rec_unit,
                                   const int64_t *ptr, const int32_t *idx, const float *val, uint32_t *t_desc,
-                                  void *t_rec, int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
+                                  void *t_split, void *t_rec, int64_t t_rec_bytes, float *t_maxabs, int32_t *t_rowshift,
                                   void *workspace, size_t workspace_bytes, int64_t nnz, void *staging,
                                   size_t staging_bytes, grf_stream_t stream);
 size_t grf_transpose_self_workspace_bytes(int64_t n_rows, int64_t n_cols, int64_t band_width);
@@ -270,10 +275,13 @@ size_t grf_gram_workspace_bytes(void);
  * K[i, band >= band(i)] (about half the work) and a mirror pass copies K[j, i] = K[i, j]
  * for band(j) > band(i).  Same arguments and per-entry values as grf_gram_sparse with
  * row_begin = 0, row_end = n_total, except that the mirrored entries carry the
- * fixed-point rounding of row i (K is exactly symmetric).  band_width multiple of 64. */
+ * fixed-point rounding of row i (K is exactly symmetric).  band_width multiple of 64.
+ * t_split: the transpose's sub-band split (grf_transpose_banded_self) or NULL; with it a tile on
+ * its row's own band fetches only the buckets' sub-bands from the row's on (the entries below the
+ * diagonal it skips are the mirror's to write). */
 int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                             int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                            const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
+                            const void *t_split, const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
                             grf_stream_t stream);
 
 /* The Gram half of grf_gram_sparse_sym alone: the tiles K[i, band >= band(i)] (the lower parts
@@ -283,7 +291,7 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
  * split so that other work can be scheduled against the Gram's tail and the HBM-bound mirror. */
 int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                               int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                              const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                              const void *t_split, const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
                               int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                               grf_stream_t stream);
 
@@ -295,7 +303,7 @@ int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t
  * an fp32 MFMA sum instead of the exact fixed-point one).  Same arguments as grf_gram_sparse_upper. */
 int32_t grf_gram_sparse_upper_add(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                                   int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                                  const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
+                                  const void *t_split, const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
                                   int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                                   grf_stream_t stream);
 
@@ -338,8 +346,8 @@ int32_t grf_gram_sparse_sym_fused(int64_t n_total, const int64_t *ptr, const int
 int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
                              const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
                              int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
-                             const void *t_rec, float *K, int64_t ldk, void *workspace, size_t workspace_bytes,
-                             grf_stream_t stream);
+                             const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
+                             size_t workspace_bytes, grf_stream_t stream);
 
 /* The Gram fixed-point row shifts of a CSR (n_rows rows; float values) and its max |value|
  * (*maxabs, device): the same rule and the same per-row summation order as the banded transpose's
@@ -354,8 +362,9 @@ int32_t grf_phi_row_shifts(int64_t n_rows, const int64_t *ptr, const float *val,
  * as in grf_gram_sparse_sym); all other tiles are the row mode's.  The multi-GPU row blocks. */
 int32_t grf_gram_sparse_block(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
                               const int32_t *idx, const float *val, int64_t band_width, int32_t rec_unit,
-                              const uint32_t *t_desc, const void *t_rec, const int32_t *t_rowshift, float *K,
-                              int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream);
+                              const uint32_t *t_desc, const void *t_rec, const void *t_split,
+                              const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
+                              size_t workspace_bytes, grf_stream_t stream);
 
 /* Partial Gram over a slice of the inner dimension: K[r, :] = sum over k in [k_begin, k_end)
  * of Phi[r, k] Phi[:, k] (same fixed-point rule as grf_gram_sparse).  The partial Grams of
@@ -393,6 +402,25 @@ int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda,
 /* CSR (float32) -> dense float32 [n_rows x lda], zero filled. */
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,
                     int64_t lda, grf_stream_t stream);
+
+/* -------------------------------------- GPflow surface: a dense (N, N, L) step tensor F
+ * Replaces efficient_graph_gp/gpflow_kernels/general_kernel_fast_grf.py:74-77 and
+ * diffusion_kernel_fast_grf.py:52-60 (Phi = F f by tf.linalg.matmul, K = Phi Phi^T) and the
+ * modulator gradient TensorFlow takes through them.  F float64 [n][n][L] contiguous (the
+ * RandomWalk.get_random_walk_matrices tensor, random_walk_samplers/sampler.py:188-203).
+ * grf_dense_steps_phi: Phi[i, j] = sum_l F[i, j, l] f[l] (fp64, l ascending) -> phi64 [n x n]
+ * (optional, NULL to skip) and the zero-padded fp32 image phi32 [n x lda32] (lda32 >= n) that
+ * grf_gram_dense / grf_gram_dense_ws read as A.
+ * grf_dense_steps_grad: grad[l] = sum_ij F[i, j, l] ((G + G^T) Phi)[i, j] for the upstream gradient
+ * G [n x ldg] of L w.r.t. K = Phi Phi^T (fp64 MFMA GEMM with the reduction fused into its
+ * epilogue; partials summed in a fixed order: deterministic).  workspace:
+ * grf_dense_steps_grad_workspace_bytes(n, L) bytes. */
+int32_t grf_dense_steps_phi(int64_t n, int32_t L, const double *F, const double *f, double *phi64, float *phi32,
+                            int64_t lda32, grf_stream_t stream);
+size_t grf_dense_steps_grad_workspace_bytes(int64_t n, int32_t L);
+int32_t grf_dense_steps_grad(int64_t n, int32_t L, const double *F, const double *phi64, const double *G,
+                             int64_t ldg, double *grad, void *workspace, size_t workspace_bytes,
+                             grf_stream_t stream);
 
 /* ------------------------------------------- K.v and the pathwise-conditioning CG
  * The step after the path: SparseGraphGP.predict

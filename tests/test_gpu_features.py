@@ -151,3 +151,64 @@ def test_full_graph_forward_on_enron_without_densifying(golden):
     dfdsig = [fm[l] / sig for l in range(8)]
     np.testing.assert_allclose(dk.raw_sigma_f.grad.item(),
                                sum(g * df for g, df in zip(g_phi, dfdsig)) * (1 - np.exp(-sig)), rtol=1e-3)
+
+
+def test_dense_steps_kernels_cora_size(golden):
+    """The GPflow surface's per-call algebra on HIP (grf_dense_steps_phi / grf_dense_steps_grad,
+    gpflow_kernels/general_kernel_fast_grf.py:74-77) at Cora size: F = the reference's own Cora step
+    matrices (m = 16, 4 steps, tests/golden/cora.npz) as the dense (N, N, L) tensor, against the numpy
+    restatement Phi = F f, K = Phi Phi^T, dL/df_l = <F_l, (G + G^T) Phi> (parity unpinned by the
+    reference: GPflow / TF absent).  Phi fp64 within 1e-15 relative (order of the L-term sum), K within
+    the fp32 MFMA tolerance, the gradient rtol 1e-9 (fp64 MFMA GEMM, fused reduction, fixed order)."""
+    from grf_amd.engine import get_engine
+    from grf_amd.features import DenseGramFunction, DenseSteps
+    d = golden("cora")
+    n = len(d["A_indptr"]) - 1
+    L = 4
+    F = np.zeros((n, n, L))
+    for l in range(L):
+        F[:, :, l] = csr(d, f"m16_l{l}", n).toarray()
+    f = np.array([1.0, -0.5, 0.125, -0.0208])
+    st = DenseSteps(F, get_engine())
+    P = F @ f
+    phi = st.phi(torch.from_numpy(f)).cpu().numpy()
+    assert np.all(np.abs(phi - P) <= 1e-15 * np.abs(F) @ np.abs(f) + 1e-300)
+    K = st.gram(torch.from_numpy(f)).cpu().numpy()
+    aP = np.abs(P)
+    ok, e = _close(K, P @ P.T, aP @ aP.T)
+    assert ok, e
+    # the learnable path: d sum(W * K) / d f through DenseGramFunction
+    W = np.random.default_rng(5).standard_normal((n, n))
+    fp = torch.tensor(f, device="cuda", requires_grad=True)
+    (DenseGramFunction.apply(fp, st) * torch.tensor(W, device="cuda")).sum().backward()
+    H = (W + W.T) @ P
+    gref = np.einsum("ijl,ij->l", F, H)
+    np.testing.assert_allclose(fp.grad.cpu().numpy(), gref, rtol=1e-9, atol=1e-12 * np.abs(gref).max())
+    # a CPU modulator parameter gets its gradient on its own device
+    fc = torch.tensor(f, requires_grad=True)
+    (DenseGramFunction.apply(fc, st) * torch.tensor(W, device="cuda")).sum().backward()
+    assert fc.grad.device.type == "cpu"
+    np.testing.assert_allclose(fc.grad.numpy(), gref, rtol=1e-9, atol=1e-12 * np.abs(gref).max())
+
+
+def test_kernel_block_shift_bound_takes_both_operands(golden):
+    """K[x1, x2] with x1 one low-magnitude row and x2 holding the row with the largest |Phi|: the
+    fixed-point shift of x1's row must bound its products with the OTHER operand's values too
+    (shifts from Phi[x1] alone let terms pass 2^51 on degree-skewed graphs)."""
+    from efficient_graph_gp_sparse.gptorch_kernels_sparse import SparseGRFKernel
+    d = golden("small_graphs")
+    steps = [csr(d, f"er40_sp_n3_s7_l{l}", 40) for l in range(4)]
+    scale = np.ones(40)
+    scale[7] = 1e6  # a hub-like row of huge loads
+    steps = [sp.diags(scale) @ M for M in steps]
+    dense = [M.toarray().astype(np.float32).astype(np.float64) for M in steps]
+    kern = SparseGRFKernel(4, _ops(steps)).cuda()
+    f = kern.modulator_vector.detach().cpu().numpy().astype(np.float64)
+    Phi = sum(fl * M for fl, M in zip(f, dense))
+    aPhi = np.abs(Phi)
+    lo = int(np.argmin(np.where(aPhi.max(1) > 0, aPhi.max(1), np.inf)))
+    i1, i2 = [lo], [7, lo, 3]
+    K = kern(torch.tensor(i1, device="cuda"), torch.tensor(i2, device="cuda")).detach().cpu().numpy()
+    # elementwise, relative to each entry's own |Phi||Phi|^T (no absolute slack from the huge row)
+    err = np.abs(K.astype(np.float64) - Phi[i1] @ Phi[i2].T)
+    assert np.all(err <= 3e-5 * (aPhi[i1] @ aPhi[i2].T) + 1e-30), err

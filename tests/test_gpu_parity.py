@@ -349,6 +349,68 @@ def test_transpose_staged_fill_matches_atomic_fill(eng, n, deg, m, L, bw, unit):
         assert np.array_equal(eng.gram_sparse_sym(phi, other).cpu().numpy(), eng.gram_sparse_sym(phi, ts).cpu().numpy())
 
 
+@pytest.mark.parametrize("n,bw,unit", [(20000, 4096, 128), (20000, 8192, 128), (5000, 64, 128), (9000, 1024, 12),
+                                        (3000, 4096, 128)])
+def test_transpose_sub_band_split(eng, n, bw, unit):
+    """The self-count transpose's sub-band split: every bucket lists its entries by sub-band (the 8
+    row ranges of bw / 8 rows, in order) and t_split holds the entry offsets of the sub-bands; the
+    symmetric Gram's diagonal tiles start their buckets at their row's sub-band (no pairs of the
+    earlier sub-bands fetched) -- K is bit-identical to the unsplit transpose's in every symmetric
+    entry point (whole K, the upper tiles in parts + mirror, the column block's square, the row
+    block's interior, the hub-column split), because the skipped products only reach entries below
+    the diagonal, which the mirror overwrites."""
+    import torch
+    A = er_graph(n, 8, n + 3)
+    G = eng.laplacian(A)
+    phi = eng.compact(eng.walk_phi(G, 32, 0.15, 5, [1.0, -0.5, 0.25, -0.125, 0.1], seed=9))
+    ts = eng.transpose_banded(phi, bw, rec_unit=unit)
+    tn = eng.transpose_banded(phi, bw, rec_unit=unit, split=False)
+    assert ts.t_split is not None and tn.t_split is None
+    nb = -(-n // bw)
+    desc = ts.t_desc.cpu().numpy().view(np.uint32).reshape(-1, 2)
+    split = ts.t_split.cpu().numpy().view(np.uint16).reshape(-1, 8).astype(np.int64)
+    rec = ts.t_rec.cpu().numpy()
+    P = phi.to_scipy().tocsc()
+    rng = np.random.default_rng(1)
+    for b in rng.choice(nb * n, size=min(nb * n, 2000), replace=False):
+        J, k = divmod(int(b), n)
+        lo, hi = J * bw, min(n, (J + 1) * bw)
+        rows = P.indices[P.indptr[k]:P.indptr[k + 1]]
+        rows = rows[(rows >= lo) & (rows < hi)] - lo
+        c = len(rows)
+        assert int(desc[b, 1]) == (c + 1) // 2
+        if c == 0:
+            continue
+        seg = rec[int(desc[b, 0]) * unit: int(desc[b, 0]) * unit + 12 * ((c + 1) // 2)].reshape(-1, 12)
+        got = seg[:, :4].copy().view(np.uint16).reshape(-1)[:c].astype(np.int64) // 8  # rows in the band
+        sub = got * 8 // bw
+        assert np.all(np.diff(sub) >= 0), b  # sub-band order
+        exp = np.searchsorted(sub, np.arange(8), side="left")
+        if split[b].any():  # (0 everywhere: a region over the LDS image cap, order unspecified)
+            assert np.array_equal(split[b], exp), b
+        assert sorted(got.tolist()) == sorted(rows.tolist())
+    Ks = eng.gram_sparse_sym(phi, ts)
+    assert torch.equal(Ks, eng.gram_sparse_sym(phi, tn))
+    Ku = torch.full((n, eng.leading_dim(n)), float("nan"), dtype=torch.float32, device=eng.device)
+    eng.gram_sparse_upper(phi, ts, Ku, parts=(0, 3, 7))
+    eng.gram_sparse_upper(phi, ts, Ku, parts=(3, 7, 7))
+    assert torch.equal(eng.gram_mirror(Ku, n), Ks)
+    b0, b1 = (n // 3) // bw * bw, n  # a row block whose interior holds whole bands
+    assert torch.equal(eng.gram_sparse_block(phi, ts, b0, b1), eng.gram_sparse_block(phi, tn, b0, b1))
+    # column block with its symmetric square (rows [b, e) transposed with their own bands)
+    b, e = n // 4, n // 4 + min(n // 2, 3 * bw // 2)
+    loc = eng.compact(eng.walk_phi(G, 32, 0.15, 5, [1.0, -0.5, 0.25, -0.125, 0.1], seed=9, src_begin=b, src_end=e))
+    sh = eng.phi_row_shifts(phi)
+    Kc = eng.gram_sparse_cols(phi, sh, eng.transpose_banded(loc, bw, rec_unit=unit), sym_row0=b)
+    Kn = eng.gram_sparse_cols(phi, sh, eng.transpose_banded(loc, bw, rec_unit=unit, split=False), sym_row0=b)
+    assert torch.equal(Kc, Kn)
+    # the hub-column split adds to the dense panel's K with the same skip
+    if unit == 128 and bw >= 1024:
+        Kh = eng.gram_sparse_sym_hubs(phi, eng.transpose_banded(phi, bw), 32)
+        Khn = eng.gram_sparse_sym_hubs(phi, eng.transpose_banded(phi, bw, split=False), 32)
+        assert torch.equal(Kh, Khn)
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_gram_kslice_partials_sum_to_K(eng, world):
     """The all-reduce option: partial Grams over disjoint inner-dimension slices
@@ -955,3 +1017,37 @@ def test_bench_path_on_degenerate_graphs(eng, name):
         loc = eng.compact(eng.walk_phi(G, 16, 0.2, 4, f, seed=4, src_begin=b, src_end=e), want64=False)
         Kc = eng.gram_sparse_cols(phi, eng.phi_row_shifts(phi), eng.transpose_banded(loc, 64), sym_row0=b)
         assert torch.equal(Kc, _sym_square(K[:, b:e], b, e))
+
+
+@pytest.mark.parametrize("mode", ["cols", "allreduce"])
+def test_bench_line_n2_reports_parity_and_collectives_gloo(mode):
+    """bench.py's N > 1 line is self-validating and collective-evident (what the driver's 8-GPU run
+    will print): two gloo ranks on one GPU (GRF_DIST_BACKEND=gloo, the host-staged rehearsal of the
+    RCCL path) run the bench's own step; the line carries the communicator's backend and world size,
+    every rank's Gram ms, all-gather ms and bytes, and the in-run K block check
+    (pipeline.k_block_check: K_blk u and K_blk^T v against the gathered Phi) passing on every rank."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, GRF_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--n-nodes", "20000",
+           "--edges", "200000", "--mode", mode]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    d = line["distributed"]
+    assert d["backend"] == "gloo" and d["world_size"] == 2
+    assert len(d["gram_ms_per_rank"]) == 2 and all(x > 0 for x in d["gram_ms_per_rank"])
+    assert all(x > 0 for x in d["gather_bytes_sent_per_rank"]) and all(x > 0 for x in d["gather_ms_per_rank"])
+    assert sum(d["rank_rows"]) == 20000
+    assert line["parity"]["ok"] and line["parity"]["max_ratio"] <= 1.0 and len(line["parity"]["per_rank"]) == 2

@@ -357,3 +357,38 @@ def test_shard_entries_from_row_pointer():
         shards = [shard_range(57, r, world) for r in range(world)]
         got = shard_entries(SimpleNamespace(ptr=ptr), shards)
         assert got == [int(cnt[b:e].sum()) for b, e in shards] and sum(got) == int(cnt.sum())
+
+
+def _empty_shard_gather_worker(rank, world, port, q):
+    """gather_phi with a rank that owns no rows (n < world): every rank must take the same gather path
+    (the bounded one: chosen from global information -- shards and the row capacity -- not from its
+    own row count), so the collectives match and the full CSR comes back on every rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import scipy.sparse as sp
+        from grf_amd.dist import gather_phi, shard_range
+        from grf_amd.engine import DeviceCSR
+        n, cap = 2, 5
+        full = sp.csr_matrix(np.array([[1.0, 0.0], [2.0, 3.0]]))
+        shards = [shard_range(n, r, world) for r in range(world)]
+        b, e = shards[rank]
+        part = full[b:e]
+        ptr = torch.from_numpy(np.asarray(part.indptr, np.int64))
+        idx = torch.zeros(max(1, (e - b) * cap), dtype=torch.int32)
+        val = torch.zeros(max(1, (e - b) * cap), dtype=torch.float32)
+        idx[:part.nnz] = torch.from_numpy(part.indices.astype(np.int32))
+        val[:part.nnz] = torch.from_numpy(part.data.astype(np.float32))
+        local = DeviceCSR(e - b, n, ptr, idx, None, val, None)
+        local.nnz_bound = (e - b) * cap
+        out = gather_phi(None, local, shards=shards, row_cap=cap)
+        nnz = int(out.ptr[-1])
+        ok = (np.array_equal(out.ptr.numpy(), full.indptr) and np.array_equal(out.idx[:nnz].numpy(), full.indices)
+              and np.array_equal(out.val32[:nnz].numpy(), full.data.astype(np.float32)))
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_phi_empty_shard_same_path_gloo():
+    assert _spawn(_empty_shard_gather_worker, 3) == [(r, True) for r in range(3)]

@@ -20,13 +20,13 @@ modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["sym", "mirror", "rows
 A = DeviceCSR.from_scipy(er_graph_exact_edges(n, 10 * n, 0), eng.device)
 G = eng.laplacian(A)
 bw = int(os.environ.get("GRF_BW", DEFAULT_BAND_WIDTH))
-tws = eng.transpose_workspace(n, n, bw)
-phi = eng.compact(eng.walk_phi(G, 128, 0.1, 8, diffusion_modulator(8), seed=42, count_ws=tws,
-                               band_width=bw), want64=False, sync_free=True)
+phi = eng.compact(eng.walk_phi(G, 128, 0.1, 8, diffusion_modulator(8), seed=42), want64=False, sync_free=True)
 ru = int(os.environ["GRF_REC_UNIT"]) if "GRF_REC_UNIT" in os.environ else None
-tr = eng.transpose_banded(phi, bw, counted_ws=tws, nnz_bound=phi.nnz_bound, rec_unit=ru)
+# the bench's transpose (self-counting, sub-band split for the symmetric diagonal tiles)
+tr = eng.transpose_banded(phi, bw, nnz_bound=phi.nnz_bound, rec_unit=ru)
 K = torch.empty((n, eng.leading_dim(n)), dtype=torch.float32, device=eng.device)
-out = {"n": n, "bw": bw, "rec_unit": tr.rec_unit, "t_rec_MB": tr.t_rec.numel() / 1e6}
+out = {"n": n, "bw": bw, "rec_unit": tr.rec_unit, "t_rec_MB": tr.t_rec.numel() / 1e6,
+       "split": os.environ.get("GRF_GRAM_SPLIT", "1")}
 
 
 def timed(fn):
@@ -50,6 +50,8 @@ for mode in modes:
     if mode == "sym":
         out["sym_ms"] = timed(lambda: eng.gram_sparse_sym(phi, tr, out=K))
         out["sym_digest"] = digest()
+    elif mode == "upper":  # the Gram tiles alone (the mirror's input)
+        out["upper_ms"] = timed(lambda: eng.gram_sparse_upper(phi, tr, K))
     elif mode == "mirror":
         out["mirror_ms"] = timed(lambda: eng.gram_mirror(K, n))
     elif mode == "rows":
