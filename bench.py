@@ -78,13 +78,8 @@ def auto_hubs(eng, A_dev, m, p, L, f, share: float = 0.13) -> int:
     records and costs n^2 / 2 MFMA multiply-adds, ~60x cheaper each, so it pays from c / n ~ 1 / sqrt(60) = 0.13
     (measured: Enron's best split is 128 columns, whose c reaches 13 % of n; Facebook's 64th column is in 9 % of
     the rows and the split loses there, profiles/r02_hubs_sweep.txt).  Multiples of 32 (the panel's width)."""
-    import torch
-
     from grf_amd.dist import setup_phi
-    phi = setup_phi(eng, A_dev, m, p, L, f, seed=42)
-    n = phi.n_cols
-    c = torch.bincount(phi.idx[:phi.nnz].long(), minlength=n)
-    return int((c >= share * n).sum().item()) // 32 * 32
+    return eng.hub_count(setup_phi(eng, A_dev, m, p, L, f, seed=42), share)
 
 
 def init_distributed(local_rank: int) -> int:
@@ -117,7 +112,9 @@ def workload_name(args, A):
     n, nnz = A.shape[0], A.nnz
     if args.graph == "er":
         return {"short": f"N={n // 1000}k ER graph" if n % 1000 == 0 else f"N={n} ER graph",
-                "long": f"C4: ER N={n}, {args.edges} undirected edges",
+                "long": (f"{'C4: ' if (n, args.edges) == DEFAULT_WORKLOAD[:2] else 'C2: ' if (n, args.edges) == C2_DENSE else ''}"
+                         f"ER N={n}, {args.edges} undirected edges"
+                         + (" (CSR sparse path)" if (n, args.edges) == C2_DENSE else "")),
                 "data": "synthetic Erdos-Renyi graph (seed 0), unit weights"}
     if args.graph == "powerlaw":
         return {"short": f"N={n // 1000}k power-law graph",
@@ -495,6 +492,9 @@ def main():
                          "the padded row capacity")
     ap.add_argument("--no-mfma-leg", action="store_true",
                     help="skip the C3 dense MFMA Gram leg that adds roofline_mfma to the headline line")
+    ap.add_argument("--path", choices=["dense", "sparse"], default="dense",
+                    help="c2: the reference's dense path (dense adjacency, MFMA Gram; default) or its sparse path "
+                         "as BASELINE config 2 names it (CSR adjacency, fused walks, transpose, symmetric sparse Gram)")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
     ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
@@ -505,7 +505,9 @@ def main():
         args.n = None
     if args.workload == "predict":
         return main_predict(args)
-    if args.workload in ("c3", "c2"):
+    if args.workload == "c2" and args.path == "sparse":
+        args.n, args.edges = C2_DENSE  # G(10k, 0.001) through the CSR path (the headline machinery)
+    elif args.workload in ("c3", "c2"):
         return main_c3(args)
 
     import torch

@@ -590,13 +590,14 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
             lline[i] = (uint32_t)run_u * (uint32_t)unit;
             run_u += (int32_t)((kPairBytes * ((c + 1) >> 1) + unit - 1) / unit);
             if (kSplit) {
-                // entry offsets of the sub-bands; the counters become the sub-band cursors
+                // entry offsets of the sub-bands; the counters become the sub-band cursors (an oversized
+                // region keeps its counts for the padding below and reports no split)
                 uint32_t off[kSub], o = 0;
 #pragma unroll
                 for (int sb = 0; sb < kSub; ++sb) {
                     off[sb] = lds ? o : 0u;
                     o += lcur[i * kSub + sb];
-                    lcur[i * kSub + sb] = off[sb];
+                    if (lds) lcur[i * kSub + sb] = off[sb];
                 }
                 t_split[b0 + i] = make_uint4(off[0] | (off[1] << 16), off[2] | (off[3] << 16), off[4] | (off[5] << 16),
                                              off[6] | (off[7] << 16));

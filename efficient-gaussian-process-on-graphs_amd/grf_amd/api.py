@@ -105,8 +105,13 @@ def sparse_features(adj, modulator_vector, walks_per_node, p_halt, max_walk_leng
     """Phi = sum_l f_l M_l on the normalised Laplacian (graph_kernels_sparse/fast_grf_kernel_general.py:42-52)."""
     eng = get_engine(device)
     G = eng.laplacian(_canonical_csr(adj))
-    slots = _sparse_walk(eng, G, walks_per_node, p_halt, max_walk_length, seed, n_processes, rng)
     f = np.asarray(modulator_vector, dtype=np.float64).reshape(-1)
+    if resolve_rng(rng) == "philox" and walks_per_node * max_walk_length <= 4096:
+        # the benchmarked kernel: fused Philox walks straight to Phi rows (no visit slots; the same
+        # numbers as walk + features)
+        return eng.compact(eng.walk_phi(G, walks_per_node, p_halt, max_walk_length, f, seed=int(seed or 42),
+                                        norm=C.NORM_MUL_RECIP))
+    slots = _sparse_walk(eng, G, walks_per_node, p_halt, max_walk_length, seed, n_processes, rng)
     return eng.compact(eng.features(slots, f, C.NORM_MUL_RECIP))
 
 

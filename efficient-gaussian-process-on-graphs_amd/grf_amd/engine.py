@@ -31,6 +31,10 @@ DEFAULT_BAND_WIDTH = 4096  # transpose band = one Gram tile (32 KB int64 LDS acc
 # tiles (C4: 25.9 vs 27.5 ms); the symmetric whole-K mode stays at 4096 (21.9 vs 22.7 ms: with 13
 # bands the diagonal band tiles' lower halves cost more than the wider buckets save)
 ROWS_BAND_WIDTH = 8192
+# hub-column split: columns in at least this share of Phi's rows go to the dense MFMA panel (hub_count)
+HUB_SHARE = 0.13
+# gram(method="auto"): the dense MFMA path up to this many rows, the sparse path above
+DENSE_GRAM_MAX_N = 8192
 # the banded transpose counts its buckets itself (grf_transpose_banded_self: no count atomics in the
 # walk, no scan over every bucket); GRF_TRANSPOSE_SELF=0 restores the walk-counted plan (A/B)
 SELF_COUNT_TRANSPOSE = os.environ.get("GRF_TRANSPOSE_SELF", "1") != "0"
@@ -391,13 +395,16 @@ class GRFEngine:
     def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH,
                          counted_ws: Optional[torch.Tensor] = None, staged: Optional[bool] = None,
                          nnz_bound: Optional[int] = None, rec_unit: Optional[int] = None,
-                         self_count: Optional[bool] = None, split: bool = True) -> Banded:
+                         self_count: Optional[bool] = None, split: bool = False) -> Banded:
         """Banded transpose of Phi.  counted_ws: workspace whose bucket counts ``walk_phi`` filled.
         staged: two-pass binned fill (default when band_width % 64 == 0) or the atomic fill.
         self_count: the staged fill without a plan (grf_transpose_banded_self; default unless
         counted_ws is given or GRF_TRANSPOSE_SELF=0): buckets in per-region slabs.
         nnz_bound: an upper bound of nnz(Phi) (e.g. ``compact(..., sync_free=True)``'s): the record
-        buffer is then sized from bounds and no size is read back (no host synchronisation)."""
+        buffer is then sized from bounds and no size is read back (no host synchronisation).
+        split: (self-count transpose) lay every bucket out by sub-band and return the offsets
+        (``Banded.t_split``) for the symmetric Gram's diagonal-tile skip -- measured no faster (a skip
+        saves records inside lines the tile fetches anyway: profiles/r03_split_ab.txt), so off by default."""
         n_rows, n_cols = phi.n_rows, phi.n_cols
         nb = -(-n_rows // band_width)
         nbk = nb * n_cols
@@ -456,7 +463,7 @@ class GRFEngine:
         return Banded(t_desc, t_rec, t_max, t_shift, band_width, n_rows, n_cols, u)
 
     def _transpose_self(self, phi: DeviceCSR, band_width: int, nnz_bound: Optional[int], rec_unit: Optional[int],
-                        t_desc, t_max, t_shift, split: bool = True) -> Banded:
+                        t_desc, t_max, t_shift, split: bool = False) -> Banded:
         """The plan-free staged transpose (grf_transpose_banded_self): buckets counted by the placing
         workgroups themselves, no counts from the walk and no scan over every bucket."""
         n_rows, n_cols = phi.n_rows, phi.n_cols
@@ -696,16 +703,37 @@ class GRFEngine:
                                            ws.numel(), self.stream), "grf_gram_dense_ws")
         return out[:, :n]
 
+    @staticmethod
+    def hub_count(phi: DeviceCSR, share: float = HUB_SHARE) -> int:
+        """Hub columns worth the dense MFMA panel of the hub-column split: the columns of Phi present in
+        at least ``share`` of its rows, in multiples of 32 (the panel's width).  A column in c of the n
+        rows saves ~c^2 / 2 gathered records and costs n^2 / 2 MFMA multiply-adds, ~60x cheaper each,
+        so it pays from c / n ~ 1 / sqrt(60) = 0.13 (Enron 96 columns, C4 / Facebook 0:
+        profiles/r02_hubs_sweep.txt).  One host read."""
+        n = phi.n_cols
+        if phi.nnz == 0 or n == 0:
+            return 0
+        c = torch.bincount(phi.idx[:phi.nnz].long(), minlength=n)
+        return int((c >= share * phi.n_rows).sum().item()) // 32 * 32
+
+    def gram_sparse_auto(self, phi: DeviceCSR, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Whole K on the sparse path exactly as the bench assembles it: the symmetric tiles + mirror,
+        with the hub-column split when Phi has hub columns (``hub_count``)."""
+        tr = self.transpose_banded(phi)
+        hubs = self.hub_count(phi)
+        if hubs:
+            return self.gram_sparse_sym_hubs(phi, tr, hubs, out=out)
+        return self.gram_sparse_sym(phi, tr, out=out)
+
     def gram(self, phi: DeviceCSR, method: str = "auto") -> torch.Tensor:
-        """K = Phi Phi^T (float32).  'dense' = MFMA on densified Phi, 'sparse' = LDS Gustavson."""
+        """K = Phi Phi^T (float32).  'dense' = MFMA on densified Phi, 'sparse' = LDS Gustavson (+ the
+        hub-column split when Phi has hub columns); 'auto' picks by the measured crossover."""
         if method == "auto":
-            n = phi.n_rows
-            # dense MFMA costs 2 n^3 flop at ~100 TF/s; sparse ~ (sum_k c_k^2) * 8 B at a few TB/s
-            method = "dense" if n <= 8192 else "sparse"
+            method = "dense" if phi.n_rows <= DENSE_GRAM_MAX_N else "sparse"
         if method == "dense":
             return self.gram_dense(self.densify(phi), phi.n_cols)
         if method == "sparse":
-            return self.gram_sparse_sym(phi, self.transpose_banded(phi))
+            return self.gram_sparse_auto(phi)
         if method == "sparse-rows":
             return self.gram_sparse(phi, self.transpose_banded(phi, ROWS_BAND_WIDTH))
         raise ValueError(f"unknown gram method {method!r}")

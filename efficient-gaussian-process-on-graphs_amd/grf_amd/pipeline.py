@@ -148,8 +148,7 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                          row_cap=pl.rows_cap) if pl.world > 1 else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
                                             local.val32)
-        tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap,
-                                  split=pl.cols_sym)
+        tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap)
         return Front(phi, tr, local, eng.phi_row_shifts(phi))
     # (the transpose counts its own buckets unless GRF_TRANSPOSE_SELF=0: then the walk counts them)
     tws = None if SELF_COUNT_TRANSPOSE else eng.transpose_workspace(n, n, pl.band_width)
@@ -160,8 +159,9 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
     phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards,
                      entries_bound=pl.gather_bound or None, row_cap=pl.rows_cap) if pl.world > 1 else local
     # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
-    # (the sub-band split serves the symmetric mode's diagonal tiles only)
-    tr = eng.transpose_banded(phi, pl.band_width, counted_ws=tws, nnz_bound=n * pl.rows_cap, split=pl.mode == "sym")
+    # (no sub-band split: the symmetric diagonal tiles' skip saves records, not lines, and measured no
+    # faster: profiles/r03_split_ab.txt)
+    tr = eng.transpose_banded(phi, pl.band_width, counted_ws=tws, nnz_bound=n * pl.rows_cap)
     return Front(phi, tr, local)
 
 

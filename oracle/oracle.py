@@ -331,3 +331,52 @@ def dense_random_walk(walk_matrix, num_walks, p_halt, max_walk_length, n_process
     for l, M in enumerate(mats):
         F[:, :, l] = M.toarray()
     return F
+
+
+def step_functionals(node, load, src0: int = 0) -> np.ndarray:
+    """Per-step functionals of one replica of walk slots (``node`` / ``load`` [n_src, L, m], node -1 =
+    no visit; the reference's accumulator ``M_l[start, node] += load`` divided by m, sparse_sampler.py:40-54,
+    130): for every step l the rows [visits V_l, sum |load| A_l, sum load T_l, sum of the loads that
+    return to their source D_l, sum of the step's multipliers |load_l / load_(l-1)| G_l], each divided by
+    m.  Array (L, 5).  Slot [s, l, w] is walk w's visit at step l.  G_l is bounded per walk
+    ((deg + 1) max|w| / (1 - p)), so it pins the load rule of every single step without the heavy tail
+    that the products A_l, T_l carry.  Equal in distribution for any two samplers of the same walk (the
+    two-sample statistic below compares them)."""
+    node = np.asarray(node)
+    load = np.asarray(load, np.float64)
+    m = node.shape[2]
+    vis = node >= 0
+    lv = np.where(vis, load, 0.0)
+    src = (src0 + np.arange(node.shape[0]))[:, None, None]
+    back = np.where(node == src, lv, 0.0)
+    mult = np.zeros_like(lv)
+    prev = lv[:, :-1, :]
+    mult[:, 1:, :] = np.where(vis[:, 1:, :] & (prev != 0), np.abs(lv[:, 1:, :]) / np.where(prev != 0, np.abs(prev), 1.0),
+                              0.0)
+    return np.stack([vis.sum(axis=(0, 2)), np.abs(lv).sum(axis=(0, 2)), lv.sum(axis=(0, 2)),
+                     back.sum(axis=(0, 2)), mult.sum(axis=(0, 2))], axis=1) / m
+
+
+def mann_whitney_z(x: np.ndarray, y: np.ndarray) -> np.ndarray:
+    """Two-sample Mann-Whitney U statistic as a z-score, per column of x (R_x, ...) and y (R_y, ...)
+    (tie-corrected normal approximation).  Distribution-free under H0 (all replicas exchangeable), so
+    the rare huge loads of the signed Laplacian's later steps (hub self-loops multiply a load by
+    deg + 1) move one rank each instead of a mean: a statistic that tolerates those tails where a
+    CLT bound on means does not."""
+    from scipy.stats import rankdata
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    nx, ny = x.shape[0], y.shape[0]
+    both = np.concatenate([x, y], axis=0)
+    ranks = rankdata(both, axis=0)
+    U = ranks[:nx].sum(axis=0) - nx * (nx + 1) / 2.0
+    n = nx + ny
+    # tie correction: sum over tie groups of (t^3 - t), per column
+    flat = both.reshape(n, -1)
+    tc = np.zeros(flat.shape[1])
+    for c in range(flat.shape[1]):
+        _, cnt = np.unique(flat[:, c], return_counts=True)
+        tc[c] = ((cnt ** 3) - cnt).sum()
+    var = nx * ny / 12.0 * ((n + 1) - tc.reshape(U.shape) / (n * (n - 1)))
+    z = (U - nx * ny / 2.0) / np.sqrt(np.maximum(var, 1e-300))
+    return np.where(var > 0, z, 0.0)

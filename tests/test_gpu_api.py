@@ -292,3 +292,29 @@ def test_degenerate_graphs_match_oracle(name):
         Phi = np.einsum("ijl,l->ij", F, np.asarray(f))
         Kd = dense_k(A, f, walks_per_node=m, p_halt=p, max_walk_length=L, n_processes=nproc)
         np.testing.assert_allclose(Kd, Phi @ Phi.T, rtol=3e-5, atol=1e-6 * max(np.abs(Phi @ Phi.T).max(), 1e-30))
+
+
+def test_sparse_api_philox_routes_through_bench_path(golden):
+    """The drop-in sparse entry point (graph_kernels_sparse/fast_grf_kernel_general.py:20-55) with
+    rng="philox" runs the benchmarked machinery: fused Philox walks straight to Phi rows (no visit
+    slots) and the bench's K assembly, hub-column split included (Enron: hub_count = the bench's
+    --hubs auto).  Its K equals the bench pipeline's K (grf_amd.pipeline, the code bench.py times)
+    on the reference's Enron graph, bit for bit."""
+    import math
+    from efficient_graph_gp_sparse.graph_kernels_sparse.fast_grf_kernel_general import fast_general_grf_kernel
+    from golden_util import snap_adjacency
+    from grf_amd import pipeline as P
+    from grf_amd.dist import setup_phi
+    from grf_amd.engine import DeviceCSR, get_engine
+    A = snap_adjacency(golden("snap"), "enron")
+    n, m, L, p = A.shape[0], 128, 8, 0.1
+    f = np.array([(-1.0) ** l / (2.0 ** l * math.factorial(l)) for l in range(L)])
+    K_api = fast_general_grf_kernel(A, f, m, p, L, rng="philox", return_format="torch")
+    eng = get_engine()
+    A_dev = DeviceCSR.from_scipy(A, eng.device)
+    pl = P.plan_step(n, m, L, p, f)
+    pl.hubs = eng.hub_count(setup_phi(eng, A_dev, m, p, L, f))
+    assert pl.mode == "sym" and pl.hubs > 0  # (Enron's hubs: the split is on)
+    Kb, _ = P.kernel_step(eng, A_dev, pl)
+    assert torch.equal(K_api, P.k_view(Kb, pl))
+    del K_api, Kb

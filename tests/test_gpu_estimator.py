@@ -85,3 +85,50 @@ def test_degree_one_walks_exact(eng, golden):
     G = eng.to_device(sp.csr_matrix(P))
     phi = eng.compact(eng.walk_phi(G, 64, 0.0, T.shape[2], f, seed=3)).to_scipy().toarray()
     np.testing.assert_array_equal(phi, T @ f)
+
+
+def _gpu_functionals(eng, G, m, p, L, rng, seed, n_chunks=1):
+    """oracle.step_functionals of one GPU replica, computed on the device from the walk slots."""
+    import torch
+    sl = eng.walk(G, m, p, L, rng=rng, seed=seed, n_chunks=n_chunks)
+    node, load = sl.node, sl.load
+    vis = node >= 0
+    lv = torch.where(vis, load, torch.zeros((), dtype=load.dtype, device=load.device))
+    src = torch.arange(node.shape[0], device=node.device)[:, None, None]
+    back = torch.where(node == src, lv, torch.zeros((), dtype=lv.dtype, device=lv.device))
+    prev = lv[:, :-1, :]
+    mult = torch.zeros_like(lv)
+    mult[:, 1:, :] = torch.where(vis[:, 1:, :] & (prev != 0), lv[:, 1:, :].abs() / torch.where(prev != 0, prev.abs(),
+                                                                                               torch.ones_like(prev)),
+                                 torch.zeros((), dtype=lv.dtype, device=lv.device))
+    f = torch.stack([vis.sum(dim=(0, 2)).to(torch.float64), lv.abs().sum(dim=(0, 2)), lv.sum(dim=(0, 2)),
+                     back.sum(dim=(0, 2)), mult.sum(dim=(0, 2))], dim=1) / m
+    return f.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["cora", "wer30"])
+def test_philox_vs_reference_stream_all_steps(eng, golden, name):
+    """Every step the bench walks (L = 8) on the signed normalised Laplacian: the GPU's Philox walker
+    against the GPU's replay of the reference's own PCG64 stream (bit-exact to the reference's golden
+    step matrices elsewhere in this suite), by the two-sample rank statistic of
+    tests/test_estimator_twosample.py (per-step visits, sum |load|, sum load, loads back at the source,
+    summed step multipliers; Mann-Whitney |z| <= 5 for each of the 35 (step, functional) pairs; a planted
+    1 % bias at step 5 reaches |z| = 6.8 on the oracle).  Cora: the golden adjacency, m = 1024;
+    wer30: the weighted 30-node golden graph, m = 65536."""
+    from grf_amd import _lib as C
+    if name == "cora":
+        d = golden("cora")
+        n = len(d["A_indptr"]) - 1
+        A = sp.csr_matrix((d["A_data"], d["A_indices"], d["A_indptr"]), shape=(n, n))
+        G = eng.laplacian(A)
+        m = 1024
+    else:
+        sg = golden("small_graphs")
+        n = sg["wer30_A"].shape[0]
+        G = eng.to_device(csr(sg, "wer30_Lsp", n))
+        m = 65536
+    R, L, p = 32, 8, 0.1
+    x = np.stack([_gpu_functionals(eng, G, m, p, L, C.RNG_PHILOX, 3000 + r) for r in range(R)])
+    y = np.stack([_gpu_functionals(eng, G, m, p, L, C.RNG_PCG64, 200000 + 10000 * r, n_chunks=n) for r in range(R)])
+    z = O.mann_whitney_z(x, y)
+    assert np.abs(z).max() <= 5.0, np.round(z, 2)

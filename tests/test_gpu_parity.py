@@ -363,8 +363,8 @@ def test_transpose_sub_band_split(eng, n, bw, unit):
     A = er_graph(n, 8, n + 3)
     G = eng.laplacian(A)
     phi = eng.compact(eng.walk_phi(G, 32, 0.15, 5, [1.0, -0.5, 0.25, -0.125, 0.1], seed=9))
-    ts = eng.transpose_banded(phi, bw, rec_unit=unit)
-    tn = eng.transpose_banded(phi, bw, rec_unit=unit, split=False)
+    ts = eng.transpose_banded(phi, bw, rec_unit=unit, split=True)
+    tn = eng.transpose_banded(phi, bw, rec_unit=unit)
     assert ts.t_split is not None and tn.t_split is None
     nb = -(-n // bw)
     desc = ts.t_desc.cpu().numpy().view(np.uint32).reshape(-1, 2)
@@ -401,13 +401,13 @@ def test_transpose_sub_band_split(eng, n, bw, unit):
     b, e = n // 4, n // 4 + min(n // 2, 3 * bw // 2)
     loc = eng.compact(eng.walk_phi(G, 32, 0.15, 5, [1.0, -0.5, 0.25, -0.125, 0.1], seed=9, src_begin=b, src_end=e))
     sh = eng.phi_row_shifts(phi)
-    Kc = eng.gram_sparse_cols(phi, sh, eng.transpose_banded(loc, bw, rec_unit=unit), sym_row0=b)
-    Kn = eng.gram_sparse_cols(phi, sh, eng.transpose_banded(loc, bw, rec_unit=unit, split=False), sym_row0=b)
+    Kc = eng.gram_sparse_cols(phi, sh, eng.transpose_banded(loc, bw, rec_unit=unit, split=True), sym_row0=b)
+    Kn = eng.gram_sparse_cols(phi, sh, eng.transpose_banded(loc, bw, rec_unit=unit), sym_row0=b)
     assert torch.equal(Kc, Kn)
     # the hub-column split adds to the dense panel's K with the same skip
     if unit == 128 and bw >= 1024:
-        Kh = eng.gram_sparse_sym_hubs(phi, eng.transpose_banded(phi, bw), 32)
-        Khn = eng.gram_sparse_sym_hubs(phi, eng.transpose_banded(phi, bw, split=False), 32)
+        Kh = eng.gram_sparse_sym_hubs(phi, eng.transpose_banded(phi, bw, split=True), 32)
+        Khn = eng.gram_sparse_sym_hubs(phi, eng.transpose_banded(phi, bw), 32)
         assert torch.equal(Kh, Khn)
 
 

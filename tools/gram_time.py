@@ -23,7 +23,7 @@ bw = int(os.environ.get("GRF_BW", DEFAULT_BAND_WIDTH))
 phi = eng.compact(eng.walk_phi(G, 128, 0.1, 8, diffusion_modulator(8), seed=42), want64=False, sync_free=True)
 ru = int(os.environ["GRF_REC_UNIT"]) if "GRF_REC_UNIT" in os.environ else None
 # the bench's transpose (self-counting, sub-band split for the symmetric diagonal tiles)
-tr = eng.transpose_banded(phi, bw, nnz_bound=phi.nnz_bound, rec_unit=ru)
+tr = eng.transpose_banded(phi, bw, nnz_bound=phi.nnz_bound, rec_unit=ru, split=os.environ.get("GRF_SPLIT", "0") == "1")
 K = torch.empty((n, eng.leading_dim(n)), dtype=torch.float32, device=eng.device)
 out = {"n": n, "bw": bw, "rec_unit": tr.rec_unit, "t_rec_MB": tr.t_rec.numel() / 1e6,
        "split": os.environ.get("GRF_GRAM_SPLIT", "1")}
