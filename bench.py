@@ -540,6 +540,9 @@ def main():
                      band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused)
     if args.hubs and pl.mode == "sym" and not pl.fused:
         pl.hubs = int(args.hubs) if args.hubs > 0 else auto_hubs(eng, A_dev, m, p, L, f)
+    elif args.hubs > 0 and pl.mode == "cols" and world == 1:
+        # the column block's hub-column split (C5 A/B: profiles/r03_c5_hubs_ab.txt); explicit counts only
+        pl.hubs = int(args.hubs)
     if phi0 is not None:
         if args.gather_bound == "exact":
             # the Phi all-gather moves each rank's actual entries (C4: 435 per row) instead of its rows x

@@ -1160,11 +1160,11 @@ int32_t grf_gram_sparse_sym_fused(int64_t n_total, const int64_t *ptr, const int
 // against the t_rows rows of another matrix Phi_B (a rank's own rows) whose banded transpose is
 // given; the row shifts come from grf_phi_row_shifts over all of Phi.  With Phi_B = Phi[b:e] this
 // is K[:, b:e] -- entry for entry the row mode's K[r, b + j] -- so a rank transposes only its rows.
-int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
-                             const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
-                             int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
-                             const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
-                             size_t workspace_bytes, grf_stream_t stream) {
+static int32_t gram_sparse_cols_impl(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                                     const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
+                                     int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
+                                     const void *t_rec, const void *t_split, float *K, int64_t ldk, bool add_k,
+                                     grf_stream_t stream) {
     GRF_REQUIRE(n_cols > 0 && 0 <= row_begin && row_begin <= row_end && ptr && idx && val && row_shift &&
                     t_rows >= 0 && t_desc && t_rec && K && ldk >= t_rows,
                 GRF_EINVAL, "grf_gram_sparse_cols: bad arguments");
@@ -1175,8 +1175,6 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
                 "grf_gram_sparse_cols: bad rec_unit");
     GRF_REQUIRE(sym_row0 < 0 || (row_begin <= sym_row0 && sym_row0 + t_rows <= row_end), GRF_EINVAL,
                 "grf_gram_sparse_cols: the symmetric square [sym_row0, sym_row0 + t_rows) must lie in the rows");
-    (void)workspace;
-    (void)workspace_bytes;
     if (row_end == row_begin || t_rows == 0) return GRF_OK;
     const int64_t nb = cdiv<int64_t>(t_rows, band_width);
     hipStream_t st = S(stream);
@@ -1185,6 +1183,7 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
         if (r1 <= r0) return GRF_OK;
         GramTiles tl{r1 - r0, band_width, nb, sym, 0, (int32_t)n_cols};
         tl.t_rows = t_rows;
+        tl.add_k = add_k;
         return gram_tiles_launch(n_cols, r0, tl, 0, tl.total(), ptr, idx, val, t_desc, t_rec, rec_unit, row_shift,
                                  K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr);
     };
@@ -1196,6 +1195,30 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
     if (rc == GRF_OK) rc = launch(sym_row0 + t_rows, row_end, false);
     if (rc != GRF_OK) return rc;
     return grf_gram_mirror(t_rows, K + (sym_row0 - row_begin) * ldk, ldk, 0, stream);
+}
+
+int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                             const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
+                             int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
+                             const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
+                             size_t workspace_bytes, grf_stream_t stream) {
+    (void)workspace;
+    (void)workspace_bytes;
+    return gram_sparse_cols_impl(n_cols, row_begin, row_end, ptr, idx, val, row_shift, t_rows, sym_row0, band_width,
+                                 rec_unit, t_desc, t_rec, t_split, K, ldk, false, stream);
+}
+
+// grf_gram_sparse_cols whose write-out ADDS the rounded fixed-point sums to the block (which holds the
+// dense hub-column part first: the column-block hub-column split)
+int32_t grf_gram_sparse_cols_add(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                                 const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
+                                 int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
+                                 const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
+                                 size_t workspace_bytes, grf_stream_t stream) {
+    (void)workspace;
+    (void)workspace_bytes;
+    return gram_sparse_cols_impl(n_cols, row_begin, row_end, ptr, idx, val, row_shift, t_rows, sym_row0, band_width,
+                                 rec_unit, t_desc, t_rec, t_split, K, ldk, true, stream);
 }
 
 // K rows [row_begin, row_end) of the whole K using the symmetry inside the row block: the bands

@@ -78,6 +78,8 @@ SIGNATURES = {
     "grf_gram_workspace_bytes": (_sz, []),
     "grf_gram_sparse_cols": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp,
                                     _i64, _vp, _sz, _vp]),
+    "grf_gram_sparse_cols_add": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp,
+                                        _vp, _i64, _vp, _sz, _vp]),
     "grf_phi_row_shifts_workspace_bytes": (_sz, [_i64]),
     "grf_phi_row_shifts": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),

@@ -34,7 +34,7 @@ ROWS_BAND_WIDTH = 8192
 # hub-column split: columns in at least this share of Phi's rows go to the dense MFMA panel (hub_count)
 HUB_SHARE = 0.13
 # gram(method="auto"): the dense MFMA path up to this many rows, the sparse path above
-DENSE_GRAM_MAX_N = 8192
+DENSE_GRAM_MAX_N = 4500  # measured crossover, profiles/r03_gram_crossover.txt
 # the banded transpose counts its buckets itself (grf_transpose_banded_self: no count atomics in the
 # walk, no scan over every bucket); GRF_TRANSPOSE_SELF=0 restores the walk-counted plan (A/B)
 SELF_COUNT_TRANSPOSE = os.environ.get("GRF_TRANSPOSE_SELF", "1") != "0"
@@ -556,6 +556,31 @@ class GRFEngine:
                                               _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_cols")
         return out[:, :t_rows]
+
+    def gram_sparse_cols_hubs(self, phi: DeviceCSR, row_shift: torch.Tensor, tr_b: Banded, b0: int, hubs: int,
+                              out: Optional[torch.Tensor] = None, sym_row0: Optional[int] = None) -> torch.Tensor:
+        """Column block K[:, b0:b0+t] = Phi Phi[b0:b0+t]^T (``gram_sparse_cols`` with Phi_B = Phi[b0:b0+t]) with
+        the hub-column split: the ``hubs`` columns with the most entries in the block's transpose go to a
+        dense fp32 panel P of all rows (``hub_split``: their buckets emptied from ``tr_b``, which is
+        consumed), the block gets K_blk = P P[b0:b0+t]^T from a plain GEMM (rocBLAS / hipBLASLt through
+        torch.mm: a library GEMM, n x t x hubs multiply-adds), and the sparse tiles add the remaining
+        columns' fixed-point sums (``grf_gram_sparse_cols_add``).  Within the fp32 K tolerance."""
+        n, t = phi.n_rows, tr_b.n_rows
+        if out is None:
+            out = torch.empty((n, self.leading_dim(max(t, 1))), dtype=torch.float32, device=self.device)
+        P, cols = self.hub_split(phi, tr_b, hubs)
+        blk = out[:, :t]
+        if blk.is_contiguous():
+            torch.mm(P, P[b0:b0 + t].t(), out=blk)
+        else:
+            blk.copy_(P @ P[b0:b0 + t].t())
+        del P
+        C.check(self.lib.grf_gram_sparse_cols_add(phi.n_cols, 0, n, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
+                                                  _p(row_shift), t, -1 if sym_row0 is None else int(sym_row0),
+                                                  tr_b.band_width, tr_b.rec_unit, _p(tr_b.t_desc), _p(tr_b.t_rec),
+                                                  _p(tr_b.t_split), _p(out), out.stride(0), _p(self._gram_ws),
+                                                  self._gram_ws.numel(), self.stream), "grf_gram_sparse_cols_add")
+        return out[:, :t]
 
     def gram_sparse_kslice(self, phi: DeviceCSR, tr: Banded, k_begin: int, k_end: int, row_begin: int = 0,
                            row_end: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:

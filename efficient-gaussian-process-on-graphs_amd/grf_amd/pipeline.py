@@ -48,7 +48,7 @@ class StepPlan:
     band_width: int = DEFAULT_BAND_WIDTH
     cols_sym: bool = False         # column blocks: the square K[b:e, b:e] by the symmetric enumeration
     fused: bool = False            # "sym": symmetric completion fused into the Gram tiles (no mirror pass)
-    hubs: int = 0                  # "sym": Phi's densest columns as a dense MFMA panel (hub-column split)
+    hubs: int = 0                  # "sym" / "cols": Phi's densest columns as a dense panel (hub-column split)
     group: object = None           # torch.distributed group (N > 1)
     gather_bound: int = 0          # N > 1: per-rank Phi entries moved by the all-gather (0: rows x rows_cap;
     #                                dist.shard_entries of the setup walk: exact, checked by check_gather_overflow)
@@ -173,7 +173,10 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
     the HBM-bound mirror; ``mirror_workgroups`` then bounds the mirror's grid, 1024 measured best)."""
     from .dist import allreduce_buckets
 
-    if pl.mode == "cols":
+    if pl.mode == "cols" and pl.hubs > 0:
+        eng.gram_sparse_cols_hubs(fr.phi, fr.row_shift, fr.tr, pl.b, pl.hubs, out=K,
+                                  sym_row0=pl.b if pl.cols_sym else None)
+    elif pl.mode == "cols":
         eng.gram_sparse_cols(fr.phi, fr.row_shift, fr.tr, out=K, sym_row0=pl.b if pl.cols_sym else None)
     elif pl.mode == "allreduce":
         eng.gram_sparse_kslice(fr.phi, fr.tr, pl.b, pl.e, out=K)  # all rows, inner slice [b, e)

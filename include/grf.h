@@ -348,6 +348,16 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
                              int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
                              const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
                              size_t workspace_bytes, grf_stream_t stream);
+/* grf_gram_sparse_cols whose tile write-out ADDS the rounded fixed-point sums to the block instead of
+ * storing them: the block must hold the dense part first.  The column-block hub-column split: the
+ * densest columns' entries in dense panels P (all rows) and P_B (the block's rows), K_blk = P P_B^T by
+ * a plain GEMM, those columns' buckets emptied from the block's transpose (grf_transpose_drop_columns),
+ * then this adds the rest.  Same arguments as grf_gram_sparse_cols. */
+int32_t grf_gram_sparse_cols_add(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
+                                 const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
+                                 int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
+                                 const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
+                                 size_t workspace_bytes, grf_stream_t stream);
 
 /* The Gram fixed-point row shifts of a CSR (n_rows rows; float values) and its max |value|
  * (*maxabs, device): the same rule and the same per-row summation order as the banded transpose's

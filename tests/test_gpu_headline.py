@@ -232,3 +232,22 @@ def test_c3_dense_leg_cora(eng):
     ok, e, nbad = _rows_close(K, ref, np.arange(n))
     assert ok, (e, nbad)
     assert np.array_equal(K, K.T)
+
+
+def test_c5_column_block_with_hub_split(eng):
+    """C5 (the bench's --workload c5 plan) with the column block's hub-column split (bench.py --hubs 32
+    on c5): the bench's in-run check (pipeline.k_block_check: K_blk u and K_blk^T v over the whole 32 GB
+    block against the gathered Phi) within the K tolerance."""
+    import torch
+    from grf_amd import pipeline as P
+    from grf_amd.engine import DeviceCSR
+    from grf_amd.graphs import powerlaw_graph
+    n, m, L, p, kr = 1_000_000, 64, 8, 0.1, 8192
+    A = powerlaw_graph(n, 10.0, 2.5, seed=0)
+    pl = P.plan_step(n, m, L, p, _diffusion(L), k_rows=kr)
+    pl.hubs = 32
+    K, fr = P.kernel_step(eng, DeviceCSR.from_scipy(A, eng.device), pl)
+    torch.cuda.synchronize()
+    res = P.k_block_check(eng, fr, pl, K)
+    assert res["ok"], res
+    del K, fr

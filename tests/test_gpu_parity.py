@@ -1051,3 +1051,32 @@ def test_bench_line_n2_reports_parity_and_collectives_gloo(mode):
     assert all(x > 0 for x in d["gather_bytes_sent_per_rank"]) and all(x > 0 for x in d["gather_ms_per_rank"])
     assert sum(d["rank_rows"]) == 20000
     assert line["parity"]["ok"] and line["parity"]["max_ratio"] <= 1.0 and len(line["parity"]["per_rank"]) == 2
+
+
+@pytest.mark.parametrize("hubs", [32, 64])
+def test_column_block_hub_split(eng, hubs):
+    """The column block's hub-column split (engine.gram_sparse_cols_hubs: the block's densest columns in
+    a dense panel, K_blk = P P_B^T by a library GEMM, the other columns' fixed-point tiles added on top):
+    within the K tolerance of the exact product of the same fp32 Phi, on a hub-heavy power-law graph,
+    with and without the block's symmetric square."""
+    from grf_amd.graphs import powerlaw_graph
+    n = 20000
+    A = powerlaw_graph(n, 10.0, 2.5, seed=3)
+    G = eng.laplacian(A)
+    phi = eng.compact(eng.walk_phi(G, 32, 0.1, 6, [1.0, -0.5, 0.125, -0.02, 0.003, -0.0005], seed=5, want64=False),
+                      want64=False)
+    P64 = phi.to_scipy().astype(np.float64)
+    sh = eng.phi_row_shifts(phi)
+    for b, e, sym in [(0, 4096, False), (5000, 10000, True)]:
+        loc = eng.compact(eng.walk_phi(G, 32, 0.1, 6, [1.0, -0.5, 0.125, -0.02, 0.003, -0.0005], seed=5,
+                                       src_begin=b, src_end=e, want64=False), want64=False)
+        Kh = eng.gram_sparse_cols_hubs(phi, sh, eng.transpose_banded(loc, 4096), b, hubs,
+                                       sym_row0=b if sym else None).cpu().numpy()
+        K0 = eng.gram_sparse_cols(phi, sh, eng.transpose_banded(loc, 4096), sym_row0=b if sym else None).cpu().numpy()
+        ref = (P64 @ P64[b:e].T).toarray()
+        bound = 3e-5 * (abs(P64) @ abs(P64[b:e]).T).toarray() + 1e-30
+        assert np.all(np.abs(Kh - ref) <= bound), float((np.abs(Kh - ref) / bound).max())
+        assert np.all(np.abs(K0 - ref) <= bound)
+        if sym:  # the square stays exactly symmetric
+            sq = Kh[b:e]
+            assert np.array_equal(sq, sq.T)
