@@ -68,9 +68,10 @@ def pmc_counter(kernel, counter):
     return hits[0].get(counter) if hits else None
 
 
-# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 4 cycles at the 2.4 GHz
-# peak engine clock (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s
-VALU_PEAK_GINST = 256 * 4 * 2.4 / 4
+# VALU issue ceiling per SIMD-32: one wave64 VALU instruction per 2 cycles (MI355X_MICROARCH.md, wave
+# scheduling: 32 lanes per cycle; one wave alone issues every 4 cycles, several waves interleaved every 2)
+VALU_PEAK_PER_SIMD_CYCLE = 0.5
+N_SIMDS = 256 * 4
 
 
 def auto_hubs(eng, A_dev, m, p, L, f, share: float = 0.13) -> int:
@@ -352,8 +353,10 @@ def main_c3(args):
 
     def step(record):
         G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY)
-        # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule
-        phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False)
+        # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule (sync-free compaction:
+        # no host read inside the step)
+        phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False,
+                          sync_free=True)
         dense = eng.densify(phi)
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -475,6 +478,11 @@ def main():
     ap.add_argument("--no-overlap", dest="overlap", action="store_false", help="serial steps")
     ap.add_argument("--front-at", type=float, default=1.0,
                     help="pipelined: the next front starts after this fraction of the Gram tiles (1 = at the mirror)")
+    ap.add_argument("--front-split", action="store_true",
+                    help="pipelined symmetric K: only the next step's Laplacian, walks and compaction run beside the "
+                         "mirror; its transpose follows on the main stream after the mirror")
+    ap.add_argument("--mirror-wgs", type=int, default=1024,
+                    help="pipelined symmetric K: the mirror pass's workgroups beside the next front (0 = one per block)")
     ap.add_argument("--fused", dest="fused", action="store_true", default=None,
                     help="one GPU, whole K: the symmetric completion inside the Gram tiles (the last tile of every "
                          "32-row group writes the group's block transposed; no mirror pass)")
@@ -567,7 +575,11 @@ def main():
     side = torch.cuda.Stream(dev)  # the next step's front runs here while the Gram runs on `main`
     main = torch.cuda.current_stream(dev)
 
+    split_front = [False]  # (set while the timed / warm-up steps run with --front-split)
+
     def front(record_walk: bool = False):
+        if split_front[0]:
+            return P.front_walk(eng, A_dev, pl)  # the transpose follows on `main` (back_on_main)
         if record_walk:
             # the walk kernel timed alone (serial steps): events around the front's walk_phi launch
             orig = eng.walk_phi
@@ -592,8 +604,8 @@ def main():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         # (pipelined: a 1024-workgroup mirror leaves CU slots to the next front)
-        P.k_assembly(eng, fr, pl, K, after_tiles=after_gram, mirror_workgroups=1024 if after_gram else 0,
-                     front_at=args.front_at)
+        P.k_assembly(eng, fr, pl, K, after_tiles=after_gram,
+                     mirror_workgroups=args.mirror_wgs if after_gram else 0, front_at=args.front_at)
         if record:
             ev[1].record()
             gram_ev.append(ev)
@@ -624,6 +636,10 @@ def main():
             for v in ([obj] if torch.is_tensor(obj) else vars(obj).values()):
                 if torch.is_tensor(v) and v.is_cuda:
                     v.record_stream(main)
+        if fr.tr is None:
+            # --front-split: the transpose runs on `main` after the previous step's mirror (alone, not
+            # beside it: beside the HBM-bound mirror its latency-bound region gathers ran 5x slower)
+            P.front_transpose(eng, pl, fr)
         back(fr, record, after_gram)
 
     def run(steps: int, record: bool, record_walk: bool = False):
@@ -654,6 +670,7 @@ def main():
                 back_on_main(cur, record)
                 cur = front_on_side(independent=True) if s_ + 1 < steps else None
 
+    split_front[0] = bool(args.front_split and args.overlap and pl.mode == "sym")
     run(args.warmup, False)
     torch.cuda.synchronize()
     if world > 1:
@@ -671,6 +688,7 @@ def main():
     # the walk kernel timed alone there
     ov = args.overlap
     args.overlap = False
+    split_front[0] = False
     run(1, False)  # (warm-up of the serial order)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -738,9 +756,12 @@ def main():
     walk_alg = 16.0 * moves + 8.0 * local_nnz
     walk_achieved = walk_alg / (walk_ms * 1e-3) / 1e9
     walk_traffic = pmc_traffic(["grf::phi_fused_kernel"]) if headline else None
-    # the walk is VALU-issue-bound: its wave-instructions per launch over its live time
+    # the walk's VALU issue rate from ONE rocprofv3 --pmc pass (SQ_INSTS_VALU and GRBM_GUI_ACTIVE counted
+    # together, tools/pmc_passes.sh "sq"): wave-instructions per SIMD-cycle, the cycles of the dispatch being
+    # GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs, MI355X_MICROARCH.md); no clock or timer involved
     walk_valu = pmc_counter("grf::phi_fused_kernel", "SQ_INSTS_VALU") if headline else None
-    walk_valu_rate = walk_valu / (walk_ms * 1e-3) / 1e9 if walk_valu and walk_ms else None
+    walk_gui = pmc_counter("grf::phi_fused_kernel", "GRBM_GUI_ACTIVE") if headline else None
+    walk_valu_rate = walk_valu / (walk_gui / 8.0 * N_SIMDS) if walk_valu and walk_gui else None
     wl = workload_name(args, A)
     if args.k_rows:
         metric = (f"GRF kernel rows/sec ({wl['short']}, m={m} walks: Phi of all N nodes + a {args.k_rows}-row "
@@ -792,23 +813,30 @@ def main():
                      "algorithmic_bytes": alg_bytes},
         "roofline_walk": {"bound": "valu" if walk_valu_rate is not None else "hbm",
                           "achieved": walk_valu_rate if walk_valu_rate is not None else walk_achieved,
-                          "peak": VALU_PEAK_GINST if walk_valu_rate is not None else HBM_PEAK_GBS,
-                          "unit": "G VALU wave-instructions/s" if walk_valu_rate is not None else "GB/s",
-                          "frac": (walk_valu_rate / VALU_PEAK_GINST) if walk_valu_rate is not None
+                          "peak": VALU_PEAK_PER_SIMD_CYCLE if walk_valu_rate is not None else HBM_PEAK_GBS,
+                          "unit": "VALU wave-instructions per SIMD-cycle" if walk_valu_rate is not None else "GB/s",
+                          "frac": (walk_valu_rate / VALU_PEAK_PER_SIMD_CYCLE) if walk_valu_rate is not None
                           else walk_achieved / HBM_PEAK_GBS,
                           "valu_insts_per_launch": walk_valu,
-                          "valu_source": (f"rocprofv3 --pmc SQ_INSTS_VALU of the same kernel on this workload, "
-                                          f"{os.path.relpath(PMC_SUMMARY, ROOT)}") if walk_valu is not None else None,
+                          "gui_active_cycles_per_launch": walk_gui / 8.0 if walk_gui else None,
+                          "valu_source": (f"one rocprofv3 --pmc pass of this workload (SQ_INSTS_VALU, GRBM_GUI_ACTIVE), "
+                                          f"{os.path.relpath(PMC_SUMMARY, ROOT)}: SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x "
+                                          f"1024 SIMDs) against 1 wave64 VALU instruction per 2 cycles per SIMD "
+                                          f"(fp64 VALU and transcendental instructions take longer: a lower bound "
+                                          f"of the VALU pipe's busy share)") if walk_valu_rate is not None else None,
                           "hbm": {"achieved": walk_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": walk_achieved / HBM_PEAK_GBS, "traffic": walk_traffic},
                           "kernel": "phi_fused_kernel (fused Philox walks -> Phi rows)",
-                          "kernel_ms": walk_ms, "algorithmic_bytes": walk_alg,
+                          "kernel_ms": walk_ms, "kernel_ms_note": "HIP events around the launch in this run's serial "
+                                                                  "steps (the hbm rate's time; not the valu frac's)",
+                          "algorithmic_bytes": walk_alg,
                           "algorithmic_note": f"16 B per expected recorded move ({moves:.4g}) + 8 B per Phi "
                                               f"entry written ({local_nnz}); timed alone in the serial steps "
                                               f"(pipelined it shares HBM with the mirror)"},
         "nnz_phi": nnz_phi,
         "parity": parity,
         "pipelined": bool(ov),
+        "front_split": bool(args.front_split and ov and pl.mode == "sym"),
         "serial_ms_per_step": serial_ms,
     }
     if dist_info is not None:

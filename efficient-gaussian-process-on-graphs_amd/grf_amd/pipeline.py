@@ -150,6 +150,17 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                                             local.val32)
         tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap)
         return Front(phi, tr, local, eng.phi_row_shifts(phi))
+    return front_transpose(eng, pl, front_walk(eng, A_dev, pl, G))
+
+
+def front_walk(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan, G: Optional[DeviceCSR] = None) -> Front:
+    """The first part of a row / symmetric-mode front: Laplacian -> fused walks -> compaction -> [gather]
+    (``Front.tr`` is None until ``front_transpose``).  The bench may issue the two parts on different
+    streams (--front-split)."""
+    from .dist import gather_phi
+
+    n, b, e = pl.n, pl.b, pl.e
+    G = eng.laplacian(A_dev) if G is None else G
     # (the transpose counts its own buckets unless GRF_TRANSPOSE_SELF=0: then the walk counts them)
     tws = None if SELF_COUNT_TRANSPOSE else eng.transpose_workspace(n, n, pl.band_width)
     local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
@@ -158,11 +169,18 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                         want64=False, want32=True, sync_free=True)
     phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards,
                      entries_bound=pl.gather_bound or None, row_cap=pl.rows_cap) if pl.world > 1 else local
-    # sizes from bounds (n x the padded row capacity): no host round trip for the transpose
-    # (no sub-band split: the symmetric diagonal tiles' skip saves records, not lines, and measured no
-    # faster: profiles/r03_split_ab.txt)
-    tr = eng.transpose_banded(phi, pl.band_width, counted_ws=tws, nnz_bound=n * pl.rows_cap)
-    return Front(phi, tr, local)
+    fr = Front(phi, None, local)
+    fr.tws = tws
+    return fr
+
+
+def front_transpose(eng: GRFEngine, pl: StepPlan, fr: Front) -> Front:
+    """The second part: the banded transpose of the (gathered) Phi, sized from bounds (n x the padded
+    row capacity): no host round trip.  (No sub-band split: the symmetric diagonal tiles' skip saves
+    records, not lines, and measured no faster: profiles/r03_split_ab.txt.)"""
+    fr.tr = eng.transpose_banded(fr.phi, pl.band_width, counted_ws=getattr(fr, "tws", None),
+                                 nnz_bound=pl.n * pl.rows_cap)
+    return fr
 
 
 def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
