@@ -6,8 +6,11 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$1; shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
+# PASSES="fetch write ..." runs only those passes (default: all five)
+PASSES=${PASSES:-fetch write sq lds ta}
 run() {
     local name=$1; shift
+    case " $PASSES " in *" $name "*) ;; *) return 0;; esac
     timeout -k 10 420 rocprofv3 --pmc "$@" -d "$OUT/$name" -o run --output-format csv -- python3 "${ARGS[@]}" \
         > "$OUT/$name.log" 2>&1 || { echo "pass $name failed"; tail -20 "$OUT/$name.log"; exit 1; }
     echo "pass $name ok"
