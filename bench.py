@@ -350,14 +350,26 @@ def main_c3(args):
     f = diffusion_modulator(L, 1.0)
     Wt = torch.from_numpy(W).to(eng.device)
     gram_ev = []
+    side = torch.cuda.Stream(eng.device)  # the next step's front runs here beside this step's Gram
+    main = torch.cuda.current_stream(eng.device)
 
-    def step(record):
+    def front():
         G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY)
         # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule (sync-free compaction:
         # no host read inside the step)
         phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False,
                           sync_free=True)
-        dense = eng.densify(phi)
+        return eng.densify(phi)
+
+    def front_on_side():
+        # independent of `main`: a front reads only the resident adjacency and writes fresh buffers
+        with torch.cuda.stream(side):
+            dense = front()
+            done = torch.cuda.Event()
+            done.record(side)
+        return dense, done
+
+    def back(dense, record):
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -367,14 +379,37 @@ def main_c3(args):
             gram_ev.append(ev)
         return K
 
-    for _ in range(args.warmup):
-        step(False)
+    def run(steps, record, pipelined):
+        """`steps` whole steps.  Pipelined (the default; --no-overlap: serial): step s+1's front is
+        issued on the side stream before step s's Gram, so the latency-bound walks run beside the
+        MFMA tiles; every step still runs its whole path, and the call's first front is not
+        overlapped (nothing is carried across the call's boundary)."""
+        if not pipelined:
+            for _ in range(steps):
+                back(front(), record)
+            return
+        cur = front_on_side()
+        for s_ in range(steps):
+            dense, done = cur
+            main.wait_event(done)
+            dense.record_stream(main)  # (allocated on `side`, read on `main`)
+            cur = front_on_side() if s_ + 1 < steps else None
+            back(dense, record)
+
+    pipelined = args.overlap is not False
+    run(args.warmup, False, pipelined)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    run(args.steps, True, pipelined)
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
+    # latency of one un-pipelined step (reported beside the throughput; not part of `value`)
+    run(2, False, False)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    run(5, False, False)
+    torch.cuda.synchronize()
+    serial_ms = 1000.0 * (time.perf_counter() - t1) / 5
     gram_ms = float(np.mean([a.elapsed_time(b) for a, b in gram_ev]))
     # the symmetric product's unique entries, 2 k flops each (the kernel computes the tiles on and
     # above the diagonal and mirrors them; counting 2 n^2 k would credit work it does not do; k = n,
@@ -401,6 +436,8 @@ def main_c3(args):
         "roofline": {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": tfs / MFMA_F32_PEAK_TFS, "traffic": None, "kernel": "gram_dense_kernel",
                      "kernel_ms": gram_ms, "algorithmic_flops": flops},
+        "pipelined": pipelined,
+        "serial_ms_per_step": serial_ms,
     }
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_dense(W, f, m, p, L,
