@@ -169,6 +169,38 @@ __global__ __launch_bounds__(256) void csr_rows_dot_cols_kernel(int64_t n_sel, c
     if (lane == 0) out[r] = acc;
 }
 
+// K (dense fp32 on the device) -> the scipy CSR the reference's sparse entry point returns
+// (graph_kernels_sparse/fast_grf_kernel_general.py:55: `Phi @ Phi.T` is a scipy CSR: float64 values,
+// sorted columns, exact zeros absent).  One wave per row, 64 columns per step: the nonzero lanes'
+// positions from a ballot (mbcnt prefix), kFill = false counts the row's entries, true writes them
+// (int32 column, the fp32 value widened) at out_ptr[row].
+template <bool kFill>
+__global__ __launch_bounds__(256) void dense_to_csr_kernel(int64_t n_rows, int64_t n_cols,
+                                                           const float *__restrict__ K, int64_t ldk,
+                                                           int32_t *__restrict__ cnt,
+                                                           const int64_t *__restrict__ out_ptr,
+                                                           int32_t *__restrict__ out_idx,
+                                                           double *__restrict__ out_val) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const float *krow = K + row * ldk;
+    int64_t o = kFill ? out_ptr[row] : 0;
+    for (int64_t c0 = 0; c0 < n_cols; c0 += 64) {
+        const int64_t c = c0 + lane;
+        const float v = c < n_cols ? krow[c] : 0.f;
+        const bool nz = v != 0.f;  // (-0.0 counts as zero, like scipy's dense -> CSR)
+        const unsigned long long m = __ballot(nz);
+        if (kFill && nz) {
+            const int64_t at = o + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            out_idx[at] = (int32_t)c;
+            out_val[at] = (double)v;
+        }
+        o += __popcll(m);
+    }
+    if (!kFill && lane == 0) cnt[row] = (int32_t)o;
+}
+
 }  // namespace grf
 
 using namespace grf;
@@ -275,6 +307,32 @@ int32_t grf_csr_rows_dot_cols(int64_t n_sel, const int64_t *ptr, const int32_t *
     csr_rows_dot_cols_kernel<<<(unsigned)cdiv<int64_t>(n_sel, 4), 256, 0, S(stream)>>>(n_sel, ptr, idx, val, row_map,
                                                                                       Z, ldz, out);
     GRF_CHECK_LAUNCH("csr_rows_dot_cols_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_dense_to_csr_count(int64_t n_rows, int64_t n_cols, const float *K, int64_t ldk, int32_t *cnt,
+                               grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_cols >= 0 && n_cols < ((int64_t)1 << 31) && ldk >= n_cols &&
+                    (n_rows == 0 || (K && cnt)),
+                GRF_EINVAL, "grf_dense_to_csr_count: bad arguments");
+    if (n_rows == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "dense_to_csr_kernel");
+    dense_to_csr_kernel<false><<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, S(stream)>>>(n_rows, n_cols, K, ldk, cnt,
+                                                                                        nullptr, nullptr, nullptr);
+    GRF_CHECK_LAUNCH("dense_to_csr_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_dense_to_csr_fill(int64_t n_rows, int64_t n_cols, const float *K, int64_t ldk, const int64_t *out_ptr,
+                              int32_t *out_idx, double *out_val, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_cols >= 0 && n_cols < ((int64_t)1 << 31) && ldk >= n_cols &&
+                    (n_rows == 0 || (K && out_ptr && out_idx && out_val)),
+                GRF_EINVAL, "grf_dense_to_csr_fill: bad arguments");
+    if (n_rows == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "dense_to_csr_kernel");
+    dense_to_csr_kernel<true><<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, S(stream)>>>(
+        n_rows, n_cols, K, ldk, nullptr, out_ptr, out_idx, out_val);
+    GRF_CHECK_LAUNCH("dense_to_csr_kernel");
     return GRF_OK;
 }
 

@@ -123,6 +123,8 @@ SIGNATURES = {
     "grf_csr_gather_rows": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "grf_csr_rowdot": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "grf_csr_rows_dot_cols": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "grf_dense_to_csr_count": (_i32, [_i64, _i64, _vp, _i64, _vp, _vp]),
+    "grf_dense_to_csr_fill": (_i32, [_i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
     # the GPflow surface's algebra on a dense (N, N, L) step tensor
     "grf_dense_steps_phi": (_i32, [_i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "grf_dense_steps_grad_workspace_bytes": (_sz, [_i64, _i32]),

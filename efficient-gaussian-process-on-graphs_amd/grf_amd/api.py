@@ -130,10 +130,8 @@ def sparse_kernel(adj, modulator_vector, walks_per_node=50, p_halt=0.1, max_walk
         n = K.shape[0]
         if n * n > 4_000_000_000:
             raise MemoryError(f"K has {n}x{n} entries; request return_format='torch' to keep it on the GPU")
-        Kh = K.cpu().numpy().astype(np.float64)
-        out = sp.csr_matrix(Kh)  # drops exact zeros, like scipy's SpGEMM
-        out.sort_indices()
-        return out
+        # built on the device, one host copy of (indptr, indices, data); drops exact zeros, like scipy's SpGEMM
+        return eng.dense_to_scipy_csr(K)
     raise ValueError(f"unknown return_format {return_format!r}")
 
 

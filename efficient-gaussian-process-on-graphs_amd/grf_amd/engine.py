@@ -369,6 +369,31 @@ class GRFEngine:
         out.nnz_bound = nnz
         return out
 
+    def dense_to_scipy_csr(self, K: torch.Tensor):
+        """K (dense fp32, on the device) as the scipy CSR the reference's sparse entry point returns
+        (``Phi @ Phi.T``: float64 values, sorted int32 columns, exact zeros absent), built on the device
+        (``grf_dense_to_csr_count`` / ``_fill``) and copied to the host once: indptr, indices, data."""
+        import scipy.sparse as sp
+        n_rows, n_cols = K.shape
+        if K.dtype != torch.float32 or K.device != self.device or K.stride(1) != 1:
+            raise ValueError("dense_to_scipy_csr: K must be a row-major float32 tensor on the engine's device")
+        cnt = self._empty(n_rows, torch.int32)
+        C.check(self.lib.grf_dense_to_csr_count(n_rows, n_cols, _p(K), K.stride(0), _p(cnt), self.stream),
+                "grf_dense_to_csr_count")
+        ptr = self._empty(n_rows + 1, torch.int64)
+        ws = self._ws(self.lib.grf_scan_workspace_bytes(n_rows))
+        C.check(self.lib.grf_scan_counts(n_rows, _p(cnt), _p(ptr), _p(ws), ws.numel(), self.stream),
+                "grf_scan_counts")
+        nnz = int(ptr[-1].item())
+        idx, val = self._empty(nnz, torch.int32), self._empty(nnz, torch.float64)
+        if nnz:
+            C.check(self.lib.grf_dense_to_csr_fill(n_rows, n_cols, _p(K), K.stride(0), _p(ptr), _p(idx), _p(val),
+                                                   self.stream), "grf_dense_to_csr_fill")
+        out = sp.csr_matrix((val.cpu().numpy(), idx.cpu().numpy(), ptr.cpu().numpy()), shape=(n_rows, n_cols),
+                            copy=False)
+        out.has_sorted_indices = True  # (columns ascending within every row by construction)
+        return out
+
     def step_matrices(self, st: StepRows) -> list[DeviceCSR]:
         """Per-step CSR matrices (rows = the sources of this step block)."""
         out = []

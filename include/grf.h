@@ -527,6 +527,15 @@ int32_t grf_csr_rowdot(int64_t n_pairs, const int64_t *a_ptr, const int32_t *a_i
 int32_t grf_csr_rows_dot_cols(int64_t n_sel, const int64_t *ptr, const int32_t *idx, const float *val,
                               const int32_t *row_map, const float *Z, int64_t ldz, double *out, grf_stream_t stream);
 
+/* K (dense fp32 on the device, n_rows x n_cols, row pitch ldk) -> the scipy CSR the reference's sparse
+ * entry point returns (graph_kernels_sparse/fast_grf_kernel_general.py:55: `Phi @ Phi.T`, float64
+ * values, sorted columns, exact zeros absent).  _count: cnt[r] = nonzeros of row r; with
+ * out_ptr = grf_scan_counts(cnt), _fill writes the int32 columns and the float64-widened values. */
+int32_t grf_dense_to_csr_count(int64_t n_rows, int64_t n_cols, const float *K, int64_t ldk, int32_t *cnt,
+                               grf_stream_t stream);
+int32_t grf_dense_to_csr_fill(int64_t n_rows, int64_t n_cols, const float *K, int64_t ldk, const int64_t *out_ptr,
+                              int32_t *out_idx, double *out_val, grf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -318,3 +318,28 @@ def test_sparse_api_philox_routes_through_bench_path(golden):
     Kb, _ = P.kernel_step(eng, A_dev, pl)
     assert torch.equal(K_api, P.k_view(Kb, pl))
     del K_api, Kb
+
+
+@pytest.mark.parametrize("n_rows,n_cols", [(1, 1), (3, 5), (7, 63), (130, 200), (1000, 1000)])
+def test_dense_to_scipy_csr_matches_scipy(n_rows, n_cols):
+    """The drop-in sparse entry point's return format, built on the device (grf_dense_to_csr_count /
+    _fill): identical to scipy's own dense -> CSR of the float64-widened K (exact zeros and -0.0 dropped,
+    sorted columns, empty rows), on ragged shapes and a pitched view."""
+    from grf_amd.engine import get_engine
+    eng = get_engine()
+    r = np.random.default_rng(n_rows * 7 + n_cols)
+    Kh = (r.standard_normal((n_rows, n_cols)) * (r.random((n_rows, n_cols)) < 0.4)).astype(np.float32)
+    Kh[r.random((n_rows, n_cols)) < 0.05] = -0.0
+    if n_rows > 2:
+        Kh[1] = 0.0  # an empty row
+    if (n_rows, n_cols) == (3, 5):
+        Kh[:] = -0.0  # no entry at all (nnz = 0)
+    pitch = -(-n_cols // 64) * 64 + 64
+    Kd = torch.zeros((n_rows, pitch), dtype=torch.float32, device=eng.device)
+    Kd[:, :n_cols] = torch.from_numpy(Kh).to(eng.device)
+    got = eng.dense_to_scipy_csr(Kd[:, :n_cols])
+    ref = sp.csr_matrix(Kh.astype(np.float64))
+    ref.sort_indices()
+    assert got.dtype == np.float64 and got.shape == ref.shape and got.has_sorted_indices
+    assert np.array_equal(got.indptr, ref.indptr) and np.array_equal(got.indices, ref.indices)
+    assert np.array_equal(got.data, ref.data)
