@@ -21,7 +21,8 @@ namespace grf {
 
 __global__ __launch_bounds__(256) void walk_philox_kernel(const int64_t *__restrict__ g_ptr,
                                                           const int32_t *__restrict__ g_idx,
-                                                          const double *__restrict__ g_val, int64_t m, double p,
+                                                          const double *__restrict__ g_val,
+                                                          const unsigned char *__restrict__ g_aug, int64_t m, double p,
                                                           int32_t L, int32_t rule, uint32_t k0, uint32_t k1,
                                                           int64_t src_begin, int64_t n_src,
                                                           int32_t *__restrict__ slot_node,
@@ -31,11 +32,13 @@ __global__ __launch_bounds__(256) void walk_philox_kernel(const int64_t *__restr
     const int64_t sl = gid / m, w = gid - sl * m, s = src_begin + sl;
     int32_t *nd = slot_node + sl * L * m + w;
     double *ld = slot_load + sl * L * m + w;
-    const int32_t n_vis = philox_walk(g_ptr, g_idx, g_val, s, (uint32_t)w, p, L, rule, k0, k1,
-                                      [&](int32_t l, int32_t node, double load) {
-                                          nd[(int64_t)l * m] = node;
-                                          ld[(int64_t)l * m] = load;
-                                      });
+    auto visit = [&](int32_t l, int32_t node, double load) {
+        nd[(int64_t)l * m] = node;
+        ld[(int64_t)l * m] = load;
+    };
+    // (g_aug: one dependent round trip per step instead of two; the same draws and slots)
+    const int32_t n_vis = g_aug ? philox_walk_aug(g_ptr, g_aug, s, (uint32_t)w, p, L, rule, k0, k1, visit)
+                                : philox_walk(g_ptr, g_idx, g_val, s, (uint32_t)w, p, L, rule, k0, k1, visit);
     for (int32_t l = n_vis; l < L; ++l) nd[(int64_t)l * m] = -1;
 }
 
@@ -121,9 +124,14 @@ __device__ inline void pcg64_seed(uint64_t seed, Pcg64 &g) {
     g.u32 = 0;
 }
 
+// kAug: the steps read the augmented walk matrix (grf_walk_aug: the chosen entry's target, the target's
+// row start and length and the weight in one record), so each step is ONE dependent memory round trip
+// instead of two (the row bounds of the new node, then its entry); the draws and slots are identical.
+template <bool kAug>
 __global__ __launch_bounds__(64) void walk_pcg64_kernel(int64_t n, const int64_t *__restrict__ g_ptr,
                                                         const int32_t *__restrict__ g_idx,
-                                                        const double *__restrict__ g_val, int64_t m, double p,
+                                                        const double *__restrict__ g_val,
+                                                        const unsigned char *__restrict__ g_aug, int64_t m, double p,
                                                         int32_t L, int32_t rule, int64_t n_chunks, uint64_t seed,
                                                         int64_t chunk_begin, int64_t chunk_end, int64_t src_begin,
                                                         int32_t *__restrict__ slot_node,
@@ -134,23 +142,54 @@ __global__ __launch_bounds__(64) void walk_pcg64_kernel(int64_t n, const int64_t
     const int64_t b = c * base + (c < extra ? c : extra), e = b + base + (c < extra ? 1 : 0);
     Pcg64 g;
     pcg64_seed(seed + (uint64_t)c, g);
+    bool compact = false;
+    int tb = 0, rb = 0;
+    const unsigned char *recs = nullptr;
+    if (kAug) {
+        const int4 hd = *reinterpret_cast<const int4 *>(g_aug);
+        compact = hd.x == 1;
+        tb = hd.y;
+        rb = hd.z;
+        recs = g_aug + kAugHeader;
+    }
+    const uint64_t tmask = (1ull << tb) - 1, rmask = (1ull << rb) - 1;
     for (int64_t s = b; s < e; ++s) {
         const int64_t sl = s - src_begin;
+        const int64_t rs0 = g_ptr[s], deg0 = g_ptr[s + 1] - rs0;
         for (int64_t w = 0; w < m; ++w) {
             int32_t *nd = slot_node + sl * L * m + w;
             double *ld = slot_load + sl * L * m + w;
-            int64_t cur = s;
+            int64_t cur = s, rs = rs0, deg = deg0;
             double load = 1.0;
             int32_t l = 0;
             for (; l < L; ++l) {
                 nd[(int64_t)l * m] = (int32_t)cur;
                 ld[(int64_t)l * m] = load;
-                const int64_t rs = g_ptr[cur], deg = g_ptr[cur + 1] - rs;
+                if (!kAug) {
+                    rs = g_ptr[cur];
+                    deg = g_ptr[cur + 1] - rs;
+                }
                 if (deg == 0 || g.random() < p) { ++l; break; }
                 const uint32_t k = g.integers((uint32_t)deg);
-                const double wt = g_val[rs + k];
-                load = load_update(rule, load, deg, wt, p);
-                cur = g_idx[rs + k];
+                if (!kAug) {
+                    const double wt = g_val[rs + k];
+                    load = load_update(rule, load, deg, wt, p);
+                    cur = g_idx[rs + k];
+                } else if (compact) {
+                    const int4 a = *reinterpret_cast<const int4 *>(recs + (size_t)(rs + k) * sizeof(AugRec16));
+                    const uint64_t pk = ((uint64_t)(uint32_t)a.y << 32) | (uint32_t)a.x;
+                    load = load_update(rule, load, deg, __hiloint2double(a.w, a.z), p);
+                    cur = (int64_t)(pk & tmask);
+                    rs = (int64_t)((pk >> tb) & rmask);
+                    deg = (int64_t)(pk >> (tb + rb));
+                } else {
+                    const AugRec *rec = reinterpret_cast<const AugRec *>(recs) + rs + k;
+                    const int4 a = *reinterpret_cast<const int4 *>(rec);
+                    load = load_update(rule, load, deg, rec->w, p);
+                    cur = a.x;
+                    rs = (int64_t)(uint32_t)a.y;
+                    deg = a.z;
+                }
             }
             for (; l < L; ++l) nd[(int64_t)l * m] = -1;
         }
@@ -161,9 +200,11 @@ __global__ __launch_bounds__(64) void walk_pcg64_kernel(int64_t n, const int64_t
 
 using namespace grf;
 
-extern "C" __attribute__((visibility("default"))) int32_t grf_walk(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
-                            const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t *slot_node,
-                            double *slot_load, grf_stream_t stream) {
+static int32_t walk_impl(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
+                         const void *g_aug_v, const grf_walk_params *params, int64_t src_begin, int64_t src_end,
+                         int32_t *slot_node, double *slot_load, grf_stream_t stream) {
+    const unsigned char *g_aug = reinterpret_cast<const unsigned char *>(g_aug_v);
+    GRF_REQUIRE(!g_aug || ((uintptr_t)g_aug & 31) == 0, GRF_EINVAL, "grf_walk: g_aug must be 32-byte aligned");
     GRF_REQUIRE(params != nullptr, GRF_EINVAL, "grf_walk: params is NULL");
     const grf_walk_params P = *params;
     GRF_REQUIRE(n >= 0 && g_ptr && slot_node && slot_load, GRF_EINVAL, "grf_walk: bad arguments");
@@ -182,7 +223,7 @@ extern "C" __attribute__((visibility("default"))) int32_t grf_walk(int64_t n, co
         const int64_t total = n_src * P.walks_per_node;
         GRF_REQUIRE_GRID(cdiv<int64_t>(total, 256), 256, "walk_philox_kernel");
         walk_philox_kernel<<<(unsigned)cdiv<int64_t>(total, 256), 256, 0, st>>>(
-            g_ptr, g_idx, g_val, P.walks_per_node, P.p_halt, P.max_walk_length, P.load_rule, (uint32_t)P.seed,
+            g_ptr, g_idx, g_val, g_aug, P.walks_per_node, P.p_halt, P.max_walk_length, P.load_rule, (uint32_t)P.seed,
             (uint32_t)(P.seed >> 32), src_begin, n_src, slot_node, slot_load);
         GRF_CHECK_LAUNCH("walk_philox_kernel");
         return GRF_OK;
@@ -208,9 +249,29 @@ extern "C" __attribute__((visibility("default"))) int32_t grf_walk(int64_t n, co
     const int64_t nch = ce - cb;
     if (nch <= 0) return GRF_OK;
     GRF_REQUIRE_GRID(cdiv<int64_t>(nch, 64), 64, "walk_pcg64_kernel");
-    walk_pcg64_kernel<<<(unsigned)cdiv<int64_t>(nch, 64), 64, 0, st>>>(
-        n, g_ptr, g_idx, g_val, P.walks_per_node, P.p_halt, P.max_walk_length, P.load_rule, P.n_chunks, P.seed, cb,
-        ce, src_begin, slot_node, slot_load);
+    if (g_aug)
+        walk_pcg64_kernel<true><<<(unsigned)cdiv<int64_t>(nch, 64), 64, 0, st>>>(
+            n, g_ptr, g_idx, g_val, g_aug, P.walks_per_node, P.p_halt, P.max_walk_length, P.load_rule, P.n_chunks,
+            P.seed, cb, ce, src_begin, slot_node, slot_load);
+    else
+        walk_pcg64_kernel<false><<<(unsigned)cdiv<int64_t>(nch, 64), 64, 0, st>>>(
+            n, g_ptr, g_idx, g_val, nullptr, P.walks_per_node, P.p_halt, P.max_walk_length, P.load_rule, P.n_chunks,
+            P.seed, cb, ce, src_begin, slot_node, slot_load);
     GRF_CHECK_LAUNCH("walk_pcg64_kernel");
     return GRF_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int32_t grf_walk(int64_t n, const int64_t *g_ptr, const int32_t *g_idx,
+                                                                  const double *g_val, const grf_walk_params *params,
+                                                                  int64_t src_begin, int64_t src_end, int32_t *slot_node,
+                                                                  double *slot_load, grf_stream_t stream) {
+    return walk_impl(n, g_ptr, g_idx, g_val, nullptr, params, src_begin, src_end, slot_node, slot_load, stream);
+}
+
+extern "C" __attribute__((visibility("default"))) int32_t grf_walk_ex(int64_t n, const int64_t *g_ptr, const int32_t *g_idx,
+                                                                     const double *g_val, const void *g_aug,
+                                                                     const grf_walk_params *params, int64_t src_begin,
+                                                                     int64_t src_end, int32_t *slot_node,
+                                                                     double *slot_load, grf_stream_t stream) {
+    return walk_impl(n, g_ptr, g_idx, g_val, g_aug, params, src_begin, src_end, slot_node, slot_load, stream);
 }

@@ -55,6 +55,7 @@ SIGNATURES = {
     "grf_laplacian_dense": (_i32, [_i64, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _sz, _vp]),
     "grf_laplacian_dense_workspace_bytes": (_sz, [_i64]),
     "grf_walk": (_i32, [_i64, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _vp, _vp, _vp]),
+    "grf_walk_ex": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _vp, _vp, _vp]),
     "grf_chunk_bounds": (_i64, [_i64, _i64, _i64]),
     "grf_steps": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "grf_steps_densify": (_i32, [_i64, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),

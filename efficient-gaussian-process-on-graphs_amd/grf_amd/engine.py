@@ -228,7 +228,9 @@ class GRFEngine:
     # ---------------------------------------------------------------- walks
     def walk(self, G: DeviceCSR, walks_per_node: int, p_halt: float, max_walk_length: int, *, rng: int = C.RNG_PHILOX,
              seed: int = 42, n_chunks: int = 1, load_rule: int = C.LOAD_CUMULATIVE, src_begin: int = 0,
-             src_end: Optional[int] = None) -> Slots:
+             src_end: Optional[int] = None, use_aug: bool = True) -> Slots:
+        """Visit slots of the walks from sources [src_begin, src_end).  use_aug: step through the
+        augmented walk matrix (one dependent round trip per step; the same slots bit for bit)."""
         n = G.n_rows
         src_end = n if src_end is None else src_end
         m, L = int(walks_per_node), int(max_walk_length)
@@ -239,8 +241,9 @@ class GRFEngine:
         load = torch.empty((ns, L, m), dtype=torch.float64, device=self.device)
         prm = C.GrfWalkParams(m, float(p_halt), L, int(load_rule), int(rng), 0, int(n_chunks),
                               int(seed) & 0xFFFFFFFFFFFFFFFF)
-        C.check(self.lib.grf_walk(n, _p(G.ptr), _p(G.idx), _p(G.val), ctypes.byref(prm), src_begin, src_end,
-                                  _p(node), _p(load), self.stream), "grf_walk")
+        aug = self.walk_aug(G) if use_aug else None
+        C.check(self.lib.grf_walk_ex(n, _p(G.ptr), _p(G.idx), _p(G.val), _p(aug), ctypes.byref(prm), src_begin,
+                                     src_end, _p(node), _p(load), self.stream), "grf_walk_ex")
         return Slots(node, load, src_begin, n)
 
     def chunk_bounds(self, n: int, n_chunks: int) -> list[int]:

@@ -120,6 +120,12 @@ typedef struct grf_walk_params {
 int32_t grf_walk(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
                  const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t *slot_node,
                  double *slot_load, grf_stream_t stream);
+/* grf_walk with the augmented walk matrix (grf_walk_aug of the same walk matrix; NULL: grf_walk):
+ * each step is one dependent memory round trip instead of two; the same draws, bit-identical slots in
+ * both RNG modes (the PCG64 replay's one lane per chunk is latency-bound on exactly that chain). */
+int32_t grf_walk_ex(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
+                    const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t *slot_node,
+                    double *slot_load, grf_stream_t stream);
 
 /* host helper: first source of chunk c (np.array_split boundaries) */
 int64_t grf_chunk_bounds(int64_t n, int64_t n_chunks, int64_t c);

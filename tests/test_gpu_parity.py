@@ -842,6 +842,42 @@ def test_walk_phi_augmented_matrix_bitexact(eng, rule):
     assert same_csr(eng.compact(a).to_scipy(), ref)
 
 
+@pytest.mark.parametrize("rule", [0, 1, 2])
+def test_walk_slots_augmented_matrix_bitexact(eng, rule):
+    """The slot walks (grf_walk_ex: the PCG64 reference-stream replay and Philox) over the augmented
+    walk matrix take the same draws and give the same visit slots as grf_walk's two round trips per
+    step, in both record formats, on a weighted heavy-tailed graph with isolated nodes; and the PCG64
+    replay still matches the oracle's reference stream."""
+    import os
+    import torch
+    from grf_amd.graphs import powerlaw_graph
+    A = powerlaw_graph(3000, 5.0, 2.2, seed=7)
+    A.data = np.random.default_rng(3).uniform(0.2, 3.0, A.nnz)
+    A = ((A + A.T) * 0.5).tocsr()
+    A.sort_indices()
+    G = eng.laplacian(A)
+    os.environ["GRF_WALK_AUG16"] = "0"
+    try:
+        G32 = eng.laplacian(A)
+        assert eng.walk_aug(G32)[:16].view(torch.int32).cpu().numpy()[0] == 0  # (32-byte records)
+    finally:
+        del os.environ["GRF_WALK_AUG16"]
+    assert eng.walk_aug(G)[:16].view(torch.int32).cpu().numpy()[0] == 1      # (16-byte records)
+    for rng, chunks in ((0, 1), (0, 5), (0, 64), (1, 1)):
+        kw = dict(rng=rng, seed=13, n_chunks=chunks, load_rule=rule)
+        a = eng.walk(G, 12, 0.2, 6, use_aug=False, **kw)
+        for g in (G, G32):
+            b = eng.walk(g, 12, 0.2, 6, use_aug=True, **kw)
+            assert torch.equal(a.node, b.node), (rng, chunks)
+            mask = a.node >= 0
+            assert torch.equal(a.load[mask], b.load[mask]), (rng, chunks)
+    Ls, _ = O.laplacian_sparse(A)
+    ip, ix, dx = O._csr_arrays(Ls)
+    got = eng.walk(G, 12, 0.2, 6, rng=0, seed=13, n_chunks=5, load_rule=rule)
+    ref = O.walk_slots(ip, ix, dx, 12, 0.2, 6, rng=O.RNG_PCG64, n_chunks=5, seed=13, load_rule=rule)
+    assert slots_equal(got, ref)
+
+
 def _sharded_worker(rank, world, port, mode, q, graph="er", policy="nodes"):
     """One rank of a gloo group on cuda:0 (device tensors staged through host memory)."""
     import os
