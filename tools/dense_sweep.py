@@ -1,5 +1,7 @@
 """MFMA dense Gram throughput (grf_gram_dense incl. its mirror) at several n: N (N + 1) k flops over
-HIP-event time.  usage: python tools/dense_sweep.py [n ...]  (GRF_DENSE_TILE / GRF_DENSE_BK knobs)."""
+HIP-event time, and a digest of K (knob A/Bs that keep the MFMA order must agree bit for bit).
+usage: python tools/dense_sweep.py [n ...]  (GRF_DENSE_TILE / GRF_DENSE_BK / GRF_DENSE_DB knobs)."""
+import hashlib
 import os
 import sys
 
@@ -13,7 +15,8 @@ eng = GRFEngine("cuda:0")
 for n in [int(a) for a in sys.argv[1:]] or [2708, 4096, 10000]:
     lda = -(-n // 64) * 64
     A = torch.zeros((n, lda), dtype=torch.float32, device=eng.device)
-    A[:, :n] = torch.rand((n, n), device=eng.device) * (torch.rand((n, n), device=eng.device) < 0.05)
+    g = torch.Generator(device=eng.device).manual_seed(n)
+    A[:, :n] = torch.rand((n, n), device=eng.device, generator=g) * (torch.rand((n, n), device=eng.device, generator=g) < 0.05)
     for _ in range(3):
         eng.gram_dense(A, n)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
@@ -27,4 +30,5 @@ for n in [int(a) for a in sys.argv[1:]] or [2708, 4096, 10000]:
     ref = (A[:, :n].double() @ A[:, :n].double().t())
     err = ((K.double() - ref).abs().max() / ref.abs().max()).item()
     print(f"n={n} tile={os.environ.get('GRF_DENSE_TILE', 'auto')} bk={os.environ.get('GRF_DENSE_BK', 'auto')} "
-          f"{ms:.3f} ms {flops / ms / 1e9:.1f} TF/s frac={flops / ms / 1e9 / 157.3:.3f} relerr={err:.2e}", flush=True)
+          f"db={os.environ.get('GRF_DENSE_DB', 'auto')} {ms:.4f} ms {flops / ms / 1e9:.1f} TF/s frac={flops / ms / 1e9 / 157.3:.3f} "
+          f"relerr={err:.2e} digest={hashlib.sha256(K.contiguous().cpu().numpy().tobytes()).hexdigest()[:12]}", flush=True)
