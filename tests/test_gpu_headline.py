@@ -251,3 +251,28 @@ def test_c5_column_block_with_hub_split(eng):
     res = P.k_block_check(eng, fr, pl, K)
     assert res["ok"], res
     del K, fr
+
+
+def test_dense_path_bench_pipelined_line():
+    """bench.py's dense-path workload (C3) pipelined: the next step's front on a side stream beside this
+    step's MFMA Gram.  The line keeps the contract fields, reports the pipelining, the serial latency
+    beside it and the Gram's roofline from its time alone (the C3 parity of the same kernels:
+    test_c3_dense_leg_cora)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for flag in ("", "--no-overlap"):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--workload", "c3", "--steps", "5",
+                            "--warmup", "1", "--no-cpu-baseline"] + ([flag] if flag else []),
+                           cwd=root, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[flag] = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    pipe, ser = out[""], out["--no-overlap"]
+    assert pipe["pipelined"] is True and ser["pipelined"] is False
+    for d in (pipe, ser):
+        assert d["unit"] == "K-matrices/s" and d["value"] > 0 and d["ms_per_step"] > 0 and d["serial_ms_per_step"] > 0
+        rf = d["roofline"]
+        assert rf["bound"] == "mfma" and 0 < rf["frac"] < 1 and rf["kernel_ms"] > 0 and rf["kernel_ms_pipelined"] > 0
