@@ -118,6 +118,7 @@ struct GramStream {
     __amdgpu_buffer_rsrc_t rec; // the band's record pairs, 12 bytes each (global, 32-bit offsets)
     unsigned char *acc;         // tile accumulator (LDS), addressed by byte offset
     double S;                   // the row's fixed-point scale 2^sh
+    int32_t safe;               // byte offset of a pair with finite values (masked positions read it)
 };
 
 // one 12-byte record pair: {u16 col0 | u16 col1 << 16, f32 v0, f32 v1}
@@ -151,7 +152,7 @@ __device__ __forceinline__ void gram_windows(const GramStream &g, int32_t w0, in
         for (int u = 0; u < NW; ++u) {
             if (TAIL == 1 && u != NW - 1) continue;
             const bool ok = w0 + u * 64 + lane < cend;
-            pos[u] = ok ? pos[u] : 0;  // the band's first pair: valid and finite
+            pos[u] = ok ? pos[u] : g.safe;  // the band's first pair (slots: slot 0's first pair): finite
             sc[u] = ok ? sc[u] : 0.0;
         }
     }
@@ -363,20 +364,27 @@ __device__ __forceinline__ void gram_fused_completion(const GramTiles &tl, int64
 // id (bucket-start markers propagated by a running maximum, one LDS read); the gathers of kGramUnroll
 // windows of 64 pairs are in flight together.  Tiles are dispatched band-major, so the
 // tiles in flight share one band's records (L2 / Infinity Cache).
-template <int kWaves, int kHalves, int kGramUnroll, bool kTailExact, bool kFuse>
+// kSlot: the transpose is in the GRF_REC_SLOT layout -- bucket b's header {pairs, first overflow pair}
+// and its first two pairs in the 32-byte slot t_rec + 32 b, the other pairs at t_rec + ovf_base + 12 p --
+// so every nonzero contributes two virtual buckets (inline part, overflow part) to the wave's stream,
+// and a small bucket costs one line (header and pairs) instead of a descriptor line and a record line.
+template <int kWaves, int kHalves, int kGramUnroll, bool kTailExact, bool kFuse, bool kSlot = false>
 __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
     const unsigned char *__restrict__ t_rec, int32_t unit, const int32_t *__restrict__ rowshift,
-    float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets, const uint16_t *__restrict__ t_split) {
+    float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets, const uint16_t *__restrict__ t_split,
+    int64_t ovf_base) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
+    static_assert(!kSlot || kHalves == 1, "slot streams: 2 virtual buckets per nonzero, u8 ids <= 128");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t W = tl.W;
-    constexpr int kB = 64 * kHalves;  // nonzeros per wave batch
-    unsigned char *st = reinterpret_cast<unsigned char *>(acc + W) + wave * wave_state_bytes(kHalves);
+    constexpr int kB = 64 * kHalves;        // nonzeros per wave batch
+    constexpr int kV = kSlot ? 2 * kHalves : kHalves;  // stream buckets per lane and batch
+    unsigned char *st = reinterpret_cast<unsigned char *>(acc + W) + wave * wave_state_bytes(kV);
     unsigned char *bidv = st;                                          // [kChunk]
-    int32_t *tbase = reinterpret_cast<int32_t *>(st + kChunk);         // [kB]
-    float *aval = reinterpret_cast<float *>(st + kChunk + kB * 4);     // [kB]
+    int32_t *tbase = reinterpret_cast<int32_t *>(st + kChunk);         // [64 kV]
+    float *aval = reinterpret_cast<float *>(st + kChunk + 64 * kV * 4);  // [64 kV]
 
     int64_t J, r;
     tl.locate(t_begin + (int64_t)blockIdx.x, J, r);
@@ -389,8 +397,8 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     const int64_t e0 = ptr[row], e1 = ptr[row + 1];
     const int64_t boff = J * n_total;
     const int sh = rowshift[row];
-    const int32_t line0 = (int32_t)t_desc[boff].x;                  // the band's first unit
-    const unsigned char *brec = t_rec + (int64_t)line0 * unit;  // the band's records
+    const int32_t line0 = kSlot ? 0 : (int32_t)t_desc[boff].x;      // the band's first unit
+    const unsigned char *brec = t_rec + (int64_t)line0 * unit;  // the band's records (slots: all of t_rec)
     // symmetric mode on the row's own band (a diagonal tile): only the columns j >= row are kept (the
     // mirror overwrites the rest), so with sub-band ordered buckets (t_split) every bucket stream starts
     // at the row's sub-band -- the pairs of the earlier sub-bands are never fetched -- and the write-out
@@ -407,31 +415,45 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     const GramStream gs{bidv, tbase, aval,
                         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char *>(brec), (short)0, 0x7fffffff,
                                                           0x00020000),
-                        reinterpret_cast<unsigned char *>(acc), ldexp(1.0, sh)};
+                        reinterpret_cast<unsigned char *>(acc), ldexp(1.0, sh), kSlot ? 8 : 0};
     for (int64_t g0 = e0 + (int64_t)wave * kB; g0 < e1; g0 += kB * kWaves) {
-        int32_t cnt[kHalves], excl[kHalves], t0[kHalves];
-        float av[kHalves];
+        int32_t cnt[kV], excl[kV], t0[kV];
+        float av[kV];
 #pragma unroll
         for (int h = 0; h < kHalves; ++h) {
             const int64_t e = g0 + h * 64 + lane;
             int32_t k = e < e1 ? idx[e] : -1;
             if (k < tl.k_begin || k >= tl.k_end) k = -1;  // (k-slice mode)
-            av[h] = k >= 0 ? val[e] : 0.f;
-            const uint2 d = k >= 0 ? t_desc[boff + k] : make_uint2((uint32_t)line0, 0u);
-            // pairs of the sub-bands before the row's (diagonal tiles; capped: a dropped hub bucket has 0)
-            const int32_t skip = (dsub > 0 && k >= 0) ? min((int32_t)(t_split[(boff + k) * kSub + dsub] >> 1), (int32_t)d.y) : 0;
-            t0[h] = ((int32_t)d.x - line0) * unit + kPairBytesG * skip;  // first fetched byte within the band
-            cnt[h] = (int32_t)d.y - skip;                                   // pairs
+            const float a = k >= 0 ? val[e] : 0.f;
+            if constexpr (kSlot) {
+                // the slot's header and inline pairs share its line; the overflow pairs follow all slots
+                const int64_t sb = 32 * (boff + (k >= 0 ? k : 0));
+                const uint2 d = k >= 0 ? *reinterpret_cast<const uint2 *>(t_rec + sb) : make_uint2(0u, 0u);
+                const int32_t inl = min((int32_t)d.x, 2);
+                t0[2 * h] = (int32_t)sb + 8;
+                cnt[2 * h] = inl;
+                t0[2 * h + 1] = (int32_t)ovf_base + kPairBytesG * (int32_t)d.y;
+                cnt[2 * h + 1] = (int32_t)d.x - inl;
+                av[2 * h] = a;
+                av[2 * h + 1] = a;
+            } else {
+                av[h] = a;
+                const uint2 d = k >= 0 ? t_desc[boff + k] : make_uint2((uint32_t)line0, 0u);
+                // pairs of the sub-bands before the row's (diagonal tiles; capped: a dropped hub bucket has 0)
+                const int32_t skip = (dsub > 0 && k >= 0) ? min((int32_t)(t_split[(boff + k) * kSub + dsub] >> 1), (int32_t)d.y) : 0;
+                t0[h] = ((int32_t)d.x - line0) * unit + kPairBytesG * skip;  // first fetched byte within the band
+                cnt[h] = (int32_t)d.y - skip;                                   // pairs
+            }
         }
         int32_t total = 0;
 #pragma unroll
-        for (int h = 0; h < kHalves; ++h) {
+        for (int h = 0; h < kV; ++h) {
             const int32_t inc = wave_inclusive_scan<int32_t>(cnt[h]) + total;  // (DPP: grf_block.h)
             excl[h] = inc - cnt[h];
             total = __builtin_amdgcn_readlane(inc, 63);
         }
 #pragma unroll
-        for (int h = 0; h < kHalves; ++h) {
+        for (int h = 0; h < kV; ++h) {
             tbase[h * 64 + lane] = t0[h] - 12 * excl[h];  // byte offset = tbase + 12 * position
             aval[h * 64 + lane] = av[h];
         }
@@ -442,7 +464,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             reinterpret_cast<uint4 *>(bidv)[lane] = make_uint4(0u, 0u, 0u, 0u);
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int h = 0; h < kHalves; ++h)
+            for (int h = 0; h < kV; ++h)
                 if (cnt[h] > 0 && excl[h] >= c0 && excl[h] < cend)
                     bidv[excl[h] - c0] = (unsigned char)(h * 64 + lane + 1);
             __builtin_amdgcn_wave_barrier();
@@ -951,7 +973,25 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
                                  const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
                                  float *K, int64_t ldk, hipStream_t st, int32_t *tickets = nullptr,
-                                 const void *t_split = nullptr) {
+                                 const void *t_split = nullptr, int64_t slot_buckets = 0) {
+    if (unit == GRF_REC_SLOT) {
+        // the slot layout: 8-wave tiles (one batch of 64 nonzeros per wave: two stream buckets each),
+        // the default unroll and exact tails; the overflow pairs follow the slot_buckets slots
+        GRF_REQUIRE(!tickets && !t_split, GRF_EUNSUPPORTED, "gram: GRF_REC_SLOT has no fused / split variant");
+        GRF_REQUIRE(32 * slot_buckets < ((int64_t)1 << 30), GRF_EUNSUPPORTED,
+                    "gram: GRF_REC_SLOT slots beyond 32-bit record offsets");
+        const size_t lds = gram_lds_bytes(tl.W, 8, 2);
+        const int64_t max_tiles = ((1ll << 32) - 1) / (64 * 8);
+        for (int64_t t0 = t_first; t0 < t_last; t0 += max_tiles) {
+            const int64_t nt = (t_last - t0) < max_tiles ? (t_last - t0) : max_tiles;
+            gram_sparse_kernel<8, 1, 8, true, false, true><<<(unsigned)nt, 512, lds, st>>>(
+                n_total, row_begin, tl, t0, ptr, idx, val, reinterpret_cast<const uint2 *>(t_desc),
+                reinterpret_cast<const unsigned char *>(t_rec), unit, t_rowshift, K, ldk, nullptr, nullptr,
+                32 * slot_buckets);
+            GRF_CHECK_LAUNCH("gram_sparse_kernel");
+        }
+        return GRF_OK;
+    }
     // GRF_GRAM_SPLIT=0: ignore the sub-band split (A/B of the diagonal tiles' skip)
     static const bool use_split = [] {
         const char *e = getenv("GRF_GRAM_SPLIT");
@@ -982,7 +1022,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
     gram_sparse_kernel<WV, H, U, T, F><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx,   \
                                                                         val, reinterpret_cast<const uint2 *>(t_desc), \
                                                                         reinterpret_cast<const unsigned char *>(t_rec), \
-                                                                        unit, t_rowshift, K, ldk, tickets, split)
+                                                                        unit, t_rowshift, K, ldk, tickets, split, 0)
 #define GRF_GRAM_LAUNCH_T(WV, H, U, T) GRF_GRAM_LAUNCH_F(WV, H, U, T, false)
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     do {                                                                                                          \
@@ -1018,14 +1058,14 @@ static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t ro
     const int64_t n_tiles = tl.total();
     if (n_tiles == 0) return GRF_OK;
     return gram_tiles_launch(n_total, row_begin, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, unit, t_rowshift, K,
-                             ldk, st, nullptr, t_split);
+                             ldk, st, nullptr, t_split, nb * n_total);
 }
 
 static int32_t gram_sparse_check(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
                                  int64_t band_width, int32_t unit, const uint32_t *t_desc, const void *t_rec,
                                  const int32_t *t_rowshift, float *K, int64_t ldk) {
-    GRF_REQUIRE(unit == GRF_REC_LINE || unit == GRF_REC_PACKED, GRF_EINVAL,
-                "grf_gram_sparse: rec_unit must be GRF_REC_LINE or GRF_REC_PACKED");
+    GRF_REQUIRE(unit == GRF_REC_LINE || unit == GRF_REC_PACKED || unit == GRF_REC_SLOT, GRF_EINVAL,
+                "grf_gram_sparse: rec_unit must be GRF_REC_LINE, GRF_REC_PACKED or GRF_REC_SLOT");
     GRF_REQUIRE(n_total >= 0 && 0 <= row_begin && row_begin <= row_end && row_end <= n_total && ptr && t_desc && K &&
                     t_rowshift && t_rec,
                 GRF_EINVAL, "grf_gram_sparse: bad arguments");
@@ -1076,7 +1116,7 @@ static int32_t gram_sparse_upper_impl(int64_t n_total, const int64_t *ptr, const
     const int64_t t0 = total * part_begin / n_parts, t1 = total * part_end / n_parts;
     if (t1 <= t0) return GRF_OK;
     return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
-                             S(stream), nullptr, t_split);
+                             S(stream), nullptr, t_split, tl.nb * n_total);
 }
 
 int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
@@ -1171,7 +1211,7 @@ static int32_t gram_sparse_cols_impl(int64_t n_cols, int64_t row_begin, int64_t 
     GRF_REQUIRE(band_width >= 64 && band_width % 64 == 0 && band_width <= 8192, GRF_EUNSUPPORTED,
                 "grf_gram_sparse_cols: band_width must be a multiple of 64 in [64, 8192]");
     GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_gram_sparse_cols: t_rec must be 128-byte aligned");
-    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED, GRF_EINVAL,
+    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED || rec_unit == GRF_REC_SLOT, GRF_EINVAL,
                 "grf_gram_sparse_cols: bad rec_unit");
     GRF_REQUIRE(sym_row0 < 0 || (row_begin <= sym_row0 && sym_row0 + t_rows <= row_end), GRF_EINVAL,
                 "grf_gram_sparse_cols: the symmetric square [sym_row0, sym_row0 + t_rows) must lie in the rows");
@@ -1185,7 +1225,7 @@ static int32_t gram_sparse_cols_impl(int64_t n_cols, int64_t row_begin, int64_t 
         tl.t_rows = t_rows;
         tl.add_k = add_k;
         return gram_tiles_launch(n_cols, r0, tl, 0, tl.total(), ptr, idx, val, t_desc, t_rec, rec_unit, row_shift,
-                                 K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr);
+                                 K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr, nb * n_cols);
     };
     if (sym_row0 < 0) return launch(row_begin, row_end, false);
     // Phi_B = Phi[sym_row0, sym_row0 + t_rows): the square K[B, B] is symmetric and its bands start at
@@ -1248,7 +1288,7 @@ int32_t grf_gram_sparse_block(int64_t n_total, int64_t row_begin, int64_t row_en
         tl.J_off = ja;
         const int64_t n_tiles = tl.total();
         return gram_tiles_launch(n_total, r0, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift,
-                                 K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr);
+                                 K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr, nb * n_total);
     };
     if ((rc = launch(B0, B1, J0, J1, true)) != GRF_OK) return rc;            // interior, symmetric
     if ((rc = launch(row_begin, row_end, 0, J0, false)) != GRF_OK) return rc;  // bands before

@@ -656,6 +656,100 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
     }
 }
 
+// GRF_REC_SLOT: bucket b owns the 32-byte slot t_rec + 32 b = {u32 pairs, u32 first overflow pair,
+// pair 0, pair 1}: its first four entries inline, the rest as packed pairs in the overflow area after
+// all nbk slots (t_rec + 32 nbk + 12 * pair).  The Gram reads a bucket of <= 2 pairs -- almost every
+// bucket of a column block over a power-law Phi (C5: ~1.4 entries) -- with its header in one line,
+// instead of a descriptor line and a record line.  Same staging and region bases as the packed
+// placement (the region's units bound its overflow pairs); one workgroup per region, slots written
+// whole (header + zeroed payload) before the entries land in them.
+__global__ __launch_bounds__(256) void tr_place_slots_kernel(int64_t n_rows, int64_t n_cols, int64_t bw, int32_t cr,
+                                                             int32_t nreg, int64_t nbk, const int64_t *ptr,
+                                                             const int64_t *region_base, const uint2 *staging,
+                                                             const int32_t *tab, int32_t *gcur,
+                                                             unsigned char *t_rec) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char tps_smem[];
+    const int tid = threadIdx.x;
+    const int64_t nblk = gridDim.x, per8 = nblk / 8, rem8 = nblk % 8;
+    const int64_t x8 = blockIdx.x % 8, k8 = blockIdx.x / 8;
+    const int64_t rg = x8 * per8 + (x8 < rem8 ? x8 : rem8) + k8, band = rg / nreg, g = rg - band * nreg;
+    const int64_t c0 = g * cr, c1 = min<int64_t>(n_cols, c0 + cr);
+    const int nbk_r = (int)(c1 - c0);
+    const int64_t b0 = band * n_cols + c0;
+    const int64_t U0 = region_base[rg];                          // the region's first overflow pair
+    uint32_t *lcur = reinterpret_cast<uint32_t *>(tps_smem);     // [cr] counts, then cursors
+    uint32_t *lovf = lcur + cr;                                  // [cr] first overflow pair (local)
+    int32_t *scratch = reinterpret_cast<int32_t *>(lovf + cr);   // [8]
+    unsigned char *image = reinterpret_cast<unsigned char *>(scratch + 8);
+    unsigned char *slots = t_rec + 32 * b0, *ovf = t_rec + 32 * nbk + (int64_t)kPairBytes * U0;
+    const int64_t w0 = band * bw / kBinRows, w1 = cdiv<int64_t>(min<int64_t>(n_rows, (band + 1) * bw), kBinRows);
+    for (int i = tid; i < nbk_r; i += 256) lcur[i] = 0u;
+    __syncthreads();
+    for (int64_t w = w0 + tid; w < w1; w += 256) {  // pass 1: the region's bucket counts
+        const int32_t *trow = tab + w * (nreg + 1);
+        const int32_t o0 = trow[g], o1 = trow[g + 1];
+        const uint2 *run = staging + ptr[w * kBinRows];
+        for (int32_t o = o0; o < o1; ++o) atomicAdd(&lcur[run[o].x >> 16], 1u);
+    }
+    __syncthreads();
+    const int per = (nbk_r + 255) / 256;
+    int32_t sum = 0;
+    for (int q = 0; q < per; ++q) {
+        const int i = tid * per + q;
+        if (i < nbk_r) sum += max(0, (int32_t)((lcur[i] + 1) >> 1) - 2);
+    }
+    int32_t total;
+    int32_t run_p = block_exclusive_scan<int32_t>(sum, scratch, &total);
+    const bool lds = ((int64_t)total * kPairBytes + 15) / 16 * 16 <= kPlaceCap;
+    for (int q = 0; q < per; ++q) {
+        const int i = tid * per + q;
+        if (i < nbk_r) {
+            const uint32_t c = lcur[i], pairs = (c + 1) >> 1;
+            lovf[i] = (uint32_t)run_p;
+            uint4 *sl = reinterpret_cast<uint4 *>(slots + 32 * (int64_t)i);
+            sl[0] = make_uint4(pairs, (uint32_t)(U0 + run_p), 0u, 0u);
+            sl[1] = make_uint4(0u, 0u, 0u, 0u);
+            run_p += max(0, (int32_t)pairs - 2);
+            lcur[i] = 0u;  // (the counts become cursors)
+        }
+    }
+    const int64_t img = (int64_t)total * kPairBytes;
+    if (lds) {
+        for (int64_t i = tid; i < (img + 15) / 16; i += 256) reinterpret_cast<uint4 *>(image)[i] = make_uint4(0u, 0u, 0u, 0u);
+    } else {  // oversized region: overflow pairs straight to global, zeroed first
+        for (int64_t i = tid; i < img / 4; i += 256) reinterpret_cast<uint32_t *>(ovf)[i] = 0u;
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int64_t w = w0 + tid; w < w1; w += 256) {  // pass 2: place the entries
+        const int32_t *trow = tab + w * (nreg + 1);
+        const int32_t o0 = trow[g], o1 = trow[g + 1];
+        const uint2 *run = staging + ptr[w * kBinRows];
+        for (int32_t o = o0; o < o1; ++o) {
+            const uint2 x = run[o];
+            const uint32_t kk = x.x >> 16;
+            const uint32_t s = atomicAdd(&lcur[kk], 1u);
+            unsigned char *pair;
+            uint32_t half;
+            if (s < 4) {
+                pair = slots + 32 * (int64_t)kk + 8 + kPairBytes * (s >> 1);
+                half = s & 1;
+            } else {
+                const uint32_t q = s - 4;
+                pair = (lds ? image : ovf) + kPairBytes * (int64_t)(lovf[kk] + (q >> 1));
+                half = q & 1;
+            }
+            reinterpret_cast<uint16_t *>(pair)[half] = (uint16_t)(x.x & 0xffffu);
+            reinterpret_cast<uint32_t *>(pair + 4)[half] = x.y;
+        }
+    }
+    if (!lds || img == 0) return;
+    __syncthreads();
+    uint32_t *dst = reinterpret_cast<uint32_t *>(ovf);
+    for (int64_t i = tid; i < img / 4; i += 256) dst[i] = reinterpret_cast<const uint32_t *>(image)[i];
+    (void)gcur;
+}
+
 // Region width: at most 4096 regions per band, and every placing workgroup reads one table
 // entry per binning workgroup of its band, n_rows * n_cols / (16 cr) scattered reads in all --
 // kept <= 32 M (C4: cr = 128, 4.9 M; C5, N = 1M: cr = 2048 instead of 256, where 244 M reads
@@ -881,6 +975,8 @@ int64_t grf_transpose_self_units_bound(int64_t n_rows, int64_t n_cols, int64_t b
     const int64_t n_regions = nb * cdiv<int64_t>(n_cols, tr_region_cols(n_rows, n_cols));
     // the sum of tr_region_units over the regions, for any split of nnz entries
     if (rec_unit == GRF_REC_PACKED) return (nnz + nbk) / 2 + n_regions + 1;
+    // GRF_REC_SLOT: 32-byte units covering the slots and the overflow pairs (at most the packed bound)
+    if (rec_unit == GRF_REC_SLOT) return nbk + cdiv<int64_t>(kPairBytes * ((nnz + nbk) / 2 + n_regions + 1), 32);
     return (6 * (nnz + nbk)) / rec_unit + nbk + 2 * n_regions + 1;
 }
 
@@ -892,8 +988,10 @@ int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_w
     GRF_REQUIRE(n_rows >= 0 && n_cols > 0 && band_width > 0 && band_width <= 8192 && ptr && idx && val && t_desc &&
                     t_rec && t_maxabs && t_rowshift && t_rec_bytes >= 0 && staging && workspace,
                 GRF_EINVAL, "grf_transpose_banded_self: bad arguments");
-    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED, GRF_EINVAL,
-                "grf_transpose_banded_self: rec_unit must be GRF_REC_LINE or GRF_REC_PACKED");
+    GRF_REQUIRE(rec_unit == GRF_REC_LINE || rec_unit == GRF_REC_PACKED || rec_unit == GRF_REC_SLOT, GRF_EINVAL,
+                "grf_transpose_banded_self: rec_unit must be GRF_REC_LINE, GRF_REC_PACKED or GRF_REC_SLOT");
+    GRF_REQUIRE(rec_unit != GRF_REC_SLOT || !t_split, GRF_EUNSUPPORTED,
+                "grf_transpose_banded_self: GRF_REC_SLOT has no sub-band split");
     GRF_REQUIRE(band_width % 64 == 0, GRF_EUNSUPPORTED, "grf_transpose_banded_self: band_width must be a multiple of 64");
     GRF_REQUIRE(((uintptr_t)t_rec & 127) == 0, GRF_EINVAL, "grf_transpose_banded_self: t_rec must be 128-byte aligned");
     const int64_t nb = cdiv<int64_t>(n_rows, band_width), nbk = nb * n_cols;
@@ -946,12 +1044,22 @@ int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_w
     GRF_CHECK_LAUNCH("tr_rowshift_kernel");
     GRF_REQUIRE_GRID(cdiv<int64_t>(n_regions, 4), 256, "tr_region_units_kernel");
     tr_region_units_kernel<<<(unsigned)cdiv<int64_t>(n_regions, 4), 256, 0, st>>>(n_rows, n_cols, band_width, cr, nreg,
-                                                                                 n_regions, tab, rec_unit, region_units);
+                                                                                 n_regions, tab,
+                                                                                 rec_unit == GRF_REC_SLOT ? kPairBytes : rec_unit,
+                                                                                 region_units);
     GRF_CHECK_LAUNCH("tr_region_units_kernel");
     int32_t rc = scan_exclusive<int64_t>(n_regions, region_units, ScanIdentity{},
                                          RegionBaseOut{region_base, desc + nbk}, (int64_t *)scan_ws, st);
     if (rc != GRF_OK) return rc;
     GRF_REQUIRE_GRID(n_regions, 256, "tr_place_self_kernel");
+    if (rec_unit == GRF_REC_SLOT) {
+        const size_t lds2 = (size_t)8 * cr + 32 + kPlaceCap;
+        tr_place_slots_kernel<<<(unsigned)n_regions, 256, lds2, st>>>(n_rows, n_cols, band_width, cr, nreg, nbk, ptr,
+                                                                       region_base, ent, tab, gcur,
+                                                                       (unsigned char *)t_rec);
+        GRF_CHECK_LAUNCH("tr_place_slots_kernel");
+        return GRF_OK;
+    }
     if (t_split) {
         const size_t lds2 = (size_t)4 * cr * (kSub + 1) + 32 + kPlaceCap;
         tr_place_self_kernel<true><<<(unsigned)n_regions, 256, lds2, st>>>(

@@ -25,7 +25,7 @@ LAP_SCIPY, LAP_NUMPY, LAP_NUMPY_SAFE, LAP_COMBINATORIAL, LAP_NONE = 0, 1, 2, 3, 
 RNG_PCG64, RNG_PHILOX = 0, 1
 LOAD_CUMULATIVE, LOAD_NONCUMULATIVE, LOAD_ABLATION = 0, 1, 2
 NORM_DIV, NORM_MUL_RECIP = 0, 1
-REC_LINE, REC_PACKED = 128, 12
+REC_LINE, REC_PACKED, REC_SLOT = 128, 12, 32
 
 
 class GrfWalkParams(ctypes.Structure):

@@ -423,7 +423,7 @@ class GRFEngine:
     def transpose_banded(self, phi: DeviceCSR, band_width: int = DEFAULT_BAND_WIDTH,
                          counted_ws: Optional[torch.Tensor] = None, staged: Optional[bool] = None,
                          nnz_bound: Optional[int] = None, rec_unit: Optional[int] = None,
-                         self_count: Optional[bool] = None, split: bool = False) -> Banded:
+                         self_count: Optional[bool] = None, split: bool = False, slots: bool = False) -> Banded:
         """Banded transpose of Phi.  counted_ws: workspace whose bucket counts ``walk_phi`` filled.
         staged: two-pass binned fill (default when band_width % 64 == 0) or the atomic fill.
         self_count: the staged fill without a plan (grf_transpose_banded_self; default unless
@@ -432,7 +432,11 @@ class GRFEngine:
         buffer is then sized from bounds and no size is read back (no host synchronisation).
         split: (self-count transpose) lay every bucket out by sub-band and return the offsets
         (``Banded.t_split``) for the symmetric Gram's diagonal-tile skip -- measured no faster (a skip
-        saves records inside lines the tile fetches anyway: profiles/r03_split_ab.txt), so off by default."""
+        saves records inside lines the tile fetches anyway: profiles/r03_split_ab.txt), so off by default.
+        slots: (self-count transpose) where the buckets are sparse enough for packed pairs and the bands
+        wider than 4096 (8-wave Gram tiles), the GRF_REC_SLOT layout instead: each bucket's header and
+        first two pairs in one 32-byte slot, so the Gram reads a small bucket with one line (the column
+        blocks over power-law graphs, C5).  Not for the hub-column split (which edits descriptors)."""
         n_rows, n_cols = phi.n_rows, phi.n_cols
         nb = -(-n_rows // band_width)
         nbk = nb * n_cols
@@ -446,6 +450,10 @@ class GRFEngine:
         if self_count:
             if counted_ws is not None or not staged:
                 raise ValueError("self_count: the staged transpose counts its own buckets (no counted_ws)")
+            if slots and not split and rec_unit is None and band_width > 4096:
+                u0 = choose_rec_unit(phi.nnz if phi._nnz is not None or nnz_bound is None else nnz_bound,
+                                     n_rows, n_cols, band_width)
+                rec_unit = C.REC_SLOT if u0 == C.REC_PACKED else u0
             return self._transpose_self(phi, band_width, nnz_bound, rec_unit, t_desc, t_max, t_shift, split)
         ws = counted_ws if counted_ws is not None else self._ws(self.lib.grf_transpose_workspace_bytes(nbk))
         if rec_unit is None:
@@ -507,6 +515,9 @@ class GRFEngine:
         if n_rows and band_units * u >= 2 ** 31:
             raise NotImplementedError("a transpose band holds >= 2 GiB of records; use a smaller band_width")
         units = self.lib.grf_transpose_self_units_bound(n_rows, n_cols, band_width, u, nnz)
+        if u == C.REC_SLOT and units * u >= 2 ** 30:
+            # (slot offsets are counted from the first slot of all bands: fall back to packed pairs)
+            return self._transpose_self(phi, band_width, nnz_bound, C.REC_PACKED, t_desc, t_max, t_shift, split)
         t_rec = self._empty(max(units, 1) * u + 128, torch.uint8)
         ws = self._ws(self.lib.grf_transpose_self_workspace_bytes(n_rows, n_cols, band_width))
         sg = self._ws(self.lib.grf_transpose_staging_bytes(n_rows, n_cols, band_width, nnz))
@@ -657,6 +668,8 @@ class GRFEngine:
         no host read), ties by column id; the panel holds them in ascending column order.
         Returns (P, cols).  Hub-heavy graphs: a column in a large share of the rows costs the sparse
         Gram one gathered record per multiply-add, the MFMA Gram of the panel ~60x less."""
+        if tr.rec_unit == C.REC_SLOT:
+            raise ValueError("hub_split: the GRF_REC_SLOT layout keeps no descriptor table to edit")
         n_rows, n = phi.n_rows, tr.n_cols
         h = max(0, min(int(hubs), n))
         nb = -(-tr.n_rows // tr.band_width)

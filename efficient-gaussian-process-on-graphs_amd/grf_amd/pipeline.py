@@ -27,6 +27,8 @@ import torch
 from .engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, SELF_COUNT_TRANSPOSE, DeviceCSR, GRFEngine, cols_band_width
 
 FUSED_DEFAULT = os.environ.get("GRF_GRAM_FUSED", "0") == "1"
+# column blocks with sparse buckets take the GRF_REC_SLOT transpose (GRF_REC_SLOTS=0: packed pairs, A/B)
+SLOTS_DEFAULT = os.environ.get("GRF_REC_SLOTS", "1") == "1"
 
 
 @dataclass
@@ -148,7 +150,9 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                          row_cap=pl.rows_cap) if pl.world > 1 else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
                                             local.val32)
-        tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap)
+        # (sparse buckets: the slot layout -- one line per small bucket in the Gram; not under the hub split)
+        tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap,
+                                  slots=SLOTS_DEFAULT and pl.hubs == 0 and tws is None)
         return Front(phi, tr, local, eng.phi_row_shifts(phi))
     return front_transpose(eng, pl, front_walk(eng, A_dev, pl, G))
 

@@ -36,7 +36,11 @@ enum grf_status {
 /* Record unit of the banded transpose (bytes per descriptor unit) */
 enum grf_rec_unit {
     GRF_REC_LINE = 128,  /* every bucket starts on a 128-byte line: dense buckets (C4)      */
-    GRF_REC_PACKED = 12  /* buckets packed pair after pair: sparse buckets (C5, N = 1M)     */
+    GRF_REC_PACKED = 12, /* buckets packed pair after pair: sparse buckets (C5, N = 1M)     */
+    GRF_REC_SLOT = 32    /* one 32-byte slot per bucket: {u32 pairs, u32 first overflow pair,
+                            the first two pairs inline}, the rest packed after all the slots:
+                            the Gram reads a small bucket with its header in ONE line
+                            (grf_transpose_banded_self and the 8-wave Gram tiles only)           */
 };
 
 /* Laplacian semantics */

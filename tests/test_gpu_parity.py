@@ -779,6 +779,48 @@ def test_column_block_gram_from_local_transpose(eng, world):
                            K[:, b:b + k])
 
 
+@pytest.mark.parametrize("graph", ["powerlaw", "er"])
+def test_slot_transpose_gram_bit_identical(eng, graph):
+    """The GRF_REC_SLOT transpose (each bucket's header and first two pairs in a 32-byte slot, the rest
+    in the overflow area) gives the Gram the same bits as the packed pairs it replaces: column blocks
+    with and without the symmetric square, a row sub-block, the whole symmetric K and the row mode, on
+    a hub-heavy power-law graph (buckets of hundreds of entries overflow, oversized regions place
+    through global memory) and an Erdos-Renyi one; ragged block sizes."""
+    import torch
+    from grf_amd import _lib as C
+    from grf_amd.graphs import powerlaw_graph
+    n = 30000
+    A = powerlaw_graph(n, 8.0, 2.2, seed=4) if graph == "powerlaw" else er_graph(n, 6, 21)
+    G = eng.laplacian(A)
+    m, L = 24, 6
+    f = [1.0, -0.5, 0.125, -0.02, 0.003, -0.0004]
+    phi = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=5), want64=False)
+    shift = eng.phi_row_shifts(phi)
+    for b, e in ((0, 8192), (1000, 6077), (n - 5003, n)):
+        loc = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=5, src_begin=b, src_end=e), want64=False)
+        bw = 8192 if e - b > 4096 else 4160
+        tp = eng.transpose_banded(loc, bw, rec_unit=C.REC_PACKED)
+        ts = eng.transpose_banded(loc, bw, rec_unit=C.REC_SLOT)  # (any bucket size: most overflow here)
+        assert torch.equal(ts.t_rowshift[:e - b], tp.t_rowshift[:e - b])
+        assert torch.equal(eng.gram_sparse_cols(phi, shift, ts), eng.gram_sparse_cols(phi, shift, tp)), (b, e)
+        assert torch.equal(eng.gram_sparse_cols(phi, shift, ts, sym_row0=b),
+                           eng.gram_sparse_cols(phi, shift, tp, sym_row0=b)), (b, e)
+        assert torch.equal(eng.gram_sparse_cols(phi, shift, ts, 77, 2345),
+                           eng.gram_sparse_cols(phi, shift, tp, 77, 2345)), (b, e)
+    # the whole K: slot transposes of all rows through the symmetric and the row-mode Gram
+    tp = eng.transpose_banded(phi, 8192, rec_unit=C.REC_PACKED)
+    ts = eng.transpose_banded(phi, 8192, rec_unit=C.REC_SLOT)
+    assert torch.equal(eng.gram_sparse_sym(phi, ts), eng.gram_sparse_sym(phi, tp))
+    assert torch.equal(eng.gram_sparse(phi, ts, 0, 3000), eng.gram_sparse(phi, tp, 0, 3000))
+    # (the packed path's K is pinned to the oracle by test_gram_sparse_vs_oracle / the C5 headline test)
+    # slots=True takes the slot layout where packed pairs would be chosen (sparse buckets, bands > 4096)
+    phs = eng.compact(eng.walk_phi(G, 4, 0.3, 3, f[:3], seed=5), want64=False)
+    t_auto = eng.transpose_banded(phs, 8192, slots=True)
+    assert t_auto.rec_unit == C.REC_SLOT
+    assert torch.equal(eng.gram_sparse(phs, t_auto, 0, 2000),
+                       eng.gram_sparse(phs, eng.transpose_banded(phs, 8192, rec_unit=C.REC_PACKED), 0, 2000))
+
+
 @pytest.mark.parametrize("unit", [128, 12])
 def test_transpose_wide_regions(eng, unit):
     """A graph large enough that the staged fill widens its column regions (n_rows * n_cols / (16 cr)
