@@ -525,6 +525,9 @@ def main():
                          "mirror; its transpose follows on the main stream after the mirror")
     ap.add_argument("--mirror-wgs", type=int, default=1024,
                     help="pipelined symmetric K: the mirror pass's workgroups beside the next front (0 = one per block)")
+    ap.add_argument("--k-buffers", type=int, choices=[1, 2], default=1,
+                    help="pipelined symmetric K: 2 = alternate two resident K buffers, the mirror of step s on a "
+                         "third stream beside step s+1's front and Gram tiles (+1 K of HBM)")
     ap.add_argument("--fused", dest="fused", action="store_true", default=None,
                     help="one GPU, whole K: the symmetric completion inside the Gram tiles (the last tile of every "
                          "32-row group writes the group's block transposed; no mirror pass)")
@@ -602,6 +605,10 @@ def main():
         del phi0
     b, e, kr_end = pl.b, pl.e, pl.kr_end
     K = P.alloc_k(eng, pl)  # resident output block, reused
+    Ks = [K]
+    mstream = None
+    mirror_done = [None, None]  # per K buffer: the event after its last mirror (the next tiles wait)
+    kbuf = [0]
     if args.overlap is None:
         # one GPU, whole K: the next front beside the mirror; N > 1 row / column blocks: the next
         # front's collectives beside this step's Gram (the compute of a front beside a Gram gains
@@ -613,9 +620,14 @@ def main():
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     walk_ev = []  # (start, end) events around walk_phi in the serial-latency steps (kernel alone)
     last = [None]
+    last_k = [None]
 
     side = torch.cuda.Stream(dev)  # the next step's front runs here while the Gram runs on `main`
     main = torch.cuda.current_stream(dev)
+
+    if args.k_buffers == 2 and pl.mode == "sym" and (args.overlap is not False):
+        Ks.append(P.alloc_k(eng, pl))
+        mstream = torch.cuda.Stream(dev)  # the mirror of step s, beside step s+1's front and tiles
 
     split_front = [False]  # (set while the timed / warm-up steps run with --front-split)
 
@@ -646,12 +658,22 @@ def main():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         # (pipelined: a 1024-workgroup mirror leaves CU slots to the next front)
-        P.k_assembly(eng, fr, pl, K, after_tiles=after_gram,
-                     mirror_workgroups=args.mirror_wgs if after_gram else 0, front_at=args.front_at)
+        paired = mstream is not None and after_gram is not None
+        i = kbuf[0] if paired else 0
+        if paired:
+            kbuf[0] ^= 1
+            if mirror_done[i] is not None:
+                main.wait_event(mirror_done[i])  # this K's previous mirror still reads its upper triangle
+        out = P.k_assembly(eng, fr, pl, Ks[i], after_tiles=after_gram,
+                           mirror_workgroups=args.mirror_wgs if after_gram else 0, front_at=args.front_at,
+                           mirror_stream=mstream if paired else None)
+        if paired:
+            mirror_done[i] = out
         if record:
-            ev[1].record()
+            ev[1].record(mstream if paired else main)
             gram_ev.append(ev)
         last[0] = fr
+        last_k[0] = Ks[i]
 
     def front_on_side(after=None, independent=False):
         # after: an event on `main`; default: everything issued on `main` so far.  independent: no
@@ -731,6 +753,8 @@ def main():
     ov = args.overlap
     args.overlap = False
     split_front[0] = False
+    if mstream is not None:
+        main.wait_stream(mstream)
     run(1, False)  # (warm-up of the serial order)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -742,7 +766,7 @@ def main():
         from grf_amd.dist import check_gather_overflow
         check_gather_overflow(dev)  # (raises if a bounded all-gather truncated a rank's Phi)
     # in-run parity of the last step's K block against the Phi that step gathered (every rank)
-    parity = P.k_block_check(eng, last[0], pl, K)
+    parity = P.k_block_check(eng, last[0], pl, last_k[0])
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
     walk_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in walk_ev]))
     coll_ms = float(np.mean([a.elapsed_time(b_) for a, b_, _, _ in gather_stats])) if gather_stats else 0.0
@@ -879,6 +903,7 @@ def main():
         "parity": parity,
         "pipelined": bool(ov),
         "front_split": bool(args.front_split and ov and pl.mode == "sym"),
+        "k_buffers": len(Ks),
         "serial_ms_per_step": serial_ms,
     }
     if dist_info is not None:

@@ -189,10 +189,13 @@ def front_transpose(eng: GRFEngine, pl: StepPlan, fr: Front) -> Front:
 
 def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
                after_tiles: Optional[Callable[[torch.cuda.Event], None]] = None, mirror_workgroups: int = 0,
-               front_at: float = 1.0) -> torch.Tensor:
+               front_at: float = 1.0, mirror_stream: Optional[torch.cuda.Stream] = None):
     """The K assembly of one step from its front.  Symmetric mode: ``after_tiles(event)`` is called
     between the Gram tiles and the mirror (the pipelined bench issues the next front there, beside
-    the HBM-bound mirror; ``mirror_workgroups`` then bounds the mirror's grid, 1024 measured best)."""
+    the HBM-bound mirror; ``mirror_workgroups`` then bounds the mirror's grid, 1024 measured best).
+    mirror_stream (symmetric mode): the mirror runs there after the tiles, so that the caller's stream
+    can start the next step's Gram tiles -- into another K buffer -- before it ends; returns the event
+    recorded after the mirror (the caller orders the next write of this K after it) instead of K."""
     from .dist import allreduce_buckets
 
     if pl.mode == "cols" and pl.hubs > 0:
@@ -238,6 +241,18 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
             if after_tiles is not None:
                 tiles_done = torch.cuda.Event()
                 tiles_done.record(main)
+        if mirror_stream is not None:
+            if tiles_done is None:
+                tiles_done = torch.cuda.Event()
+                tiles_done.record(main)
+            mirror_stream.wait_event(tiles_done)
+            with torch.cuda.stream(mirror_stream):
+                eng.gram_mirror(K, pl.n, mirror_workgroups)
+                mirror_done = torch.cuda.Event()
+                mirror_done.record(mirror_stream)
+            if after_tiles is not None:
+                after_tiles(tiles_done)
+            return mirror_done
         eng.gram_mirror(K, pl.n, mirror_workgroups)
         if after_tiles is not None:
             after_tiles(tiles_done)  # (issued after the mirror: the host's launch time does not delay it)
