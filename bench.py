@@ -574,7 +574,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # GRF_DIST_FORCE=1 (under torch.distributed.run, one rank): the N > 1 path with its RCCL collectives
+    # on a one-GPU box (the all-gather of one shard, the timing / parity all-reduces)
+    coll = world > 1 or os.environ.get("GRF_DIST_FORCE", "0") == "1"
+    if coll:
         local_rank = init_distributed(local_rank)
     eng = GRFEngine(f"cuda:{local_rank}")
     dev = eng.device
@@ -584,16 +587,17 @@ def main():
     A_dev = DeviceCSR.from_scipy(A, dev)
     shards = None
     phi0 = None
-    if world > 1:
+    if coll:
         from grf_amd.dist import balanced_shards, setup_phi
         phi0 = setup_phi(eng, A_dev, m, p, L, f, seed=42)  # (setup, untimed: the Phi every step makes)
         if args.balance != "nodes":
             shards = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance, phi=phi0)
     pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
-                     band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused)
+                     band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused,
+                     collective=coll)
     if args.hubs and pl.mode == "sym" and not pl.fused:
         pl.hubs = int(args.hubs) if args.hubs > 0 else auto_hubs(eng, A_dev, m, p, L, f)
-    elif args.hubs > 0 and pl.mode == "cols" and world == 1:
+    elif args.hubs > 0 and pl.mode == "cols" and not coll:
         # the column block's hub-column split (C5 A/B: profiles/r03_c5_hubs_ab.txt); explicit counts only
         pl.hubs = int(args.hubs)
     if phi0 is not None:
@@ -615,7 +619,7 @@ def main():
         # ~1 %: single-GPU row modes stay serial)
         # K-row-block workloads (C5) on one GPU: the next front beside this step's column-block Gram
         # (22.3 vs 22.9 ms per step, profiles/r02_c5_overlap.txt)
-        args.overlap = pl.mode == "sym" or (world > 1 and pl.mode != "allreduce") or \
+        args.overlap = pl.mode == "sym" or (coll and pl.mode != "allreduce") or \
             (pl.mode == "cols" and bool(args.k_rows))
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     walk_ev = []  # (start, end) events around walk_phi in the serial-latency steps (kernel alone)
@@ -737,13 +741,13 @@ def main():
     split_front[0] = bool(args.front_split and args.overlap and pl.mode == "sym")
     run(args.warmup, False)
     torch.cuda.synchronize()
-    if world > 1:
+    if coll:
         dist.barrier()
         D.GATHER_STATS = []  # HIP events around every Phi all-gather of the timed steps
     t0 = time.perf_counter()
     run(args.steps, True)
     torch.cuda.synchronize()
-    if world > 1:
+    if coll:
         dist.barrier()
     t = time.perf_counter() - t0
     gather_stats = D.GATHER_STATS or []
@@ -762,7 +766,7 @@ def main():
     torch.cuda.synchronize()
     serial_ms = 1000.0 * (time.perf_counter() - t1) / 3
     args.overlap = ov
-    if world > 1:
+    if coll:
         from grf_amd.dist import check_gather_overflow
         check_gather_overflow(dev)  # (raises if a bounded all-gather truncated a rank's Phi)
     # in-run parity of the last step's K block against the Phi that step gathered (every rank)
@@ -772,7 +776,7 @@ def main():
     coll_ms = float(np.mean([a.elapsed_time(b_) for a, b_, _, _ in gather_stats])) if gather_stats else 0.0
     coll_sent = float(np.mean([x for _, _, x, _ in gather_stats])) if gather_stats else 0.0
     coll_recv = float(np.mean([x for _, _, _, x in gather_stats])) if gather_stats else 0.0
-    if world > 1:
+    if coll:
         tt = torch.tensor([t, float(np.mean(gram_ms)), walk_ms], dtype=torch.float64, device=dev)
         dist_all_reduce(tt, op=dist.ReduceOp.MAX)
         t, gram_avg, walk_ms = (float(x) for x in tt.tolist())
@@ -859,7 +863,7 @@ def main():
                                   if args.k_rows else "")
                                + " resident in HBM",
                    "n_nodes": n, "n_edges": int(A.nnz // 2), "walks_per_node": m, "max_walk_length": L,
-                   "k_rows_per_gpu": rows, "shard": [b, e], "balance": args.balance if world > 1 else None,
+                   "k_rows_per_gpu": rows, "shard": [b, e], "balance": args.balance if coll else None,
                    "gather_entries_per_rank": pl.gather_bound or None,
                    "hub_columns": pl.hubs or None,
                    "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
@@ -930,7 +934,7 @@ def main():
             out["cpu_baseline"] = {"error": f"{type(exc).__name__}: {exc}"}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
 
 

@@ -313,7 +313,7 @@ def allgather_csr_rows(ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, 
 
 
 def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards=None, entries_bound=None,
-               row_cap=None):
+               row_cap=None, always=False):
     """All ranks' Phi rows (CSR, float32) from this rank's compacted rows ``local``.
 
     shards: every rank's (begin, end) source range.  When given and ``local`` came from a
@@ -329,14 +329,17 @@ def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards
     buckets for its own rows (global band ids, bands of ``band_width``).  The per-rank counts are
     summed in place with one all-reduce (n_bands * n int32, 5-10 MB at N = 100k), so the caller's
     ``transpose_banded(..., counted_ws=count_ws)`` skips the counting pass over the gathered Phi --
-    the same workspace a single GPU's fused count leaves."""
+    the same workspace a single GPU's fused count leaves.
+
+    always: gather even with one rank (the pipeline's planned collective step: one rank rehearses the
+    RCCL all-gather); otherwise one rank returns ``local`` as it is."""
     from .engine import DEFAULT_BAND_WIDTH, DeviceCSR
 
     n = local.n_cols
     if count_ws is not None and dist.get_world_size(group) > 1:
         nbk = -(-n // (band_width or DEFAULT_BAND_WIDTH)) * n
         all_reduce(count_ws[:4 * nbk].view(torch.int32), group=group)
-    if dist.get_world_size(group) == 1:
+    if dist.get_world_size(group) == 1 and not always:
         return local
     bound = getattr(local, "nnz_bound", None)
     if shards is not None and (bound is not None or row_cap is not None) and (row_cap or entries_bound
@@ -357,9 +360,8 @@ def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards
 def allreduce_buckets(t: torch.Tensor, bucket_bytes: int = 1 << 30, group=None) -> torch.Tensor:
     """In-place sum of a (possibly row-padded, row-strided) 2-D tensor over the ranks, one
     contiguous row bucket of at most ``bucket_bytes`` per collective (bounds RCCL's staging)."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if world == 1:
-        return t
+    if not dist.is_initialized():
+        return t  # (one rank in an initialised group still runs the collectives: the RCCL rehearsal)
     rows_per = max(1, bucket_bytes // max(1, t.stride(0) * t.element_size()))
     base = t.as_strided((t.shape[0], t.stride(0)), (t.stride(0), 1)) if t.dim() == 2 else t.view(-1, 1)
     for r0 in range(0, base.shape[0], rows_per):

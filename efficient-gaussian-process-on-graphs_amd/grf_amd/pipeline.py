@@ -52,6 +52,7 @@ class StepPlan:
     fused: bool = False            # "sym": symmetric completion fused into the Gram tiles (no mirror pass)
     hubs: int = 0                  # "sym" / "cols": Phi's densest columns as a dense panel (hub-column split)
     group: object = None           # torch.distributed group (N > 1)
+    collective: bool = False       # the Phi all-gather runs (N > 1; or one rank, to rehearse RCCL on one GPU)
     gather_bound: int = 0          # N > 1: per-rank Phi entries moved by the all-gather (0: rows x rows_cap;
     #                                dist.shard_entries of the setup walk: exact, checked by check_gather_overflow)
     extra: dict = field(default_factory=dict)
@@ -81,12 +82,15 @@ class StepPlan:
 
 def plan_step(n: int, m: int, L: int, p_halt: float, f, *, seed: int = 42, world: int = 1, rank: int = 0,
               mode: str = "cols", k_rows: int = 0, band_width: int = 0, no_sym: bool = False,
-              shards: Optional[List[Tuple[int, int]]] = None, group=None, fused: Optional[bool] = None) -> StepPlan:
+              shards: Optional[List[Tuple[int, int]]] = None, group=None, fused: Optional[bool] = None,
+              collective: Optional[bool] = None) -> StepPlan:
     """The bench's mode rules: one GPU whole K -> symmetric mode; N > 1 or K-row workloads -> column
     blocks (``mode="cols"``), row blocks (``"rows"``) or the all-reduce option (``"allreduce"``).
     shards: every rank's source range (default: equal node counts; dist.balanced_shards for equal
     estimated work).  fused: the symmetric mode's completion inside the Gram tiles (default: env
-    GRF_GRAM_FUSED, off)."""
+    GRF_GRAM_FUSED, off).  collective (default: world > 1): plan the multi-GPU step -- column / row
+    blocks after a Phi all-gather -- even for one rank (bench.py's GRF_DIST_FORCE=1 runs RCCL's
+    collectives on a one-GPU box through exactly the N > 1 code)."""
     from .dist import shard_range
 
     if mode not in ("cols", "rows", "allreduce"):
@@ -100,13 +104,14 @@ def plan_step(n: int, m: int, L: int, p_halt: float, f, *, seed: int = 42, world
     b, e = shards[rank]
     pl = StepPlan(n, int(m), int(L), float(p_halt), np.asarray(f, np.float64), int(seed), world, rank, (b, e),
                   shards, int(k_rows), mode, group=group)
-    if mode == "cols" and (world > 1 or k_rows):
+    pl.collective = world > 1 if collective is None else bool(collective)
+    if mode == "cols" and (pl.collective or k_rows):
         pl.mode = "cols"
         pl.band_width = band_width or cols_band_width(pl.block_rows)
         pl.cols_sym = not no_sym and 4 * pl.block_rows >= n
     elif mode == "allreduce":
         pl.band_width = band_width or ROWS_BAND_WIDTH
-    elif world == 1 and not no_sym and not k_rows:
+    elif not pl.collective and not no_sym and not k_rows:
         pl.mode = "sym"
         pl.band_width = band_width or DEFAULT_BAND_WIDTH
         pl.fused = FUSED_DEFAULT if fused is None else bool(fused)
@@ -147,7 +152,7 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                                          want64=False),
                             want64=False, want32=True, sync_free=True)
         phi = gather_phi(eng, local, group=pl.group, shards=pl.shards, entries_bound=pl.gather_bound or None,
-                         row_cap=pl.rows_cap) if pl.world > 1 else local
+                         row_cap=pl.rows_cap, always=True) if pl.collective else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
                                             local.val32)
         # (sparse buckets: the slot layout -- one line per small bucket in the Gram; not under the hub split)
@@ -172,7 +177,7 @@ def front_walk(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan, G: Optional[Devic
                                      want64=False),
                         want64=False, want32=True, sync_free=True)
     phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards,
-                     entries_bound=pl.gather_bound or None, row_cap=pl.rows_cap) if pl.world > 1 else local
+                     entries_bound=pl.gather_bound or None, row_cap=pl.rows_cap, always=True) if pl.collective else local
     fr = Front(phi, None, local)
     fr.tws = tws
     return fr

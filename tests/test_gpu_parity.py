@@ -1131,6 +1131,39 @@ def test_bench_line_n2_reports_parity_and_collectives_gloo(mode):
     assert line["parity"]["ok"] and line["parity"]["max_ratio"] <= 1.0 and len(line["parity"]["per_rank"]) == 2
 
 
+@pytest.mark.parametrize("mode", ["cols", "rows", "allreduce"])
+def test_bench_multi_gpu_path_on_rccl_one_rank(mode):
+    """The N > 1 bench step on RCCL itself (backend "nccl"), one rank on the one-GPU box
+    (GRF_DIST_FORCE=1): the Phi all-gather, the timing / parity all-reduces and the all-reduce mode's
+    bucketed K sums run through RCCL with exactly the code the driver's 8-GPU run takes; the in-run
+    K block check passes.  (Several ranks on one GPU need gloo: the test above.)"""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, GRF_DIST_FORCE="1")
+    env.pop("GRF_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--n-nodes", "20000",
+           "--edges", "200000", "--mode", mode]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    d = line["distributed"]
+    assert d["backend"] == "nccl" and d["world_size"] == 1
+    assert d["rank_rows"] == [20000] and d["gram_ms_per_rank"][0] > 0
+    if mode != "allreduce":
+        assert d["gather_bytes_sent_per_rank"][0] > 0 and d["gather_ms_per_rank"][0] > 0
+    assert line["parity"]["ok"] and line["parity"]["max_ratio"] <= 1.0
+
+
 @pytest.mark.parametrize("hubs", [32, 64])
 def test_column_block_hub_split(eng, hubs):
     """The column block's hub-column split (engine.gram_sparse_cols_hubs: the block's densest columns in
