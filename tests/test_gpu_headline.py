@@ -276,3 +276,22 @@ def test_dense_path_bench_pipelined_line():
         assert d["unit"] == "K-matrices/s" and d["value"] > 0 and d["ms_per_step"] > 0 and d["serial_ms_per_step"] > 0
         rf = d["roofline"]
         assert rf["bound"] == "mfma" and 0 < rf["frac"] < 1 and rf["kernel_ms"] > 0 and rf["kernel_ms_pipelined"] > 0
+
+
+def test_sym_bench_two_k_buffers_line():
+    """bench.py's symmetric step with two resident K buffers (--k-buffers 2: step s's mirror on a third
+    stream beside step s+1's front and Gram tiles, measured slower and kept opt-in): the in-run check of
+    the last K written passes, on a 20k-node graph, as with one buffer."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for kb in ("1", "2"):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--n-nodes", "20000", "--edges", "200000",
+                            "--steps", "4", "--warmup", "1", "--no-cpu-baseline", "--no-mfma-leg", "--k-buffers", kb],
+                           cwd=root, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+        assert d["k_buffers"] == int(kb) and d["pipelined"] is True
+        assert d["parity"]["ok"] and d["parity"]["max_ratio"] <= 1.0
