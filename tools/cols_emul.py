@@ -2,7 +2,7 @@
 Phi is precomputed): the row-block mode (replicated transpose of all of Phi, K[b:e, :]) against the
 column-block mode (transpose of the rank's own rows, K[:, b:e]).  Prints one JSON line per world size.
 
-usage: python tools/cols_emul.py [worlds=2,4,8] [reps=3]"""
+usage: python tools/cols_emul.py [worlds=2,4,8] [reps=3]   (COLS_MAX_BAND=4096: local bands of at most 4096)"""
 import json
 import os
 import sys
@@ -56,7 +56,7 @@ for world in worlds:
             tr = eng.transpose_banded(phi, bw, counted_ws=ws, nnz_bound=n * m * L)
             return eng.gram_sparse(phi, tr, b, e, out=K)
 
-        wl = cols_band_width(e - b)
+        wl = cols_band_width(e - b, int(os.environ.get("COLS_MAX_BAND", ROWS_BAND_WIDTH)))
         Kc = torch.empty((n, eng.leading_dim(e - b)), dtype=torch.float32, device=eng.device)
         ws_l = eng.transpose_workspace(e - b, n, wl)
 
