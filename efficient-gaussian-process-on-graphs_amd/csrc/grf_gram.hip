@@ -374,7 +374,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
     const unsigned char *__restrict__ t_rec, int32_t unit, const int32_t *__restrict__ rowshift,
     float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets, const uint16_t *__restrict__ t_split,
-    int64_t ovf_base) {
+    int64_t ovf_base, int32_t balance) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     static_assert(!kSlot || kHalves == 1, "slot streams: 2 virtual buckets per nonzero, u8 ids <= 128");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -416,13 +416,21 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
                         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char *>(brec), (short)0, 0x7fffffff,
                                                           0x00020000),
                         reinterpret_cast<unsigned char *>(acc), ldexp(1.0, sh), kSlot ? 8 : 0};
-    for (int64_t g0 = e0 + (int64_t)wave * kB; g0 < e1; g0 += kB * kWaves) {
+    // the row's nonzeros over the waves: balance = 1: wave w takes the w-th of kWaves equal contiguous
+    // shares, in batches of kB (a tile ends with its slowest wave: C4's ~435 nonzeros as 109 per wave
+    // instead of 128 / 128 / 128 / 51); 0: batches w, w + kWaves, ... of kB
+    const int64_t nnz_row = e1 - e0, share = (nnz_row + kWaves - 1) / kWaves;
+    const int64_t ws0 = balance ? e0 + (wave * share < nnz_row ? wave * share : nnz_row) : e0 + (int64_t)wave * kB;
+    const int64_t ws1 = balance ? e0 + ((wave + 1) * share < nnz_row ? (wave + 1) * share : nnz_row) : e1;
+    const int64_t gstep = balance ? kB : (int64_t)kB * kWaves;
+    for (int64_t g0 = ws0; g0 < ws1; g0 += gstep) {
+        const int64_t gend = balance ? ((g0 + kB) < ws1 ? g0 + kB : ws1) : e1;
         int32_t cnt[kV], excl[kV], t0[kV];
         float av[kV];
 #pragma unroll
         for (int h = 0; h < kHalves; ++h) {
             const int64_t e = g0 + h * 64 + lane;
-            int32_t k = e < e1 ? idx[e] : -1;
+            int32_t k = e < gend ? idx[e] : -1;
             if (k < tl.k_begin || k >= tl.k_end) k = -1;  // (k-slice mode)
             const float a = k >= 0 ? val[e] : 0.f;
             if constexpr (kSlot) {
@@ -969,6 +977,15 @@ extern "C" {
 size_t grf_gram_workspace_bytes(void) { return 256; }
 
 // tiles [t_first, t_last) of one Gram call
+// GRF_GRAM_BALANCE=0: the row's nonzeros in round-robin batches over the tile's waves (A/B knob)
+static int32_t gram_balance() {
+    static const int32_t b = [] {
+        const char *e = getenv("GRF_GRAM_BALANCE");
+        return e ? (int32_t)(atoi(e) != 0) : (int32_t)1;
+    }();
+    return b;
+}
+
 static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramTiles &tl, int64_t t_first,
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
                                  const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
@@ -987,7 +1004,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
             gram_sparse_kernel<8, 1, 8, true, false, true><<<(unsigned)nt, 512, lds, st>>>(
                 n_total, row_begin, tl, t0, ptr, idx, val, reinterpret_cast<const uint2 *>(t_desc),
                 reinterpret_cast<const unsigned char *>(t_rec), unit, t_rowshift, K, ldk, nullptr, nullptr,
-                32 * slot_buckets);
+                32 * slot_buckets, gram_balance());
             GRF_CHECK_LAUNCH("gram_sparse_kernel");
         }
         return GRF_OK;
@@ -1022,7 +1039,8 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
     gram_sparse_kernel<WV, H, U, T, F><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx,   \
                                                                         val, reinterpret_cast<const uint2 *>(t_desc), \
                                                                         reinterpret_cast<const unsigned char *>(t_rec), \
-                                                                        unit, t_rowshift, K, ldk, tickets, split, 0)
+                                                                        unit, t_rowshift, K, ldk, tickets, split, 0, \
+                                                                        gram_balance())
 #define GRF_GRAM_LAUNCH_T(WV, H, U, T) GRF_GRAM_LAUNCH_F(WV, H, U, T, false)
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     do {                                                                                                          \
