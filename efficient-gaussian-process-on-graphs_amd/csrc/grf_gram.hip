@@ -977,13 +977,18 @@ extern "C" {
 size_t grf_gram_workspace_bytes(void) { return 256; }
 
 // tiles [t_first, t_last) of one Gram call
-// GRF_GRAM_BALANCE=0: the row's nonzeros in round-robin batches over the tile's waves (A/B knob)
-static int32_t gram_balance() {
-    static const int32_t b = [] {
+// Equal contiguous shares of a row's nonzeros per wave (1) or round-robin batches (0): measured
+// (profiles/r03_gram_balance_ab.txt) C5's slot tiles 19.2 -> 18.4 ms per step, Enron 9.4 -> 8.7 ms,
+// C4's whole-K tiles -0.5 %; the N > 1 column blocks of line buckets (8-wave tiles, ~435 nonzeros:
+// round-robin keeps 7 waves of 64) +2..5 %, so those keep round-robin batches.
+// GRF_GRAM_BALANCE=0 / 1 forces either (A/B knob).
+static int32_t gram_balance(const GramTiles &tl, int32_t unit) {
+    static const int32_t force = [] {
         const char *e = getenv("GRF_GRAM_BALANCE");
-        return e ? (int32_t)(atoi(e) != 0) : (int32_t)1;
+        return e ? (int32_t)(atoi(e) != 0) : (int32_t)-1;
     }();
-    return b;
+    if (force >= 0) return force;
+    return (unit == GRF_REC_SLOT || tl.t_rows < 0) ? 1 : 0;
 }
 
 static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramTiles &tl, int64_t t_first,
@@ -1004,7 +1009,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
             gram_sparse_kernel<8, 1, 8, true, false, true><<<(unsigned)nt, 512, lds, st>>>(
                 n_total, row_begin, tl, t0, ptr, idx, val, reinterpret_cast<const uint2 *>(t_desc),
                 reinterpret_cast<const unsigned char *>(t_rec), unit, t_rowshift, K, ldk, nullptr, nullptr,
-                32 * slot_buckets, gram_balance());
+                32 * slot_buckets, gram_balance(tl, unit));
             GRF_CHECK_LAUNCH("gram_sparse_kernel");
         }
         return GRF_OK;
@@ -1040,7 +1045,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
                                                                         val, reinterpret_cast<const uint2 *>(t_desc), \
                                                                         reinterpret_cast<const unsigned char *>(t_rec), \
                                                                         unit, t_rowshift, K, ldk, tickets, split, 0, \
-                                                                        gram_balance())
+                                                                        gram_balance(tl, unit))
 #define GRF_GRAM_LAUNCH_T(WV, H, U, T) GRF_GRAM_LAUNCH_F(WV, H, U, T, false)
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     do {                                                                                                          \
