@@ -74,13 +74,15 @@ VALU_PEAK_PER_SIMD_CYCLE = 0.5
 N_SIMDS = 256 * 4
 
 
-def auto_hubs(eng, A_dev, m, p, L, f, share: float = 0.13) -> int:
-    """Hub columns worth a dense panel (setup, untimed): a column in c of the n rows saves ~c^2 / 2 gathered
-    records and costs n^2 / 2 MFMA multiply-adds, ~60x cheaper each, so it pays from c / n ~ 1 / sqrt(60) = 0.13
-    (measured: Enron's best split is 128 columns, whose c reaches 13 % of n; Facebook's 64th column is in 9 % of
-    the rows and the split loses there, profiles/r02_hubs_sweep.txt).  Multiples of 32 (the panel's width)."""
+def auto_hubs(eng, A_dev, m, p, L, f, share: float = 0.13):
+    """(hub columns worth a dense panel, skewed) from one setup walk (untimed): a column in c of the n rows
+    saves ~c^2 / 2 gathered records and costs n^2 / 2 MFMA multiply-adds, ~60x cheaper each, so it pays from
+    c / n ~ 1 / sqrt(60) = 0.13 (measured: Enron's best split is 128 columns, whose c reaches 13 % of n;
+    Facebook's 64th column is in 9 % of the rows and the split loses there, profiles/r02_hubs_sweep.txt).
+    Multiples of 32 (the panel's width).  skewed: the Gram's waves take pair-balanced shares
+    (engine.row_cuts)."""
     from grf_amd.dist import setup_phi
-    return eng.hub_count(setup_phi(eng, A_dev, m, p, L, f, seed=42), share)
+    return eng.column_stats(setup_phi(eng, A_dev, m, p, L, f, seed=42), share)
 
 
 def init_distributed(local_rank: int) -> int:
@@ -570,6 +572,7 @@ def main():
     from grf_amd import pipeline as P
     from grf_amd.dist import all_reduce as dist_all_reduce
     from grf_amd.engine import DeviceCSR, GRFEngine
+    import grf_amd.engine as engine_mod
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -595,8 +598,9 @@ def main():
     pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
                      band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused,
                      collective=coll)
-    if args.hubs and pl.mode == "sym" and not pl.fused:
-        pl.hubs = int(args.hubs) if args.hubs > 0 else auto_hubs(eng, A_dev, m, p, L, f)
+    if pl.mode == "sym" and not pl.fused:
+        hubs_auto, pl.skewed = auto_hubs(eng, A_dev, m, p, L, f)
+        pl.hubs = int(args.hubs) if args.hubs > 0 else (hubs_auto if args.hubs < 0 else 0)
     elif args.hubs > 0 and pl.mode == "cols" and not coll:
         # the column block's hub-column split (C5 A/B: profiles/r03_c5_hubs_ab.txt); explicit counts only
         pl.hubs = int(args.hubs)
@@ -866,6 +870,8 @@ def main():
                    "k_rows_per_gpu": rows, "shard": [b, e], "balance": args.balance if coll else None,
                    "gather_entries_per_rank": pl.gather_bound or None,
                    "hub_columns": pl.hubs or None,
+                   "pair_balanced_waves": (pl.mode == "sym" and not pl.fused) and
+                   (engine_mod.ROW_CUTS == "1" or (engine_mod.ROW_CUTS == "auto" and bool(pl.skewed))),
                    "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
                                    f"RCCL all-reduce (K replicated)") if pl.mode == "allreduce" else
                                   (f"source-sharded x{world}, Phi all-gather, K column blocks K[:, R_r] from each "

@@ -374,7 +374,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
     const unsigned char *__restrict__ t_rec, int32_t unit, const int32_t *__restrict__ rowshift,
     float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets, const uint16_t *__restrict__ t_split,
-    int64_t ovf_base, int32_t balance) {
+    int64_t ovf_base, int32_t balance, const int32_t *__restrict__ row_cuts) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     static_assert(!kSlot || kHalves == 1, "slot streams: 2 virtual buckets per nonzero, u8 ids <= 128");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -420,11 +420,19 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     // shares, in batches of kB (a tile ends with its slowest wave: C4's ~435 nonzeros as 109 per wave
     // instead of 128 / 128 / 128 / 51); 0: batches w, w + kWaves, ... of kB
     const int64_t nnz_row = e1 - e0, share = (nnz_row + kWaves - 1) / kWaves;
-    const int64_t ws0 = balance ? e0 + (wave * share < nnz_row ? wave * share : nnz_row) : e0 + (int64_t)wave * kB;
-    const int64_t ws1 = balance ? e0 + ((wave + 1) * share < nnz_row ? (wave + 1) * share : nnz_row) : e1;
-    const int64_t gstep = balance ? kB : (int64_t)kB * kWaves;
+    int64_t ws0 = balance ? e0 + (wave * share < nnz_row ? wave * share : nnz_row) : e0 + (int64_t)wave * kB;
+    int64_t ws1 = balance ? e0 + ((wave + 1) * share < nnz_row ? (wave + 1) * share : nnz_row) : e1;
+    if (row_cuts) {
+        // shares of about equal record pairs (grf_gram_row_cuts: 8 cuts per row from the columns'
+        // pair counts over all bands; a kWaves-wave tile takes every (8 / kWaves)-th)
+        static_assert(8 % kWaves == 0, "row cuts: 8 shares per row");
+        constexpr int kStep = 8 / kWaves;
+        ws0 = e0 + row_cuts[row * 8 + wave * kStep];
+        ws1 = wave + 1 < kWaves ? e0 + row_cuts[row * 8 + (wave + 1) * kStep] : e1;
+    }
+    const int64_t gstep = (balance || row_cuts) ? kB : (int64_t)kB * kWaves;
     for (int64_t g0 = ws0; g0 < ws1; g0 += gstep) {
-        const int64_t gend = balance ? ((g0 + kB) < ws1 ? g0 + kB : ws1) : e1;
+        const int64_t gend = (balance || row_cuts) ? ((g0 + kB) < ws1 ? g0 + kB : ws1) : e1;
         int32_t cnt[kV], excl[kV], t0[kV];
         float av[kV];
 #pragma unroll
@@ -995,7 +1003,8 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
                                  const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
                                  float *K, int64_t ldk, hipStream_t st, int32_t *tickets = nullptr,
-                                 const void *t_split = nullptr, int64_t slot_buckets = 0) {
+                                 const void *t_split = nullptr, int64_t slot_buckets = 0,
+                                 const int32_t *row_cuts = nullptr) {
     if (unit == GRF_REC_SLOT) {
         // the slot layout: 8-wave tiles (one batch of 64 nonzeros per wave: two stream buckets each),
         // the default unroll and exact tails; the overflow pairs follow the slot_buckets slots
@@ -1009,7 +1018,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
             gram_sparse_kernel<8, 1, 8, true, false, true><<<(unsigned)nt, 512, lds, st>>>(
                 n_total, row_begin, tl, t0, ptr, idx, val, reinterpret_cast<const uint2 *>(t_desc),
                 reinterpret_cast<const unsigned char *>(t_rec), unit, t_rowshift, K, ldk, nullptr, nullptr,
-                32 * slot_buckets, gram_balance(tl, unit));
+                32 * slot_buckets, gram_balance(tl, unit), nullptr);
             GRF_CHECK_LAUNCH("gram_sparse_kernel");
         }
         return GRF_OK;
@@ -1045,7 +1054,7 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
                                                                         val, reinterpret_cast<const uint2 *>(t_desc), \
                                                                         reinterpret_cast<const unsigned char *>(t_rec), \
                                                                         unit, t_rowshift, K, ldk, tickets, split, 0, \
-                                                                        gram_balance(tl, unit))
+                                                                        gram_balance(tl, unit), row_cuts)
 #define GRF_GRAM_LAUNCH_T(WV, H, U, T) GRF_GRAM_LAUNCH_F(WV, H, U, T, false)
 #define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
     do {                                                                                                          \
@@ -1127,7 +1136,8 @@ int32_t grf_gram_sparse_sym(int64_t n_total, const int64_t *ptr, const int32_t *
 static int32_t gram_sparse_upper_impl(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
                                       int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
                                       const void *t_split, const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
-                                      int32_t part_end, int32_t n_parts, bool add_k, grf_stream_t stream) {
+                                      int32_t part_end, int32_t n_parts, bool add_k, grf_stream_t stream,
+                                      const int32_t *row_cuts = nullptr) {
     int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
     if (rc != GRF_OK) return rc;
     GRF_REQUIRE(n_parts >= 1 && 0 <= part_begin && part_begin <= part_end && part_end <= n_parts, GRF_EINVAL,
@@ -1138,8 +1148,83 @@ static int32_t gram_sparse_upper_impl(int64_t n_total, const int64_t *ptr, const
     const int64_t total = tl.total();
     const int64_t t0 = total * part_begin / n_parts, t1 = total * part_end / n_parts;
     if (t1 <= t0) return GRF_OK;
+    GRF_REQUIRE(!row_cuts || rec_unit != GRF_REC_SLOT, GRF_EUNSUPPORTED, "grf_gram_sparse_upper: row cuts with slot buckets");
     return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
-                             S(stream), nullptr, t_split, tl.nb * n_total);
+                             S(stream), nullptr, t_split, tl.nb * n_total, row_cuts);
+}
+
+int32_t grf_gram_sparse_upper_ex(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                                 int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                                 const void *t_split, const int32_t *t_rowshift, const int32_t *row_cuts, float *K,
+                                 int64_t ldk, int32_t part_begin, int32_t part_end, int32_t n_parts, int32_t add_k,
+                                 grf_stream_t stream) {
+    return gram_sparse_upper_impl(n_total, ptr, idx, val, band_width, rec_unit, t_desc, t_rec, t_split, t_rowshift,
+                                  K, ldk, part_begin, part_end, n_parts, add_k != 0, stream, row_cuts);
+}
+
+// ---------------------------------------------------------------- wave shares by record pairs
+// col_w[k] = the record pairs of column k over all bands of the transpose (after any hub drop)
+__global__ __launch_bounds__(256) void col_pairs_kernel(int64_t n_bands, int64_t n_cols, const uint2 *__restrict__ t_desc,
+                                                        int32_t *__restrict__ col_w) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n_cols) return;
+    int64_t s = 0;
+    for (int64_t J = 0; J < n_bands; ++J) s += t_desc[J * n_cols + k].y;
+    col_w[k] = (int32_t)(s < 0x7fffffff ? s : 0x7fffffff);
+}
+
+// One wave per row: cuts[8 row + s] = the first nonzero (offset in the row) whose exclusive prefix of
+// column weights reaches s / 8 of the row's total (s = 1..7; s = 0 -> 0; none -> the row's length),
+// i.e. 8 contiguous shares of about equal weight; weights from col_w (int64 sums)
+__global__ __launch_bounds__(256) void row_cuts_kernel(int64_t n_rows, const int64_t *__restrict__ ptr,
+                                                       const int32_t *__restrict__ idx, const int32_t *__restrict__ col_w,
+                                                       int32_t *__restrict__ cuts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n_rows) return;
+    const int64_t e0 = ptr[row], e1 = ptr[row + 1], nnz = e1 - e0;
+    long long tot = 0;
+    for (int64_t e = e0 + lane; e < e1; e += 64) tot += col_w[idx[e]];
+    tot = wave_sum<long long>(tot);
+    int32_t out = (int32_t)nnz;  // lane s (1..7) holds cut s
+    long long run = 0;
+    unsigned found = 1u;  // bit s: cut s set (cut 0 = 0)
+    for (int64_t c = e0; c < e1 && found != 0xffu; c += 64) {
+        const int64_t e = c + lane;
+        const long long w = e < e1 ? (long long)col_w[idx[e]] : 0;
+        const long long inc = wave_inclusive_scan<long long>(w) + run;
+        const long long excl = inc - w;
+#pragma unroll
+        for (int sh = 1; sh < 8; ++sh) {
+            if (found & (1u << sh)) continue;
+            const unsigned long long m = __ballot(e < e1 && excl * 8 >= (long long)sh * tot);
+            if (m) {
+                found |= 1u << sh;
+                if (lane == sh) out = (int32_t)(c - e0 + __builtin_ctzll(m));
+            }
+        }
+        run = __shfl(inc, 63, 64);
+    }
+    if (lane == 0) out = 0;
+    if (lane < 8) cuts[row * 8 + lane] = out;
+}
+
+int32_t grf_gram_row_cuts(int64_t n_rows, const int64_t *ptr, const int32_t *idx, int64_t n_bands, int64_t n_cols,
+                          const uint32_t *t_desc, int32_t *col_w, int32_t *row_cuts, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && n_bands >= 0 && n_cols >= 0 &&
+                    (n_rows == 0 || (ptr && idx && t_desc && col_w && row_cuts)),
+                GRF_EINVAL, "grf_gram_row_cuts: bad arguments");
+    if (n_rows == 0) return GRF_OK;
+    if (n_cols > 0) {
+        GRF_REQUIRE_GRID(cdiv<int64_t>(n_cols, 256), 256, "col_pairs_kernel");
+        col_pairs_kernel<<<(unsigned)cdiv<int64_t>(n_cols, 256), 256, 0, S(stream)>>>(
+            n_bands, n_cols, reinterpret_cast<const uint2 *>(t_desc), col_w);
+        GRF_CHECK_LAUNCH("col_pairs_kernel");
+    }
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "row_cuts_kernel");
+    row_cuts_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, S(stream)>>>(n_rows, ptr, idx, col_w, row_cuts);
+    GRF_CHECK_LAUNCH("row_cuts_kernel");
+    return GRF_OK;
 }
 
 int32_t grf_gram_sparse_upper(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,

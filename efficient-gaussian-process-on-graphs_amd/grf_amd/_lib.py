@@ -90,6 +90,9 @@ SIGNATURES = {
                                          _vp, _sz, _vp]),
     "grf_gram_sparse_upper": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
                                      _i32, _vp, _sz, _vp]),
+    "grf_gram_row_cuts": (_i32, [_i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "grf_gram_sparse_upper_ex": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32,
+                                        _i32, _i32, _i32, _vp]),
     "grf_gram_sparse_upper_add": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32,
                                          _i32, _i32, _vp, _sz, _vp]),
     "grf_hub_panel": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),

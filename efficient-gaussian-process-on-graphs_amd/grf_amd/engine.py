@@ -38,6 +38,12 @@ DENSE_GRAM_MAX_N = 4500  # measured crossover, profiles/r03_gram_crossover.txt
 # the banded transpose counts its buckets itself (grf_transpose_banded_self: no count atomics in the
 # walk, no scan over every bucket); GRF_TRANSPOSE_SELF=0 restores the walk-counted plan (A/B)
 SELF_COUNT_TRANSPOSE = os.environ.get("GRF_TRANSPOSE_SELF", "1") != "0"
+# the whole-K Gram's waves take shares of about equal record pairs (grf_gram_row_cuts) instead of equal
+# nonzero counts: "auto" (default) when Phi's column counts are skewed (column_stats), "1" always, "0" never
+ROW_CUTS = os.environ.get("GRF_GRAM_CUTS", "auto")
+# skewed: the densest column of Phi holds at least this many times the mean column's entries (C4's
+# Erdos-Renyi Phi: ~1.2; Facebook / Enron: > 20)
+SKEW_RATIO = 4.0
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -636,12 +642,19 @@ class GRFEngine:
                                                 self._gram_ws.numel(), self.stream), "grf_gram_sparse_kslice")
         return out[:, :n]
 
-    def gram_sparse_sym(self, phi: DeviceCSR, tr: Banded, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Whole K (float32) on this device from the upper band tiles plus a mirror pass."""
+    def gram_sparse_sym(self, phi: DeviceCSR, tr: Banded, out: Optional[torch.Tensor] = None,
+                        skewed: bool = False) -> torch.Tensor:
+        """Whole K (float32) on this device from the upper band tiles plus a mirror pass (skewed: see
+        ``row_cuts``)."""
         n = tr.n_rows
         ldk = self.leading_dim(n)
         if out is None:
             out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
+        cuts = self.row_cuts(phi, tr, skewed)
+        if cuts is not None:  # (the waves' pair-balanced shares: same bits)
+            self._gram_upper_cuts(phi, tr, out, cuts, (0, 1, 1), False)
+            self.gram_mirror(out, n)
+            return out[:, :n]
         C.check(self.lib.grf_gram_sparse_sym(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
                                              tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_split), _p(tr.t_rowshift),
                                              _p(out), out.stride(0),
@@ -649,10 +662,39 @@ class GRFEngine:
                 "grf_gram_sparse_sym")
         return out[:, :n]
 
-    def gram_sparse_upper(self, phi: DeviceCSR, tr: Banded, out: torch.Tensor, parts=(0, 1, 1)) -> torch.Tensor:
+    def row_cuts(self, phi: DeviceCSR, tr: Banded, skewed: bool = False) -> Optional[torch.Tensor]:
+        """8 cuts per row of Phi splitting its nonzeros into shares of about equal record pairs (weights:
+        every column's pairs over all bands of ``tr``), for the whole-K Gram's waves; None when the
+        policy says no (GRF_GRAM_CUTS: auto = when ``skewed``, ``column_stats``) or the buckets are slots.
+        Measured: Facebook 2.86-2.91 -> 2.75-2.79 ms per K; C4 (not skewed) would pay 0.5 ms for the
+        cuts and gain nothing (profiles/r03_gram_balance_ab.txt)."""
+        on = ROW_CUTS == "1" or (ROW_CUTS == "auto" and skewed)
+        if not on or tr.rec_unit == C.REC_SLOT or phi.n_rows == 0:
+            return None
+        nb = -(-tr.n_rows // tr.band_width)
+        col_w = torch.empty(max(1, tr.n_cols), dtype=torch.int32, device=self.device)
+        cuts = torch.empty(8 * phi.n_rows, dtype=torch.int32, device=self.device)
+        C.check(self.lib.grf_gram_row_cuts(phi.n_rows, _p(phi.ptr), _p(phi.idx), nb, tr.n_cols, _p(tr.t_desc),
+                                           _p(col_w), _p(cuts), self.stream), "grf_gram_row_cuts")
+        return cuts
+
+    def _gram_upper_cuts(self, phi: DeviceCSR, tr: Banded, out: torch.Tensor, cuts: torch.Tensor, parts,
+                         add_k: bool) -> None:
+        C.check(self.lib.grf_gram_sparse_upper_ex(tr.n_rows, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
+                                                  tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_split),
+                                                  _p(tr.t_rowshift), _p(cuts), _p(out), out.stride(0), int(parts[0]),
+                                                  int(parts[1]), int(parts[2]), int(add_k), self.stream),
+                "grf_gram_sparse_upper_ex")
+
+    def gram_sparse_upper(self, phi: DeviceCSR, tr: Banded, out: torch.Tensor, parts=(0, 1, 1),
+                          cuts: Optional[torch.Tensor] = None) -> torch.Tensor:
         """The Gram half of ``gram_sparse_sym`` (tiles K[i, band >= band(i)]); ``gram_mirror`` completes K.
-        parts = (begin, end, n): only those parts of the band-major tile sequence cut into n."""
+        parts = (begin, end, n): only those parts of the band-major tile sequence cut into n.
+        cuts: ``row_cuts(phi, tr)`` (the waves' pair-balanced shares; same bits)."""
         n = tr.n_rows
+        if cuts is not None:
+            self._gram_upper_cuts(phi, tr, out, cuts, parts, False)
+            return out[:, :n]
         C.check(self.lib.grf_gram_sparse_upper(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
                                                tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_split),
                                                _p(tr.t_rowshift), _p(out),
@@ -687,7 +729,7 @@ class GRFEngine:
         return P, cols
 
     def gram_sparse_sym_hubs(self, phi: DeviceCSR, tr: Banded, hubs: int, out: Optional[torch.Tensor] = None,
-                             mirror_workgroups: int = 0, after_tiles=None) -> torch.Tensor:
+                             mirror_workgroups: int = 0, after_tiles=None, skewed: bool = False) -> torch.Tensor:
         """Whole K with the hub-column split: the panel of Phi's ``hubs`` densest columns through the
         MFMA Gram (tiles on and above the diagonal), the rest through the sparse Gram tiles adding to
         it, then the mirror.  ``tr`` is consumed (its hub buckets emptied).  Within the fp32 K
@@ -697,7 +739,7 @@ class GRFEngine:
         if out is None:
             out = torch.empty((n, self.leading_dim(n)), dtype=torch.float32, device=self.device)
         if int(hubs) <= 0:  # (no split: the plain symmetric Gram)
-            self.gram_sparse_upper(phi, tr, out)
+            self.gram_sparse_upper(phi, tr, out, cuts=self.row_cuts(phi, tr, skewed))
             ev = None
             if after_tiles is not None:
                 ev = torch.cuda.Event()
@@ -710,11 +752,15 @@ class GRFEngine:
         h = int(cols.numel())
         C.check(self.lib.grf_gram_dense_upper(n, h, _p(P), P.stride(0), _p(out), out.stride(0), self.stream),
                 "grf_gram_dense_upper")
-        C.check(self.lib.grf_gram_sparse_upper_add(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
-                                                   tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_split),
-                                                   _p(tr.t_rowshift),
-                                                   _p(out), out.stride(0), 0, 1, 1, _p(self._gram_ws),
-                                                   self._gram_ws.numel(), self.stream), "grf_gram_sparse_upper_add")
+        cuts = self.row_cuts(phi, tr, skewed)  # (after the hub drop: the weights of the columns left)
+        if cuts is not None:
+            self._gram_upper_cuts(phi, tr, out, cuts, (0, 1, 1), True)
+        else:
+            C.check(self.lib.grf_gram_sparse_upper_add(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
+                                                       tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_split),
+                                                       _p(tr.t_rowshift), _p(out), out.stride(0), 0, 1, 1,
+                                                       _p(self._gram_ws), self._gram_ws.numel(), self.stream),
+                    "grf_gram_sparse_upper_add")
         ev = None
         if after_tiles is not None:
             ev = torch.cuda.Event()
@@ -770,6 +816,17 @@ class GRFEngine:
         return out[:, :n]
 
     @staticmethod
+    def column_stats(phi: DeviceCSR, share: float = HUB_SHARE) -> Tuple[int, bool]:
+        """(hub_count, skewed) from one column count of Phi: skewed when the densest column holds at
+        least SKEW_RATIO times the mean column's entries (the policy of ``row_cuts``).  One host read."""
+        n = phi.n_cols
+        if phi.nnz == 0 or n == 0:
+            return 0, False
+        c = torch.bincount(phi.idx[:phi.nnz].long(), minlength=n)
+        hubs, cmax = (int(x) for x in torch.stack([(c >= share * phi.n_rows).sum(), c.max()]).tolist())
+        return hubs // 32 * 32, cmax >= SKEW_RATIO * phi.nnz / n
+
+    @staticmethod
     def hub_count(phi: DeviceCSR, share: float = HUB_SHARE) -> int:
         """Hub columns worth the dense MFMA panel of the hub-column split: the columns of Phi present in
         at least ``share`` of its rows, in multiples of 32 (the panel's width).  A column in c of the n
@@ -786,10 +843,10 @@ class GRFEngine:
         """Whole K on the sparse path exactly as the bench assembles it: the symmetric tiles + mirror,
         with the hub-column split when Phi has hub columns (``hub_count``)."""
         tr = self.transpose_banded(phi)
-        hubs = self.hub_count(phi)
+        hubs, skewed = self.column_stats(phi)
         if hubs:
-            return self.gram_sparse_sym_hubs(phi, tr, hubs, out=out)
-        return self.gram_sparse_sym(phi, tr, out=out)
+            return self.gram_sparse_sym_hubs(phi, tr, hubs, out=out, skewed=skewed)
+        return self.gram_sparse_sym(phi, tr, out=out, skewed=skewed)
 
     def gram(self, phi: DeviceCSR, method: str = "auto") -> torch.Tensor:
         """K = Phi Phi^T (float32).  'dense' = MFMA on densified Phi, 'sparse' = LDS Gustavson (+ the

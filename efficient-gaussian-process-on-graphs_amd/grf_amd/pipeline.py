@@ -51,6 +51,7 @@ class StepPlan:
     cols_sym: bool = False         # column blocks: the square K[b:e, b:e] by the symmetric enumeration
     fused: bool = False            # "sym": symmetric completion fused into the Gram tiles (no mirror pass)
     hubs: int = 0                  # "sym" / "cols": Phi's densest columns as a dense panel (hub-column split)
+    skewed: bool = False           # "sym": Phi's column counts are skewed -> pair-balanced wave shares (row_cuts)
     group: object = None           # torch.distributed group (N > 1)
     collective: bool = False       # the Phi all-gather runs (N > 1; or one rank, to rehearse RCCL on one GPU)
     gather_bound: int = 0          # N > 1: per-rank Phi entries moved by the all-gather (0: rows x rows_cap;
@@ -189,6 +190,9 @@ def front_transpose(eng: GRFEngine, pl: StepPlan, fr: Front) -> Front:
     records, not lines, and measured no faster: profiles/r03_split_ab.txt.)"""
     fr.tr = eng.transpose_banded(fr.phi, pl.band_width, counted_ws=getattr(fr, "tws", None),
                                  nnz_bound=pl.n * pl.rows_cap)
+    # the whole-K tiles' pair-balanced wave shares (policy: engine.ROW_CUTS; the hub split makes its own
+    # after dropping the hub columns)
+    fr.cuts = eng.row_cuts(fr.phi, fr.tr, pl.skewed) if pl.mode == "sym" and not pl.fused and pl.hubs == 0 else None
     return fr
 
 
@@ -231,18 +235,18 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
             after_tiles(tiles_done)
     elif pl.mode == "sym" and pl.hubs > 0:
         eng.gram_sparse_sym_hubs(fr.phi, fr.tr, pl.hubs, out=K, mirror_workgroups=mirror_workgroups,
-                                 after_tiles=after_tiles)
+                                 after_tiles=after_tiles, skewed=pl.skewed)
     elif pl.mode == "sym":
         main = torch.cuda.current_stream(eng.device)
         tiles_done = None
         if after_tiles is not None and front_at < 1.0:
             cut = int(round(front_at * 1000))
-            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(0, cut, 1000))
+            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(0, cut, 1000), cuts=getattr(fr, "cuts", None))
             tiles_done = torch.cuda.Event()
             tiles_done.record(main)
-            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(cut, 1000, 1000))
+            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(cut, 1000, 1000), cuts=getattr(fr, "cuts", None))
         else:
-            eng.gram_sparse_upper(fr.phi, fr.tr, out=K)
+            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, cuts=getattr(fr, "cuts", None))
             if after_tiles is not None:
                 tiles_done = torch.cuda.Event()
                 tiles_done.record(main)

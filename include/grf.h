@@ -317,6 +317,24 @@ int32_t grf_gram_sparse_upper_add(int64_t n_total, const int64_t *ptr, const int
                                   int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
                                   grf_stream_t stream);
 
+/* Wave shares by record pairs (skewed graphs, where a row's long buckets cluster in its column
+ * order).  grf_gram_row_cuts: col_w[k] = the record pairs of column k over all n_bands bands of
+ * the transpose (t_desc, after any hub drop), then for every row of Phi (ptr, idx) 8 cuts
+ * row_cuts[8 row + s] = the first nonzero (offset in the row) whose prefix of column weights
+ * reaches s / 8 of the row's total (s = 0: 0).  col_w: n_cols int32 scratch; row_cuts: 8 n_rows int32.
+ * grf_gram_sparse_upper_ex: grf_gram_sparse_upper (add_k = 0) or _add (add_k = 1) whose tiles give
+ * each wave the nonzeros between its cuts instead of equal counts; row_cuts NULL = the plain call.
+ * K is bit-identical either way (integer sums).  Line / packed buckets only (not GRF_REC_SLOT).
+ * Replaces nothing in the reference: scheduling only (the reference's Phi @ Phi.T,
+ * efficient_graph_gp_sparse/graph_kernels_sparse/fast_grf_kernel_general.py:55). */
+int32_t grf_gram_row_cuts(int64_t n_rows, const int64_t *ptr, const int32_t *idx, int64_t n_bands, int64_t n_cols,
+                          const uint32_t *t_desc, int32_t *col_w, int32_t *row_cuts, grf_stream_t stream);
+int32_t grf_gram_sparse_upper_ex(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
+                                 int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
+                                 const void *t_split, const int32_t *t_rowshift, const int32_t *row_cuts, float *K,
+                                 int64_t ldk, int32_t part_begin, int32_t part_end, int32_t n_parts, int32_t add_k,
+                                 grf_stream_t stream);
+
 /* Hub-column split (hub-heavy graphs: Enron, Facebook, power-law).  grf_hub_panel writes the entries
  * Phi[r, k] of the columns with hub_pos[k] >= 0 into the dense fp32 panel P[r, hub_pos[k]] (row-major,
  * n_rows x ldp, zeroed by the caller; int32 hub_pos[n_cols], -1 elsewhere).  grf_transpose_drop_columns

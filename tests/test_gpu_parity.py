@@ -1196,3 +1196,31 @@ def test_column_block_hub_split(eng, hubs):
         if sym:  # the square stays exactly symmetric
             sq = Kh[b:e]
             assert np.array_equal(sq, sq.T)
+
+
+@pytest.mark.parametrize("hubs", [0, 64])
+def test_gram_row_cuts_bit_identical(eng, hubs):
+    """Pair-balanced wave shares (grf_gram_row_cuts + grf_gram_sparse_upper_ex) give the same K bits as
+    the plain whole-K Gram on a hub-heavy power-law graph, with and without the hub-column split; and
+    the cuts are monotone, start at 0 and end within each row."""
+    import torch
+
+    import grf_amd.engine as E
+    from grf_amd.graphs import powerlaw_graph
+    A = powerlaw_graph(20000, 10.0, 2.5, seed=11)
+    G = eng.laplacian(A)
+    phi = eng.compact(eng.walk_phi(G, 32, 0.1, 6, [1.0, -0.5, 0.125, -0.02, 0.003, -0.0005], seed=5, want64=False),
+                      want64=False)
+    old = E.ROW_CUTS
+    try:
+        E.ROW_CUTS = "0"
+        K0 = eng.gram_sparse_sym_hubs(phi, eng.transpose_banded(phi, 4096), hubs).clone()
+        E.ROW_CUTS = "1"
+        tr = eng.transpose_banded(phi, 4096)
+        cuts = eng.row_cuts(phi, tr).view(-1, 8).cpu().numpy()
+        K1 = eng.gram_sparse_sym_hubs(phi, tr, hubs)
+    finally:
+        E.ROW_CUTS = old
+    nnz = np.diff(phi.ptr.cpu().numpy())
+    assert (cuts[:, 0] == 0).all() and (np.diff(cuts, axis=1) >= 0).all() and (cuts[:, 7] <= nnz).all()
+    assert torch.equal(K0, K1)
