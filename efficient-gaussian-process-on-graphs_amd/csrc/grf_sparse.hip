@@ -142,6 +142,44 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(int64_t n_rows, int64
     }
 }
 
+// compaction that also leaves the Gram row-shift statistics of the compact rows (row max / fp64 sum
+// of |value| and each workgroup's max): one wave per row, 4 rows per workgroup, the entries in the
+// order phi_row_stats_kernel reads them (lane + 64 i), so grf_phi_row_shifts_stats gives
+// grf_phi_row_shifts' bits without another pass over the values
+__global__ __launch_bounds__(256) void compact_rows_stats_kernel(int64_t n_rows, int64_t cap, const int32_t *cnt,
+                                                                 const int64_t *out_ptr, const int32_t *in_idx,
+                                                                 const double *in_val, const float *in_val32,
+                                                                 int32_t *out_idx, double *out_val, float *out_val32,
+                                                                 float *row_max, double *row_sum, float *wg_max) {
+    __shared__ float red[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+    float mx = 0.f;
+    if (row < n_rows) {
+        const int64_t c = cnt[row], src = row * cap, dst = out_ptr[row];
+        double sm = 0.0;
+        for (int64_t e = lane; e < c; e += 64) {
+            out_idx[dst + e] = in_idx[src + e];
+            if (out_val) out_val[dst + e] = in_val[src + e];
+            const float v = in_val32[src + e];
+            out_val32[dst + e] = v;
+            const float a = fabsf(v);
+            mx = fmaxf(mx, a);
+            sm += (double)a;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        sm = wave_sum<double>(sm);
+        if (lane == 0) {
+            row_max[row] = mx;
+            row_sum[row] = sm;
+        }
+    }
+    if (lane == 0) red[wave] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) wg_max[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 // ------------------------------------------------------------ banded transpose
 // Bucket b = band * n_cols + k holds the entries Phi[j, k], j in the band, as PAIRS of
 // records packed in 12 bytes: {u16 8 (j0 - band start), u16 8 (j1 - band start), f32 v0, f32 v1}
@@ -1078,6 +1116,51 @@ int32_t grf_transpose_banded_self(int64_t n_rows, int64_t n_cols, int64_t band_w
 size_t grf_phi_row_shifts_workspace_bytes(int64_t n_rows) {
     const int64_t n = std::max<int64_t>(n_rows, 1);
     return tr_align((size_t)n * 4) + tr_align((size_t)n * 8) + tr_align((size_t)cdiv<int64_t>(n, 4) * 4);
+}
+
+static void row_stats_layout(void *workspace, int64_t n_rows, float *&row_max, double *&row_sum, float *&wg_max) {
+    char *w = (char *)workspace;
+    row_max = (float *)w;
+    row_sum = (double *)(w + tr_align((size_t)n_rows * 4));
+    wg_max = (float *)(w + tr_align((size_t)n_rows * 4) + tr_align((size_t)n_rows * 8));
+}
+
+int32_t grf_compact_rows_stats(int64_t n_rows, int64_t cap, const int32_t *cnt, const int64_t *out_ptr,
+                               const int32_t *in_idx, const double *in_val, const float *in_val32, int32_t *out_idx,
+                               double *out_val, float *out_val32, void *stats, size_t stats_bytes,
+                               grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && cap >= 0 && cnt && out_ptr && in_idx && out_idx && in_val32 && out_val32 && stats,
+                GRF_EINVAL, "grf_compact_rows_stats: bad arguments");
+    GRF_REQUIRE(!out_val || in_val, GRF_EINVAL, "grf_compact_rows_stats: out_val needs in_val");
+    GRF_REQUIRE(stats_bytes >= grf_phi_row_shifts_workspace_bytes(n_rows), GRF_EINVAL,
+                "grf_compact_rows_stats: stats buffer too small");
+    if (n_rows == 0) return GRF_OK;
+    float *row_max, *wg_max;
+    double *row_sum;
+    row_stats_layout(stats, n_rows, row_max, row_sum, wg_max);
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 4), 256, "compact_rows_stats_kernel");
+    compact_rows_stats_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 4), 256, 0, S(stream)>>>(
+        n_rows, cap, cnt, out_ptr, in_idx, in_val, in_val32, out_idx, out_val, out_val32, row_max, row_sum, wg_max);
+    GRF_CHECK_LAUNCH("compact_rows_stats_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_phi_row_shifts_stats(int64_t n_rows, const void *stats, float *maxabs, int32_t *row_shift,
+                                 grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && stats && maxabs && row_shift, GRF_EINVAL, "grf_phi_row_shifts_stats: bad arguments");
+    hipStream_t st = S(stream);
+    GRF_CHECK_HIP(hipMemsetAsync(maxabs, 0, sizeof(float), st));
+    if (n_rows == 0) return GRF_OK;
+    float *row_max, *wg_max;
+    double *row_sum;
+    row_stats_layout(const_cast<void *>(stats), n_rows, row_max, row_sum, wg_max);
+    const int64_t nwg = cdiv<int64_t>(n_rows, 4);
+    tr_maxabs_kernel<<<1, 1024, 0, st>>>(nwg, wg_max, maxabs);
+    GRF_CHECK_LAUNCH("tr_maxabs_kernel");
+    tr_rowshift_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 256), 256, 0, st>>>(n_rows, row_max, row_sum, maxabs,
+                                                                            row_shift);
+    GRF_CHECK_LAUNCH("tr_rowshift_kernel");
+    return GRF_OK;
 }
 
 int32_t grf_phi_row_shifts(int64_t n_rows, const int64_t *ptr, const float *val, float *maxabs, int32_t *row_shift,

@@ -69,6 +69,7 @@ SIGNATURES = {
     "grf_scan_workspace_bytes": (_sz, [_i64]),
     "grf_concat_segments": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_compact_rows": (_i32, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "grf_compact_rows_stats": (_i32, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_transpose_banded_plan": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
     "grf_transpose_banded_fill": (_i32, [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _sz,
                                          _vp]),
@@ -83,6 +84,7 @@ SIGNATURES = {
                                         _vp, _i64, _vp, _sz, _vp]),
     "grf_phi_row_shifts_workspace_bytes": (_sz, [_i64]),
     "grf_phi_row_shifts": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "grf_phi_row_shifts_stats": (_i32, [_i64, _vp, _vp, _vp, _vp]),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _i64, _vp]),
     "grf_gram_sym_fused_workspace_bytes": (_sz, [_i64, _i64]),

@@ -358,9 +358,10 @@ class GRFEngine:
 
     # ------------------------------------------------------ sparse utilities
     def compact(self, rows: PaddedRows, want64: bool = True, want32: bool = True,
-                sync_free: bool = False) -> DeviceCSR:
+                sync_free: bool = False, stats: bool = False) -> DeviceCSR:
         """Compact CSR of padded rows.  sync_free: size the outputs by the padded capacity instead of
-        reading nnz back (no host synchronisation; nnz is read lazily if asked for)."""
+        reading nnz back (no host synchronisation; nnz is read lazily if asked for).  stats: also keep
+        the rows' Gram shift statistics (``phi_row_shifts`` then skips its pass over the values)."""
         n = rows.n_rows
         ptr = self._empty(n + 1, torch.int64)
         ws = self._ws(self.lib.grf_scan_workspace_bytes(n))
@@ -370,11 +371,21 @@ class GRFEngine:
         idx = self._empty(nnz, torch.int32)
         v64 = self._empty(nnz, torch.float64) if want64 else None
         v32 = self._empty(nnz, torch.float32) if (want32 and rows.val32 is not None) else None
-        C.check(self.lib.grf_compact_rows(n, rows.cap, _p(rows.cnt), _p(ptr), _p(rows.idx),
-                                          _p(rows.val if want64 else None),
-                                          _p(rows.val32 if v32 is not None else None), _p(idx), _p(v64),
-                                          _p(v32), self.stream), "grf_compact_rows")
+        st = None
+        if stats and v32 is not None:
+            st = torch.empty(int(self.lib.grf_phi_row_shifts_workspace_bytes(n)), dtype=torch.uint8,
+                             device=self.device)
+            C.check(self.lib.grf_compact_rows_stats(n, rows.cap, _p(rows.cnt), _p(ptr), _p(rows.idx),
+                                                    _p(rows.val if want64 else None), _p(rows.val32), _p(idx),
+                                                    _p(v64), _p(v32), _p(st), st.numel(), self.stream),
+                    "grf_compact_rows_stats")
+        else:
+            C.check(self.lib.grf_compact_rows(n, rows.cap, _p(rows.cnt), _p(ptr), _p(rows.idx),
+                                              _p(rows.val if want64 else None),
+                                              _p(rows.val32 if v32 is not None else None), _p(idx), _p(v64),
+                                              _p(v32), self.stream), "grf_compact_rows")
         out = DeviceCSR(n, rows.n_cols, ptr, idx, v64, v32, None if sync_free else nnz)
+        out.row_stats = st
         out.nnz_bound = nnz
         return out
 
@@ -575,6 +586,11 @@ class GRFEngine:
         n = phi.n_rows
         shift = self._empty(max(n, 1), torch.int32)
         mx = self._empty(1, torch.float32)
+        st = getattr(phi, "row_stats", None)
+        if st is not None:  # (left by compact(..., stats=True): same bits, no pass over the values)
+            C.check(self.lib.grf_phi_row_shifts_stats(n, _p(st), _p(mx), _p(shift), self.stream),
+                    "grf_phi_row_shifts_stats")
+            return shift
         ws = self._ws(self.lib.grf_phi_row_shifts_workspace_bytes(n))
         C.check(self.lib.grf_phi_row_shifts(n, _p(phi.ptr), _p(phi.val32), _p(mx), _p(shift), _p(ws), ws.numel(),
                                             self.stream), "grf_phi_row_shifts")

@@ -29,6 +29,9 @@ from .engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, SELF_COUNT_TRANSPOSE, D
 FUSED_DEFAULT = os.environ.get("GRF_GRAM_FUSED", "0") == "1"
 # column blocks with sparse buckets take the GRF_REC_SLOT transpose (GRF_REC_SLOTS=0: packed pairs, A/B)
 SLOTS_DEFAULT = os.environ.get("GRF_REC_SLOTS", "1") == "1"
+# one GPU, column blocks: the compaction leaves the rows' Gram shift statistics (GRF_COMPACT_STATS=0: a
+# separate pass over Phi's values, A/B)
+COMPACT_STATS = os.environ.get("GRF_COMPACT_STATS", "1") == "1"
 
 
 @dataclass
@@ -151,7 +154,7 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
         local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
                                          count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
                                          want64=False),
-                            want64=False, want32=True, sync_free=True)
+                            want64=False, want32=True, sync_free=True, stats=COMPACT_STATS and not pl.collective)
         phi = gather_phi(eng, local, group=pl.group, shards=pl.shards, entries_bound=pl.gather_bound or None,
                          row_cap=pl.rows_cap, always=True) if pl.collective else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,

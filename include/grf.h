@@ -201,6 +201,12 @@ size_t grf_scan_workspace_bytes(int64_t n);
 int32_t grf_compact_rows(int64_t n_rows, int64_t cap, const int32_t *cnt, const int64_t *out_ptr,
                          const int32_t *in_idx, const double *in_val, const float *in_val32, int32_t *out_idx,
                          double *out_val, float *out_val32, grf_stream_t stream);
+/* grf_compact_rows (float values required) that also writes the rows' Gram shift statistics into
+ * `stats` (grf_phi_row_shifts_workspace_bytes(n_rows) bytes) for grf_phi_row_shifts_stats. */
+int32_t grf_compact_rows_stats(int64_t n_rows, int64_t cap, const int32_t *cnt, const int64_t *out_ptr,
+                               const int32_t *in_idx, const double *in_val, const float *in_val32, int32_t *out_idx,
+                               double *out_val, float *out_val32, void *stats, size_t stats_bytes,
+                               grf_stream_t stream);
 
 /* dst[dst_off[r] + i] = src[r * stride + i] for i < seg_len[r], r < n_seg (4-byte elements; lengths
  * and offsets are device arrays): the compaction of a fixed-stride all-gather of n_seg ranks'
@@ -393,6 +399,10 @@ int32_t grf_gram_sparse_cols_add(int64_t n_cols, int64_t row_begin, int64_t row_
 size_t grf_phi_row_shifts_workspace_bytes(int64_t n_rows);
 int32_t grf_phi_row_shifts(int64_t n_rows, const int64_t *ptr, const float *val, float *maxabs, int32_t *row_shift,
                            void *workspace, size_t workspace_bytes, grf_stream_t stream);
+/* The same shifts from statistics grf_compact_rows_stats left in `stats` while compacting the rows
+ * (one pass over the values fewer; identical bits). */
+int32_t grf_phi_row_shifts_stats(int64_t n_rows, const void *stats, float *maxabs, int32_t *row_shift,
+                                 grf_stream_t stream);
 
 /* K rows [row_begin, row_end) (as grf_gram_sparse) using the symmetry inside the row block: the
  * bands lying wholly inside the block are computed only on and above the diagonal for the block's

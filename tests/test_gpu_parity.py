@@ -1224,3 +1224,21 @@ def test_gram_row_cuts_bit_identical(eng, hubs):
     nnz = np.diff(phi.ptr.cpu().numpy())
     assert (cuts[:, 0] == 0).all() and (np.diff(cuts, axis=1) >= 0).all() and (cuts[:, 7] <= nnz).all()
     assert torch.equal(K0, K1)
+
+
+def test_compaction_row_stats_give_same_shifts(eng):
+    """compact(..., stats=True) leaves the rows' Gram shift statistics; phi_row_shifts from them equals
+    the separate pass over the values bit for bit (power-law graph, rows of very different norms)."""
+    import torch
+
+    from grf_amd.graphs import powerlaw_graph
+    A = powerlaw_graph(30000, 10.0, 2.5, seed=4)
+    G = eng.laplacian(A)
+    rows = eng.walk_phi(G, 64, 0.1, 8, [1.0, 0.5, 0.25, 0.125, 0.06, 0.03, 0.015, 0.008], seed=9, want64=False)
+    a = eng.compact(rows, want64=False, want32=True, sync_free=True, stats=True)
+    b = eng.compact(rows, want64=False, want32=True, sync_free=True)
+    assert a.row_stats is not None and b.row_stats is None
+    nnz = int(a.ptr[-1])
+    assert torch.equal(a.ptr, b.ptr) and torch.equal(a.idx[:nnz], b.idx[:nnz])
+    assert torch.equal(a.val32[:nnz], b.val32[:nnz])
+    assert torch.equal(eng.phi_row_shifts(a), eng.phi_row_shifts(b))
