@@ -745,7 +745,8 @@ class GRFEngine:
         return P, cols
 
     def gram_sparse_sym_hubs(self, phi: DeviceCSR, tr: Banded, hubs: int, out: Optional[torch.Tensor] = None,
-                             mirror_workgroups: int = 0, after_tiles=None, skewed: bool = False) -> torch.Tensor:
+                             mirror_workgroups: int = 0, after_tiles=None, skewed: bool = False,
+                             early_front: bool = False) -> torch.Tensor:
         """Whole K with the hub-column split: the panel of Phi's ``hubs`` densest columns through the
         MFMA Gram (tiles on and above the diagonal), the rest through the sparse Gram tiles adding to
         it, then the mirror.  ``tr`` is consumed (its hub buckets emptied).  Within the fp32 K
@@ -766,6 +767,12 @@ class GRFEngine:
             return out[:, :n]
         P, cols = self.hub_split(phi, tr, hubs)
         h = int(cols.numel())
+        if early_front and after_tiles is not None:
+            # (the pipelined bench's next front beside the compute-bound MFMA panel, the tiles and the mirror)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            after_tiles(ev)
+            after_tiles = None
         C.check(self.lib.grf_gram_dense_upper(n, h, _p(P), P.stride(0), _p(out), out.stride(0), self.stream),
                 "grf_gram_dense_upper")
         cuts = self.row_cuts(phi, tr, skewed)  # (after the hub drop: the weights of the columns left)

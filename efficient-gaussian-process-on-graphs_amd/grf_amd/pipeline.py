@@ -32,6 +32,10 @@ SLOTS_DEFAULT = os.environ.get("GRF_REC_SLOTS", "1") == "1"
 # one GPU, column blocks: the compaction leaves the rows' Gram shift statistics (GRF_COMPACT_STATS=0: a
 # separate pass over Phi's values, A/B)
 COMPACT_STATS = os.environ.get("GRF_COMPACT_STATS", "1") == "1"
+# pipelined whole K with the hub-column split: the next front starts beside the hub panel's MFMA Gram,
+# not at the mirror (Enron 8.66-8.68 -> 8.13-8.23 ms per K, profiles/r03_hub_early_front_ab.txt;
+# GRF_HUB_EARLY_FRONT=0: at the mirror)
+HUB_EARLY_FRONT = os.environ.get("GRF_HUB_EARLY_FRONT", "1") == "1"
 
 
 @dataclass
@@ -238,7 +242,8 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
             after_tiles(tiles_done)
     elif pl.mode == "sym" and pl.hubs > 0:
         eng.gram_sparse_sym_hubs(fr.phi, fr.tr, pl.hubs, out=K, mirror_workgroups=mirror_workgroups,
-                                 after_tiles=after_tiles, skewed=pl.skewed)
+                                 after_tiles=after_tiles, skewed=pl.skewed,
+                                 early_front=HUB_EARLY_FRONT or front_at < 1.0)
     elif pl.mode == "sym":
         main = torch.cuda.current_stream(eng.device)
         tiles_done = None
