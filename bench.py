@@ -520,8 +520,10 @@ def main():
                          "front, with its RCCL collectives, runs beside this step's Gram; single-GPU row modes "
                          "gain ~1 % and default to serial steps")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false", help="serial steps")
-    ap.add_argument("--front-at", type=float, default=1.0,
-                    help="pipelined: the next front starts after this fraction of the Gram tiles (1 = at the mirror)")
+    ap.add_argument("--front-at", type=float, default=None,
+                    help="pipelined: the next front starts after this fraction of the Gram tiles (1 = at the mirror, "
+                         "0 = with the tiles); default: 0 when the front outlasts the mirror (n < 400 m: Facebook "
+                         "2.78 -> 2.45 ms per K), else 1 (C4: the front beside the Gram tiles loses)")
     ap.add_argument("--front-split", action="store_true",
                     help="pipelined symmetric K: only the next step's Laplacian, walks and compaction run beside the "
                          "mirror; its transpose follows on the main stream after the mirror")
@@ -636,6 +638,12 @@ def main():
     if args.k_buffers == 2 and pl.mode == "sym" and (args.overlap is not False):
         Ks.append(P.alloc_k(eng, pl))
         mstream = torch.cuda.Stream(dev)  # the mirror of step s, beside step s+1's front and tiles
+
+    if args.front_at is None:
+        # the mirror moves 4 n^2 bytes (~6.7e-13 n^2 s), the next front ~2.7e-10 s per walk (C4: 3.5 ms for
+        # 12.8 M walks): below n = 400 m the front outlasts the mirror and is issued with the Gram tiles
+        # (profiles/r03_front_at_ab.txt)
+        args.front_at = 0.0 if n < 400 * m else 1.0
 
     split_front = [False]  # (set while the timed / warm-up steps run with --front-split)
 
@@ -913,6 +921,7 @@ def main():
         "parity": parity,
         "pipelined": bool(ov),
         "front_split": bool(args.front_split and ov and pl.mode == "sym"),
+        "front_at": args.front_at,
         "k_buffers": len(Ks),
         "serial_ms_per_step": serial_ms,
     }
