@@ -571,16 +571,21 @@ __global__ __launch_bounds__(256) void transpose_drop_kernel(int64_t n_bands, in
     t_desc[J * n_cols + cols[t - J * n_drop]].y = 0u;
 }
 
-__device__ __forceinline__ void gram_mirror_block(int64_t n, int64_t nt, int64_t b, float *__restrict__ K, int64_t ldk,
-                                                  float (*tile)[65]) {
-    // block b -> (bi, bj), bj >= bi, row-major over the upper triangle of the nt x nt grid
+// block b of the row-major upper triangle (bj >= bi) of an nt x nt block grid -> (bi, bj)
+__device__ __forceinline__ void gram_mirror_tri_coords(int64_t nt, int64_t b, int64_t &bi_out, int64_t &bj_out) {
     int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
     auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };  // first block of block-row i
     if (bi < 0) bi = 0;
     if (bi > nt - 1) bi = nt - 1;
     while (bi > 0 && first(bi) > b) --bi;
     while (bi < nt - 1 && first(bi + 1) <= b) ++bi;
-    const int64_t bj = bi + (b - first(bi));
+    bi_out = bi;
+    bj_out = bi + (b - first(bi));
+}
+
+// K[j, i] = K[i, j] for the 64 x 64 block (bi, bj), bj >= bi (diagonal: j > i inside the block)
+__device__ __forceinline__ void gram_mirror_block_at(int64_t n, int64_t bi, int64_t bj, float *__restrict__ K,
+                                                     int64_t ldk, float (*tile)[65]) {
     const int64_t i0 = bi * 64, j0 = bj * 64;
     const int t = threadIdx.x;
     const bool full = i0 + 64 <= n && j0 + 64 <= n && (ldk & 3) == 0;
@@ -617,6 +622,13 @@ __device__ __forceinline__ void gram_mirror_block(int64_t n, int64_t nt, int64_t
     }
 }
 
+__device__ __forceinline__ void gram_mirror_block(int64_t n, int64_t nt, int64_t b, float *__restrict__ K, int64_t ldk,
+                                                  float (*tile)[65]) {
+    int64_t bi, bj;
+    gram_mirror_tri_coords(nt, b, bi, bj);
+    gram_mirror_block_at(n, bi, bj, K, ldk, tile);
+}
+
 // Symmetric completion: K[j, i] = K[i, j] for every j > i (the Gram launch in symmetric
 // mode wrote the tiles K[i, band >= band(i)], which cover the upper triangle; the lower
 // parts of the diagonal band tiles are overwritten, so K is exactly symmetric).  One
@@ -638,20 +650,13 @@ __global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, int64_t nt,
 // chunks); each thread then reads two adjacent source columns of four source rows with ds_read_b64
 // (64 banks; lanes {4k + c} x {y, y + 2} hit 32 distinct bank pairs) and stores two output rows of
 // 16 B (256 B per row and wave-instruction).
-__device__ __forceinline__ void gram_mirror_block_swz(int64_t n, int64_t nt, int64_t b, float *__restrict__ K,
-                                                      int64_t ldk, float *__restrict__ tile) {
-    int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
-    auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };
-    if (bi < 0) bi = 0;
-    if (bi > nt - 1) bi = nt - 1;
-    while (bi > 0 && first(bi) > b) --bi;
-    while (bi < nt - 1 && first(bi + 1) <= b) ++bi;
-    const int64_t bj = bi + (b - first(bi));
+__device__ __forceinline__ void gram_mirror_block_swz_at(int64_t n, int64_t bi, int64_t bj, float *__restrict__ K,
+                                                         int64_t ldk, float *__restrict__ tile) {
     const int64_t i0 = bi * 64, j0 = bj * 64;
     const int t = threadIdx.x;
     const bool full = i0 + 64 <= n && j0 + 64 <= n && (ldk & 3) == 0 && bi != bj;
     if (!full) {  // diagonal / ragged blocks: the padded-tile path (same LDS)
-        gram_mirror_block(n, nt, b, K, ldk, reinterpret_cast<float(*)[65]>(tile));
+        gram_mirror_block_at(n, bi, bj, K, ldk, reinterpret_cast<float(*)[65]>(tile));
         return;
     }
     auto swz = [](int r, int c) { return r * 64 + (c ^ (4 * ((r >> 2) & 15))); };
@@ -688,11 +693,32 @@ __device__ __forceinline__ void gram_mirror_block_swz(int64_t n, int64_t nt, int
     }
 }
 
+__device__ __forceinline__ void gram_mirror_block_swz(int64_t n, int64_t nt, int64_t b, float *__restrict__ K,
+                                                      int64_t ldk, float *__restrict__ tile) {
+    int64_t bi, bj;
+    gram_mirror_tri_coords(nt, b, bi, bj);
+    gram_mirror_block_swz_at(n, bi, bj, K, ldk, tile);
+}
+
 __global__ __launch_bounds__(256) void gram_mirror_swz_kernel(int64_t n, int64_t nt, int64_t nblocks,
                                                               float *__restrict__ K, int64_t ldk) {
     __shared__ __attribute__((aligned(16))) float tile[64 * 65];
     for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
         gram_mirror_block_swz(n, nt, b, K, ldk, tile);
+        __syncthreads();
+    }
+}
+
+// The mirror of one rectangle of 64-blocks: block rows [bi0, bi1) x block columns [bj0, bj1), the
+// blocks with bj >= bi (the others are skipped).  A trailing mirror (grf_gram_mirror_rect) completes
+// the tiles of one (row range, band) chunk right after the Gram wrote them, while they may still sit
+// in the Infinity Cache.
+__global__ __launch_bounds__(256) void gram_mirror_rect_kernel(int64_t n, int64_t bi0, int64_t bj0, int64_t nbj,
+                                                               int64_t nblocks, float *__restrict__ K, int64_t ldk) {
+    __shared__ __attribute__((aligned(16))) float tile[64 * 65];
+    for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const int64_t bi = bi0 + b / nbj, bj = bj0 + b % nbj;
+        if (bj >= bi) gram_mirror_block_swz_at(n, bi, bj, K, ldk, tile);
         __syncthreads();
     }
 }
@@ -1454,6 +1480,22 @@ int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups
         gram_mirror_edge_kernel<<<(unsigned)nedge, 256, 0, S(stream)>>>(n, nt, K, ldk);
     } else gram_mirror_swz_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
     GRF_CHECK_LAUNCH("gram_mirror_kernel");
+    return GRF_OK;
+}
+
+int32_t grf_gram_mirror_rect(int64_t n, float *K, int64_t ldk, int64_t row_begin, int64_t row_end, int64_t col_begin,
+                             int64_t col_end, int64_t max_workgroups, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && K && ldk >= n && 0 <= row_begin && row_begin <= row_end && row_end <= n && 0 <= col_begin &&
+                    col_begin <= col_end && col_end <= n && row_begin % 64 == 0 && col_begin % 64 == 0,
+                GRF_EINVAL, "grf_gram_mirror_rect: bad arguments (ranges inside [0, n), starts multiples of 64)");
+    if (row_end == row_begin || col_end == col_begin) return GRF_OK;
+    const int64_t bi0 = row_begin / 64, bj0 = col_begin / 64;
+    const int64_t nbi = cdiv<int64_t>(row_end, 64) - bi0, nbj = cdiv<int64_t>(col_end, 64) - bj0;
+    const int64_t blocks = nbi * nbj;
+    const int64_t grid = max_workgroups > 0 && max_workgroups < blocks ? max_workgroups : blocks;
+    GRF_REQUIRE_GRID(grid, 256, "gram_mirror_rect_kernel");
+    gram_mirror_rect_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, bi0, bj0, nbj, blocks, K, ldk);
+    GRF_CHECK_LAUNCH("gram_mirror_rect_kernel");
     return GRF_OK;
 }
 

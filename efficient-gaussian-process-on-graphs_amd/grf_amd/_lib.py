@@ -87,6 +87,7 @@ SIGNATURES = {
     "grf_phi_row_shifts_stats": (_i32, [_i64, _vp, _vp, _vp, _vp]),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _i64, _vp]),
+    "grf_gram_mirror_rect": (_i32, [_i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
     "grf_gram_sym_fused_workspace_bytes": (_sz, [_i64, _i64]),
     "grf_gram_sparse_sym_fused": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32,
                                          _vp, _sz, _vp]),

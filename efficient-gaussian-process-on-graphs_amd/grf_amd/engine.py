@@ -818,6 +818,13 @@ class GRFEngine:
         C.check(self.lib.grf_gram_mirror(n, _p(K), K.stride(0), int(max_workgroups), self.stream), "grf_gram_mirror")
         return K[:, :n]
 
+    def gram_mirror_rect(self, K: torch.Tensor, n: int, rows: Tuple[int, int], cols: Tuple[int, int],
+                         max_workgroups: int = 0) -> None:
+        """The mirror pass over the 64-blocks of K[rows[0]:rows[1], cols[0]:cols[1]] on or above the
+        diagonal (starts multiples of 64): K[j, i] = K[i, j] for j > i there."""
+        C.check(self.lib.grf_gram_mirror_rect(n, _p(K), K.stride(0), int(rows[0]), int(rows[1]), int(cols[0]),
+                                              int(cols[1]), int(max_workgroups), self.stream), "grf_gram_mirror_rect")
+
     def densify(self, phi: DeviceCSR) -> torch.Tensor:
         lda = max(64, -(-phi.n_cols // 64) * 64)  # (zero-padded k: every k-tile width of the MFMA Gram divides it)
         out = torch.empty((phi.n_rows, lda), dtype=torch.float32, device=self.device)

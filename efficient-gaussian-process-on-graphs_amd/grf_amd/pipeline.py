@@ -278,6 +278,52 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
     return K
 
 
+def sym_tile_chunks(n: int, W: int, chunk_rows: int):
+    """The symmetric Gram's band-major tile sequence (grf_gram_sparse_upper: band J holds the rows
+    0 .. min((J + 1) W, n) - 1) cut into (row range, band) chunks: the rows above the band's diagonal
+    square in pieces of ``chunk_rows``, then the square.  Yields (t0, t1, total, (r0, r1), (c0, c1)):
+    tiles [t0, t1) of ``total`` write K[r0:r1, c0:c1]."""
+    nb = -(-n // W)
+    full = nb - 1  # bands J < full hold (J + 1) W rows
+
+    def before(J):
+        return W * J * (J + 1) // 2 if J <= full else W * full * (full + 1) // 2 + (J - full) * n
+
+    total = before(nb)
+    for J in range(nb):
+        c0, c1 = J * W, min((J + 1) * W, n)
+        rows = min((J + 1) * W, n)
+        cuts = list(range(0, c0, chunk_rows)) + [c0, rows]
+        for r0, r1 in zip(cuts[:-1], cuts[1:]):
+            if r1 > r0:
+                yield before(J) + r0, before(J) + r1, total, (r0, r1), (c0, c1)
+
+
+def k_assembly_trailing(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, mirror_stream: torch.cuda.Stream,
+                        chunk_rows: int = 4096, mirror_workgroups: int = 0) -> torch.Tensor:
+    """Symmetric K assembly with a trailing mirror: the Gram tiles run chunk by chunk (``sym_tile_chunks``)
+    on the caller's stream, and each chunk's lower-triangle copy (``gram_mirror_rect``) follows on
+    ``mirror_stream`` as soon as that chunk is written, beside the next chunks' tiles, while its K
+    lines may still be in the Infinity Cache.  No chunk's mirror writes an entry a later tile writes
+    (a band's tiles write only columns >= the band's start; its square is mirrored after all its
+    rows), so K is bit-identical to tiles + ``gram_mirror``.  The caller's stream waits for the last
+    mirror before it returns."""
+    assert pl.mode == "sym" and not pl.fused and pl.hubs == 0, "trailing mirror: the plain symmetric mode"
+    main = torch.cuda.current_stream(eng.device)
+    cuts = getattr(fr, "cuts", None)
+    for t0, t1, total, rows, cols in sym_tile_chunks(pl.n, fr.tr.band_width, chunk_rows):
+        eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(t0, t1, total), cuts=cuts)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        mirror_stream.wait_event(ev)
+        with torch.cuda.stream(mirror_stream):
+            eng.gram_mirror_rect(K, pl.n, rows, cols, mirror_workgroups)
+    done = torch.cuda.Event()
+    done.record(mirror_stream)
+    main.wait_event(done)
+    return K
+
+
 def kernel_step(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan, K: Optional[torch.Tensor] = None,
                 mirror_workgroups: int = 0) -> Tuple[torch.Tensor, Front]:
     """One whole un-pipelined step (front + K assembly); returns (K buffer, front)."""

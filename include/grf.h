@@ -429,6 +429,14 @@ int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_e
  * 4 per CU was best beside the next step's walks: tools/gpu_mirror_ab.sh). */
 int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups, grf_stream_t stream);
 
+/* The mirror pass over one rectangle of K: for the 64 x 64 blocks of rows [row_begin, row_end) x
+ * columns [col_begin, col_end) on or above the diagonal, K[j, i] = K[i, j] (j > i).  Starts are
+ * multiples of 64.  A trailing mirror issues it per (row range, band) chunk of grf_gram_sparse_upper
+ * tiles (same reference line as grf_gram_sparse_sym: the K = Phi Phi^T of
+ * graph_kernels_sparse/fast_grf_kernel_general.py:55). */
+int32_t grf_gram_mirror_rect(int64_t n, float *K, int64_t ldk, int64_t row_begin, int64_t row_end, int64_t col_begin,
+                             int64_t col_end, int64_t max_workgroups, grf_stream_t stream);
+
 /* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
  * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */
 int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
