@@ -30,6 +30,20 @@ namespace grf {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// The Gram tiles' K stores and the swizzled mirror's K loads: non-temporal (K is write-once and
+// larger than every cache).  -DGRF_GRAM_K_NT=0 builds them with the default policy (an A/B build for
+// the trailing mirror, tools/trail_exp.py: the Infinity Cache keeps what default-policy stores wrote).
+#ifndef GRF_GRAM_K_NT
+#define GRF_GRAM_K_NT 1
+#endif
+#if GRF_GRAM_K_NT
+#define GRF_K_STORE(v, p) __builtin_nontemporal_store((v), (p))
+#define GRF_K_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define GRF_K_STORE(v, p) (*(p) = (v))
+#define GRF_K_LOAD(p) (*(p))
+#endif
+
 constexpr int kChunk = 1024;  // stream positions covered by one bucket-id chunk (16 per lane)
 constexpr int kSub = 8;       // sub-bands of the transpose's split (grf_transpose_banded_self, t_split)
 constexpr int kPairBytesG = 12;  // one record pair
@@ -534,7 +548,7 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             o[2] = fx_to_float(b[0], sh);
             o[3] = fx_to_float(b[1], sh);
             if (addk) o += __builtin_nontemporal_load(&k4[i]);
-            __builtin_nontemporal_store(o, &k4[i]);
+            GRF_K_STORE(o, &k4[i]);
         }
         for (int64_t i = n4 * 4 + tid; i < wlen; i += 64 * kWaves)
             krow[i] = addk ? fx_to_float(acc[i], sh) + krow[i] : fx_to_float(acc[i], sh);
@@ -663,7 +677,7 @@ __device__ __forceinline__ void gram_mirror_block_swz_at(int64_t n, int64_t bi, 
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
-        const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(K + (i0 + y) * ldk + j0 + x));
+        const f32x4 v = GRF_K_LOAD(reinterpret_cast<const f32x4 *>(K + (i0 + y) * ldk + j0 + x));
         *reinterpret_cast<f32x4 *>(tile + swz(y, x)) = v;
     }
     __syncthreads();

@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -300,24 +300,33 @@ def sym_tile_chunks(n: int, W: int, chunk_rows: int):
 
 
 def k_assembly_trailing(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, mirror_stream: torch.cuda.Stream,
-                        chunk_rows: int = 4096, mirror_workgroups: int = 0) -> torch.Tensor:
+                        chunk_rows: int = 4096, mirror_workgroups: int = 0,
+                        tile_streams: Sequence[torch.cuda.Stream] = ()) -> torch.Tensor:
     """Symmetric K assembly with a trailing mirror: the Gram tiles run chunk by chunk (``sym_tile_chunks``)
     on the caller's stream, and each chunk's lower-triangle copy (``gram_mirror_rect``) follows on
     ``mirror_stream`` as soon as that chunk is written, beside the next chunks' tiles, while its K
     lines may still be in the Infinity Cache.  No chunk's mirror writes an entry a later tile writes
     (a band's tiles write only columns >= the band's start; its square is mirrored after all its
-    rows), so K is bit-identical to tiles + ``gram_mirror``.  The caller's stream waits for the last
-    mirror before it returns."""
+    rows), so K is bit-identical to tiles + ``gram_mirror``.  tile_streams: further streams the tile
+    chunks are dealt to round-robin with the caller's (no chunk waits for another, so one chunk's last
+    tiles overlap the next chunk's first).  The caller's stream waits for the last mirror before it returns."""
     assert pl.mode == "sym" and not pl.fused and pl.hubs == 0, "trailing mirror: the plain symmetric mode"
     main = torch.cuda.current_stream(eng.device)
+    streams = [main] + list(tile_streams)
+    for s in streams[1:]:
+        s.wait_stream(main)  # (the front's buffers)
     cuts = getattr(fr, "cuts", None)
-    for t0, t1, total, rows, cols in sym_tile_chunks(pl.n, fr.tr.band_width, chunk_rows):
-        eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(t0, t1, total), cuts=cuts)
-        ev = torch.cuda.Event()
-        ev.record(main)
+    for c, (t0, t1, total, rows, cols) in enumerate(sym_tile_chunks(pl.n, fr.tr.band_width, chunk_rows)):
+        st = streams[c % len(streams)]
+        with torch.cuda.stream(st):
+            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(t0, t1, total), cuts=cuts)
+            ev = torch.cuda.Event()
+            ev.record(st)
         mirror_stream.wait_event(ev)
         with torch.cuda.stream(mirror_stream):
             eng.gram_mirror_rect(K, pl.n, rows, cols, mirror_workgroups)
+    for s in streams[1:]:
+        main.wait_stream(s)
     done = torch.cuda.Event()
     done.record(mirror_stream)
     main.wait_event(done)

@@ -22,7 +22,7 @@ def main():
             if mode == "cold":
                 flush.fill_(2.0)
             s.record()
-            torch.sum(x, out=out[:1])  # read only
+            x.sum()  # read only
             e.record()
             torch.cuda.synchronize()
             ms = s.elapsed_time(e)
