@@ -529,6 +529,11 @@ def main():
                          "mirror; its transpose follows on the main stream after the mirror")
     ap.add_argument("--mirror-wgs", type=int, default=1024,
                     help="pipelined symmetric K: the mirror pass's workgroups beside the next front (0 = one per block)")
+    ap.add_argument("--trailing", type=int, default=0,
+                    help="symmetric mode: Gram tiles in (row range, band) chunks of this many rows, each chunk's "
+                         "mirror trailing it on its own stream (pipeline.k_assembly_trailing); 0 = one mirror pass")
+    ap.add_argument("--tile-streams", type=int, default=3,
+                    help="--trailing: streams the tile chunks are dealt to")
     ap.add_argument("--k-buffers", type=int, choices=[1, 2], default=1,
                     help="pipelined symmetric K: 2 = alternate two resident K buffers, the mirror of step s on a "
                          "third stream beside step s+1's front and Gram tiles (+1 K of HBM)")
@@ -634,6 +639,8 @@ def main():
 
     side = torch.cuda.Stream(dev)  # the next step's front runs here while the Gram runs on `main`
     main = torch.cuda.current_stream(dev)
+    # --trailing: the trailing mirror's stream, then the extra tile-chunk streams
+    trail_streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.tile_streams))] if args.trailing else []
 
     if args.k_buffers == 2 and pl.mode == "sym" and (args.overlap is not False):
         Ks.append(P.alloc_k(eng, pl))
@@ -682,7 +689,8 @@ def main():
                 main.wait_event(mirror_done[i])  # this K's previous mirror still reads its upper triangle
         out = P.k_assembly(eng, fr, pl, Ks[i], after_tiles=after_gram,
                            mirror_workgroups=args.mirror_wgs if after_gram else 0, front_at=args.front_at,
-                           mirror_stream=mstream if paired else None)
+                           mirror_stream=mstream if paired else None, trailing=args.trailing,
+                           trail_streams=trail_streams)
         if paired:
             mirror_done[i] = out
         if record:
@@ -923,6 +931,8 @@ def main():
         "front_split": bool(args.front_split and ov and pl.mode == "sym"),
         "front_at": args.front_at,
         "k_buffers": len(Ks),
+        "trailing": args.trailing,
+        "tile_streams": args.tile_streams if args.trailing else None,
         "serial_ms_per_step": serial_ms,
     }
     if dist_info is not None:

@@ -205,13 +205,16 @@ def front_transpose(eng: GRFEngine, pl: StepPlan, fr: Front) -> Front:
 
 def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
                after_tiles: Optional[Callable[[torch.cuda.Event], None]] = None, mirror_workgroups: int = 0,
-               front_at: float = 1.0, mirror_stream: Optional[torch.cuda.Stream] = None):
+               front_at: float = 1.0, mirror_stream: Optional[torch.cuda.Stream] = None,
+               trailing: int = 0, trail_streams: Sequence[torch.cuda.Stream] = ()):
     """The K assembly of one step from its front.  Symmetric mode: ``after_tiles(event)`` is called
     between the Gram tiles and the mirror (the pipelined bench issues the next front there, beside
     the HBM-bound mirror; ``mirror_workgroups`` then bounds the mirror's grid, 1024 measured best).
     mirror_stream (symmetric mode): the mirror runs there after the tiles, so that the caller's stream
     can start the next step's Gram tiles -- into another K buffer -- before it ends; returns the event
-    recorded after the mirror (the caller orders the next write of this K after it) instead of K."""
+    recorded after the mirror (the caller orders the next write of this K after it) instead of K.
+    trailing > 0 (symmetric mode): ``k_assembly_trailing`` with chunks of that many rows, the mirror on
+    ``trail_streams[0]``, the tile chunks dealt to the caller's stream and ``trail_streams[1:]``."""
     from .dist import allreduce_buckets
 
     if pl.mode == "cols" and pl.hubs > 0:
@@ -240,6 +243,9 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
                 tiles_done.record(main)
         if after_tiles is not None:
             after_tiles(tiles_done)
+    elif pl.mode == "sym" and trailing > 0 and not pl.fused and pl.hubs == 0 and mirror_stream is None:
+        k_assembly_trailing(eng, fr, pl, K, trail_streams[0], chunk_rows=trailing, tile_streams=trail_streams[1:],
+                            after_tiles=after_tiles, front_at=front_at)
     elif pl.mode == "sym" and pl.hubs > 0:
         eng.gram_sparse_sym_hubs(fr.phi, fr.tr, pl.hubs, out=K, mirror_workgroups=mirror_workgroups,
                                  after_tiles=after_tiles, skewed=pl.skewed,
@@ -301,7 +307,9 @@ def sym_tile_chunks(n: int, W: int, chunk_rows: int):
 
 def k_assembly_trailing(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, mirror_stream: torch.cuda.Stream,
                         chunk_rows: int = 4096, mirror_workgroups: int = 0,
-                        tile_streams: Sequence[torch.cuda.Stream] = ()) -> torch.Tensor:
+                        tile_streams: Sequence[torch.cuda.Stream] = (),
+                        after_tiles: Optional[Callable[[torch.cuda.Event], None]] = None,
+                        front_at: float = 1.0) -> torch.Tensor:
     """Symmetric K assembly with a trailing mirror: the Gram tiles run chunk by chunk (``sym_tile_chunks``)
     on the caller's stream, and each chunk's lower-triangle copy (``gram_mirror_rect``) follows on
     ``mirror_stream`` as soon as that chunk is written, beside the next chunks' tiles, while its K
@@ -309,14 +317,27 @@ def k_assembly_trailing(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor
     (a band's tiles write only columns >= the band's start; its square is mirrored after all its
     rows), so K is bit-identical to tiles + ``gram_mirror``.  tile_streams: further streams the tile
     chunks are dealt to round-robin with the caller's (no chunk waits for another, so one chunk's last
-    tiles overlap the next chunk's first).  The caller's stream waits for the last mirror before it returns."""
+    tiles overlap the next chunk's first).  after_tiles(event) (the pipelined bench's next front) is
+    called once ``front_at`` of the chunks are issued, with an event on the caller's stream after them.
+    The caller's stream waits for the last mirror before it returns."""
     assert pl.mode == "sym" and not pl.fused and pl.hubs == 0, "trailing mirror: the plain symmetric mode"
     main = torch.cuda.current_stream(eng.device)
     streams = [main] + list(tile_streams)
     for s in streams[1:]:
         s.wait_stream(main)  # (the front's buffers)
     cuts = getattr(fr, "cuts", None)
-    for c, (t0, t1, total, rows, cols) in enumerate(sym_tile_chunks(pl.n, fr.tr.band_width, chunk_rows)):
+    chunks = list(sym_tile_chunks(pl.n, fr.tr.band_width, chunk_rows))
+    at = min(len(chunks), max(0, int(round(front_at * len(chunks)))))
+
+    def issue_front():
+        if after_tiles is not None:
+            ev = torch.cuda.Event()
+            ev.record(main)
+            after_tiles(ev)
+
+    for c, (t0, t1, total, rows, cols) in enumerate(chunks):
+        if c == at:
+            issue_front()
         st = streams[c % len(streams)]
         with torch.cuda.stream(st):
             eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(t0, t1, total), cuts=cuts)
@@ -327,6 +348,8 @@ def k_assembly_trailing(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor
             eng.gram_mirror_rect(K, pl.n, rows, cols, mirror_workgroups)
     for s in streams[1:]:
         main.wait_stream(s)
+    if at == len(chunks):
+        issue_front()
     done = torch.cuda.Event()
     done.record(mirror_stream)
     main.wait_event(done)

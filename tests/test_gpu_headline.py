@@ -253,6 +253,36 @@ def test_c5_column_block_with_hub_split(eng):
     del K, fr
 
 
+@pytest.mark.parametrize("graph", ["er_odd", "powerlaw"])
+def test_trailing_mirror_bit_identical(eng, graph):
+    """bench --trailing: the symmetric Gram tiles in (row range, band) chunks dealt to several streams, each
+    chunk's mirror trailing it on another (pipeline.k_assembly_trailing), give the whole K of tiles + one
+    mirror pass bit for bit -- odd n (ragged last band and 64-block), chunk rows below / at / above the
+    band width, pair-balanced wave shares on the skewed graph."""
+    import torch
+    from grf_amd import pipeline as P
+    from grf_amd.engine import DeviceCSR
+    from grf_amd.graphs import er_graph_exact_edges, powerlaw_graph
+
+    A = er_graph_exact_edges(30_001, 200_000, seed=3) if graph == "er_odd" else powerlaw_graph(60_000, 10.0, 2.5, seed=1)
+    n = A.shape[0]
+    pl = P.plan_step(n, 32, 6, 0.1, _diffusion(6))
+    assert pl.mode == "sym"
+    K, fr = P.kernel_step(eng, DeviceCSR.from_scipy(A, eng.device), pl)
+    streams = [torch.cuda.Stream(eng.device) for _ in range(3)]
+    for chunk in (192, 4096, 8192):
+        K2 = P.alloc_k(eng, pl)
+        K2.fill_(float("nan"))
+        fired = []
+        P.k_assembly(eng, fr, pl, K2, trailing=chunk, trail_streams=streams, front_at=0.5,
+                     after_tiles=lambda ev: fired.append(ev))
+        torch.cuda.synchronize()
+        assert len(fired) == 1
+        assert torch.equal(P.k_view(K2, pl), P.k_view(K, pl)), chunk
+        del K2
+    del K, fr
+
+
 def test_dense_path_bench_pipelined_line():
     """bench.py's dense-path workload (C3) pipelined: the next step's front on a side stream beside this
     step's MFMA Gram.  The line keeps the contract fields, reports the pipelining, the serial latency
