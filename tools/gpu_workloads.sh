@@ -8,7 +8,10 @@ run() {  # run <name> <timeout> <bench args...>
     timeout -k 10 $t python -u bench.py "$@" > $O/$name.json 2> $O/$name.err && echo "$name ok $(tail -c 300 $O/$name.json)"
 }
 run enron 300 --graph enron && \
+run facebook 300 --graph facebook && \
 run c5 400 --workload c5 && \
+run c2 300 --workload c2 && \
+run c2_sparse 300 --workload c2 --path sparse && \
 run rows 300 --no-sym && \
 run predict 300 --workload predict --steps 5 --warmup 1 && \
 run c3 300 --workload c3 && \
