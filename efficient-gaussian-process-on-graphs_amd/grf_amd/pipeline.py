@@ -244,7 +244,8 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
         if after_tiles is not None:
             after_tiles(tiles_done)
     elif pl.mode == "sym" and trailing > 0 and not pl.fused and pl.hubs == 0 and mirror_stream is None:
-        k_assembly_trailing(eng, fr, pl, K, trail_streams[0], chunk_rows=trailing, tile_streams=trail_streams[1:],
+        streams = list(trail_streams) or [torch.cuda.Stream(eng.device)]
+        k_assembly_trailing(eng, fr, pl, K, streams[0], chunk_rows=trailing, tile_streams=streams[1:],
                             after_tiles=after_tiles, front_at=front_at)
     elif pl.mode == "sym" and pl.hubs > 0:
         eng.gram_sparse_sym_hubs(fr.phi, fr.tr, pl.hubs, out=K, mirror_workgroups=mirror_workgroups,
