@@ -524,23 +524,8 @@ def main():
                     help="pipelined: the next front starts after this fraction of the Gram tiles (1 = at the mirror, "
                          "0 = with the tiles); default: 0 when the front outlasts the mirror (n < 400 m: Facebook "
                          "2.78 -> 2.45 ms per K), else 1 (C4: the front beside the Gram tiles loses)")
-    ap.add_argument("--front-split", action="store_true",
-                    help="pipelined symmetric K: only the next step's Laplacian, walks and compaction run beside the "
-                         "mirror; its transpose follows on the main stream after the mirror")
     ap.add_argument("--mirror-wgs", type=int, default=1024,
                     help="pipelined symmetric K: the mirror pass's workgroups beside the next front (0 = one per block)")
-    ap.add_argument("--trailing", type=int, default=0,
-                    help="symmetric mode: Gram tiles in (row range, band) chunks of this many rows, each chunk's "
-                         "mirror trailing it on its own stream (pipeline.k_assembly_trailing); 0 = one mirror pass")
-    ap.add_argument("--tile-streams", type=int, default=3,
-                    help="--trailing: streams the tile chunks are dealt to")
-    ap.add_argument("--k-buffers", type=int, choices=[1, 2], default=1,
-                    help="pipelined symmetric K: 2 = alternate two resident K buffers, the mirror of step s on a "
-                         "third stream beside step s+1's front and Gram tiles (+1 K of HBM)")
-    ap.add_argument("--fused", dest="fused", action="store_true", default=None,
-                    help="one GPU, whole K: the symmetric completion inside the Gram tiles (the last tile of every "
-                         "32-row group writes the group's block transposed; no mirror pass)")
-    ap.add_argument("--no-fused", dest="fused", action="store_false", help="Gram tiles + a separate mirror pass")
     ap.add_argument("--balance", choices=["nodes", "phi"], default="nodes",
                     help="N > 1 source shards: equal node ranges (default), or ranges of equal estimated step work "
                          "from the per-source Phi row counts of one setup walk (dist.balanced_shards)")
@@ -603,14 +588,10 @@ def main():
         if args.balance != "nodes":
             shards = balanced_shards(eng, A_dev, m, p, L, f, world, policy=args.balance, phi=phi0)
     pl = P.plan_step(n, m, L, p, f, seed=42, world=world, rank=rank, mode=args.mode, k_rows=args.k_rows,
-                     band_width=args.band_width, no_sym=args.no_sym, shards=shards, fused=args.fused,
-                     collective=coll)
-    if pl.mode == "sym" and not pl.fused:
+                     band_width=args.band_width, no_sym=args.no_sym, shards=shards, collective=coll)
+    if pl.mode == "sym":
         hubs_auto, pl.skewed = auto_hubs(eng, A_dev, m, p, L, f)
         pl.hubs = int(args.hubs) if args.hubs > 0 else (hubs_auto if args.hubs < 0 else 0)
-    elif args.hubs > 0 and pl.mode == "cols" and not coll:
-        # the column block's hub-column split (C5 A/B: profiles/r03_c5_hubs_ab.txt); explicit counts only
-        pl.hubs = int(args.hubs)
     if phi0 is not None:
         if args.gather_bound == "exact":
             # the Phi all-gather moves each rank's actual entries (C4: 435 per row) instead of its rows x
@@ -620,10 +601,6 @@ def main():
         del phi0
     b, e, kr_end = pl.b, pl.e, pl.kr_end
     K = P.alloc_k(eng, pl)  # resident output block, reused
-    Ks = [K]
-    mstream = None
-    mirror_done = [None, None]  # per K buffer: the event after its last mirror (the next tiles wait)
-    kbuf = [0]
     if args.overlap is None:
         # one GPU, whole K: the next front beside the mirror; N > 1 row / column blocks: the next
         # front's collectives beside this step's Gram (the compute of a front beside a Gram gains
@@ -635,16 +612,9 @@ def main():
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     walk_ev = []  # (start, end) events around walk_phi in the serial-latency steps (kernel alone)
     last = [None]
-    last_k = [None]
 
     side = torch.cuda.Stream(dev)  # the next step's front runs here while the Gram runs on `main`
     main = torch.cuda.current_stream(dev)
-    # --trailing: the trailing mirror's stream, then the extra tile-chunk streams
-    trail_streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.tile_streams))] if args.trailing else []
-
-    if args.k_buffers == 2 and pl.mode == "sym" and (args.overlap is not False):
-        Ks.append(P.alloc_k(eng, pl))
-        mstream = torch.cuda.Stream(dev)  # the mirror of step s, beside step s+1's front and tiles
 
     if args.front_at is None:
         # the mirror moves 4 n^2 bytes (~6.7e-13 n^2 s), the next front ~2.7e-10 s per walk (C4: 3.5 ms for
@@ -652,11 +622,7 @@ def main():
         # (profiles/r03_front_at_ab.txt)
         args.front_at = 0.0 if n < 400 * m else 1.0
 
-    split_front = [False]  # (set while the timed / warm-up steps run with --front-split)
-
     def front(record_walk: bool = False):
-        if split_front[0]:
-            return P.front_walk(eng, A_dev, pl)  # the transpose follows on `main` (back_on_main)
         if record_walk:
             # the walk kernel timed alone (serial steps): events around the front's walk_phi launch
             orig = eng.walk_phi
@@ -681,23 +647,12 @@ def main():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         # (pipelined: a 1024-workgroup mirror leaves CU slots to the next front)
-        paired = mstream is not None and after_gram is not None
-        i = kbuf[0] if paired else 0
-        if paired:
-            kbuf[0] ^= 1
-            if mirror_done[i] is not None:
-                main.wait_event(mirror_done[i])  # this K's previous mirror still reads its upper triangle
-        out = P.k_assembly(eng, fr, pl, Ks[i], after_tiles=after_gram,
-                           mirror_workgroups=args.mirror_wgs if after_gram else 0, front_at=args.front_at,
-                           mirror_stream=mstream if paired else None, trailing=args.trailing,
-                           trail_streams=trail_streams)
-        if paired:
-            mirror_done[i] = out
+        P.k_assembly(eng, fr, pl, K, after_tiles=after_gram, mirror_workgroups=args.mirror_wgs if after_gram else 0,
+                     front_at=args.front_at)
         if record:
-            ev[1].record(mstream if paired else main)
+            ev[1].record(main)
             gram_ev.append(ev)
         last[0] = fr
-        last_k[0] = Ks[i]
 
     def front_on_side(after=None, independent=False):
         # after: an event on `main`; default: everything issued on `main` so far.  independent: no
@@ -718,16 +673,14 @@ def main():
     def back_on_main(frd, record, after_gram=None):
         fr, done = frd
         main.wait_event(done)
-        for obj in (fr.phi, fr.tr, fr.local, fr.row_shift):  # allocated on `side`, used on `main`
+        # every device buffer the front allocated on `side` (Phi, the transpose, the row cuts, ...) is
+        # used on `main`: recorded there, so the allocator does not hand it out before `main` is done
+        for obj in vars(fr).values():
             if obj is None:
                 continue
-            for v in ([obj] if torch.is_tensor(obj) else vars(obj).values()):
+            for v in ([obj] if torch.is_tensor(obj) else vars(obj).values() if hasattr(obj, "__dict__") else []):
                 if torch.is_tensor(v) and v.is_cuda:
                     v.record_stream(main)
-        if fr.tr is None:
-            # --front-split: the transpose runs on `main` after the previous step's mirror (alone, not
-            # beside it: beside the HBM-bound mirror its latency-bound region gathers ran 5x slower)
-            P.front_transpose(eng, pl, fr)
         back(fr, record, after_gram)
 
     def run(steps: int, record: bool, record_walk: bool = False):
@@ -758,7 +711,6 @@ def main():
                 back_on_main(cur, record)
                 cur = front_on_side(independent=True) if s_ + 1 < steps else None
 
-    split_front[0] = bool(args.front_split and args.overlap and pl.mode == "sym")
     run(args.warmup, False)
     torch.cuda.synchronize()
     if coll:
@@ -772,13 +724,16 @@ def main():
     t = time.perf_counter() - t0
     gather_stats = D.GATHER_STATS or []
     D.GATHER_STATS = None
+    if coll:
+        from grf_amd.dist import check_gather_overflow
+        check_gather_overflow(dev)  # (raises if a bounded all-gather truncated a rank's Phi)
+    # in-run parity of the LAST TIMED step's K block (the pipelined path itself) against the Phi that
+    # step gathered (every rank), before the serial steps below overwrite K
+    parity = P.k_block_check(eng, last[0], pl, K)
     # latency of one un-pipelined step (reported beside the throughput; not part of `value`), with
     # the walk kernel timed alone there
     ov = args.overlap
     args.overlap = False
-    split_front[0] = False
-    if mstream is not None:
-        main.wait_stream(mstream)
     run(1, False)  # (warm-up of the serial order)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -786,11 +741,6 @@ def main():
     torch.cuda.synchronize()
     serial_ms = 1000.0 * (time.perf_counter() - t1) / 3
     args.overlap = ov
-    if coll:
-        from grf_amd.dist import check_gather_overflow
-        check_gather_overflow(dev)  # (raises if a bounded all-gather truncated a rank's Phi)
-    # in-run parity of the last step's K block against the Phi that step gathered (every rank)
-    parity = P.k_block_check(eng, last[0], pl, last_k[0])
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
     walk_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in walk_ev]))
     coll_ms = float(np.mean([a.elapsed_time(b_) for a, b_, _, _ in gather_stats])) if gather_stats else 0.0
@@ -834,8 +784,7 @@ def main():
         alg_bytes = 4.0 * n * n + 8.0 * nnz_phi + 8.0 * nnz_phi * rows / n
     achieved = alg_bytes / (gram_avg * 1e-3) / 1e9
     sym = pl.mode == "sym"
-    mirror = "grf::gram_mirror_kernel" if os.environ.get("GRF_MIRROR_PADDED", "0") == "1" else "grf::gram_mirror_swz_kernel"
-    kernels = ["grf::gram_sparse_kernel", mirror] if sym and not pl.fused else ["grf::gram_sparse_kernel"]
+    kernels = ["grf::gram_sparse_kernel", "grf::gram_mirror_swz_kernel"] if sym else ["grf::gram_sparse_kernel"]
     headline = (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and args.graph == "er" and world == 1 and sym
     traffic = pmc_traffic(kernels) if headline else None
     # the walk kernel (phi_fused_kernel): per walk, E[moves] = (1-p)(1-(1-p)^(L-1))/p recorded moves,
@@ -886,15 +835,14 @@ def main():
                    "k_rows_per_gpu": rows, "shard": [b, e], "balance": args.balance if coll else None,
                    "gather_entries_per_rank": pl.gather_bound or None,
                    "hub_columns": pl.hubs or None,
-                   "pair_balanced_waves": (pl.mode == "sym" and not pl.fused) and
+                   "pair_balanced_waves": pl.mode == "sym" and
                    (engine_mod.ROW_CUTS == "1" or (engine_mod.ROW_CUTS == "auto" and bool(pl.skewed))),
                    "parallelism": (f"source-sharded x{world}, Phi all-gather, partial K over inner slices + "
                                    f"RCCL all-reduce (K replicated)") if pl.mode == "allreduce" else
                                   (f"source-sharded x{world}, Phi all-gather, K column blocks K[:, R_r] from each "
                                    f"rank's own-rows transpose") if cols else
                                   f"source-sharded x{world}, Phi all-gather, K row blocks"
-                                  + ((" (one GPU: symmetric tiles completing K by their last arrivers)" if pl.fused
-                                      else " (one GPU: symmetric tiles + mirror)") if sym else "")},
+                                  + (" (one GPU: symmetric tiles + mirror)" if sym else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": (f"rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of the same kernels on this workload, "
@@ -927,12 +875,9 @@ def main():
                                               f"(pipelined it shares HBM with the mirror)"},
         "nnz_phi": nnz_phi,
         "parity": parity,
+        "parity_note": "the last timed (pipelined) step's K block, checked after the timed region",
         "pipelined": bool(ov),
-        "front_split": bool(args.front_split and ov and pl.mode == "sym"),
         "front_at": args.front_at,
-        "k_buffers": len(Ks),
-        "trailing": args.trailing,
-        "tile_streams": args.tile_streams if args.trailing else None,
         "serial_ms_per_step": serial_ms,
     }
     if dist_info is not None:

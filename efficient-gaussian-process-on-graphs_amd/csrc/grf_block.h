@@ -107,8 +107,9 @@ __device__ inline void block_bitonic_sort(KT *key, int P) {
 // bitmask mode for 4..16 (within 32 lanes, no address operand), ds_bpermute for 32.
 template <int TJ>
 __device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v) {
-    if constexpr (TJ == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
-    else if constexpr (TJ == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    // (mov_dpp with bound_ctrl: no `old` operand to zero first -- a quad permute never leaves the quad)
+    if constexpr (TJ == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+    else if constexpr (TJ == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);
     else if constexpr (TJ < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (TJ << 10));
     else return (uint32_t)__shfl_xor((int)v, TJ, 64);
 }
@@ -130,14 +131,29 @@ __device__ __forceinline__ KT bitonic_keep(KT a, KT o, bool take_min) {
     return take_min ? mn : mx;
 }
 
+// u32 keys: the same keep as ONE v_med3_u32 against a per-stage selector (0: the minimum, ~0: the
+// maximum -- the median of {a, o, 0} is min(a, o), of {a, o, ~0} max(a, o)), instead of a min, a
+// max and a select per key
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+template <typename KT>
+__device__ __forceinline__ KT bitonic_keep_sel(KT a, KT o, bool take_min, uint32_t sel) {
+    if constexpr (sizeof(KT) == 4) return (KT)med3_u32((uint32_t)a, (uint32_t)o, sel);
+    else return bitonic_keep(a, o, take_min);
+}
+
 template <int TJ, typename KT, int R>
 __device__ __forceinline__ void bitonic_lane_stage(KT (&v)[R], int tid, int k) {
     if (TJ * R < k) {
         // k > TJ R >= R: bit k of the position tid R + r is bit k of tid R for every r (r < R), so
         // the direction is the thread's, computed once per stage
         const bool take_min = ((tid & TJ) == 0) == (((tid * R) & k) == 0);
+        const uint32_t sel = take_min ? 0u : ~0u;
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[r] = bitonic_keep(v[r], lane_xor<TJ>(v[r]), take_min);
+        for (int r = 0; r < R; ++r) v[r] = bitonic_keep_sel(v[r], lane_xor<TJ>(v[r]), take_min, sel);
     }
 }
 
@@ -154,8 +170,9 @@ __device__ __forceinline__ void bitonic_regs_level(KT (&v)[R], KT *key, int tid,
         for (int r = 0; r < R; ++r) key[tid * R + r] = v[r];
         __syncthreads();
         const bool take_min = lo == (((tid * R) & k) == 0);  // (k > R: the thread's direction)
+        const uint32_t sel = take_min ? 0u : ~0u;
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[r] = bitonic_keep(v[r], key[(tid ^ tj) * R + r], take_min);
+        for (int r = 0; r < R; ++r) v[r] = bitonic_keep_sel(v[r], key[(tid ^ tj) * R + r], take_min, sel);
     }
     // partner lane tid ^ tj in this wave
     bitonic_lane_stage<32>(v, tid, k);
@@ -169,14 +186,20 @@ __device__ __forceinline__ void bitonic_regs_level(KT (&v)[R], KT *key, int tid,
         if (jj < k) {
             if (k >= R) {  // one direction for the whole thread (bit k of tid R + r is tid R's)
                 const bool asc = ((tid * R) & k) == 0;
+                const uint32_t sel = asc ? 0u : ~0u;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const int p = r ^ jj;
                     if (p > r) {
                         const KT a = v[r], b = v[p];
-                        const KT mn = b < a ? b : a, mx = b < a ? a : b;
-                        v[r] = asc ? mn : mx;
-                        v[p] = asc ? mx : mn;
+                        if constexpr (sizeof(KT) == 4) {  // (two medians: the kept minimum / maximum)
+                            v[r] = (KT)med3_u32((uint32_t)a, (uint32_t)b, sel);
+                            v[p] = (KT)med3_u32((uint32_t)a, (uint32_t)b, ~sel);
+                        } else {
+                            const KT mn = b < a ? b : a, mx = b < a ? a : b;
+                            v[r] = asc ? mn : mx;
+                            v[p] = asc ? mx : mn;
+                        }
                     }
                 }
             } else {

@@ -19,7 +19,7 @@ extern "C" {
 
 const char *grf_last_error(void) { return grf::g_err; }
 
-int32_t grf_version(void) { return 1; }
+int32_t grf_version(void) { return GRF_ABI_VERSION; }
 
 int32_t grf_device_count(void) {
     int n = 0;

@@ -64,6 +64,15 @@ __global__ __launch_bounds__(256) void csr_tr_gather_kernel(int64_t n_sel, const
     }
 }
 
+// nnz given as an upper bound (no host read of the gathered count): the positions past the gathered
+// entries get the key n_cols, so they sort after every column and t_ptr[n_cols] ends at the real count
+__global__ __launch_bounds__(256) void csr_tr_pad_kernel(int64_t nnz, int64_t n_sel, const int64_t *off,
+                                                         int64_t n_cols, uint32_t *keys) {
+    const int64_t total = n_sel > 0 ? off[n_sel] : 0;
+    for (int64_t i = total + (int64_t)blockIdx.x * 256 + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * 256)
+        keys[i] = (uint32_t)n_cols;
+}
+
 // sorted keys -> t_ptr (first position of every column, n_cols + 1 entries) and t_idx / t_val
 __global__ __launch_bounds__(256) void csr_tr_unpack_kernel(int64_t nnz, int64_t n_cols, const uint32_t *keys,
                                                             const uint64_t *vals, int64_t *t_ptr, int32_t *t_idx,
@@ -631,6 +640,12 @@ int32_t grf_csr_transpose(int64_t n_sel, const int64_t *ptr, const int32_t *idx,
         csr_tr_gather_kernel<<<(unsigned)cdiv<int64_t>(n_sel, 4), 256, 0, st>>>(n_sel, ptr, idx, val, row_map, off, k0,
                                                                                v0);
         GRF_CHECK_LAUNCH("csr_tr_gather_kernel");
+    }
+    if (nnz > 0) {
+        // (nnz may bound the gathered entries from above: pad the tail with the key n_cols)
+        csr_tr_pad_kernel<<<(unsigned)std::min<int64_t>(cdiv<int64_t>(nnz, 256), 1024), 256, 0, st>>>(nnz, n_sel, off,
+                                                                                                    n_cols, k0);
+        GRF_CHECK_LAUNCH("csr_tr_pad_kernel");
     }
     if (nnz > 0) {
         GRF_CHECK_HIP(rocprim::radix_sort_pairs(w, temp_bytes, (const uint32_t *)k0, k1, (const uint64_t *)v0, v1,

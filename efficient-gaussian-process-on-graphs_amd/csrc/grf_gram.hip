@@ -17,8 +17,7 @@
 // that miss L2; the symmetric mode computes the tiles on and above the diagonal
 // band and a mirror pass copies the upper triangle down.
 //
-// Dense path: LDS-tiled fp32 MFMA (v_mfma_f32_32x32x2f32, exact f32 FMA chain),
-// 128x128 tile per 256-thread workgroup, 2x2 waves of 64x64.
+// Dense path: grf_gram_dense.hip (fp32 MFMA, 128 x 128 tiles on and above the diagonal).
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -31,8 +30,8 @@ namespace grf {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // The Gram tiles' K stores and the swizzled mirror's K loads: non-temporal (K is write-once and
-// larger than every cache).  -DGRF_GRAM_K_NT=0 builds them with the default policy (an A/B build for
-// the trailing mirror, tools/trail_exp.py: the Infinity Cache keeps what default-policy stores wrote).
+// larger than every cache).  -DGRF_GRAM_K_NT=0 builds them with the default policy (A/B build: the
+// Infinity Cache keeps what default-policy stores wrote, profiles/r03_gram_persist_ab.txt).
 #ifndef GRF_GRAM_K_NT
 #define GRF_GRAM_K_NT 1
 #endif
@@ -246,126 +245,6 @@ struct GramTiles {
     }
 };
 
-// ---------------------------------------------------------------- fused symmetric completion
-// grf_gram_sparse_sym_fused: the Gram tiles of the symmetric mode complete K themselves (no
-// separate mirror pass re-reading the upper triangle from HBM).  The tiles of one band are
-// dispatched row after row, so the 64 tiles of a row group g = rows [gs, gs + 64) of band J run
-// together; each writes its row K[i, band J] write-through (sc1: visible to every XCD without a
-// release fence), drains its stores and takes a ticket on the group's counter.  The last arriver
-// (no waiting: the others exit) acquires and transposes the group's 64 x W block into
-// K[band J, gs : gs + 64] (256-byte row segments, 4 x 4 register transposes).  Ownership keeps
-// every lower entry single-writer and ordered after the upper one: on the diagonal band a tile
-// writes only the columns >= its group's first row (the columns before it are lower entries that
-// the earlier groups' last arrivers write), and inside the group's own diagonal block the last
-// arriver overwrites the entries below the diagonal after all rows have been stored.  K is
-// bit-identical to grf_gram_sparse_sym's.
-// MEASURED SLOWER (profiles/r02_fused_ab.txt): 100-150 ms per K against 22.6 for tiles + mirror.
-// The tiles with their tickets cost +0.8 ms and the block loads +5 ms (a timing-only decomposition,
-// since removed), but the last arrivers' transposed stores (20 GB, one workgroup per 1 MB block)
-// add ~100 ms: one workgroup cannot keep enough stores in flight, where the mirror pass spreads the
-// same bytes over every CU.  Kept as a
-// tested option (bench --fused); the default stays tiles + mirror.
-#ifndef GRF_FUSE_GROUP
-#define GRF_FUSE_GROUP 64
-#endif
-constexpr int kFuseGroup = GRF_FUSE_GROUP;         // rows per ticket group (64: 256-byte K row segments)
-
-// The completion's edge cases, element by element: K[j, i] = K[i, j] for the K rows j = j0 + col
-// .. j0 + col + 3 (< j0 + wlen) and i = gs + 4q .. gs + 4q + 3 (< ge, < j: the group's diagonal block)
-__device__ __attribute__((noinline)) void gram_fused_edge(float *__restrict__ K, int64_t ldk, int64_t gs, int64_t ge,
-                                                          int64_t j0, int64_t col, int64_t wlen, int q) {
-    for (int u = 0; u < 4; ++u) {
-        const int64_t i = gs + 4 * q + u;
-        if (i >= ge) break;
-        for (int e = 0; e < 4 && col + e < wlen; ++e) {
-            const int64_t j = j0 + col + e;
-            if (i < j) K[j * ldk + i] = __hip_atomic_load(K + i * ldk + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-template <int kWaves>
-__device__ __forceinline__ void gram_fused_completion(const GramTiles &tl, int64_t J, int64_t r, int64_t j0,
-                                                      int64_t wlen, int sh, unsigned long long *acc,
-                                                      float *__restrict__ K, int64_t ldk,
-                                                      int32_t *__restrict__ tickets) {
-    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    constexpr int kT = 64 * kWaves;
-    const int tid = threadIdx.x;
-    const int64_t gs = r & ~(int64_t)(kFuseGroup - 1);
-    const int64_t rows_J = tl.count(J);
-    const int64_t ge = (gs + kFuseGroup) < rows_J ? gs + kFuseGroup : rows_J;
-    const int gn = (int)(ge - gs);
-    const bool diag = gs >= j0;  // the group's rows lie in this band (j0 <= gs < j0 + W)
-    // 1. the tile's row, write-through: on the diagonal band from the group's first row on
-    const u64x2 *acc2 = reinterpret_cast<const u64x2 *>(acc);
-    float *krow = K + r * ldk + j0;
-    const int64_t c_lo = diag ? gs - j0 : 0;  // a multiple of 32
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(krow, (short)0, 0x7fffffff, 0x00020000);
-    const int64_t n4 = wlen / 4;
-    for (int64_t i = c_lo / 4 + tid; i < n4; i += kT) {
-        const u64x2 a = acc2[2 * i], b = acc2[2 * i + 1];
-        u32x4 o;
-        o[0] = __float_as_uint(fx_to_float(a[0], sh));
-        o[1] = __float_as_uint(fx_to_float(a[1], sh));
-        o[2] = __float_as_uint(fx_to_float(b[0], sh));
-        o[3] = __float_as_uint(fx_to_float(b[1], sh));
-        __builtin_amdgcn_raw_buffer_store_b128(o, rs, (int)(i * 16), 0, 16);  // aux 16: sc1 (write-through)
-    }
-    for (int64_t i = n4 * 4 + tid; i < wlen; i += kT)
-        __hip_atomic_store(krow + i, fx_to_float(acc[i], sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // 2. every storing wave drains, then one ticket for the workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int *flag = reinterpret_cast<int *>(acc);
-    if (tid == 0) {
-        const int64_t ngroups = (tl.rows + kFuseGroup - 1) / kFuseGroup;
-        const int old = __hip_atomic_fetch_add(tickets + J * ngroups + (r / kFuseGroup), 1, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-        flag[0] = old == gn - 1;
-    }
-    __syncthreads();
-    if (!flag[0]) return;  // (uniform) not the last of the group
-    if (tid < 64) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    // 3. the last arriver: K[j, gs : ge] = K[gs : ge, j] for the band's columns j (j > i), in 4 x 4
-    // register transposes (no LDS, no barrier: the tiles still running on this CU keep the LDS
-    // pipe).  Lane (q, g) = (lane % 8, lane / 8) of a wave loads rows 4q .. 4q + 3 of the group at
-    // columns c + 4g .. c + 4g + 3 (8 lanes = one 128-byte segment of a row) and stores them as
-    // rows c + 4g .. c + 4g + 3 of K at columns gs + 4q .. gs + 4q + 3 (8 lanes = one 128-byte
-    // row segment); a wave covers 32 columns, kFuseUnroll column blocks in flight.
-    constexpr int kQ = kFuseGroup / 4, kCols = 4 * (64 / kQ);  // lanes per row segment, columns per wave
-    const int lane = tid & 63, wave = tid >> 6, q = lane % kQ, g = lane / kQ;
-    const auto grs = __builtin_amdgcn_make_buffer_rsrc(K + gs * ldk + j0, (short)0, 0x7fffffff, 0x00020000);
-    const int64_t cb0 = diag ? gs - j0 : 0;
-    // compact code on purpose: this path runs once per 32 tiles, and its instructions share the
-    // instruction cache with the tiles' loop (edge columns / rows go to a separate function)
-    const int32_t row_off = (int32_t)(4 * q * ldk * 4);
-    for (int64_t cb = cb0 + wave * kCols; cb < wlen; cb += kWaves * kCols) {
-        const int64_t col = cb + 4 * g;
-        const int64_t j = j0 + col;  // K rows j .. j + 3 are written
-        if (gn == kFuseGroup && col + 4 <= wlen && j >= ge) {
-            f32x4 x[4];
-            const int32_t off = row_off + (int32_t)(col * 4);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const auto y = __builtin_amdgcn_raw_buffer_load_b128(grs, off + (int32_t)(u * ldk * 4), 0, 16);
-                x[u] = f32x4{__uint_as_float(y[0]), __uint_as_float(y[1]), __uint_as_float(y[2]), __uint_as_float(y[3])};
-            }
-            float *dst = K + j * ldk + gs + 4 * q;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                __builtin_nontemporal_store(f32x4{x[0][e], x[1][e], x[2][e], x[3][e]}, reinterpret_cast<f32x4 *>(dst + e * ldk));
-        } else {
-            gram_fused_edge(K, ldk, gs, ge, j0, col, wlen, q);
-        }
-    }
-}
-
 // One workgroup of kWaves waves = one tile K[row, j0 : j0 + W] (W = a band of the banded
 // transpose), accumulated in LDS in exact int64 fixed point with the per-row power-of-two
 // scale S = 2^rowshift[row] (from the transpose) such that every term |Phi[row,k] Phi[j,k]| S
@@ -382,12 +261,12 @@ __device__ __forceinline__ void gram_fused_completion(const GramTiles &tl, int64
 // and its first two pairs in the 32-byte slot t_rec + 32 b, the other pairs at t_rec + ovf_base + 12 p --
 // so every nonzero contributes two virtual buckets (inline part, overflow part) to the wave's stream,
 // and a small bucket costs one line (header and pairs) instead of a descriptor line and a record line.
-template <int kWaves, int kHalves, int kGramUnroll, bool kTailExact, bool kFuse, bool kSlot = false>
+template <int kWaves, int kHalves, int kGramUnroll, bool kTailExact, bool kSlot = false>
 __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     int64_t n_total, int64_t row_begin, GramTiles tl, int64_t t_begin, const int64_t *__restrict__ ptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val, const uint2 *__restrict__ t_desc,
     const unsigned char *__restrict__ t_rec, int32_t unit, const int32_t *__restrict__ rowshift,
-    float *__restrict__ K, int64_t ldk, int32_t *__restrict__ tickets, const uint16_t *__restrict__ t_split,
+    float *__restrict__ K, int64_t ldk, const uint16_t *__restrict__ t_split,
     int64_t ovf_base, int32_t balance, const int32_t *__restrict__ row_cuts) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W]
     static_assert(!kSlot || kHalves == 1, "slot streams: 2 virtual buckets per nonzero, u8 ids <= 128");
@@ -528,10 +407,6 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
     if (kWaves > 1) __syncthreads();
     else __builtin_amdgcn_wave_barrier();
 
-    if constexpr (kFuse) {
-        gram_fused_completion<kWaves>(tl, J_local, r, j0, wlen, sh, acc, K, ldk, tickets);
-        return;
-    }
     // write the tile once (non-temporal: K is write-once); add_k: K already holds the dense
     // hub-column part of these entries, and the fixed-point sum is rounded once and added to it
     float *krow = K + r * ldk + j0;
@@ -636,28 +511,6 @@ __device__ __forceinline__ void gram_mirror_block_at(int64_t n, int64_t bi, int6
     }
 }
 
-__device__ __forceinline__ void gram_mirror_block(int64_t n, int64_t nt, int64_t b, float *__restrict__ K, int64_t ldk,
-                                                  float (*tile)[65]) {
-    int64_t bi, bj;
-    gram_mirror_tri_coords(nt, b, bi, bj);
-    gram_mirror_block_at(n, bi, bj, K, ldk, tile);
-}
-
-// Symmetric completion: K[j, i] = K[i, j] for every j > i (the Gram launch in symmetric
-// mode wrote the tiles K[i, band >= band(i)], which cover the upper triangle; the lower
-// parts of the diagonal band tiles are overwritten, so K is exactly symmetric).  One
-// workgroup per upper-triangle 64 x 64 block (triangular grid: no idle workgroups) moves
-// it through LDS with 16-byte loads and 16-byte non-temporal stores.  A bounded grid
-// (grid-stride over the blocks) leaves CU slots to work on another stream.
-__global__ __launch_bounds__(256) void gram_mirror_kernel(int64_t n, int64_t nt, int64_t nblocks,
-                                                          float *__restrict__ K, int64_t ldk) {
-    __shared__ float tile[64][65];
-    for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-        gram_mirror_block(n, nt, b, K, ldk, tile);
-        __syncthreads();  // (the tile is reused by the next block)
-    }
-}
-
 // The LDS block without bank conflicts: the 64 x 64 block is stored unpadded with its 16-byte chunks
 // XOR-swizzled by row (element (r, c) at word r * 64 + (c ^ 4 ((r >> 2) & 15))).  Loads of K rows
 // (256 B per row and wave-instruction) go in with ds_write_b128 (8 lanes per LDS cycle: 8 distinct
@@ -723,288 +576,7 @@ __global__ __launch_bounds__(256) void gram_mirror_swz_kernel(int64_t n, int64_t
     }
 }
 
-// The mirror of one rectangle of 64-blocks: block rows [bi0, bi1) x block columns [bj0, bj1), the
-// blocks with bj >= bi (the others are skipped).  A trailing mirror (grf_gram_mirror_rect) completes
-// the tiles of one (row range, band) chunk right after the Gram wrote them, while they may still sit
-// in the Infinity Cache.
-__global__ __launch_bounds__(256) void gram_mirror_rect_kernel(int64_t n, int64_t bi0, int64_t bj0, int64_t nbj,
-                                                               int64_t nblocks, float *__restrict__ K, int64_t ldk) {
-    __shared__ __attribute__((aligned(16))) float tile[64 * 65];
-    for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-        const int64_t bi = bi0 + b / nbj, bj = bj0 + b % nbj;
-        if (bj >= bi) gram_mirror_block_swz_at(n, bi, bj, K, ldk, tile);
-        __syncthreads();
-    }
-}
-
-// The bounded grid (grid-stride over the blocks: the pipelined bench gives the mirror 1024
-// workgroups beside the next step's front), GRF_MIRROR_PIPE=1: a workgroup's loads of its next block
-// are issued before the stores of the current one.  On gfx950 one vmcnt counter covers loads and stores, so a wait for
-// loads issued after stores also waits for those stores' acknowledgements; issued before them, the
-// next block's loads are in flight while the current block is written (profiles/r02_fused_ab.txt,
-// where one workgroup per 1 MB block lost ~100 ms to that serialisation).  Measured beside the next
-// front (profiles/r02_mirror_pipe_ab.txt): the K assembly ends at the same time but the front beside
-// it is slowed (24.9 vs 24.0 ms per step, same box), so it is off by default.
-// Strictly-upper full blocks only (the diagonal blocks and, for n % 64 != 0, the ragged last block
-// column go to gram_mirror_edge_kernel): nf = nt - 1 (n % 64 == 0) or nt - 2 block columns are full,
-// and the strictly-upper blocks of that nf x nf grid are enumerated row-major (bi < bj < nf).
-__device__ __forceinline__ void gram_mirror_upper_coords(int64_t nf, int64_t b, int64_t &i0, int64_t &j0) {
-    // row bi holds nf - 1 - bi blocks; first(bi) = bi (2 nf - bi - 1) / 2
-    const double m = (double)(2 * nf - 1);
-    int64_t bi = (int64_t)((m - sqrt(m * m - 8.0 * (double)b)) * 0.5);
-    auto first = [nf](int64_t i) { return i * (2 * nf - i - 1) / 2; };
-    if (bi < 0) bi = 0;
-    if (bi > nf - 2) bi = nf - 2;
-    while (bi > 0 && first(bi) > b) --bi;
-    while (bi < nf - 2 && first(bi + 1) <= b) ++bi;
-    i0 = bi * 64;
-    j0 = (bi + 1 + (b - first(bi))) * 64;
-}
-
-__global__ __launch_bounds__(256) void gram_mirror_pipe_kernel(int64_t nf, int64_t nblocks, float *__restrict__ K,
-                                                               int64_t ldk) {
-    __shared__ __attribute__((aligned(16))) float tile[64 * 64];
-    const int t = threadIdx.x;
-    auto swz = [](int r, int c) { return r * 64 + (c ^ (4 * ((r >> 2) & 15))); };
-    f32x4 v[4];
-    int64_t i0 = 0, j0 = 0;
-    auto load = [&](int64_t b) {
-        gram_mirror_upper_coords(nf, b, i0, j0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
-            v[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(K + (i0 + y) * ldk + j0 + x));
-        }
-    };
-    auto to_lds = [&]() {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
-            *reinterpret_cast<f32x4 *>(tile + swz(y, x)) = v[q];
-        }
-    };
-    int64_t b = blockIdx.x;
-    if (b >= nblocks) return;
-    load(b);
-    to_lds();
-    __syncthreads();
-    for (; b < nblocks; b += gridDim.x) {
-        const int64_t ci0 = i0, cj0 = j0;
-        // the next block's loads, issued before this block's stores (unconditional, clamped: the wait
-        // for them below is then vmcnt(4), the 4 stores behind them, on every path)
-        load(b + gridDim.x < nblocks ? b + gridDim.x : nblocks - 1);
-        const int k = t & 15, pr = t >> 4;
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-            const int y = 2 * pr + 32 * it;
-            typedef float f32x2 __attribute__((ext_vector_type(2)));
-            typedef __attribute__((address_space(3))) float lds_float;
-            uint32_t a[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) a[c] = (uint32_t)(uintptr_t)(lds_float *)(tile + swz(4 * k + c, y));
-            f32x2 w[4];
-            asm volatile(
-                "ds_read_b64 %0, %4\n\tds_read_b64 %1, %5\n\tds_read_b64 %2, %6\n\tds_read_b64 %3, %7\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
-                : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
-                : "memory");
-            f32x4 o0, o1;
-            o0[0] = w[0].x; o0[1] = w[1].x; o0[2] = w[2].x; o0[3] = w[3].x;
-            o1[0] = w[0].y; o1[1] = w[1].y; o1[2] = w[2].y; o1[3] = w[3].y;
-            __builtin_nontemporal_store(o0, reinterpret_cast<f32x4 *>(K + (cj0 + y) * ldk + ci0 + 4 * k));
-            __builtin_nontemporal_store(o1, reinterpret_cast<f32x4 *>(K + (cj0 + y + 1) * ldk + ci0 + 4 * k));
-        }
-        __syncthreads();  // (this block's LDS reads are done)
-        to_lds();
-        __syncthreads();
-    }
-}
-
-// The blocks gram_mirror_pipe_kernel leaves: the nt diagonal blocks, then the blocks of the last
-// (ragged) block column when n % 64 != 0, then the strictly-upper blocks of full block columns beyond
-// the pipelined grid's enumeration (none: every full strictly-upper block is in it).
-__global__ __launch_bounds__(256) void gram_mirror_edge_kernel(int64_t n, int64_t nt, float *__restrict__ K,
-                                                               int64_t ldk) {
-    __shared__ float tile[64][65];
-    const int64_t e = blockIdx.x;
-    // express the edge block as its index in the triangular enumeration of gram_mirror_block
-    const int64_t bi = e < nt ? e : e - nt, bj = e < nt ? e : nt - 1;
-    const int64_t b = bi * nt - bi * (bi - 1) / 2 + (bj - bi);
-    gram_mirror_block(n, nt, b, K, ldk, tile);
-}
-
 __global__ void absmax_reset_kernel(float *m) { *m = 0.f; }
-
-// ------------------------------------------------------------------ dense MFMA
-// K = A A^T (A: n x k_dim fp32, row-major) on v_mfma_f32_32x32x2f32 (exact f32 FMA chains).
-// Symmetric: only the tiles on and above the diagonal are computed (the mirror pass copies the
-// upper triangle down), so a launch does n^2 k instead of 2 n^2 k flops.  A workgroup of 4 waves
-// (2 x 2) owns a BM x BM tile, each wave (BM/2)^2 as (BM/64)^2 MFMA blocks of 32 x 32; the
-// k-tiles (BK deep, staged k-major through LDS) are software-pipelined: the next tile's global
-// loads are in flight in registers while the current one feeds the MFMAs.  BM = 64 for small n
-// (more workgroups than CUs), 128 otherwise.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-// k-major LDS image, row pitch BM + 32 (the two k-rows one MFMA operand read spans fall on
-// disjoint bank halves) and rows XOR-swizzled by the k group: the transposing stores (8 k-groups
-// x 8 rows per wave) and the operand reads are both conflict-free
-constexpr int kDensePad = 32;
-__device__ __forceinline__ int dense_swz(int k) { return ((k >> 2) & 7) << 3; }
-
-// Split-K (gridDim.y = S > 1, small n: too few tiles to fill the CUs): slice s of the k range,
-// k_split wide, goes to the partial buffer K + s * part_stride; gram_dense_combine_kernel sums the
-// S partials in slice order and writes both triangles.
-template <int BM, int BK>
-__global__ __launch_bounds__(256) void gram_dense_kernel(int64_t n, int64_t nt, int64_t k_dim,
-                                                         const float *__restrict__ A, int64_t lda,
-                                                         float *__restrict__ K, int64_t ldk, int64_t k_split,
-                                                         int64_t part_stride, int32_t n_split) {
-    constexpr int NB = BM / 64;          // 32 x 32 MFMA blocks per wave and dimension
-    constexpr int F4 = BM * BK / 4 / 256;  // float4 loads per thread and operand per k-tile
-    __shared__ __attribute__((aligned(16))) float As[BK][BM + kDensePad];
-    __shared__ __attribute__((aligned(16))) float Bs[BK][BM + kDensePad];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    // workgroup -> (tile b, k slice): the slice is the fastest index, so with round-robin workgroup
-    // placement over the 8 XCDs all tiles of one slice share an XCD (8 slices: one XCD's L2 holds its
-    // slice of the operand; speed only, never correctness); tile b -> (bi, bj), bj >= bi, row-major
-    // over the upper triangle of the nt x nt tile grid
-    const int64_t b = (int64_t)blockIdx.x / n_split;
-    const int32_t slice = (int32_t)((int64_t)blockIdx.x - b * n_split);
-    int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
-    auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };
-    if (bi < 0) bi = 0;
-    if (bi > nt - 1) bi = nt - 1;
-    while (bi > 0 && first(bi) > b) --bi;
-    while (bi < nt - 1 && first(bi + 1) <= b) ++bi;
-    const int64_t bj = bi + (b - first(bi));
-    const int64_t m0 = bi * BM, n0 = bj * BM;
-
-    f32x16 c[NB][NB];
-#pragma unroll
-    for (int x = 0; x < NB; ++x)
-#pragma unroll
-        for (int y = 0; y < NB; ++y)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) c[x][y][q] = 0.f;
-
-    const int64_t kb = (int64_t)slice * k_split;
-    const int64_t ke = (kb + k_split) < k_dim ? kb + k_split : k_dim;
-    K += (int64_t)slice * part_stride;
-    float4 ra[F4], rb[F4];
-    auto load = [&](int64_t k0) {
-#pragma unroll
-        for (int it = 0; it < F4; ++it) {
-            const int idx = tid + it * 256;
-            const int row = idx / (BK / 4), kq = (idx % (BK / 4)) * 4;
-            ra[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-            rb[it] = ra[it];
-            if (m0 + row < n) ra[it] = *reinterpret_cast<const float4 *>(A + (m0 + row) * lda + k0 + kq);
-            if (n0 + row < n) rb[it] = *reinterpret_cast<const float4 *>(A + (n0 + row) * lda + k0 + kq);
-        }
-    };
-    load(kb);
-    for (int64_t k0 = kb; k0 < ke; k0 += BK) {
-        __syncthreads();  // (the previous tile's MFMA reads are done)
-#pragma unroll
-        for (int it = 0; it < F4; ++it) {
-            const int idx = tid + it * 256;
-            const int row = idx / (BK / 4), kq = (idx % (BK / 4)) * 4;
-            const int sr = row ^ dense_swz(kq);
-            As[kq + 0][sr] = ra[it].x; As[kq + 1][sr] = ra[it].y; As[kq + 2][sr] = ra[it].z; As[kq + 3][sr] = ra[it].w;
-            Bs[kq + 0][sr] = rb[it].x; Bs[kq + 1][sr] = rb[it].y; Bs[kq + 2][sr] = rb[it].z; Bs[kq + 3][sr] = rb[it].w;
-        }
-        __syncthreads();
-        if (k0 + BK < ke) load(k0 + BK);  // in flight during the MFMAs below
-#pragma unroll
-        for (int kk = 0; kk < BK; kk += 2) {
-            const int kr = kk + (lane >> 5), rc = lane & 31, sw = dense_swz(kr);
-            float a[NB], bv[NB];
-#pragma unroll
-            for (int x = 0; x < NB; ++x) {
-                a[x] = As[kr][(wm * (BM / 2) + x * 32 + rc) ^ sw];
-                bv[x] = Bs[kr][(wn * (BM / 2) + x * 32 + rc) ^ sw];
-            }
-#pragma unroll
-            for (int x = 0; x < NB; ++x)
-#pragma unroll
-                for (int y = 0; y < NB; ++y) c[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], bv[y], c[x][y], 0, 0, 0);
-        }
-    }
-    // C/D map (32x32): col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
-#pragma unroll
-    for (int x = 0; x < NB; ++x)
-#pragma unroll
-        for (int y = 0; y < NB; ++y)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int64_t row = m0 + wm * (BM / 2) + x * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
-                const int64_t col = n0 + wn * (BM / 2) + y * 32 + (lane & 31);
-                if (row < n && col < n) K[row * ldk + col] = c[x][y][q];
-            }
-}
-
-// Split-K epilogue: K[i, j] = sum_s P_s[i, j] (slices in order: deterministic) for the 64 x 64 blocks
-// on and above the diagonal, written to the upper block and, transposed through LDS, to the lower one
-// (the diagonal block: its upper half, mirrored), so K comes out exactly symmetric.
-__global__ __launch_bounds__(256) void gram_dense_combine_kernel(int64_t n, int64_t nt, int n_parts,
-                                                                 const float *__restrict__ P, int64_t ldp,
-                                                                 int64_t part_stride, float *__restrict__ K,
-                                                                 int64_t ldk) {
-    __shared__ float tile[64][65];
-    const int64_t b = blockIdx.x;
-    int64_t bi = (int64_t)(((double)(2 * nt + 1) - sqrt((double)(2 * nt + 1) * (double)(2 * nt + 1) - 8.0 * (double)b)) * 0.5);
-    auto first = [nt](int64_t i) { return i * nt - i * (i - 1) / 2; };
-    if (bi < 0) bi = 0;
-    if (bi > nt - 1) bi = nt - 1;
-    while (bi > 0 && first(bi) > b) --bi;
-    while (bi < nt - 1 && first(bi + 1) <= b) ++bi;
-    const int64_t bj = bi + (b - first(bi));
-    const int64_t i0 = bi * 64, j0 = bj * 64;
-    const int t = threadIdx.x;
-    const bool full = i0 + 64 <= n && j0 + 64 <= n && (ldk & 3) == 0 && (ldp & 3) == 0 && (part_stride & 3) == 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
-        const int64_t i = i0 + y;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        if (full) {
-            for (int sl = 0; sl < n_parts; ++sl)
-                acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(P + sl * part_stride + i * ldp + j0 + x));
-        } else {
-            for (int sl = 0; sl < n_parts; ++sl)
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (i < n && j0 + x + c < n) acc[c] += P[sl * part_stride + i * ldp + j0 + x + c];
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) tile[y][x + c] = acc[c];
-        if (full && bi != bj) {
-            __builtin_nontemporal_store(acc, reinterpret_cast<f32x4 *>(K + i * ldk + j0 + x));
-        } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (i < n && j0 + x + c < n && j0 + x + c >= i) K[i * ldk + j0 + x + c] = acc[c];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int y = (t >> 4) + 16 * q, x = (t & 15) * 4;
-        const int64_t j = j0 + y;
-        if (full && bi != bj) {
-            f32x4 v;
-            v[0] = tile[x][y]; v[1] = tile[x + 1][y]; v[2] = tile[x + 2][y]; v[3] = tile[x + 3][y];
-            __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(K + j * ldk + i0 + x));
-        } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int64_t i = i0 + x + c;
-                if (j < n && i < n && j > i) K[j * ldk + i] = tile[x + c][y];
-            }
-        }
-    }
-}
 
 __global__ __launch_bounds__(256) void densify_kernel(int64_t n_rows, const int64_t *__restrict__ ptr,
                                                       const int32_t *__restrict__ idx, const float *__restrict__ val,
@@ -1014,6 +586,11 @@ __global__ __launch_bounds__(256) void densify_kernel(int64_t n_rows, const int6
     const int lane = threadIdx.x & 63;
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) out[row * lda + idx[e]] = val[e];
 }
+
+// grf_gram_dense.hip: the dense path's MFMA Gram
+size_t dense_gram_workspace_bytes(int64_t n, int64_t k_dim);
+int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk, void *workspace,
+                   size_t workspace_bytes, bool upper_only, grf_stream_t stream);
 
 }  // namespace grf
 
@@ -1042,22 +619,21 @@ static int32_t gram_balance(const GramTiles &tl, int32_t unit) {
 static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramTiles &tl, int64_t t_first,
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
                                  const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
-                                 float *K, int64_t ldk, hipStream_t st, int32_t *tickets = nullptr,
-                                 const void *t_split = nullptr, int64_t slot_buckets = 0,
-                                 const int32_t *row_cuts = nullptr) {
+                                 float *K, int64_t ldk, hipStream_t st, const void *t_split = nullptr,
+                                 int64_t slot_buckets = 0, const int32_t *row_cuts = nullptr) {
     if (unit == GRF_REC_SLOT) {
         // the slot layout: 8-wave tiles (one batch of 64 nonzeros per wave: two stream buckets each),
         // the default unroll and exact tails; the overflow pairs follow the slot_buckets slots
-        GRF_REQUIRE(!tickets && !t_split, GRF_EUNSUPPORTED, "gram: GRF_REC_SLOT has no fused / split variant");
+        GRF_REQUIRE(!t_split, GRF_EUNSUPPORTED, "gram: GRF_REC_SLOT has no split variant");
         GRF_REQUIRE(32 * slot_buckets < ((int64_t)1 << 30), GRF_EUNSUPPORTED,
                     "gram: GRF_REC_SLOT slots beyond 32-bit record offsets");
         const size_t lds = gram_lds_bytes(tl.W, 8, 2);
         const int64_t max_tiles = ((1ll << 32) - 1) / (64 * 8);
         for (int64_t t0 = t_first; t0 < t_last; t0 += max_tiles) {
             const int64_t nt = (t_last - t0) < max_tiles ? (t_last - t0) : max_tiles;
-            gram_sparse_kernel<8, 1, 8, true, false, true><<<(unsigned)nt, 512, lds, st>>>(
+            gram_sparse_kernel<8, 1, 8, true, true><<<(unsigned)nt, 512, lds, st>>>(
                 n_total, row_begin, tl, t0, ptr, idx, val, reinterpret_cast<const uint2 *>(t_desc),
-                reinterpret_cast<const unsigned char *>(t_rec), unit, t_rowshift, K, ldk, nullptr, nullptr,
+                reinterpret_cast<const unsigned char *>(t_rec), unit, t_rowshift, K, ldk, nullptr,
                 32 * slot_buckets, gram_balance(tl, unit), nullptr);
             GRF_CHECK_LAUNCH("gram_sparse_kernel");
         }
@@ -1068,53 +644,30 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
         const char *e = getenv("GRF_GRAM_SPLIT");
         return !e || atoi(e) != 0;
     }();
-    const uint16_t *split = (use_split && tl.sym && !tickets) ? (const uint16_t *)t_split : nullptr;
-    // tuning knobs (defaults = measured best on MI355X): gathers in flight per wave, waves per tile
-    static const int knobs = [] {
-        const char *e = getenv("GRF_GRAM_UNROLL"), *w = getenv("GRF_GRAM_WAVES"), *t = getenv("GRF_GRAM_TAIL");
-        const int u = e ? atoi(e) : 8, ww = w ? atoi(w) : 0, tt = t ? atoi(t) : 1;
-        return (tt ? 1000 : 0) + ((u == 4 || u == 8 || u == 16) ? u : 8) * 10 + (ww == 8 ? 8 : ww == 4 ? 4 : 0);
-    }();
-    const bool tail_exact = knobs >= 1000;
+    const uint16_t *split = (use_split && tl.sym) ? (const uint16_t *)t_split : nullptr;
     // waves per tile: 4 for W <= 4096 (4 tiles of 40 KiB per CU), 8 for wider bands (2 tiles of
-    // 76 KiB per CU: 16 waves per CU either way); measured best at both widths (GRF_GRAM_WAVES overrides)
-    const int waves = knobs % 10 ? knobs % 10 : (tl.W > 4096 ? 8 : 4);
-    const int unroll = (knobs % 1000) / 10, halves = waves == 8 ? 1 : 2;
-    static const size_t lds_pad = [] {  // (experiments: GRF_GRAM_LDS_PAD bytes per tile -> fewer tiles per CU)
-        const char *e = getenv("GRF_GRAM_LDS_PAD");
-        return e ? (size_t)atoll(e) : (size_t)0;
+    // 76 KiB per CU: 16 waves per CU either way); measured best at both widths (GRF_GRAM_WAVES=4/8
+    // overrides); 8 windows of gathers in flight per wave and an exact-size last window group (the
+    // round-1..3 sweeps of 4 / 16 windows and of masked tails: profiles/AB_LOG.md)
+    static const int env_waves = [] {
+        const char *w = getenv("GRF_GRAM_WAVES");
+        const int ww = w ? atoi(w) : 0;
+        return ww == 8 ? 8 : ww == 4 ? 4 : 0;
     }();
-    const size_t lds = gram_lds_bytes(tl.W, waves, halves) + lds_pad;
+    const int waves = env_waves ? env_waves : (tl.W > 4096 ? 8 : 4);
+    const size_t lds = gram_lds_bytes(tl.W, waves, waves == 8 ? 1 : 2);
     // one launch covers at most 2^32 - 1 work-items: split the tile range
     const int64_t max_tiles = ((1ll << 32) - 1) / (64 * waves);
     for (int64_t t0 = t_first; t0 < t_last; t0 += max_tiles) {
         const int64_t nt = (t_last - t0) < max_tiles ? (t_last - t0) : max_tiles;
-#define GRF_GRAM_LAUNCH_F(WV, H, U, T, F)                                                                         \
-    gram_sparse_kernel<WV, H, U, T, F><<<(unsigned)nt, 64 * WV, lds, st>>>(n_total, row_begin, tl, t0, ptr, idx,   \
-                                                                        val, reinterpret_cast<const uint2 *>(t_desc), \
-                                                                        reinterpret_cast<const unsigned char *>(t_rec), \
-                                                                        unit, t_rowshift, K, ldk, tickets, split, 0, \
-                                                                        gram_balance(tl, unit), row_cuts)
-#define GRF_GRAM_LAUNCH_T(WV, H, U, T) GRF_GRAM_LAUNCH_F(WV, H, U, T, false)
-#define GRF_GRAM_LAUNCH(WV, H, U)                                                                                 \
-    do {                                                                                                          \
-        if (tail_exact) GRF_GRAM_LAUNCH_T(WV, H, U, true);                                                        \
-        else GRF_GRAM_LAUNCH_T(WV, H, U, false);                                                                  \
-    } while (0)
-        if (tickets) {  // fused symmetric completion: the default unroll and exact tails only
-            if (waves == 8) GRF_GRAM_LAUNCH_F(8, 1, 8, true, true);
-            else GRF_GRAM_LAUNCH_F(4, 2, 8, true, true);
-        } else if (waves == 8) {
-            if (unroll == 4) GRF_GRAM_LAUNCH(8, 1, 4);
-            else GRF_GRAM_LAUNCH(8, 1, 8);
-        } else {
-            if (unroll == 4) GRF_GRAM_LAUNCH(4, 2, 4);
-            else if (unroll == 16) GRF_GRAM_LAUNCH(4, 2, 16);
-            else GRF_GRAM_LAUNCH(4, 2, 8);
-        }
+#define GRF_GRAM_LAUNCH(WV, H)                                                                                    \
+    gram_sparse_kernel<WV, H, 8, true><<<(unsigned)nt, 64 * WV, lds, st>>>(                                       \
+        n_total, row_begin, tl, t0, ptr, idx, val, reinterpret_cast<const uint2 *>(t_desc),                       \
+        reinterpret_cast<const unsigned char *>(t_rec), unit, t_rowshift, K, ldk, split, 0, gram_balance(tl, unit), \
+        row_cuts)
+        if (waves == 8) GRF_GRAM_LAUNCH(8, 1);
+        else GRF_GRAM_LAUNCH(4, 2);
 #undef GRF_GRAM_LAUNCH
-#undef GRF_GRAM_LAUNCH_T
-#undef GRF_GRAM_LAUNCH_F
         GRF_CHECK_LAUNCH("gram_sparse_kernel");
     }
     return GRF_OK;
@@ -1130,7 +683,7 @@ static int32_t gram_sparse_launch(int64_t n_total, int64_t row_begin, int64_t ro
     const int64_t n_tiles = tl.total();
     if (n_tiles == 0) return GRF_OK;
     return gram_tiles_launch(n_total, row_begin, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, unit, t_rowshift, K,
-                             ldk, st, nullptr, t_split, nb * n_total);
+                             ldk, st, t_split, nb * n_total);
 }
 
 static int32_t gram_sparse_check(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
@@ -1190,7 +743,7 @@ static int32_t gram_sparse_upper_impl(int64_t n_total, const int64_t *ptr, const
     if (t1 <= t0) return GRF_OK;
     GRF_REQUIRE(!row_cuts || rec_unit != GRF_REC_SLOT, GRF_EUNSUPPORTED, "grf_gram_sparse_upper: row cuts with slot buckets");
     return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk,
-                             S(stream), nullptr, t_split, tl.nb * n_total, row_cuts);
+                             S(stream), t_split, tl.nb * n_total, row_cuts);
 }
 
 int32_t grf_gram_sparse_upper_ex(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
@@ -1311,39 +864,6 @@ int32_t grf_transpose_drop_columns(int64_t n_bands, int64_t n_cols, uint32_t *t_
     return GRF_OK;
 }
 
-size_t grf_gram_sym_fused_workspace_bytes(int64_t n_total, int64_t band_width) {
-    if (n_total <= 0 || band_width <= 0) return 16;
-    const int64_t nb = cdiv<int64_t>(n_total, band_width), ng = cdiv<int64_t>(n_total, kFuseGroup);
-    return (size_t)cdiv<int64_t>(nb * ng * 4, 16) * 16;
-}
-
-int32_t grf_gram_sparse_sym_fused(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
-                                  int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                                  const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
-                                  int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
-                                  grf_stream_t stream) {
-    int32_t rc = gram_sparse_check(n_total, 0, n_total, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift, K, ldk);
-    if (rc != GRF_OK) return rc;
-    GRF_REQUIRE(n_parts >= 1 && 0 <= part_begin && part_begin <= part_end && part_end <= n_parts, GRF_EINVAL,
-                "grf_gram_sparse_sym_fused: bad tile parts [%d, %d) of %d", part_begin, part_end, n_parts);
-    GRF_REQUIRE(ldk % 4 == 0 && ((uintptr_t)K & 15) == 0, GRF_EINVAL,
-                "grf_gram_sparse_sym_fused: K must be 16-byte aligned with ldk a multiple of 4");
-    const size_t need = grf_gram_sym_fused_workspace_bytes(n_total, band_width);
-    GRF_REQUIRE(workspace && workspace_bytes >= need && ((uintptr_t)workspace & 15) == 0, GRF_EINVAL,
-                "grf_gram_sparse_sym_fused: workspace needs %zu bytes (16-byte aligned), got %zu", need,
-                workspace_bytes);
-    if (n_total == 0 || part_begin == part_end) return GRF_OK;
-    hipStream_t st = S(stream);
-    // the group tickets are zeroed by the call that issues the first part
-    if (part_begin == 0) GRF_CHECK_HIP(hipMemsetAsync(workspace, 0, need, st));
-    const GramTiles tl{n_total, band_width, cdiv<int64_t>(n_total, band_width), true, 0, (int32_t)n_total};
-    const int64_t total = tl.total();
-    const int64_t t0 = total * part_begin / n_parts, t1 = total * part_end / n_parts;
-    if (t1 <= t0) return GRF_OK;
-    return gram_tiles_launch(n_total, 0, tl, t0, t1, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift, K, ldk, st,
-                             reinterpret_cast<int32_t *>(workspace));
-}
-
 // Column block: K[r - row_begin, 0 : t_rows] = sum_k Phi[r, k] Phi_B[:, k] for the rows r of Phi
 // against the t_rows rows of another matrix Phi_B (a rank's own rows) whose banded transpose is
 // given; the row shifts come from grf_phi_row_shifts over all of Phi.  With Phi_B = Phi[b:e] this
@@ -1351,7 +871,7 @@ int32_t grf_gram_sparse_sym_fused(int64_t n_total, const int64_t *ptr, const int
 static int32_t gram_sparse_cols_impl(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
                                      const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
                                      int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
-                                     const void *t_rec, const void *t_split, float *K, int64_t ldk, bool add_k,
+                                     const void *t_rec, const void *t_split, float *K, int64_t ldk,
                                      grf_stream_t stream) {
     GRF_REQUIRE(n_cols > 0 && 0 <= row_begin && row_begin <= row_end && ptr && idx && val && row_shift &&
                     t_rows >= 0 && t_desc && t_rec && K && ldk >= t_rows,
@@ -1371,9 +891,8 @@ static int32_t gram_sparse_cols_impl(int64_t n_cols, int64_t row_begin, int64_t 
         if (r1 <= r0) return GRF_OK;
         GramTiles tl{r1 - r0, band_width, nb, sym, 0, (int32_t)n_cols};
         tl.t_rows = t_rows;
-        tl.add_k = add_k;
         return gram_tiles_launch(n_cols, r0, tl, 0, tl.total(), ptr, idx, val, t_desc, t_rec, rec_unit, row_shift,
-                                 K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr, nb * n_cols);
+                                 K + (r0 - row_begin) * ldk, ldk, st, sym ? t_split : nullptr, nb * n_cols);
     };
     if (sym_row0 < 0) return launch(row_begin, row_end, false);
     // Phi_B = Phi[sym_row0, sym_row0 + t_rows): the square K[B, B] is symmetric and its bands start at
@@ -1393,57 +912,7 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
     (void)workspace;
     (void)workspace_bytes;
     return gram_sparse_cols_impl(n_cols, row_begin, row_end, ptr, idx, val, row_shift, t_rows, sym_row0, band_width,
-                                 rec_unit, t_desc, t_rec, t_split, K, ldk, false, stream);
-}
-
-// grf_gram_sparse_cols whose write-out ADDS the rounded fixed-point sums to the block (which holds the
-// dense hub-column part first: the column-block hub-column split)
-int32_t grf_gram_sparse_cols_add(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
-                                 const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
-                                 int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
-                                 const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
-                                 size_t workspace_bytes, grf_stream_t stream) {
-    (void)workspace;
-    (void)workspace_bytes;
-    return gram_sparse_cols_impl(n_cols, row_begin, row_end, ptr, idx, val, row_shift, t_rows, sym_row0, band_width,
-                                 rec_unit, t_desc, t_rec, t_split, K, ldk, true, stream);
-}
-
-// K rows [row_begin, row_end) of the whole K using the symmetry inside the row block: the bands
-// that lie inside the block ("interior", rows [B0, B1)) are computed only on and above the
-// diagonal for the block's interior rows and mirrored; everything else is the row mode.
-int32_t grf_gram_sparse_block(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
-                              const int32_t *idx, const float *val, int64_t band_width, int32_t rec_unit,
-                              const uint32_t *t_desc, const void *t_rec, const void *t_split,
-                              const int32_t *t_rowshift, float *K,
-                              int64_t ldk, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
-    int32_t rc = gram_sparse_check(n_total, row_begin, row_end, ptr, band_width, rec_unit, t_desc, t_rec, t_rowshift,
-                                   K, ldk);
-    if (rc != GRF_OK) return rc;
-    if (row_end == row_begin || n_total == 0) return GRF_OK;
-    hipStream_t st = S(stream);
-    const int64_t W = band_width, nb = cdiv<int64_t>(n_total, W);
-    const int64_t J0 = cdiv<int64_t>(row_begin, W);
-    const int64_t J1 = row_end == n_total ? nb : row_end / W;
-    if (J1 <= J0) {
-        return gram_sparse_launch(n_total, row_begin, row_end - row_begin, false, 0, n_total, ptr, idx, val, W,
-                                  rec_unit, t_desc, t_rec, t_rowshift, K, ldk, st);
-    }
-    const int64_t B0 = J0 * W, B1 = std::min<int64_t>(J1 * W, n_total);
-    auto launch = [&](int64_t r0, int64_t r1, int64_t ja, int64_t jb, bool sym) -> int32_t {
-        if (r1 <= r0 || jb <= ja) return GRF_OK;
-        GramTiles tl{r1 - r0, W, jb - ja, sym, 0, (int32_t)n_total};
-        tl.J_off = ja;
-        const int64_t n_tiles = tl.total();
-        return gram_tiles_launch(n_total, r0, tl, 0, n_tiles, ptr, idx, val, t_desc, t_rec, rec_unit, t_rowshift,
-                                 K + (r0 - row_begin) * ldk, ldk, st, nullptr, sym ? t_split : nullptr, nb * n_total);
-    };
-    if ((rc = launch(B0, B1, J0, J1, true)) != GRF_OK) return rc;            // interior, symmetric
-    if ((rc = launch(row_begin, row_end, 0, J0, false)) != GRF_OK) return rc;  // bands before
-    if ((rc = launch(row_begin, row_end, J1, nb, false)) != GRF_OK) return rc; // bands after
-    if ((rc = launch(row_begin, B0, J0, J1, false)) != GRF_OK) return rc;     // edge rows x interior
-    if ((rc = launch(B1, row_end, J0, J1, false)) != GRF_OK) return rc;
-    return grf_gram_mirror(B1 - B0, K + (B0 - row_begin) * ldk + B0, ldk, 0, stream);
+                                 rec_unit, t_desc, t_rec, t_split, K, ldk, stream);
 }
 
 int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,
@@ -1475,112 +944,19 @@ int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups
     }();
     const int64_t cap = env_cap >= 0 ? env_cap : max_workgroups;
     const int64_t grid = cap > 0 && cap < blocks ? cap : blocks;
-    GRF_REQUIRE_GRID(grid, 256, "gram_mirror_kernel");
-    static const int padded = [] {  // GRF_MIRROR_PADDED=1: the padded 64 x 65 tile (A/B against the swizzle)
-        const char *e = getenv("GRF_MIRROR_PADDED");
-        return e ? atoi(e) : 0;
-    }();
-    static const int pipe = [] {  // GRF_MIRROR_PIPE=1: the bounded grid with the next block's loads in flight
-        const char *e = getenv("GRF_MIRROR_PIPE");  // (measured slower beside the next front: off by default)
-        return e ? atoi(e) : 0;
-    }();
-    if (padded) gram_mirror_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
-    else if (pipe && grid < blocks && (ldk & 3) == 0 && nt >= 3) {
-        // the full strictly-upper blocks, with the next block's loads in flight, then the edges
-        const int64_t nf = n % 64 == 0 ? nt : nt - 1, nfull = nf * (nf - 1) / 2;
-        const int64_t g = grid < nfull ? grid : nfull;
-        if (nfull > 0) gram_mirror_pipe_kernel<<<(unsigned)g, 256, 0, S(stream)>>>(nf, nfull, K, ldk);
-        const int64_t nedge = nt + (n % 64 == 0 ? 0 : nt - 1);
-        gram_mirror_edge_kernel<<<(unsigned)nedge, 256, 0, S(stream)>>>(n, nt, K, ldk);
-    } else gram_mirror_swz_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
-    GRF_CHECK_LAUNCH("gram_mirror_kernel");
+    GRF_REQUIRE_GRID(grid, 256, "gram_mirror_swz_kernel");
+    gram_mirror_swz_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, nt, blocks, K, ldk);
+    GRF_CHECK_LAUNCH("gram_mirror_swz_kernel");
     return GRF_OK;
 }
 
-int32_t grf_gram_mirror_rect(int64_t n, float *K, int64_t ldk, int64_t row_begin, int64_t row_end, int64_t col_begin,
-                             int64_t col_end, int64_t max_workgroups, grf_stream_t stream) {
-    GRF_REQUIRE(n >= 0 && K && ldk >= n && 0 <= row_begin && row_begin <= row_end && row_end <= n && 0 <= col_begin &&
-                    col_begin <= col_end && col_end <= n && row_begin % 64 == 0 && col_begin % 64 == 0,
-                GRF_EINVAL, "grf_gram_mirror_rect: bad arguments (ranges inside [0, n), starts multiples of 64)");
-    if (row_end == row_begin || col_end == col_begin) return GRF_OK;
-    const int64_t bi0 = row_begin / 64, bj0 = col_begin / 64;
-    const int64_t nbi = cdiv<int64_t>(row_end, 64) - bi0, nbj = cdiv<int64_t>(col_end, 64) - bj0;
-    const int64_t blocks = nbi * nbj;
-    const int64_t grid = max_workgroups > 0 && max_workgroups < blocks ? max_workgroups : blocks;
-    GRF_REQUIRE_GRID(grid, 256, "gram_mirror_rect_kernel");
-    gram_mirror_rect_kernel<<<(unsigned)grid, 256, 0, S(stream)>>>(n, bi0, bj0, nbj, blocks, K, ldk);
-    GRF_CHECK_LAUNCH("gram_mirror_rect_kernel");
-    return GRF_OK;
-}
+size_t grf_gram_dense_workspace_bytes(int64_t n, int64_t k_dim) { return grf::dense_gram_workspace_bytes(n, k_dim); }
 
-// split-K slices for a dense Gram of n rows (128-row tiles on and above the diagonal): measured on
-// MI355X (tools/dense_sweep.py, profiles/r02_dense_splitk.txt) 2 slices below 384 tiles (n < 3.5 k:
-// C3's 253 tiles, 0.209-0.214 ms vs 0.221 with 4), 4 below 1024 tiles (n < 5.8 k), 2 below 4096
-// (n < 11.6 k), none above; every slice at least 256 deep
-static int dense_splits(int64_t n, int64_t k_dim) {
-    static const int env_split = [] {  // GRF_DENSE_SPLIT: A/B knob (1 = never split)
-        const char *e = getenv("GRF_DENSE_SPLIT");
-        return e ? atoi(e) : 0;
-    }();
-    if (env_split > 0) return env_split;
-    const int64_t nt = cdiv<int64_t>(n, 128), tiles = nt * (nt + 1) / 2;
-    const int64_t S = tiles < 384 ? 2 : tiles < 1024 ? 4 : tiles < 4096 ? 2 : 1;
-    return (int)std::max<int64_t>(1, std::min<int64_t>(S, k_dim / 256));
-}
-
-size_t grf_gram_dense_workspace_bytes(int64_t n, int64_t k_dim) {
-    const int S = n > 0 ? dense_splits(n, k_dim) : 1;
-    if (S <= 1) return 16;
-    const int64_t ldp = cdiv<int64_t>(n, 64) * 64;
-    return (size_t)S * (size_t)n * (size_t)ldp * sizeof(float);
-}
-
+// the MFMA Gram (grf_gram_dense.hip): tiles on and above the diagonal written to both triangles
+// (upper_only: the tiles' K[row][col] only, the seed of the hub-column split's sparse tiles)
 static int32_t gram_dense_impl(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                                void *workspace, size_t workspace_bytes, bool upper_only, grf_stream_t stream) {
-    GRF_REQUIRE(n >= 0 && k_dim >= 0 && A && K && ldk >= n && lda >= k_dim, GRF_EINVAL,
-                "grf_gram_dense: bad arguments");
-    GRF_REQUIRE(lda % 16 == 0 && ((uintptr_t)A & 15) == 0, GRF_EINVAL,
-                "grf_gram_dense: lda must be a multiple of 16 and A 16-byte aligned");
-    if (n == 0) return GRF_OK;
-    // tile: 128 when the upper triangle of 128-tiles gives >= 2 workgroups per CU (n >= ~4.5 k), else
-    // 64 -- or 128 with split-K slices when a workspace for the partials is given (small n)
-    const int64_t nt128 = cdiv<int64_t>(n, 128);
-    static const int env_tile = [] {  // GRF_DENSE_TILE=64/128, GRF_DENSE_BK=16/32: A/B knobs
-        const char *e = getenv("GRF_DENSE_TILE");
-        return e ? atoi(e) : 0;
-    }();
-    static const int env_bk = [] {
-        const char *e = getenv("GRF_DENSE_BK");
-        return e ? atoi(e) : 0;
-    }();
-    int ns = (workspace && !upper_only) ? dense_splits(n, k_dim) : 1;
-    const int64_t ldp = cdiv<int64_t>(n, 64) * 64;
-    if (ns > 1 && workspace_bytes < (size_t)ns * (size_t)n * (size_t)ldp * sizeof(float)) ns = 1;
-    const bool big = ns > 1 || (env_tile ? env_tile == 128 : nt128 * (nt128 + 1) / 2 >= 512);
-    int bk = (!big && lda % 32 == 0) ? 32 : 16;  // (zero padding up to lda covers the last k-tile)
-    if (env_bk == 32 && lda % 32 == 0) bk = 32;
-    if (env_bk == 16) bk = 16;
-    const int64_t kpad = cdiv<int64_t>(k_dim, bk) * bk;
-    GRF_REQUIRE(kpad <= lda, GRF_EINVAL, "grf_gram_dense: lda must cover k_dim rounded up to %d", bk);
-    const int64_t nt = cdiv<int64_t>(n, big ? 128 : 64), tiles = nt * (nt + 1) / 2;
-    GRF_REQUIRE_GRID(tiles, 256, "gram_dense_kernel");
-    const int64_t k_split = ns > 1 ? cdiv<int64_t>(cdiv<int64_t>(kpad, ns), bk) * bk : kpad;
-    if (ns > 1) ns = (int)cdiv<int64_t>(kpad, k_split);
-    float *out = ns > 1 ? reinterpret_cast<float *>(workspace) : K;
-    const int64_t ldo = ns > 1 ? ldp : ldk, pstride = ns > 1 ? n * ldp : 0;
-    GRF_REQUIRE_GRID(tiles * ns, 256, "gram_dense_kernel");
-    const unsigned grid = (unsigned)(tiles * ns);
-    if (big && bk == 32) gram_dense_kernel<128, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
-    else if (big) gram_dense_kernel<128, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
-    else if (bk == 32) gram_dense_kernel<64, 32><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
-    else gram_dense_kernel<64, 16><<<grid, 256, 0, S(stream)>>>(n, nt, kpad, A, lda, out, ldo, k_split, pstride, ns);
-    GRF_CHECK_LAUNCH("gram_dense_kernel");
-    if (ns == 1) return upper_only ? GRF_OK : grf_gram_mirror(n, K, ldk, 0, stream);  // the lower triangle
-    const int64_t nt64 = cdiv<int64_t>(n, 64), blocks = nt64 * (nt64 + 1) / 2;
-    GRF_REQUIRE_GRID(blocks, 256, "gram_dense_combine_kernel");
-    gram_dense_combine_kernel<<<(unsigned)blocks, 256, 0, S(stream)>>>(n, nt64, ns, out, ldp, pstride, K, ldk);
-    GRF_CHECK_LAUNCH("gram_dense_combine_kernel");
-    return GRF_OK;
+    return grf::dense_gram(n, k_dim, A, lda, K, ldk, workspace, workspace_bytes, upper_only, stream);
 }
 
 int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,

@@ -1,0 +1,664 @@
+// grf_gram_dense.hip -- the dense path's Gram K = A A^T on the fp32 MFMA.
+//
+// Reference: efficient_graph_gp/graph_kernels/fast_grf_kernel_general.py:38-39 (Phi = F f; K = Phi Phi^T,
+// a numpy dgemm); here A is the dense fp32 Phi (n x k_dim, row-major, zero-padded to lda).
+//
+// Tiles.  K is symmetric, so only the 128 x 128 tiles on and above the diagonal are computed
+// (n^2 k flops instead of 2 n^2 k); every tile writes its entries to both triangles, so there is no
+// mirror pass.  A workgroup of 4 waves (2 x 2) owns one tile, each wave a 64 x 64 quarter: 4 x 4 blocks
+// of v_mfma_f32_16x16x4f32 (MF = 16) or 2 x 2 blocks of v_mfma_f32_32x32x2f32 (MF = 32), 64 accumulator
+// VGPRs either way.  A wave whose quarter lies wholly below the diagonal (diagonal tiles) or past n
+// (edge tiles) issues no MFMAs.
+//
+// Staging.  Both operands are rows of A (k contiguous), so the k-tiles go global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: no VGPR round trip, no transposing LDS writes) into a ring of NST stages with
+// ONE barrier per k-tile and NST - 2 k-tiles in flight behind a counted `s_waitcnt vmcnt` (never 0 in the
+// loop).  The loop is software-pipelined across the k-tile boundary: the next fragments are read from
+// LDS before the current MFMAs, and the boundary (retire k-tile t + 1, barrier, DMA of k-tile
+// t + NST - 1, read of t + 1's first fragments) sits before the MFMAs of tile t's last fragment group,
+// so no MFMA waits on a read issued after a barrier.  WAR: the DMA issued at boundary t -> t + 1 refills
+// the stage of tile t - 1, which every wave has consumed before reaching that barrier.  A diagonal tile
+// stages one operand (B = A).  The LDS image of a k-tile is row-major, BK floats a row; one DMA piece
+// (64 lanes x 16 B) is lane-linear, so the bank swizzle (16-B chunk c of row r stored at c ^ swz(r)) is
+// applied on the per-lane SOURCE address and on the fragment read (conflict-free ds_read_b128).
+//
+// k order.  MF = 32: lane (r, h) holds k = h BK/2 + 4 g + s at step (g, s); MF = 16: lane (r, q) holds
+// k = 4 q + s at step s (BK = 16): one ds_read_b128 gives a lane the operands of four MFMA steps.  Each K
+// entry is a fixed chain of exact f32 FMAs over that order (bitwise reproducible run to run); diagonal
+// tiles write each entry computed at (i, j >= i) to both (i, j) and (j, i), so K is exactly symmetric.
+//
+// Split-K (small n: too few tiles for the CUs; large n: the last `tail` tiles, so that the last partial
+// round of workgroups is cut finer): a tile's pieces are k-slices; each writes its partial tile (16-B
+// stores, register layout) to a slab, and the piece that draws the last ticket sums the slabs in slice
+// order (its own from registers) and writes the tile.  Hand-off (cdna_hip_programming.md, "Projection
+// GEMM" item 2): slab stores -> every wave vmcnt(0) -> barrier -> agent release -> ticket fetch_add; the
+// last arriver: agent acquire -> barrier -> plain loads.  The last arriver resets its ticket, so the
+// ticket array stays zero between launches (it must be zero on first use).
+#include "grf_common.h"
+
+namespace grf {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 128;  // tile edge (rows and columns)
+
+struct DenseArgs {
+    const float *A;
+    float *K;
+    float *slabs;      // split pieces: [split tile][slice][4 waves][16 float4][64 lanes]
+    int32_t *tickets;  // one per split tile (zero between launches)
+    int64_t n, nt, lda, ldk;
+    int64_t kpad;      // k range (multiple of BK, zero-padded up to lda)
+    int64_t n_whole;   // work items [0, n_whole) are the whole tiles 0 .. n_whole - 1
+    int64_t k_split;   // k-slice width of a split tile's piece (multiple of BK)
+    int32_t n_split;   // pieces per split tile (the tiles from n_whole on)
+    int32_t upper_only;  // write only K[row][col] of the computed tiles (the hub panel's seed)
+    int32_t abl;       // A/B ablations (GRF_DENSE_ABL; timing only): 1 no DMA, 4 no barrier, 8 no mirror
+};
+
+// Fragment layout of one wave's 64 x 64 quarter.
+template <int MF, int BK>
+struct Layout;
+
+template <int BK>
+struct Layout<32, BK> {  // 2 x 2 blocks of 32 x 32; lane (r = lane & 31, h = lane >> 5)
+    static constexpr int NBLK = 2, GG = BK / 8;  // blocks per side; fragment groups per k-tile
+    typedef f32x16 acc_t;
+    static constexpr int C = BK / 4;  // 16-B chunks per LDS row
+    static __device__ __forceinline__ int swz(int row) { return (row / (16 / C)) & (C - 1); }
+    // LDS float offset of block x's fragment, group g, in an operand image whose quarter starts at row q0
+    static __device__ __forceinline__ int off(int q0, int x, int g, int lane) {
+        const int row = q0 + x * 32 + (lane & 31), chunk = ((lane >> 5) * (C / 2) + g) ^ swz(row);
+        return (row * C + chunk) * 4;
+    }
+    static constexpr int XSTRIDE = 32 * C * 16;  // bytes between the blocks x and x + 1 of one group
+    static __device__ __forceinline__ acc_t mfma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+    }
+    // float4 j (0..15) of the quarter: block (x, y) = (j >> 3, (j >> 2) & 1), rows
+    // 32 x + 8 (j & 3) + 4 h + 0..3, column 32 y + (lane & 31)
+    static __device__ __forceinline__ f32x4v get(const acc_t (&c)[2][2], int j) {
+        const acc_t &b = c[j >> 3][(j >> 2) & 1];
+        const int g = j & 3;
+        return f32x4v{b[4 * g], b[4 * g + 1], b[4 * g + 2], b[4 * g + 3]};
+    }
+    static __device__ __forceinline__ void set(acc_t (&c)[2][2], int j, f32x4v v) {
+        acc_t &b = c[j >> 3][(j >> 2) & 1];
+        const int g = j & 3;
+        b[4 * g] = v[0], b[4 * g + 1] = v[1], b[4 * g + 2] = v[2], b[4 * g + 3] = v[3];
+    }
+    static __device__ __forceinline__ int row0(int j, int lane) { return 32 * (j >> 3) + 8 * (j & 3) + 4 * (lane >> 5); }
+    static __device__ __forceinline__ int col(int j, int lane) { return 32 * ((j >> 2) & 1) + (lane & 31); }
+};
+
+template <int BK>
+struct Layout<16, BK> {  // 4 x 4 blocks of 16 x 16; lane (r = lane & 15, q = lane >> 4)
+    static_assert(BK == 16, "the 16 x 16 layout stages k-tiles of 16");
+    static constexpr int NBLK = 4, GG = 1;
+    typedef f32x4v acc_t;
+    static constexpr int C = 4;
+    // (row / 4) & 2: the four lanes of a ds_read_b128 lane group that share row % 4 get distinct chunks
+    static __device__ __forceinline__ int swz(int row) { return (row >> 2) & 2; }
+    static __device__ __forceinline__ int off(int q0, int x, int, int lane) {
+        const int row = q0 + x * 16 + (lane & 15), chunk = (lane >> 4) ^ swz(row);
+        return (row * C + chunk) * 4;
+    }
+    static constexpr int XSTRIDE = 16 * C * 16;
+    static __device__ __forceinline__ acc_t mfma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // float4 j: block (x, y) = (j >> 2, j & 3), rows 16 x + 4 q + 0..3, column 16 y + (lane & 15)
+    static __device__ __forceinline__ f32x4v get(const acc_t (&c)[4][4], int j) { return c[j >> 2][j & 3]; }
+    static __device__ __forceinline__ void set(acc_t (&c)[4][4], int j, f32x4v v) { c[j >> 2][j & 3] = v; }
+    static __device__ __forceinline__ int row0(int j, int lane) { return 16 * (j >> 2) + 4 * (lane >> 4); }
+    static __device__ __forceinline__ int col(int j, int lane) { return 16 * (j & 3) + (lane & 15); }
+};
+
+template <int BK>
+struct Stage {
+    static constexpr int F = kTile * BK;          // floats per operand per stage
+    static constexpr int PW = kTile * BK / 1024;  // 1-KiB DMA pieces per wave per operand (4 waves)
+};
+
+__device__ __forceinline__ void dma16(const float *src, float *lds_piece) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)lds_piece, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// LDS fragment reads in inline asm: hipcc's own lgkmcnt bookkeeping waited for the NEXT fragments'
+// reads before the current MFMAs (lgkmcnt(0) where the older reads alone were needed), so the reads are
+// issued here and retired by lgkm_done(), a wait that names every destination register ("+v": no
+// consumer or copy of them can move above it; cdna_hip_programming.md, inline-asm VGPR loads, form ii).
+template <int OFF>
+__device__ __forceinline__ f32x4v ds_read16(uint32_t addr) {
+    f32x4v r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const float *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)p;
+}
+
+// tile b (row-major over the upper triangle of the nt x nt grid) -> (bi, bj), bj >= bi
+__device__ __forceinline__ void tile_coords(int64_t b, int64_t nt, int64_t &bi, int64_t &bj) {
+    const double t = (double)(2 * nt + 1);
+    int64_t i = (int64_t)((t - sqrt(t * t - 8.0 * (double)b)) * 0.5);
+    auto first = [nt](int64_t r) { return r * nt - r * (r - 1) / 2; };
+    if (i < 0) i = 0;
+    if (i > nt - 1) i = nt - 1;
+    while (i > 0 && first(i) > b) --i;
+    while (i < nt - 1 && first(i + 1) <= b) ++i;
+    bi = i;
+    bj = i + (b - first(i));
+}
+
+// The k-loop over [kb, ke) of one tile.  DIAG: B = A (one operand staged).  LIVE: this wave computes
+// (a dead wave still stages its share of the DMA and joins the barriers).  XABL (timing-only builds):
+// 16 = no fragment reads after the first.
+template <int MF, int BK, int NST, bool DIAG, bool LIVE, int XABL, bool PRIO, int IL>
+__device__ __forceinline__ void kloop(float *lds, const float *const *srcA, const float *const *srcB, int64_t kb,
+                                      int64_t ke, int wave, const int *aoff, const int *boff,
+                                      typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK][Layout<MF, BK>::NBLK],
+                                      int abl) {
+    using L = Layout<MF, BK>;
+    using St = Stage<BK>;
+    constexpr int NB = L::NBLK, GG = L::GG;
+    constexpr int D = NST - 2;  // k-tiles in flight behind the one being published
+    static_assert(D >= 1, "the pipelined k-loop needs NST >= 3");
+    constexpr int G = DIAG ? St::PW : 2 * St::PW;  // DMA instructions per wave per k-tile
+    const int64_t nk = (ke - kb) / BK;
+    auto issue = [&](int64_t t) {
+        if (abl & 1) return;
+        float *base = lds + (int)(t % NST) * 2 * St::F + wave * St::PW * 256;
+        const int64_t k0 = kb + t * BK;
+#pragma unroll
+        for (int j = 0; j < St::PW; ++j) dma16(srcA[j] + k0, base + j * 256);
+        if (!DIAG) {
+#pragma unroll
+            for (int j = 0; j < St::PW; ++j) dma16(srcB[j] + k0, base + St::F + j * 256);
+        }
+    };
+    // retire the oldest k-tile in flight (`ahead` younger ones may stay in flight) and publish it
+    auto retire = [&](int64_t ahead) {  // (ahead <= D - 1)
+        static_assert(D <= 3, "add the vmcnt cases for D > 3");
+        if constexpr (D == 3) {
+            if (ahead >= 2) wait_vm<2 * G>();
+            else if (ahead == 1) wait_vm<G>();
+            else wait_vm<0>();
+        } else if constexpr (D == 2) {
+            if (ahead >= 1) wait_vm<G>();
+            else wait_vm<0>();
+        } else {
+            wait_vm<0>();
+        }
+        if (!(abl & 4)) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    struct Frag { f32x4v a[NB], b[NB]; };
+    Frag fixed{};
+    const uint32_t lds0 = lds_addr(lds);
+    auto read = [&](int64_t t, int g) {
+        if constexpr ((XABL & 16) != 0) {
+            if (t > 0 || g > 0) return fixed;
+        }
+        const uint32_t As = lds0 + (uint32_t)(t % NST) * (2 * St::F * 4);
+        const uint32_t Bs = DIAG ? As : As + St::F * 4;
+        const uint32_t ab = As + (uint32_t)aoff[g] * 4, bb = Bs + (uint32_t)boff[g] * 4;
+        Frag f;
+        f.a[0] = ds_read16<0>(ab);
+        f.b[0] = ds_read16<0>(bb);
+        f.a[1] = ds_read16<L::XSTRIDE>(ab);
+        f.b[1] = ds_read16<L::XSTRIDE>(bb);
+        if constexpr (NB == 4) {
+            f.a[2] = ds_read16<2 * L::XSTRIDE>(ab);
+            f.b[2] = ds_read16<2 * L::XSTRIDE>(bb);
+            f.a[3] = ds_read16<3 * L::XSTRIDE>(ab);
+            f.b[3] = ds_read16<3 * L::XSTRIDE>(bb);
+        }
+        return f;
+    };
+    // every read issued so far has landed; f's registers are redefined here (nothing reads them earlier)
+    auto lgkm_done = [&](Frag &f) {
+        if constexpr (NB == 4)
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.b[0]), "+v"(f.b[1]),
+                           "+v"(f.b[2]), "+v"(f.b[3])::"memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.b[0]), "+v"(f.b[1])::"memory");
+    };
+    auto mfma = [&](const Frag &f) {
+        if constexpr (LIVE) {
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int x = 0; x < NB; ++x)
+#pragma unroll
+                    for (int y = 0; y < NB; ++y) c[x][y] = L::mfma(f.a[x][s], f.b[y][s], c[x][y]);
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        }
+    };
+    if (nk <= 0) return;
+#pragma unroll
+    for (int t = 0; t < D; ++t)
+        if (t < nk) issue(t);
+    retire(D - 1 < nk - 1 ? D - 1 : nk - 1);
+    if (D < nk) issue(D);
+    // one step = the MFMAs of fragment group g of k-tile t, with the next group's reads in flight; the
+    // two fragment sets alternate by name (no register copies between steps)
+    // interleaved form (IL): the MFMAs of one step in four chunks (one k-step s each), each followed by a
+    // quarter of the next fragments' reads and of the boundary's DMA pieces
+    auto read_q = [&](int64_t t, int g, int q, Frag &f) {
+        const uint32_t As = lds0 + (uint32_t)(t % NST) * (2 * St::F * 4);
+        const uint32_t Bs = DIAG ? As : As + St::F * 4;
+        const uint32_t ab = As + (uint32_t)aoff[g] * 4, bb = Bs + (uint32_t)boff[g] * 4;
+        if constexpr (NB == 4) {
+            switch (q) {
+                case 0: f.a[0] = ds_read16<0>(ab); f.b[0] = ds_read16<0>(bb); break;
+                case 1: f.a[1] = ds_read16<L::XSTRIDE>(ab); f.b[1] = ds_read16<L::XSTRIDE>(bb); break;
+                case 2: f.a[2] = ds_read16<2 * L::XSTRIDE>(ab); f.b[2] = ds_read16<2 * L::XSTRIDE>(bb); break;
+                default: f.a[3] = ds_read16<3 * L::XSTRIDE>(ab); f.b[3] = ds_read16<3 * L::XSTRIDE>(bb); break;
+            }
+        } else {
+            switch (q) {
+                case 0: f.a[0] = ds_read16<0>(ab); break;
+                case 1: f.b[0] = ds_read16<0>(bb); break;
+                case 2: f.a[1] = ds_read16<L::XSTRIDE>(ab); break;
+                default: f.b[1] = ds_read16<L::XSTRIDE>(bb); break;
+            }
+        }
+    };
+    auto issue_q = [&](int64_t t, int q) {  // pieces q, q + 4, ... of the tile's G
+        if (abl & 1) return;
+        float *base = lds + (int)(t % NST) * 2 * St::F + wave * St::PW * 256;
+        const int64_t k0 = kb + t * BK;
+#pragma unroll
+        for (int j = q; j < G; j += 4) {
+            if (j < St::PW) dma16(srcA[j] + k0, base + j * 256);
+            else dma16(srcB[j - St::PW] + k0, base + St::F + (j - St::PW) * 256);
+        }
+    };
+    auto mfma_q = [&](const Frag &f, int s) {
+        if constexpr (LIVE) {
+#pragma unroll
+            for (int x = 0; x < NB; ++x)
+#pragma unroll
+                for (int y = 0; y < NB; ++y) c[x][y] = L::mfma(f.a[x][s], f.b[y][s], c[x][y]);
+        }
+    };
+    auto step_il = [&](int64_t t, int g, const Frag &cur, Frag &nxt) {
+        const bool boundary = g + 1 == GG;
+        const int64_t tn = boundary ? t + 1 : t;
+        const int gn = boundary ? 0 : g + 1;
+        const bool dma = boundary && t + 1 + D < nk;
+        if (boundary) retire((t + D < nk - 1 ? t + D : nk - 1) - (t + 1));
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+        if constexpr (IL == 1) {  // chunk q: MFMAs, then a quarter of the reads and of the DMA
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_q(cur, q);
+                __builtin_amdgcn_sched_barrier(0);
+                read_q(tn, gn, q, nxt);
+                if (dma) issue_q(t + 1 + D, q);
+            }
+        } else if constexpr (IL == 2) {  // reads ahead of each chunk's MFMAs: the last read has 4 MFMAs behind it
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+                read_q(tn, gn, q, nxt);
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_q(cur, q);
+                __builtin_amdgcn_sched_barrier(0);
+                if (dma) issue_q(t + 1 + D, q);
+            }
+        } else {  // all reads in the first two chunks, the DMA in the last two
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (q < 2) {
+                    read_q(tn, gn, 2 * q, nxt);
+                    read_q(tn, gn, 2 * q + 1, nxt);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_q(cur, q);
+                __builtin_amdgcn_sched_barrier(0);
+                if (dma && q >= 2) {
+                    issue_q(t + 1 + D, 2 * (q - 2));
+                    issue_q(t + 1 + D, 2 * (q - 2) + 1);
+                }
+            }
+        }
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        lgkm_done(nxt);
+    };
+    auto step = [&](int64_t t, int g, const Frag &cur, Frag &nxt) {
+        if constexpr (IL != 0) {
+            step_il(t, g, cur, nxt);
+            return;
+        }
+        if (g + 1 < GG) {
+            nxt = read(t, g + 1);
+        } else {
+            // boundary t -> t + 1: k-tiles up to min(t + D, nk - 1) are issued
+            retire((t + D < nk - 1 ? t + D : nk - 1) - (t + 1));
+            nxt = read(t + 1, 0);
+            if (t + 1 + D < nk) issue(t + 1 + D);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // (the next fragments' reads go out before these MFMAs)
+        mfma(cur);
+        __builtin_amdgcn_sched_barrier(0);
+        lgkm_done(nxt);  // (landed during the MFMAs)
+    };
+    auto last = [&](const Frag &cur) {  // the last step: no reads after it
+        __builtin_amdgcn_sched_barrier(0);
+        mfma(cur);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    Frag fa = read(0, 0), fb;
+    lgkm_done(fa);
+    fixed = fa;
+    if constexpr (GG == 2) {
+        for (int64_t t = 0; t + 1 < nk; ++t) {
+            step(t, 0, fa, fb);
+            step(t, 1, fb, fa);
+        }
+        step(nk - 1, 0, fa, fb);  // (g = 0 of the last k-tile reads g = 1: no boundary)
+        last(fb);
+    } else {
+        int64_t t = 0;
+        for (; t + 2 < nk; t += 2) {
+            step(t, 0, fa, fb);
+            step(t + 1, 0, fb, fa);
+        }
+        if (t + 1 < nk) {
+            step(t, 0, fa, fb);
+            last(fb);
+        } else {
+            last(fa);
+        }
+    }
+}
+
+// Writes the wave's 64 x 64 quarter (rows r0.., cols c0.. of K) to K[row][col] and, mirrored,
+// K[col][row] (a lane's float4 j holds 4 consecutive rows of one column: one 16-B store mirrored).
+// diag: the quarter straddles the diagonal (a diagonal tile): only entries with col >= row are written
+// (each to both places).  upper: K[row][col] only (the whole quarter, nothing mirrored).
+template <int MF, int BK>
+__device__ __forceinline__ void write_quarter(const DenseArgs &a,
+                                              const typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK]
+                                                                                       [Layout<MF, BK>::NBLK],
+                                              int64_t r0, int64_t c0, bool diag, bool upper, int lane) {
+    using L = Layout<MF, BK>;
+    const int64_t n = a.n, ldk = a.ldk;
+    float *K = a.K;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const f32x4v v = L::get(c, j);
+        const int64_t row = r0 + L::row0(j, lane), col = c0 + L::col(j, lane);
+        if (col >= n) continue;
+        if (upper) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                if (row + s < n) K[(row + s) * ldk + col] = v[s];
+        } else if (!diag && row + 3 < n) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) K[(row + s) * ldk + col] = v[s];
+            if (!(a.abl & 8)) *reinterpret_cast<f32x4v *>(K + col * ldk + row) = v;  // the mirrored entries
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int64_t rr = row + s;
+                if (rr < n && (!diag || col >= rr)) {
+                    K[rr * ldk + col] = v[s];
+                    K[col * ldk + rr] = v[s];
+                }
+            }
+        }
+    }
+}
+
+template <int MF, int BK, int NST, int WPE, int XABL = 0, bool PRIO = false, int IL = 0>
+__global__ __launch_bounds__(256, WPE) void gram_dense_mfma_kernel(DenseArgs a) {
+    using L = Layout<MF, BK>;
+    using St = Stage<BK>;
+    constexpr int NB = L::NBLK;
+    __shared__ __attribute__((aligned(16))) float lds[NST * 2 * St::F];  // (one array: the DMA ring)
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int wm = wave >> 1, wn = wave & 1;
+
+    // work item -> (tile, k slice)
+    const int64_t w = blockIdx.x;
+    int64_t tile, slice = 0, pieces = 1;
+    if (w < a.n_whole) {
+        tile = w;
+    } else {
+        tile = a.n_whole + (w - a.n_whole) / a.n_split;
+        slice = (w - a.n_whole) % a.n_split;
+        pieces = a.n_split;
+    }
+    int64_t bi, bj;
+    tile_coords(tile, a.nt, bi, bj);
+    const int64_t m0 = bi * kTile, n0 = bj * kTile;
+    const bool diag = bi == bj;
+    const int64_t kb = pieces > 1 ? slice * a.k_split : 0;
+    const int64_t ke = pieces > 1 ? (kb + a.k_split < a.kpad ? kb + a.k_split : a.kpad) : a.kpad;
+
+    // per-lane DMA sources: piece j of this wave covers LDS chunks p = (wave * PW + j) * 64 + lane,
+    // i.e. row p / C, stored chunk p % C, which holds logical chunk (p % C) ^ swz(row)
+    const float *srcA[St::PW], *srcB[St::PW];
+#pragma unroll
+    for (int j = 0; j < St::PW; ++j) {
+        const int p = (wave * St::PW + j) * 64 + lane;
+        const int row = p / L::C, kc = (p % L::C) ^ L::swz(row);
+        int64_t ra = m0 + row, rb = n0 + row;
+        ra = ra < a.n ? ra : a.n - 1;  // (rows past n: a valid row, its products are never written)
+        rb = rb < a.n ? rb : a.n - 1;
+        srcA[j] = a.A + ra * a.lda + 4 * kc;
+        srcB[j] = a.A + rb * a.lda + 4 * kc;
+    }
+    int aoff[L::GG], boff[L::GG];  // float offsets of block 0's fragment per group (block x: + x XSTRIDE bytes)
+#pragma unroll
+    for (int g = 0; g < L::GG; ++g) {
+        aoff[g] = L::off(wm * 64, 0, g, lane);
+        boff[g] = L::off(wn * 64, 0, g, lane);
+    }
+    // this wave's quarter: rows m0 + wm*64 .., cols n0 + wn*64 ..; no MFMAs when it lies wholly below the
+    // diagonal or past n
+    const int64_t qr = m0 + wm * 64, qc = n0 + wn * 64;
+    const bool below = diag && wn < wm;
+    const bool live = !below && qr < a.n && qc < a.n;
+
+    typename L::acc_t c[NB][NB];
+#pragma unroll
+    for (int x = 0; x < NB; ++x)
+#pragma unroll
+        for (int y = 0; y < NB; ++y) c[x][y] = typename L::acc_t{};
+    if (diag) {
+        if (live) kloop<MF, BK, NST, true, true, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
+        else kloop<MF, BK, NST, true, false, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
+    } else {
+        if (live) kloop<MF, BK, NST, false, true, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
+        else kloop<MF, BK, NST, false, false, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
+    }
+
+    if (pieces > 1) {
+        // partial tile -> slab; the last of the tile's pieces sums the slabs in slice order
+        const int64_t u = tile - a.n_whole;
+        f32x4v *slab = reinterpret_cast<f32x4v *>(a.slabs) + ((u * pieces + slice) * 4 + wave) * 16 * 64 + lane;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) slab[j * 64] = L::get(c, j);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int32_t *flag = reinterpret_cast<int32_t *>(lds);  // (the ring is idle: every wave is past its k-loop)
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int32_t old = __hip_atomic_fetch_add(a.tickets + u, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int32_t last = old == pieces - 1;
+            if (last) {
+                __hip_atomic_store(a.tickets + u, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            *flag = last;
+        }
+        __syncthreads();
+        if (!*flag) return;
+        const f32x4v *base = reinterpret_cast<const f32x4v *>(a.slabs) + (u * pieces * 4 + wave) * 16 * 64 + lane;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const f32x4v own = L::get(c, j);
+            f32x4v acc = slice == 0 ? own : base[j * 64];
+            for (int64_t s = 1; s < pieces; ++s) acc += s == slice ? own : base[(s * 4 * 16 + j) * 64];
+            L::set(c, j, acc);
+        }
+    }
+    if (qr >= a.n || qc >= a.n) return;
+    if (a.upper_only) {
+        write_quarter<MF, BK>(a, c, qr, qc, false, true, lane);
+    } else if (!below) {
+        write_quarter<MF, BK>(a, c, qr, qc, diag && wm == wn, false, lane);
+    }
+}
+
+constexpr int kCUs = 256;
+
+int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+// Workspace layout, the same for every (n, k): kMaxSplitTiles tickets at a fixed place, then the slabs.
+// A ticket is zero between launches (the last arriver resets it) and slabs never overlap the ticket
+// block, so one workspace, zeroed once, serves calls of any size in any order on its stream.
+constexpr int64_t kMaxSplitTiles = 1024;  // (tiles < 512 when all split; the tail is < 1024)
+constexpr size_t kTicketBytes = kMaxSplitTiles * sizeof(int32_t);
+
+struct DensePlan {
+    int64_t nt, tiles, n_whole, k_split, kpad;
+    int32_t n_split;
+    size_t ws_bytes;  // tickets + slabs
+};
+
+// Work plan: whole tiles, and split pieces where whole tiles would leave CUs idle -- every tile split
+// when the tiles alone do not fill the GPU (small n), else the last `tail` tiles.
+// A/B knobs (read once): GRF_DENSE_SPLIT (pieces per split tile), GRF_DENSE_TAIL (split tiles at the end)
+DensePlan dense_plan(int64_t n, int64_t k_dim, int bk) {
+    DensePlan p{};
+    p.nt = cdiv<int64_t>(n, kTile);
+    p.tiles = p.nt * (p.nt + 1) / 2;
+    p.kpad = cdiv<int64_t>(k_dim, bk) * bk;
+    static const int env_split = env_int("GRF_DENSE_SPLIT", -1);
+    static const int env_tail = env_int("GRF_DENSE_TAIL", -1);
+    constexpr int64_t slots = 2 * kCUs;  // workgroups resident at once (2 per CU: 64 KiB of LDS ring each)
+    int64_t split = 1, tail = 0;
+    if (p.tiles < slots) {  // small n: every tile split, ~2 pieces per CU slot
+        split = std::max<int64_t>(1, std::min<int64_t>(4, slots / std::max<int64_t>(p.tiles, 1)));
+        tail = p.tiles;
+    } else if (p.tiles % slots != 0) {
+        // large n: the last round of whole tiles would leave (slots - tiles % slots) slots idle; the
+        // last slots + tiles % slots tiles go in thirds instead, so the final rounds are cut 3x finer
+        split = 3;
+        tail = std::min<int64_t>(p.tiles, slots + p.tiles % slots);
+    }
+    if (env_split >= 1) split = env_split;
+    if (env_tail >= 0) tail = std::min<int64_t>(env_tail, p.tiles);
+    tail = std::min<int64_t>(tail, kMaxSplitTiles);
+    const int64_t ktiles = p.kpad / bk;
+    split = std::max<int64_t>(1, std::min<int64_t>(split, ktiles));
+    if (split == 1) tail = 0;
+    p.n_split = (int32_t)split;
+    p.n_whole = p.tiles - tail;
+    p.k_split = cdiv<int64_t>(ktiles, split) * bk;
+    if (tail > 0) p.n_split = (int32_t)cdiv<int64_t>(p.kpad, p.k_split);  // (no empty piece)
+    if (p.n_split <= 1) {
+        p.n_split = 1;
+        p.n_whole = p.tiles;
+    }
+    const int64_t split_tiles = p.tiles - p.n_whole;
+    p.ws_bytes = split_tiles > 0 ? kTicketBytes + (size_t)split_tiles * p.n_split * kTile * kTile * sizeof(float) : 0;
+    return p;
+}
+
+}  // namespace
+
+size_t dense_gram_workspace_bytes(int64_t n, int64_t k_dim) {
+    if (n <= 0) return 16;
+    const DensePlan p = dense_plan(n, k_dim, 16);
+    return std::max<size_t>(16, p.ws_bytes);
+}
+
+int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk, void *workspace,
+                   size_t workspace_bytes, bool upper_only, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && k_dim >= 0 && A && K && ldk >= n && lda >= k_dim, GRF_EINVAL,
+                "grf_gram_dense: bad arguments");
+    GRF_REQUIRE(lda % 16 == 0 && ((uintptr_t)A & 15) == 0, GRF_EINVAL,
+                "grf_gram_dense: lda must be a multiple of 16 and A 16-byte aligned");
+    GRF_REQUIRE(upper_only || (ldk % 4 == 0 && ((uintptr_t)K & 15) == 0), GRF_EINVAL,
+                "grf_gram_dense: ldk must be a multiple of 4 and K 16-byte aligned");
+    if (n == 0) return GRF_OK;
+    static const int variant = env_int("GRF_DENSE_VARIANT", 0);
+    const int BK = variant / 100 % 100 == 32 ? 32 : 16;
+    DensePlan p = dense_plan(n, k_dim, BK);
+    GRF_REQUIRE(p.kpad <= lda, GRF_EINVAL, "grf_gram_dense: lda must cover k_dim rounded up to %d", BK);
+    if (p.ws_bytes > 0 && (!workspace || workspace_bytes < p.ws_bytes || ((uintptr_t)workspace & 255))) {
+        // no (or too small) workspace: whole tiles only
+        p.n_split = 1;
+        p.n_whole = p.tiles;
+        p.ws_bytes = 0;
+    }
+    const int64_t split_tiles = p.tiles - p.n_whole;
+    const int64_t items = p.n_whole + split_tiles * p.n_split;
+    GRF_REQUIRE_GRID(items, 256, "gram_dense_mfma_kernel");
+    DenseArgs a{};
+    a.A = A;
+    a.K = K;
+    a.tickets = split_tiles > 0 ? reinterpret_cast<int32_t *>(workspace) : nullptr;
+    a.slabs = split_tiles > 0 ? reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes) : nullptr;
+    a.n = n;
+    a.nt = p.nt;
+    a.lda = lda;
+    a.ldk = ldk;
+    a.kpad = p.kpad;
+    a.n_whole = p.n_whole;
+    a.k_split = p.k_split;
+    a.n_split = p.n_split;
+    a.upper_only = upper_only ? 1 : 0;
+    static const int abl = env_int("GRF_DENSE_ABL", 0);
+    a.abl = abl;
+    const unsigned grid = (unsigned)items;
+    hipStream_t st = S(stream);
+    static const bool prio = env_int("GRF_DENSE_PRIO", 0) == 1;
+    static const int il = env_int("GRF_DENSE_IL", 1);
+    switch ((variant ? variant : 321642) + (prio ? 1000000 : 0) + il * 2000000) {  // A/B (GRF_DENSE_VARIANT): MF * 10000 + BK * 100 + stages * 10 + waves per SIMD
+        case 321642: gram_dense_mfma_kernel<32, 16, 4, 2><<<grid, 256, 0, st>>>(a); break;
+        case 321652: gram_dense_mfma_kernel<32, 16, 5, 2><<<grid, 256, 0, st>>>(a); break;
+        case 161652: gram_dense_mfma_kernel<16, 16, 5, 2><<<grid, 256, 0, st>>>(a); break;
+        case 1321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, true><<<grid, 256, 0, st>>>(a); break;
+        case 1161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, true><<<grid, 256, 0, st>>>(a); break;
+        case 2161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, false, 1><<<grid, 256, 0, st>>>(a); break;
+        case 2321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 1><<<grid, 256, 0, st>>>(a); break;
+        case 3161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, true, 1><<<grid, 256, 0, st>>>(a); break;
+        case 3321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, true, 1><<<grid, 256, 0, st>>>(a); break;
+        case 4321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 2><<<grid, 256, 0, st>>>(a); break;
+        case 6321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 3><<<grid, 256, 0, st>>>(a); break;
+        case 4161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, false, 2><<<grid, 256, 0, st>>>(a); break;
+        case 6161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, false, 3><<<grid, 256, 0, st>>>(a); break;
+        default: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 1><<<grid, 256, 0, st>>>(a); break;
+    }
+    GRF_CHECK_LAUNCH("gram_dense_mfma_kernel");
+    return GRF_OK;
+}
+
+}  // namespace grf

@@ -80,8 +80,8 @@ class GraphDiffusionFastGRFKernel(torch.nn.Module):
 
     def grf_kernel(self, beta, sigma_f) -> np.ndarray:
         """The whole K (reference :46-60), fp64 numpy."""
-        f = self.modulator(float(beta))
-        return float(sigma_f) ** 2 * self._steps.gram(f).cpu().numpy().astype(np.float64)
+        b = float(beta)
+        return float(sigma_f) ** 2 * self._steps.gram(self.modulator(b), key=("beta", b)).cpu().numpy().astype(np.float64)
 
     def K_torch(self, X1, X2=None) -> torch.Tensor:
         Kf = self.sigma_f ** 2 * DenseGramFunction.apply(self.modulator(self.beta), self._steps)
@@ -90,7 +90,8 @@ class GraphDiffusionFastGRFKernel(torch.nn.Module):
         return Kf[i1][:, i2]
 
     def _cached(self) -> torch.Tensor:
-        return float(self.sigma_f.detach()) ** 2 * self._steps.gram(self.modulator(float(self.beta.detach())))
+        b = float(self.beta.detach())
+        return float(self.sigma_f.detach()) ** 2 * self._steps.gram(self.modulator(b), key=("beta", b))
 
     def K(self, X1, X2=None) -> np.ndarray:
         Kf = self._cached()

@@ -79,9 +79,10 @@ class GraphGeneralFastGRFKernel(torch.nn.Module):
 
     def grf_kernel(self, modulator_vector) -> np.ndarray:
         """The whole K (reference :74-77), fp64 numpy."""
-        f = torch.as_tensor(np.asarray(modulator_vector, dtype=np.float64) if not torch.is_tensor(modulator_vector)
-                            else modulator_vector.detach())
-        return self._steps.gram(f).cpu().numpy().astype(np.float64)
+        if torch.is_tensor(modulator_vector):
+            return self._steps.gram(modulator_vector.detach()).cpu().numpy().astype(np.float64)
+        fv = np.asarray(modulator_vector, dtype=np.float64)  # (host values: cached by value)
+        return self._steps.gram(torch.as_tensor(fv), key=("f", fv.tobytes())).cpu().numpy().astype(np.float64)
 
     def K_torch(self, X1, X2=None) -> torch.Tensor:
         """K[X1, X2] on the device, differentiable w.r.t. ``modulator_vector``."""

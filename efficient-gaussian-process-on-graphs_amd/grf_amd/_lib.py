@@ -26,6 +26,7 @@ RNG_PCG64, RNG_PHILOX = 0, 1
 LOAD_CUMULATIVE, LOAD_NONCUMULATIVE, LOAD_ABLATION = 0, 1, 2
 NORM_DIV, NORM_MUL_RECIP = 0, 1
 REC_LINE, REC_PACKED, REC_SLOT = 128, 12, 32
+ABI_VERSION = 4  # include/grf.h GRF_ABI_VERSION: argument lists change between revisions
 
 
 class GrfWalkParams(ctypes.Structure):
@@ -75,22 +76,14 @@ SIGNATURES = {
                                          _vp]),
     "grf_transpose_workspace_bytes": (_sz, [_i64]),
     "grf_gram_sparse": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
-    "grf_gram_sparse_block": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
-                                     _sz, _vp]),
     "grf_gram_workspace_bytes": (_sz, []),
     "grf_gram_sparse_cols": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp,
                                     _i64, _vp, _sz, _vp]),
-    "grf_gram_sparse_cols_add": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp,
-                                        _vp, _i64, _vp, _sz, _vp]),
     "grf_phi_row_shifts_workspace_bytes": (_sz, [_i64]),
     "grf_phi_row_shifts": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_phi_row_shifts_stats": (_i32, [_i64, _vp, _vp, _vp, _vp]),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _i64, _vp]),
-    "grf_gram_mirror_rect": (_i32, [_i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
-    "grf_gram_sym_fused_workspace_bytes": (_sz, [_i64, _i64]),
-    "grf_gram_sparse_sym_fused": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32,
-                                         _vp, _sz, _vp]),
     "grf_gram_sparse_upper": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
                                      _i32, _vp, _sz, _vp]),
     "grf_gram_row_cuts": (_i32, [_i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp]),
@@ -160,9 +153,13 @@ def load():
             f"grf_amd: native library {LIB_PATH} is missing; build it with "
             f"`make -C {CSRC}` (or __graft_entry__.build()).  There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH)
+    lib.grf_version.restype = ctypes.c_int32
+    lib.grf_version.argtypes = []
+    got = int(lib.grf_version())
+    if got != ABI_VERSION:
+        raise ImportError(f"grf_amd: {LIB_PATH} implements ABI revision {got}, this binding needs {ABI_VERSION} "
+                          f"(rebuild it with `make -C {CSRC}`)")
     for name, (res, args) in SIGNATURES.items():
-        if os.environ.get("GRF_AMD_LIB") and not hasattr(lib, name):
-            continue  # (an A/B build from before this entry point existed)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -61,12 +61,20 @@ class DeviceCSR:
     val: Optional[torch.Tensor] = None    # float64
     val32: Optional[torch.Tensor] = None  # float32
     _nnz: Optional[int] = None
+    nnz_bound: Optional[int] = None  # an upper bound of nnz known without a host read (buffers sized by it)
+    row_bound: Optional[int] = None  # an upper bound of the entries of any one row
 
     @property
     def nnz(self) -> int:
         if self._nnz is None:
             self._nnz = int(self.ptr[-1].item())
         return self._nnz
+
+    def nnz_or_bound(self) -> int:
+        """nnz when it is known on the host, else the bound (no device->host read), else nnz (read)."""
+        if self._nnz is not None:
+            return self._nnz
+        return self.nnz_bound if self.nnz_bound is not None else self.nnz
 
     @classmethod
     def from_scipy(cls, A, device) -> "DeviceCSR":
@@ -566,20 +574,6 @@ class GRFEngine:
                 "grf_gram_sparse")
         return out[:, :n]
 
-    def gram_sparse_block(self, phi: DeviceCSR, tr: Banded, row_begin: int, row_end: int,
-                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """K[row_begin:row_end, :] (float32) using the symmetry inside the row block (grf_gram_sparse_block)."""
-        n = tr.n_rows
-        ldk = self.leading_dim(n)
-        if out is None:
-            out = torch.empty((row_end - row_begin, ldk), dtype=torch.float32, device=self.device)
-        C.check(self.lib.grf_gram_sparse_block(n, row_begin, row_end, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
-                                               tr.band_width, tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec),
-                                               _p(tr.t_split), _p(tr.t_rowshift), _p(out), out.stride(0),
-                                               _p(self._gram_ws), self._gram_ws.numel(), self.stream),
-                "grf_gram_sparse_block")
-        return out[:, :n]
-
     def phi_row_shifts(self, phi: DeviceCSR) -> torch.Tensor:
         """The Gram fixed-point shifts of every row of Phi (int32 [n_rows]; grf_phi_row_shifts): the
         same values as ``transpose_banded(phi).t_rowshift``, for rows that are not in the transpose."""
@@ -617,31 +611,6 @@ class GRFEngine:
                                               _p(self._gram_ws), self._gram_ws.numel(), self.stream),
                 "grf_gram_sparse_cols")
         return out[:, :t_rows]
-
-    def gram_sparse_cols_hubs(self, phi: DeviceCSR, row_shift: torch.Tensor, tr_b: Banded, b0: int, hubs: int,
-                              out: Optional[torch.Tensor] = None, sym_row0: Optional[int] = None) -> torch.Tensor:
-        """Column block K[:, b0:b0+t] = Phi Phi[b0:b0+t]^T (``gram_sparse_cols`` with Phi_B = Phi[b0:b0+t]) with
-        the hub-column split: the ``hubs`` columns with the most entries in the block's transpose go to a
-        dense fp32 panel P of all rows (``hub_split``: their buckets emptied from ``tr_b``, which is
-        consumed), the block gets K_blk = P P[b0:b0+t]^T from a plain GEMM (rocBLAS / hipBLASLt through
-        torch.mm: a library GEMM, n x t x hubs multiply-adds), and the sparse tiles add the remaining
-        columns' fixed-point sums (``grf_gram_sparse_cols_add``).  Within the fp32 K tolerance."""
-        n, t = phi.n_rows, tr_b.n_rows
-        if out is None:
-            out = torch.empty((n, self.leading_dim(max(t, 1))), dtype=torch.float32, device=self.device)
-        P, cols = self.hub_split(phi, tr_b, hubs)
-        blk = out[:, :t]
-        if blk.is_contiguous():
-            torch.mm(P, P[b0:b0 + t].t(), out=blk)
-        else:
-            blk.copy_(P @ P[b0:b0 + t].t())
-        del P
-        C.check(self.lib.grf_gram_sparse_cols_add(phi.n_cols, 0, n, _p(phi.ptr), _p(phi.idx), _p(phi.val32),
-                                                  _p(row_shift), t, -1 if sym_row0 is None else int(sym_row0),
-                                                  tr_b.band_width, tr_b.rec_unit, _p(tr_b.t_desc), _p(tr_b.t_rec),
-                                                  _p(tr_b.t_split), _p(out), out.stride(0), _p(self._gram_ws),
-                                                  self._gram_ws.numel(), self.stream), "grf_gram_sparse_cols_add")
-        return out[:, :t]
 
     def gram_sparse_kslice(self, phi: DeviceCSR, tr: Banded, k_begin: int, k_end: int, row_begin: int = 0,
                            row_end: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -793,37 +762,11 @@ class GRFEngine:
             after_tiles(ev)
         return out[:, :n]
 
-    def gram_sparse_sym_fused(self, phi: DeviceCSR, tr: Banded, out: Optional[torch.Tensor] = None,
-                              parts=(0, 1, 1)) -> torch.Tensor:
-        """Whole K as ``gram_sparse_sym`` (bit-identical) with the symmetric completion fused into the
-        Gram tiles (no mirror pass).  parts = (begin, end, n): those parts of the tile sequence; the
-        parts of one K must be issued in order on this engine's stream."""
-        n = tr.n_rows
-        if out is None:
-            out = torch.empty((n, self.leading_dim(n)), dtype=torch.float32, device=self.device)
-        need = int(self.lib.grf_gram_sym_fused_workspace_bytes(n, tr.band_width))
-        ws = getattr(self, "_fused_ws", None)
-        if ws is None or ws.numel() < need:
-            ws = self._fused_ws = self._ws(need)
-        C.check(self.lib.grf_gram_sparse_sym_fused(n, _p(phi.ptr), _p(phi.idx), _p(phi.val32), tr.band_width,
-                                                   tr.rec_unit, _p(tr.t_desc), _p(tr.t_rec), _p(tr.t_rowshift),
-                                                   _p(out), out.stride(0), int(parts[0]), int(parts[1]),
-                                                   int(parts[2]), _p(ws), ws.numel(), self.stream),
-                "grf_gram_sparse_sym_fused")
-        return out[:, :n]
-
     def gram_mirror(self, K: torch.Tensor, n: int, max_workgroups: int = 0) -> torch.Tensor:
         """K[j, i] = K[i, j] for every j > i (the second half of ``gram_sparse_sym``).
         max_workgroups > 0 bounds the grid (leaves CU slots to work on another stream)."""
         C.check(self.lib.grf_gram_mirror(n, _p(K), K.stride(0), int(max_workgroups), self.stream), "grf_gram_mirror")
         return K[:, :n]
-
-    def gram_mirror_rect(self, K: torch.Tensor, n: int, rows: Tuple[int, int], cols: Tuple[int, int],
-                         max_workgroups: int = 0) -> None:
-        """The mirror pass over the 64-blocks of K[rows[0]:rows[1], cols[0]:cols[1]] on or above the
-        diagonal (starts multiples of 64): K[j, i] = K[i, j] for j > i there."""
-        C.check(self.lib.grf_gram_mirror_rect(n, _p(K), K.stride(0), int(rows[0]), int(rows[1]), int(cols[0]),
-                                              int(cols[1]), int(max_workgroups), self.stream), "grf_gram_mirror_rect")
 
     def densify(self, phi: DeviceCSR) -> torch.Tensor:
         lda = max(64, -(-phi.n_cols // 64) * 64)  # (zero-padded k: every k-tile width of the MFMA Gram divides it)
@@ -836,11 +779,12 @@ class GRFEngine:
         n = dense_phi.shape[0]
         ldk = self.leading_dim(n)
         out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
-        # split-K partials for small n (too few tiles to fill the GPU): a cached workspace
+        # split-K partial tiles (small n, or the last tiles of a large n) and their tickets: a cached
+        # workspace, zeroed once (the kernel leaves the tickets zero after every launch)
         need = int(self.lib.grf_gram_dense_workspace_bytes(n, k_dim))
         ws = getattr(self, "_dense_ws", None)
         if ws is None or ws.numel() < need:
-            ws = self._dense_ws = self._ws(need)
+            ws = self._dense_ws = torch.zeros(max(need, 16), dtype=torch.uint8, device=self.device)
         C.check(self.lib.grf_gram_dense_ws(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, _p(ws),
                                            ws.numel(), self.stream), "grf_gram_dense_ws")
         return out[:, :n]
@@ -901,8 +845,13 @@ class GRFEngine:
         """(Phi[rows])^T as CSR (n_cols x len(rows), float32); column lists in ascending row order."""
         rmap = self._row_map(rows)
         n_sel = phi.n_rows if rmap is None else rmap.numel()
+        # the entries to transpose, or an upper bound of them (no host read; the C side ignores the tail)
+        exact = True
         if rmap is None:
-            nnz = phi.nnz
+            nnz = phi.nnz_or_bound()
+            exact = phi._nnz is not None
+        elif phi.row_bound is not None:
+            nnz, exact = n_sel * phi.row_bound, False
         else:
             rl = rmap.long()
             nnz = int((phi.ptr[rl + 1] - phi.ptr[rl]).sum().item()) if n_sel else 0
@@ -913,7 +862,7 @@ class GRFEngine:
         C.check(self.lib.grf_csr_transpose(n_sel, _p(phi.ptr), _p(phi.idx), _p(phi.val32), _p(rmap), phi.n_cols, nnz,
                                            _p(t_ptr), _p(t_idx), _p(t_val), _p(ws), ws.numel(), self.stream),
                 "grf_csr_transpose")
-        return DeviceCSR(phi.n_cols, n_sel, t_ptr, t_idx, None, t_val, nnz)
+        return DeviceCSR(phi.n_cols, n_sel, t_ptr, t_idx, None, t_val, nnz if exact else None, nnz_bound=nnz)
 
     def spmm(self, A: DeviceCSR, X: torch.Tensor, rows=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Y = A[rows] X (X float32 or float64, n_cols x S with unit column stride; Y the same type)."""

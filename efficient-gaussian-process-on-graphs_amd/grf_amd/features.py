@@ -73,6 +73,11 @@ class StepMatrices:
             idx = t.col_indices().to(dev, torch.int32).contiguous()
             val = t.values().to(dev, torch.float32).contiguous()
             self.steps.append(DeviceCSR(self.shape[0], self.shape[1], ptr, idx, None, val, int(idx.numel())))
+        # bounds of Phi = sum_l f_l M_l, from one host read here (the forward / backward read nothing back):
+        # its entries <= sum_l nnz(M_l), a row's entries <= sum_l (the longest row of M_l)
+        self.nnz_sum = sum(s.nnz for s in self.steps)
+        lens = torch.stack([(s.ptr[1:] - s.ptr[:-1]).max() if self.shape[0] else s.ptr[:1] * 0 for s in self.steps])
+        self.row_bound = int(min(self.shape[1], int(lens.sum().item())))
         # host arrays of the L device pointers (the C ABI's step_ptr / step_idx / step_val)
         self._arrays = [(ctypes.c_void_p * len(self.steps))(*[getattr(s, a).data_ptr() for s in self.steps])
                         for a in ("ptr", "idx", "val32")]
@@ -83,7 +88,8 @@ class StepMatrices:
         return len(self.steps)
 
     def phi(self, f: torch.Tensor, want64: bool = False) -> DeviceCSR:
-        """Phi = sum_l f_l M_l (compact CSR, fp32 values [+ fp64]) for the modulator f (len >= 1)."""
+        """Phi = sum_l f_l M_l (compact CSR, fp32 values [+ fp64]) for the modulator f (len >= 1).
+        No host synchronisation: the entry buffers are sized by ``nnz_sum`` (``DeviceCSR.nnz_bound``)."""
         eng = self.engine
         n = self.shape[0]
         ft = f.detach().to(eng.device, torch.float64).contiguous().flatten()
@@ -94,18 +100,19 @@ class StepMatrices:
         ptr = eng._empty(n + 1, torch.int64)
         ws = eng._ws(eng.lib.grf_scan_workspace_bytes(n))
         C.check(eng.lib.grf_scan_counts(n, _p(cnt), _p(ptr), _p(ws), ws.numel(), eng.stream), "grf_scan_counts")
-        nnz = int(ptr[-1].item())
-        idx = eng._empty(nnz, torch.int32)
-        v32 = eng._empty(nnz, torch.float32)
-        v64 = eng._empty(nnz, torch.float64) if want64 else None
+        cap = max(self.nnz_sum, 1)
+        idx = eng._empty(cap, torch.int32)
+        v32 = eng._empty(cap, torch.float32)
+        v64 = eng._empty(cap, torch.float64) if want64 else None
         C.check(eng.lib.grf_phi_steps_csr_fill(n, self.L, self._ptrs[0], self._ptrs[1], self._ptrs[2], _p(ft), nf,
                                                _p(ptr), _p(idx), _p(v64), _p(v32), eng.stream),
                 "grf_phi_steps_csr_fill")
-        return DeviceCSR(n, self.shape[1], ptr, idx, v64, v32, nnz)
+        return DeviceCSR(n, self.shape[1], ptr, idx, v64, v32, None, nnz_bound=self.nnz_sum, row_bound=self.row_bound)
 
 
 def gather_rows(eng: GRFEngine, A: DeviceCSR, rows: torch.Tensor) -> DeviceCSR:
-    """A[rows] as a compact CSR (rows may repeat)."""
+    """A[rows] as a compact CSR (rows may repeat).  With ``A.row_bound`` known the entry buffers are
+    sized by rows x that bound and nothing is read back to the host."""
     rmap = rows.to(eng.device, torch.int32).contiguous()
     n_sel = rmap.numel()
     cnt = eng._empty(n_sel, torch.int32)
@@ -113,12 +120,16 @@ def gather_rows(eng: GRFEngine, A: DeviceCSR, rows: torch.Tensor) -> DeviceCSR:
     ptr = eng._empty(n_sel + 1, torch.int64)
     ws = eng._ws(eng.lib.grf_scan_workspace_bytes(n_sel))
     C.check(eng.lib.grf_scan_counts(n_sel, _p(cnt), _p(ptr), _p(ws), ws.numel(), eng.stream), "grf_scan_counts")
-    nnz = int(ptr[-1].item()) if n_sel else 0
-    idx = eng._empty(nnz, torch.int32)
-    val = eng._empty(nnz, torch.float32)
+    if A.row_bound is not None:
+        nnz, bound = None, n_sel * A.row_bound
+    else:
+        nnz = int(ptr[-1].item()) if n_sel else 0
+        bound = nnz
+    idx = eng._empty(max(bound, 1), torch.int32)
+    val = eng._empty(max(bound, 1), torch.float32)
     C.check(eng.lib.grf_csr_gather_rows(n_sel, _p(A.ptr), _p(A.idx), _p(A.val32), _p(rmap), _p(ptr), _p(idx),
                                         _p(val), eng.stream), "grf_csr_gather_rows")
-    return DeviceCSR(n_sel, A.n_cols, ptr, idx, None, val, nnz)
+    return DeviceCSR(n_sel, A.n_cols, ptr, idx, None, val, nnz, nnz_bound=bound, row_bound=A.row_bound)
 
 
 def rowdot(eng: GRFEngine, A: DeviceCSR, rows_a: Optional[torch.Tensor], B: DeviceCSR,
@@ -154,7 +165,7 @@ def kernel_block(eng: GRFEngine, phi: DeviceCSR, x1: Optional[torch.Tensor], x2:
     n1, n2 = P1.n_rows, P2.n_rows
     if n1 == 0 or n2 == 0:
         return torch.zeros((n1, n2), dtype=torch.float32, device=eng.device)
-    tr = eng.transpose_banded(P2, cols_band_width(n2))
+    tr = eng.transpose_banded(P2, cols_band_width(n2), nnz_bound=P2.nnz_or_bound())
     # the fixed-point shift of row r bounds |Phi[r, k] Phi[j, k]| with max|Phi| over the OTHER operand's
     # rows j too: take it over all of Phi (a superset of Phi[x1] and Phi[x2]) and pick the x1 rows
     shifts = eng.phi_row_shifts(phi)
@@ -176,8 +187,12 @@ class GRFKernelFunction(torch.autograd.Function):
         dev = eng.device
         n = steps.shape[0]
         i1, i2 = _index(x1, dev), _index(x2, dev)
-        same = (i1 is None and i2 is None) or (i1 is not None and i2 is not None and i1.shape == i2.shape
-                                               and bool(torch.equal(i1, i2)))
+        # x1 and x2 the same rows (the symmetric block): decided without reading the indices back -- the
+        # same tensor, or views of the same memory (a K(x, x) call); equal values in two different tensors
+        # take the general column-block path (the same numbers within the K tolerance)
+        same = (x1 is None and x2 is None) or (x1 is x2) or (
+            i1 is not None and i2 is not None and i1.shape == i2.shape and i1.data_ptr() == i2.data_ptr()
+            and i1.stride() == i2.stride())
         phi = steps.phi(f)
         if diag:
             n1 = n if i1 is None else i1.numel()
@@ -247,7 +262,7 @@ class DenseSteps:
             raise ValueError("step tensor must be (N, N, L)")
         self.n, self.L = self.F.shape[0], self.F.shape[2]
         self.lda = max(64, -(-self.n // 64) * 64)  # (zero-padded k range of the MFMA Gram)
-        self._key = None
+        self._key = None  # the cached K's key (gram)
         self._K = None
         self._phi64 = None
 
@@ -270,13 +285,22 @@ class DenseSteps:
         """Phi = F f (N x N, fp64 on the device): ``tf.linalg.matmul(F, f[:, None])`` (:76)."""
         return self._phi_both(f)[0]
 
-    def gram(self, f: torch.Tensor) -> torch.Tensor:
-        """K = Phi Phi^T (fp32, N x N) on the MFMA Gram, cached for the last modulator value."""
-        key = f.detach().to("cpu", torch.float64).reshape(-1).numpy().tobytes()
-        if key != self._key:
+    def gram(self, f: torch.Tensor, key=None) -> torch.Tensor:
+        """K = Phi Phi^T (fp32, N x N) on the MFMA Gram, cached.  The cache key: ``key`` when the caller
+        has a host-side one (the modulator's own parameters, e.g. ("beta", b)), else the modulator
+        TENSOR -- the same memory at the same version counter (an in-place update such as an optimiser
+        step bumps it; a tensor autograd saved for the backward shares both; the cache holds the tensor,
+        so its memory cannot be reused by another).  Neither reads f back to the host."""
+        k = self._key
+        if key is not None:
+            hit = k is not None and k[0] == "host" and k[1] == key
+        else:
+            hit = k is not None and k[0] == "tensor" and f.data_ptr() == k[1].data_ptr() and \
+                f._version == k[2] and f.shape == k[1].shape and f.dtype == k[1].dtype and f.stride() == k[1].stride()
+        if not hit:
             self._phi64, phi32 = self._phi_both(f)
             self._K = self.engine.gram_dense(phi32, self.n)
-            self._key = key
+            self._key = ("host", key) if key is not None else ("tensor", f, f._version)
         return self._K
 
     def grad(self, f: torch.Tensor, G: torch.Tensor) -> torch.Tensor:

@@ -19,14 +19,13 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, List, Optional, Tuple
 
 import numpy as np
 import torch
 
 from .engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, SELF_COUNT_TRANSPOSE, DeviceCSR, GRFEngine, cols_band_width
 
-FUSED_DEFAULT = os.environ.get("GRF_GRAM_FUSED", "0") == "1"
 # column blocks with sparse buckets take the GRF_REC_SLOT transpose (GRF_REC_SLOTS=0: packed pairs, A/B)
 SLOTS_DEFAULT = os.environ.get("GRF_REC_SLOTS", "1") == "1"
 # one GPU, column blocks: the compaction leaves the rows' Gram shift statistics (GRF_COMPACT_STATS=0: a
@@ -56,8 +55,7 @@ class StepPlan:
     mode: str = "sym"              # "sym" (one GPU, whole K), "rows", "cols", "allreduce"
     band_width: int = DEFAULT_BAND_WIDTH
     cols_sym: bool = False         # column blocks: the square K[b:e, b:e] by the symmetric enumeration
-    fused: bool = False            # "sym": symmetric completion fused into the Gram tiles (no mirror pass)
-    hubs: int = 0                  # "sym" / "cols": Phi's densest columns as a dense panel (hub-column split)
+    hubs: int = 0                  # "sym": Phi's densest columns as a dense MFMA panel (hub-column split)
     skewed: bool = False           # "sym": Phi's column counts are skewed -> pair-balanced wave shares (row_cuts)
     group: object = None           # torch.distributed group (N > 1)
     collective: bool = False       # the Phi all-gather runs (N > 1; or one rank, to rehearse RCCL on one GPU)
@@ -90,13 +88,12 @@ class StepPlan:
 
 def plan_step(n: int, m: int, L: int, p_halt: float, f, *, seed: int = 42, world: int = 1, rank: int = 0,
               mode: str = "cols", k_rows: int = 0, band_width: int = 0, no_sym: bool = False,
-              shards: Optional[List[Tuple[int, int]]] = None, group=None, fused: Optional[bool] = None,
+              shards: Optional[List[Tuple[int, int]]] = None, group=None,
               collective: Optional[bool] = None) -> StepPlan:
     """The bench's mode rules: one GPU whole K -> symmetric mode; N > 1 or K-row workloads -> column
     blocks (``mode="cols"``), row blocks (``"rows"``) or the all-reduce option (``"allreduce"``).
     shards: every rank's source range (default: equal node counts; dist.balanced_shards for equal
-    estimated work).  fused: the symmetric mode's completion inside the Gram tiles (default: env
-    GRF_GRAM_FUSED, off).  collective (default: world > 1): plan the multi-GPU step -- column / row
+    estimated work).  collective (default: world > 1): plan the multi-GPU step -- column / row
     blocks after a Phi all-gather -- even for one rank (bench.py's GRF_DIST_FORCE=1 runs RCCL's
     collectives on a one-GPU box through exactly the N > 1 code)."""
     from .dist import shard_range
@@ -122,7 +119,6 @@ def plan_step(n: int, m: int, L: int, p_halt: float, f, *, seed: int = 42, world
     elif not pl.collective and not no_sym and not k_rows:
         pl.mode = "sym"
         pl.band_width = band_width or DEFAULT_BAND_WIDTH
-        pl.fused = FUSED_DEFAULT if fused is None else bool(fused)
     else:
         pl.mode = "rows"
         pl.band_width = band_width or ROWS_BAND_WIDTH
@@ -163,17 +159,16 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
                          row_cap=pl.rows_cap, always=True) if pl.collective else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
                                             local.val32)
-        # (sparse buckets: the slot layout -- one line per small bucket in the Gram; not under the hub split)
+        # (sparse buckets: the slot layout -- one line per small bucket in the Gram)
         tr = eng.transpose_banded(blk, pl.band_width, counted_ws=tws, nnz_bound=pl.block_rows * pl.rows_cap,
-                                  slots=SLOTS_DEFAULT and pl.hubs == 0 and tws is None)
+                                  slots=SLOTS_DEFAULT and tws is None)
         return Front(phi, tr, local, eng.phi_row_shifts(phi))
     return front_transpose(eng, pl, front_walk(eng, A_dev, pl, G))
 
 
 def front_walk(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan, G: Optional[DeviceCSR] = None) -> Front:
     """The first part of a row / symmetric-mode front: Laplacian -> fused walks -> compaction -> [gather]
-    (``Front.tr`` is None until ``front_transpose``).  The bench may issue the two parts on different
-    streams (--front-split)."""
+    (``Front.tr`` is None until ``front_transpose``)."""
     from .dist import gather_phi
 
     n, b, e = pl.n, pl.b, pl.e
@@ -199,54 +194,24 @@ def front_transpose(eng: GRFEngine, pl: StepPlan, fr: Front) -> Front:
                                  nnz_bound=pl.n * pl.rows_cap)
     # the whole-K tiles' pair-balanced wave shares (policy: engine.ROW_CUTS; the hub split makes its own
     # after dropping the hub columns)
-    fr.cuts = eng.row_cuts(fr.phi, fr.tr, pl.skewed) if pl.mode == "sym" and not pl.fused and pl.hubs == 0 else None
+    fr.cuts = eng.row_cuts(fr.phi, fr.tr, pl.skewed) if pl.mode == "sym" and pl.hubs == 0 else None
     return fr
 
 
 def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
                after_tiles: Optional[Callable[[torch.cuda.Event], None]] = None, mirror_workgroups: int = 0,
-               front_at: float = 1.0, mirror_stream: Optional[torch.cuda.Stream] = None,
-               trailing: int = 0, trail_streams: Sequence[torch.cuda.Stream] = ()):
+               front_at: float = 1.0):
     """The K assembly of one step from its front.  Symmetric mode: ``after_tiles(event)`` is called
     between the Gram tiles and the mirror (the pipelined bench issues the next front there, beside
-    the HBM-bound mirror; ``mirror_workgroups`` then bounds the mirror's grid, 1024 measured best).
-    mirror_stream (symmetric mode): the mirror runs there after the tiles, so that the caller's stream
-    can start the next step's Gram tiles -- into another K buffer -- before it ends; returns the event
-    recorded after the mirror (the caller orders the next write of this K after it) instead of K.
-    trailing > 0 (symmetric mode): ``k_assembly_trailing`` with chunks of that many rows, the mirror on
-    ``trail_streams[0]``, the tile chunks dealt to the caller's stream and ``trail_streams[1:]``."""
+    the HBM-bound mirror; ``mirror_workgroups`` then bounds the mirror's grid, 1024 measured best);
+    front_at < 1 issues it after that share of the tiles instead."""
     from .dist import allreduce_buckets
 
-    if pl.mode == "cols" and pl.hubs > 0:
-        eng.gram_sparse_cols_hubs(fr.phi, fr.row_shift, fr.tr, pl.b, pl.hubs, out=K,
-                                  sym_row0=pl.b if pl.cols_sym else None)
-    elif pl.mode == "cols":
+    if pl.mode == "cols":
         eng.gram_sparse_cols(fr.phi, fr.row_shift, fr.tr, out=K, sym_row0=pl.b if pl.cols_sym else None)
     elif pl.mode == "allreduce":
         eng.gram_sparse_kslice(fr.phi, fr.tr, pl.b, pl.e, out=K)  # all rows, inner slice [b, e)
         allreduce_buckets(K[:, :pl.n], group=pl.group)
-    elif pl.mode == "sym" and pl.fused:
-        # one launch completes K (the tiles' last arrivers write the lower triangle); pipelined, the
-        # next front starts after front_at of the tiles and overlaps the rest
-        main = torch.cuda.current_stream(eng.device)
-        tiles_done = None
-        if after_tiles is not None and front_at < 1.0:
-            cut = int(round(front_at * 1000))
-            eng.gram_sparse_sym_fused(fr.phi, fr.tr, out=K, parts=(0, cut, 1000))
-            tiles_done = torch.cuda.Event()
-            tiles_done.record(main)
-            eng.gram_sparse_sym_fused(fr.phi, fr.tr, out=K, parts=(cut, 1000, 1000))
-        else:
-            eng.gram_sparse_sym_fused(fr.phi, fr.tr, out=K)
-            if after_tiles is not None:
-                tiles_done = torch.cuda.Event()
-                tiles_done.record(main)
-        if after_tiles is not None:
-            after_tiles(tiles_done)
-    elif pl.mode == "sym" and trailing > 0 and not pl.fused and pl.hubs == 0 and mirror_stream is None:
-        streams = list(trail_streams) or [torch.cuda.Stream(eng.device)]
-        k_assembly_trailing(eng, fr, pl, K, streams[0], chunk_rows=trailing, tile_streams=streams[1:],
-                            after_tiles=after_tiles, front_at=front_at)
     elif pl.mode == "sym" and pl.hubs > 0:
         eng.gram_sparse_sym_hubs(fr.phi, fr.tr, pl.hubs, out=K, mirror_workgroups=mirror_workgroups,
                                  after_tiles=after_tiles, skewed=pl.skewed,
@@ -265,95 +230,11 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
             if after_tiles is not None:
                 tiles_done = torch.cuda.Event()
                 tiles_done.record(main)
-        if mirror_stream is not None:
-            if tiles_done is None:
-                tiles_done = torch.cuda.Event()
-                tiles_done.record(main)
-            mirror_stream.wait_event(tiles_done)
-            with torch.cuda.stream(mirror_stream):
-                eng.gram_mirror(K, pl.n, mirror_workgroups)
-                mirror_done = torch.cuda.Event()
-                mirror_done.record(mirror_stream)
-            if after_tiles is not None:
-                after_tiles(tiles_done)
-            return mirror_done
         eng.gram_mirror(K, pl.n, mirror_workgroups)
         if after_tiles is not None:
             after_tiles(tiles_done)  # (issued after the mirror: the host's launch time does not delay it)
     else:
         eng.gram_sparse(fr.phi, fr.tr, pl.b, pl.kr_end, out=K)
-    return K
-
-
-def sym_tile_chunks(n: int, W: int, chunk_rows: int):
-    """The symmetric Gram's band-major tile sequence (grf_gram_sparse_upper: band J holds the rows
-    0 .. min((J + 1) W, n) - 1) cut into (row range, band) chunks: the rows above the band's diagonal
-    square in pieces of ``chunk_rows``, then the square.  Yields (t0, t1, total, (r0, r1), (c0, c1)):
-    tiles [t0, t1) of ``total`` write K[r0:r1, c0:c1]."""
-    nb = -(-n // W)
-    full = nb - 1  # bands J < full hold (J + 1) W rows
-
-    def before(J):
-        return W * J * (J + 1) // 2 if J <= full else W * full * (full + 1) // 2 + (J - full) * n
-
-    total = before(nb)
-    for J in range(nb):
-        c0, c1 = J * W, min((J + 1) * W, n)
-        rows = min((J + 1) * W, n)
-        cuts = list(range(0, c0, chunk_rows)) + [c0, rows]
-        for r0, r1 in zip(cuts[:-1], cuts[1:]):
-            if r1 > r0:
-                yield before(J) + r0, before(J) + r1, total, (r0, r1), (c0, c1)
-
-
-def k_assembly_trailing(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, mirror_stream: torch.cuda.Stream,
-                        chunk_rows: int = 4096, mirror_workgroups: int = 0,
-                        tile_streams: Sequence[torch.cuda.Stream] = (),
-                        after_tiles: Optional[Callable[[torch.cuda.Event], None]] = None,
-                        front_at: float = 1.0) -> torch.Tensor:
-    """Symmetric K assembly with a trailing mirror: the Gram tiles run chunk by chunk (``sym_tile_chunks``)
-    on the caller's stream, and each chunk's lower-triangle copy (``gram_mirror_rect``) follows on
-    ``mirror_stream`` as soon as that chunk is written, beside the next chunks' tiles, while its K
-    lines may still be in the Infinity Cache.  No chunk's mirror writes an entry a later tile writes
-    (a band's tiles write only columns >= the band's start; its square is mirrored after all its
-    rows), so K is bit-identical to tiles + ``gram_mirror``.  tile_streams: further streams the tile
-    chunks are dealt to round-robin with the caller's (no chunk waits for another, so one chunk's last
-    tiles overlap the next chunk's first).  after_tiles(event) (the pipelined bench's next front) is
-    called once ``front_at`` of the chunks are issued, with an event on the caller's stream after them.
-    The caller's stream waits for the last mirror before it returns."""
-    assert pl.mode == "sym" and not pl.fused and pl.hubs == 0, "trailing mirror: the plain symmetric mode"
-    main = torch.cuda.current_stream(eng.device)
-    streams = [main] + list(tile_streams)
-    for s in streams[1:]:
-        s.wait_stream(main)  # (the front's buffers)
-    cuts = getattr(fr, "cuts", None)
-    chunks = list(sym_tile_chunks(pl.n, fr.tr.band_width, chunk_rows))
-    at = min(len(chunks), max(0, int(round(front_at * len(chunks)))))
-
-    def issue_front():
-        if after_tiles is not None:
-            ev = torch.cuda.Event()
-            ev.record(main)
-            after_tiles(ev)
-
-    for c, (t0, t1, total, rows, cols) in enumerate(chunks):
-        if c == at:
-            issue_front()
-        st = streams[c % len(streams)]
-        with torch.cuda.stream(st):
-            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, parts=(t0, t1, total), cuts=cuts)
-            ev = torch.cuda.Event()
-            ev.record(st)
-        mirror_stream.wait_event(ev)
-        with torch.cuda.stream(mirror_stream):
-            eng.gram_mirror_rect(K, pl.n, rows, cols, mirror_workgroups)
-    for s in streams[1:]:
-        main.wait_stream(s)
-    if at == len(chunks):
-        issue_front()
-    done = torch.cuda.Event()
-    done.record(mirror_stream)
-    main.wait_event(done)
     return K
 
 

@@ -68,6 +68,10 @@ enum grf_norm {
     GRF_NORM_MUL_RECIP = 1 /* value * (1/m)   (sparse_sampler.py:130 via scipy _mul_scalar) */
 };
 
+/* The ABI revision of this header: grf_version() returns it, and a binding must refuse a library whose
+ * revision differs (argument lists change between revisions). */
+#define GRF_ABI_VERSION 4
+
 const char *grf_last_error(void);
 int32_t grf_version(void);
 /* number of HIP devices visible (0 if none); never fails */
@@ -351,22 +355,6 @@ int32_t grf_hub_panel(int64_t n_rows, const int64_t *ptr, const int32_t *idx, co
 int32_t grf_transpose_drop_columns(int64_t n_bands, int64_t n_cols, uint32_t *t_desc, const int32_t *cols,
                                    int32_t n_drop, grf_stream_t stream);
 
-/* Whole K as grf_gram_sparse_sym, with the symmetric completion fused into the Gram tiles: the
- * tiles of 64 consecutive rows of a band take tickets on a group counter and the last one writes
- * the group's block transposed below the diagonal (from the Infinity Cache: no separate mirror
- * pass re-reads the upper triangle from HBM).  K is bit-identical to grf_gram_sparse_sym's.
- * Parts as grf_gram_sparse_upper (all parts of one K on one stream, in order; the call that
- * issues part 0 zeroes the tickets).  workspace: grf_gram_sym_fused_workspace_bytes bytes,
- * 16-byte aligned; K 16-byte aligned, ldk a multiple of 4.  Measured slower than
- * grf_gram_sparse_sym on MI355X (the last arrivers' transposed stores serialise:
- * profiles/r02_fused_ab.txt); an option, not the bench default. */
-size_t grf_gram_sym_fused_workspace_bytes(int64_t n_total, int64_t band_width);
-int32_t grf_gram_sparse_sym_fused(int64_t n_total, const int64_t *ptr, const int32_t *idx, const float *val,
-                                  int64_t band_width, int32_t rec_unit, const uint32_t *t_desc, const void *t_rec,
-                                  const int32_t *t_rowshift, float *K, int64_t ldk, int32_t part_begin,
-                                  int32_t part_end, int32_t n_parts, void *workspace, size_t workspace_bytes,
-                                  grf_stream_t stream);
-
 /* Column block of K against another row set: K[r - row_begin, 0 : t_rows] = sum_k Phi[r, k] Phi_B[:, k]
  * for the rows r in [row_begin, row_end) of Phi (CSR ptr/idx/val, n_cols columns), where Phi_B
  * (t_rows rows, the same n_cols columns) is given by its banded transpose (grf_transpose_banded_*
@@ -382,17 +370,6 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
                              int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
                              const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
                              size_t workspace_bytes, grf_stream_t stream);
-/* grf_gram_sparse_cols whose tile write-out ADDS the rounded fixed-point sums to the block instead of
- * storing them: the block must hold the dense part first.  The column-block hub-column split: the
- * densest columns' entries in dense panels P (all rows) and P_B (the block's rows), K_blk = P P_B^T by
- * a plain GEMM, those columns' buckets emptied from the block's transpose (grf_transpose_drop_columns),
- * then this adds the rest.  Same arguments as grf_gram_sparse_cols. */
-int32_t grf_gram_sparse_cols_add(int64_t n_cols, int64_t row_begin, int64_t row_end, const int64_t *ptr,
-                                 const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
-                                 int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
-                                 const void *t_rec, const void *t_split, float *K, int64_t ldk, void *workspace,
-                                 size_t workspace_bytes, grf_stream_t stream);
-
 /* The Gram fixed-point row shifts of a CSR (n_rows rows; float values) and its max |value|
  * (*maxabs, device): the same rule and the same per-row summation order as the banded transpose's
  * t_rowshift / t_maxabs, so grf_gram_sparse_cols reproduces grf_gram_sparse's bits. */
@@ -403,16 +380,6 @@ int32_t grf_phi_row_shifts(int64_t n_rows, const int64_t *ptr, const float *val,
  * (one pass over the values fewer; identical bits). */
 int32_t grf_phi_row_shifts_stats(int64_t n_rows, const void *stats, float *maxabs, int32_t *row_shift,
                                  grf_stream_t stream);
-
-/* K rows [row_begin, row_end) (as grf_gram_sparse) using the symmetry inside the row block: the
- * bands lying wholly inside the block are computed only on and above the diagonal for the block's
- * rows in them, then mirrored (entries below the diagonal there carry row j's fixed-point rounding,
- * as in grf_gram_sparse_sym); all other tiles are the row mode's.  The multi-GPU row blocks. */
-int32_t grf_gram_sparse_block(int64_t n_total, int64_t row_begin, int64_t row_end, const int64_t *ptr,
-                              const int32_t *idx, const float *val, int64_t band_width, int32_t rec_unit,
-                              const uint32_t *t_desc, const void *t_rec, const void *t_split,
-                              const int32_t *t_rowshift, float *K, int64_t ldk, void *workspace,
-                              size_t workspace_bytes, grf_stream_t stream);
 
 /* Partial Gram over a slice of the inner dimension: K[r, :] = sum over k in [k_begin, k_end)
  * of Phi[r, k] Phi[:, k] (same fixed-point rule as grf_gram_sparse).  The partial Grams of
@@ -429,28 +396,25 @@ int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_e
  * 4 per CU was best beside the next step's walks: tools/gpu_mirror_ab.sh). */
 int32_t grf_gram_mirror(int64_t n, float *K, int64_t ldk, int64_t max_workgroups, grf_stream_t stream);
 
-/* The mirror pass over one rectangle of K: for the 64 x 64 blocks of rows [row_begin, row_end) x
- * columns [col_begin, col_end) on or above the diagonal, K[j, i] = K[i, j] (j > i).  Starts are
- * multiples of 64.  A trailing mirror issues it per (row range, band) chunk of grf_gram_sparse_upper
- * tiles (same reference line as grf_gram_sparse_sym: the K = Phi Phi^T of
- * graph_kernels_sparse/fast_grf_kernel_general.py:55). */
-int32_t grf_gram_mirror_rect(int64_t n, float *K, int64_t ldk, int64_t row_begin, int64_t row_end, int64_t col_begin,
-                             int64_t col_end, int64_t max_workgroups, grf_stream_t stream);
-
-/* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are
- * zero padding; lda % 32 == 0).  K float32 [n x ldk].  MFMA f32 (v_mfma_f32_32x32x2f32). */
+/* Dense path: K = A A^T for A float32 row-major [n x lda] (columns >= k_dim are zero padding;
+ * lda % 16 == 0, A 16-byte aligned).  K float32 [n x ldk] (ldk % 4 == 0, K 16-byte aligned), exactly
+ * symmetric: the 128 x 128 tiles on and above the diagonal on the fp32 MFMA
+ * (v_mfma_f32_16x16x4f32 / 32x32x2f32), each written to both triangles.
+ * Replaces efficient_graph_gp/graph_kernels/fast_grf_kernel_general.py:39 (Phi @ Phi.T). */
 int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                        grf_stream_t stream);
-/* grf_gram_dense's tiles on and above the diagonal only (128 x 128 tiles J >= I, or 64 x 64 for small
- * n; no split-K, no lower triangle): every K[i, j >= i] is written, entries below the diagonal only
- * where a diagonal tile covers them.  The hub part of the hub-column split (grf_gram_sparse_upper_add). */
+/* grf_gram_dense's tiles on and above the diagonal only, nothing mirrored: every K[i, j >= i] is
+ * written, entries below the diagonal only where a diagonal tile covers them.  The hub part of the
+ * hub-column split (grf_gram_sparse_upper_add adds the sparse part on top). */
 int32_t grf_gram_dense_upper(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                              grf_stream_t stream);
-/* As grf_gram_dense, with a device workspace for split-K partials: when n is too small for the
- * tiles on and above the diagonal to fill the GPU, the k range is cut into S slices whose partial
- * Grams are summed in slice order (deterministic) by the pass that also writes the lower triangle.
- * workspace: grf_gram_dense_workspace_bytes(n, k_dim) bytes (16 when no split is used); NULL or a
- * smaller workspace runs unsplit. */
+/* As grf_gram_dense, with a device workspace for split-K: when the tiles alone would leave CUs idle
+ * (every tile for small n, the last tiles of a large n), a tile is cut into k-slices whose partial
+ * tiles are summed in slice order (deterministic) by the last of them to finish.  workspace:
+ * grf_gram_dense_workspace_bytes(n, k_dim) bytes, 256-byte aligned, ZERO on first use (its first
+ * 4 KiB hold the tiles' tickets, which every call leaves zero; the layout does not depend on n or
+ * k_dim, so one workspace serves calls of any size in stream order); NULL or a smaller workspace
+ * runs unsplit. */
 size_t grf_gram_dense_workspace_bytes(int64_t n, int64_t k_dim);
 int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                           void *workspace, size_t workspace_bytes, grf_stream_t stream);
@@ -486,9 +450,11 @@ int32_t grf_dense_steps_grad(int64_t n, int32_t L, const double *F, const double
  * row-major [rows x ld] with the S right-hand sides / samples as columns.
  * `row_map` (int32, optional) selects rows of Phi; NULL = rows 0..n-1. */
 
-/* (Phi[row_map])^T as CSR: t_ptr[n_cols + 1] (int64), t_idx / t_val [nnz = the entries of the
- * selected rows, exactly]; t_idx are positions in row_map; every column lists them in ascending
- * order (a stable radix sort by column of the entries laid out in row order). */
+/* (Phi[row_map])^T as CSR: t_ptr[n_cols + 1] (int64), t_idx / t_val [nnz]; t_idx are positions in
+ * row_map; every column lists them in ascending order (a stable radix sort by column of the entries
+ * laid out in row order).  nnz: the entries of the selected rows, or any upper bound of them (then
+ * t_ptr[n_cols] holds the real count and the tail of t_idx / t_val is unused): a caller sizing from
+ * bounds reads nothing back to the host. */
 int32_t grf_csr_transpose(int64_t n_sel, const int64_t *ptr, const int32_t *idx, const float *val,
                           const int32_t *row_map, int64_t n_cols, int64_t nnz, int64_t *t_ptr, int32_t *t_idx,
                           float *t_val, void *workspace, size_t workspace_bytes, grf_stream_t stream);

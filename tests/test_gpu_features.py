@@ -212,3 +212,57 @@ def test_kernel_block_shift_bound_takes_both_operands(golden):
     # elementwise, relative to each entry's own |Phi||Phi|^T (no absolute slack from the huge row)
     err = np.abs(K.astype(np.float64) - Phi[i1] @ Phi[i2].T)
     assert np.all(err <= 3e-5 * (aPhi[i1] @ aPhi[i2].T) + 1e-30), err
+
+
+def test_sparse_kernel_forward_backward_issue_no_host_sync(golden):
+    """The GPyTorch forward + backward read nothing back to the host: after the
+    one-time StepMatrices setup, K[x1, x2], K(x, x), the diagonal and the modulator gradient run under
+    torch.cuda.set_sync_debug_mode("error"), which raises on any device->host synchronisation
+    (.item(), .cpu(), torch.equal, ...).  Phi is sized by sum_l nnz(M_l), row gathers by rows x the
+    row bound, the transposes by those bounds (the C side pads the tail), x1 == x2 is decided by
+    identity, and the dense (GPflow) Gram cache is keyed by the modulator tensor's version counter."""
+    from efficient_graph_gp_sparse.gptorch_kernels_sparse import SparseGRFKernel
+    d = golden("small_graphs")
+    steps = [csr(d, f"er40_sp_n3_s7_l{l}", 40) for l in range(4)]
+    torch.manual_seed(0)
+    kern = SparseGRFKernel(4, _ops(steps)).cuda()
+    x1 = torch.tensor([0, 3, 5, 17, 39, 3], device="cuda")
+    x2 = torch.tensor([1, 3, 20], device="cuda")
+    W = torch.randn(6, 3, device="cuda")
+    ref_K = kern(x1, x2).detach().clone()  # (warm-up: builds the StepMatrices, one-time host reads)
+    kern.raw_modulator_vector.grad = None
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        K = kern(x1, x2)
+        Ks = kern(x1, x1)
+        Kd = kern(x1, x1, diag=True)
+        loss = (K * W).sum() + Ks.sum() + Kd.sum()
+        loss.backward()
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    torch.cuda.synchronize()
+    assert torch.equal(K.detach(), ref_K)
+    assert torch.equal(Ks.detach(), Ks.detach().t())
+    assert kern.raw_modulator_vector.grad is not None and torch.isfinite(kern.raw_modulator_vector.grad).all()
+
+
+def test_dense_gram_cache_keyed_without_host_copy():
+    """DenseSteps.gram: the cache hits for the same modulator tensor (and a detached view or the tensor
+    autograd saves), misses after an in-place update (its version counter) -- with no host copy of f."""
+    from grf_amd.features import DenseSteps
+    torch.manual_seed(0)
+    F = torch.rand(64, 64, 3, dtype=torch.float64) * (torch.rand(64, 64, 3, dtype=torch.float64) < 0.2)
+    ds = DenseSteps(F)
+    f = torch.tensor([1.0, -0.5, 0.25], dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        K1 = ds.gram(f)
+        assert ds.gram(f) is K1 and ds.gram(f.detach()) is K1
+        f.mul_(2.0)  # (an optimiser step: in place)
+        K2 = ds.gram(f)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert K2 is not K1
+    torch.testing.assert_close(K2, 4.0 * K1, rtol=1e-5, atol=1e-6)

@@ -244,14 +244,6 @@ def test_gram_sparse_vs_oracle(eng, n, deg, m, L, bw):
         eng.gram_sparse_upper(phi, tr, Ku, parts=(0, 7, 10))
         eng.gram_sparse_upper(phi, tr, Ku, parts=(7, 10, 10))
         assert np.array_equal(eng.gram_mirror(Ku, n, max_workgroups=37).cpu().numpy(), Ks)  # (grid-stride)
-        # the completion fused into the tiles (last arriver of every 32-row group): the same bits,
-        # whole and issued in parts (the tickets of a group straddling the cut carry over)
-        Kf = torch.full((n, eng.leading_dim(n)), float("nan"), dtype=torch.float32, device=eng.device)
-        assert np.array_equal(eng.gram_sparse_sym_fused(phi, tr, Kf).cpu().numpy(), Ks)
-        Kf.fill_(float("nan"))
-        for part in [(0, 3, 10), (3, 4, 10), (4, 10, 10)]:
-            eng.gram_sparse_sym_fused(phi, tr, Kf, parts=part)
-        assert np.array_equal(Kf[:, :n].cpu().numpy(), Ks)
     upper = np.triu(np.ones((n, n), bool))
     assert np.array_equal(Ks[upper], K[upper])
     ok, fro = gram_close(Ks, phi.to_scipy())
@@ -274,31 +266,6 @@ def test_gram_sparse_band_invariance(eng):
     assert np.array_equal(K_wide, K_8k)
     ok, fro = gram_close(K_wide[:16], phi.to_scipy(), (0, 16))
     assert ok, fro
-
-
-@pytest.mark.parametrize("n,bw,blocks", [(20000, 4096, [(0, 10000), (10000, 20000)]),
-                                          (20000, 1024, [(0, 5000), (5000, 10000), (10000, 15000), (15000, 20000)]),
-                                          (5000, 64, [(0, 1667), (1667, 3334), (3334, 5000)]),
-                                          (9000, 4096, [(0, 4500), (4500, 9000), (100, 8200), (0, 9000)]),
-                                          (3000, 4096, [(0, 1500), (1500, 3000)])])
-def test_gram_block_symmetric_row_blocks(eng, n, bw, blocks):
-    """The multi-GPU row-block Gram with the symmetry inside the block: every entry is the row
-    mode's bits except in the block's interior square (whole bands inside the block) below the
-    diagonal, which holds the mirrored upper entry -- as the symmetric mode fills it."""
-    A = er_graph(n, 8, n + 1)
-    G = eng.laplacian(A)
-    phi = eng.compact(eng.walk_phi(G, 32, 0.15, 5, [1.0, -0.5, 0.25, -0.125, 0.1], seed=6))
-    tr = eng.transpose_banded(phi, bw)
-    K = eng.gram_sparse(phi, tr).cpu().numpy()
-    for b0, b1 in blocks:
-        Kb = eng.gram_sparse_block(phi, tr, b0, b1).cpu().numpy()
-        exp = K[b0:b1].copy()
-        i0 = -(-b0 // bw) * bw
-        i1 = n if b1 == n else (b1 // bw) * bw
-        if i1 > i0:
-            sq = K[i0:i1, i0:i1]
-            exp[i0 - b0:i1 - b0, i0:i1] = np.triu(sq) + np.triu(sq, 1).T
-        assert np.array_equal(Kb, exp), (b0, b1)
 
 
 @pytest.mark.parametrize("unit", [128, 12])
@@ -395,8 +362,6 @@ def test_transpose_sub_band_split(eng, n, bw, unit):
     eng.gram_sparse_upper(phi, ts, Ku, parts=(0, 3, 7))
     eng.gram_sparse_upper(phi, ts, Ku, parts=(3, 7, 7))
     assert torch.equal(eng.gram_mirror(Ku, n), Ks)
-    b0, b1 = (n // 3) // bw * bw, n  # a row block whose interior holds whole bands
-    assert torch.equal(eng.gram_sparse_block(phi, ts, b0, b1), eng.gram_sparse_block(phi, tn, b0, b1))
     # column block with its symmetric square (rows [b, e) transposed with their own bands)
     b, e = n // 4, n // 4 + min(n // 2, 3 * bw // 2)
     loc = eng.compact(eng.walk_phi(G, 32, 0.15, 5, [1.0, -0.5, 0.25, -0.125, 0.1], seed=9, src_begin=b, src_end=e))
@@ -491,6 +456,26 @@ def test_gram_dense_split_k(eng, n, k):
     Ksn = Ks.cpu().numpy()
     assert np.array_equal(Ksn, Ksn.T)
     assert np.array_equal(eng.gram_dense(At, k).cpu().numpy(), Ksn)
+
+
+def test_gram_dense_workspace_reused_across_sizes(eng):
+    """One engine workspace serves split-K calls of different sizes in any order (the ticket block
+    sits at a fixed place ahead of the slabs): small -> large -> small gives each size's bits of a
+    fresh engine's call."""
+    import torch
+    from grf_amd.engine import GRFEngine
+    r = np.random.default_rng(7)
+    ops = []
+    for n in (1000, 2708, 300, 4500, 1000):
+        k = n + 17
+        lda = -(-k // 64) * 64
+        Ad = np.zeros((n, lda), np.float32)
+        Ad[:, :k] = (r.standard_normal((n, k)) * (r.random((n, k)) < 0.05)).astype(np.float32)
+        ops.append((torch.from_numpy(Ad).to(eng.device), k))
+    got = [eng.gram_dense(A, k).cpu().numpy() for A, k in ops]
+    for (A, k), K in zip(ops, got):
+        fresh = GRFEngine(eng.device).gram_dense(A, k).cpu().numpy()
+        assert np.array_equal(K, fresh) and np.isfinite(K).all()
 
 
 def test_full_pipeline_c2_scale(eng):
@@ -977,7 +962,7 @@ def _run_sharded(world, mode, graph="er", policy="nodes"):
     procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, mode, q, graph, policy)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=100) for _ in range(world))
+    res = sorted(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(timeout=30)
     return res
@@ -991,7 +976,8 @@ def test_sharded_kernel_matrix_two_ranks_gloo(mode):
 
 
 @pytest.mark.parametrize("world,mode,policy", [(2, "cols", "phi"), (3, "cols", "phi"), (3, "rows", "phi"),
-                                               (2, "rows", "nodes")])
+                                               (2, "rows", "nodes"), (5, "cols", "nodes"), (8, "cols", "nodes"),
+                                               (8, "cols", "phi")])
 def test_sharded_powerlaw_balanced_gloo(world, mode, policy):
     """A 20k-node Chung-Lu power-law graph (hubs) on 2 / 3 gloo ranks with cost-balanced shards
     (dist.balanced_shards: the per-row estimate from one setup walk) and with equal node counts:
@@ -1047,10 +1033,12 @@ def _bench_front_worker(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "cols"), (3, "cols"), (2, "rows")])
+@pytest.mark.parametrize("world,mode", [(2, "cols"), (3, "cols"), (2, "rows"), (5, "cols"), (8, "cols")])
 def test_bench_step_exact_gather_bound_gloo(world, mode):
     """The bench's N > 1 step with the Phi all-gather sized by the setup walk's exact per-rank entries
-    (not rows x the padded row capacity): every rank's K block bit-identical to the single-GPU K's."""
+    (not rows x the padded row capacity): every rank's K block bit-identical to the single-GPU K's.
+    World 5 and 8 (the driver's N = 8 node run): column blocks without the mirrored own square
+    (4 |R_r| < n), several local bands per rank, the bounded gather over 8 ranks."""
     import multiprocessing as mp
     import socket
     s = socket.socket()
@@ -1062,7 +1050,7 @@ def test_bench_step_exact_gather_bound_gloo(world, mode):
     procs = [ctx.Process(target=_bench_front_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=100) for _ in range(world))
+    res = sorted(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(timeout=30)
     assert res == [(r, True) for r in range(world)]
@@ -1088,8 +1076,6 @@ def test_bench_path_on_degenerate_graphs(eng, name):
     assert ok, fro
     Ks = eng.gram_sparse_sym(phi, tr)
     assert torch.equal(Ks, Ks.T) and torch.equal(torch.triu(Ks), torch.triu(K))
-    assert torch.equal(eng.gram_sparse_sym_fused(phi, tr), Ks)
-    assert torch.equal(eng.gram_sparse_sym_fused(phi, eng.transpose_banded(phi, 64)), Ks)
     b, e = n // 3, n - n // 4
     if e > b:
         loc = eng.compact(eng.walk_phi(G, 16, 0.2, 4, f, seed=4, src_begin=b, src_end=e), want64=False)
@@ -1097,8 +1083,8 @@ def test_bench_path_on_degenerate_graphs(eng, name):
         assert torch.equal(Kc, _sym_square(K[:, b:e], b, e))
 
 
-@pytest.mark.parametrize("mode", ["cols", "allreduce"])
-def test_bench_line_n2_reports_parity_and_collectives_gloo(mode):
+@pytest.mark.parametrize("mode,world", [("cols", 2), ("allreduce", 2), ("cols", 5), ("cols", 8)])
+def test_bench_line_n2_reports_parity_and_collectives_gloo(mode, world):
     """bench.py's N > 1 line is self-validating and collective-evident (what the driver's 8-GPU run
     will print): two gloo ranks on one GPU (GRF_DIST_BACKEND=gloo, the host-staged rehearsal of the
     RCCL path) run the bench's own step; the line carries the communicator's backend and world size,
@@ -1115,20 +1101,20 @@ def test_bench_line_n2_reports_parity_and_collectives_gloo(mode):
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, GRF_DIST_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--n-nodes", "20000",
+           "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--n-nodes", "20000",
            "--edges", "200000", "--mode", mode]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["n_gpus"] == 2
+    assert line["n_gpus"] == world
     d = line["distributed"]
-    assert d["backend"] == "gloo" and d["world_size"] == 2
-    assert len(d["gram_ms_per_rank"]) == 2 and all(x > 0 for x in d["gram_ms_per_rank"])
+    assert d["backend"] == "gloo" and d["world_size"] == world
+    assert len(d["gram_ms_per_rank"]) == world and all(x > 0 for x in d["gram_ms_per_rank"])
     assert all(x > 0 for x in d["gather_bytes_sent_per_rank"]) and all(x > 0 for x in d["gather_ms_per_rank"])
     assert sum(d["rank_rows"]) == 20000
-    assert line["parity"]["ok"] and line["parity"]["max_ratio"] <= 1.0 and len(line["parity"]["per_rank"]) == 2
+    assert line["parity"]["ok"] and line["parity"]["max_ratio"] <= 1.0 and len(line["parity"]["per_rank"]) == world
 
 
 @pytest.mark.parametrize("mode", ["cols", "rows", "allreduce"])
@@ -1162,40 +1148,6 @@ def test_bench_multi_gpu_path_on_rccl_one_rank(mode):
     if mode != "allreduce":
         assert d["gather_bytes_sent_per_rank"][0] > 0 and d["gather_ms_per_rank"][0] > 0
     assert line["parity"]["ok"] and line["parity"]["max_ratio"] <= 1.0
-
-
-@pytest.mark.parametrize("hubs", [32, 64])
-def test_column_block_hub_split(eng, hubs):
-    """The column block's hub-column split (engine.gram_sparse_cols_hubs: the block's densest columns in
-    a dense panel, K_blk = P P_B^T by a library GEMM, the other columns' fixed-point tiles added on top):
-    within the K tolerance of the exact product of the same fp32 Phi, on a hub-heavy power-law graph,
-    with and without the block's symmetric square."""
-    from grf_amd.graphs import powerlaw_graph
-    n = 20000
-    A = powerlaw_graph(n, 10.0, 2.5, seed=3)
-    G = eng.laplacian(A)
-    phi = eng.compact(eng.walk_phi(G, 32, 0.1, 6, [1.0, -0.5, 0.125, -0.02, 0.003, -0.0005], seed=5, want64=False),
-                      want64=False)
-    P64 = phi.to_scipy().astype(np.float64)
-    sh = eng.phi_row_shifts(phi)
-    for b, e, sym in [(0, 4096, False), (5000, 10000, True)]:
-        loc = eng.compact(eng.walk_phi(G, 32, 0.1, 6, [1.0, -0.5, 0.125, -0.02, 0.003, -0.0005], seed=5,
-                                       src_begin=b, src_end=e, want64=False), want64=False)
-        Kh = eng.gram_sparse_cols_hubs(phi, sh, eng.transpose_banded(loc, 4096), b, hubs,
-                                       sym_row0=b if sym else None).cpu().numpy()
-        K0 = eng.gram_sparse_cols(phi, sh, eng.transpose_banded(loc, 4096), sym_row0=b if sym else None).cpu().numpy()
-        ref = (P64 @ P64[b:e].T).toarray()
-        # the K tolerance (module docstring): the elementwise 3e-5 term + the absolute 1e-12 max_k|Phi_ik|
-        # max|Phi| term (the hub part is an fp32 GEMM: products below fp32's normal range flush to 0 there)
-        aP = abs(P64)
-        rowmax = np.asarray(aP.max(axis=1).todense()).ravel()
-        bound = 3e-5 * (aP @ aP[b:e].T).toarray() + 1e-12 * np.maximum(rowmax[:, None], rowmax[None, b:e]) * aP.max() \
-            + 1e-30
-        assert np.all(np.abs(Kh - ref) <= bound), float((np.abs(Kh - ref) / bound).max())
-        assert np.all(np.abs(K0 - ref) <= bound)
-        if sym:  # the square stays exactly symmetric
-            sq = Kh[b:e]
-            assert np.array_equal(sq, sq.T)
 
 
 @pytest.mark.parametrize("hubs", [0, 64])

@@ -328,23 +328,6 @@ def test_record_unit_choice():
     assert choose_rec_unit(0, 10, 10, 64) == C.REC_PACKED
 
 
-def test_sym_tile_chunks_cover_the_upper_tiles_in_order():
-    """The trailing mirror's chunks: the symmetric Gram's band-major tiles cut at chunk rows and at
-    each band's diagonal square, contiguous and complete; every mirror rectangle is the chunk's rows x
-    its band, above the band's square (or the square itself), starts on 64-row boundaries."""
-    from grf_amd.pipeline import sym_tile_chunks
-    for n, W, c in ((100_000, 4096, 4096), (100_000, 4096, 8192), (1000, 128, 192), (64, 64, 64), (130, 64, 64)):
-        ch = list(sym_tile_chunks(n, W, c))
-        nb = -(-n // W)
-        assert ch[0][0] == 0 and ch[-1][1] == ch[0][2]
-        assert ch[0][2] == sum(min((J + 1) * W, n) for J in range(nb))
-        assert all(a[1] == b[0] for a, b in zip(ch[:-1], ch[1:]))
-        for t0, t1, _, (r0, r1), (c0, c1) in ch:
-            assert t1 - t0 == r1 - r0 > 0 and r0 % 64 == 0 and c0 % 64 == 0 and c1 - c0 <= W
-            assert r1 <= c0 or (r0, r1) == (c0, min(c1, n)) or (r0 == c0 and r1 == min(c0 + W, n))
-            assert r1 - r0 <= max(c, W)
-
-
 def test_powerlaw_graph_is_simple_and_heavy_tailed():
     from grf_amd.graphs import powerlaw_graph
     A = powerlaw_graph(20_000, 10.0, 2.5, seed=1)

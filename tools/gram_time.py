@@ -57,13 +57,4 @@ for mode in modes:
     elif mode == "rows":
         out["rows_ms"] = timed(lambda: eng.gram_sparse(phi, tr, out=K))
         out["rows_digest"] = digest()
-    elif mode.startswith("blocks"):  # blocks<N>: every rank's row block, row mode vs block-symmetric
-        world = int(mode[6:])
-        from grf_amd.dist import shard_range
-        for r in range(world):
-            b, e = shard_range(n, r, world)
-            Kb = K[: e - b]
-            t_rows = timed(lambda: eng.gram_sparse(phi, tr, b, e, out=Kb))
-            t_blk = timed(lambda: eng.gram_sparse_block(phi, tr, b, e, out=Kb))
-            out[f"w{world}r{r}"] = [round(t_rows, 3), round(t_blk, 3)]
 print(json.dumps(out), flush=True)
