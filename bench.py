@@ -68,9 +68,11 @@ def pmc_counter(kernel, counter):
     return hits[0].get(counter) if hits else None
 
 
-# VALU issue ceiling per SIMD-32: one wave64 VALU instruction per 2 cycles (MI355X_MICROARCH.md, wave
-# scheduling: 32 lanes per cycle; one wave alone issues every 4 cycles, several waves interleaved every 2)
-VALU_PEAK_PER_SIMD_CYCLE = 0.5
+# VALU issue ceiling per SIMD: one wave64 (non-packed) VALU instruction per 4 cycles, measured on this part
+# (tools/valu_ceiling.hip, profiles/r04_valu_ceiling.txt: independent v_fma_f32 / v_xad_u32 / v_mul_hi_u32 /
+# v_fma_f64 chains at 4 waves per SIMD issue every 3.8-4.2 shader cycles by s_memtime, and the PMC formula
+# this line uses, SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x 1024), reads 0.23-0.26 on them)
+VALU_PEAK_PER_SIMD_CYCLE = 0.25
 N_SIMDS = 256 * 4
 
 
@@ -861,8 +863,8 @@ def main():
                           "gui_active_cycles_per_launch": walk_gui / 8.0 if walk_gui else None,
                           "valu_source": (f"one rocprofv3 --pmc pass of this workload (SQ_INSTS_VALU, GRBM_GUI_ACTIVE), "
                                           f"{os.path.relpath(PMC_SUMMARY, ROOT)}: SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x "
-                                          f"1024 SIMDs) against 1 wave64 VALU instruction per 2 cycles per SIMD "
-                                          f"(fp64 VALU and transcendental instructions take longer: a lower bound "
+                                          f"1024 SIMDs) against the measured 1 wave64 VALU instruction per 4 cycles per SIMD "
+                                          f"(profiles/r04_valu_ceiling.txt; fp64 transcendentals take 16: a lower bound "
                                           f"of the VALU pipe's busy share)") if walk_valu_rate is not None else None,
                           "hbm": {"achieved": walk_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": walk_achieved / HBM_PEAK_GBS, "traffic": walk_traffic},

@@ -55,6 +55,7 @@ struct DenseArgs {
     int64_t k_split;   // k-slice width of a split tile's piece (multiple of BK)
     int32_t n_split;   // pieces per split tile (the tiles from n_whole on)
     int32_t upper_only;  // write only K[row][col] of the computed tiles (the hub panel's seed)
+    int64_t sk_units, sk_kt, sk_total;  // stream-K: k-tile units per slot, per tile, in all
     int32_t abl;       // A/B ablations (GRF_DENSE_ABL; timing only): 1 no DMA, 4 no barrier, 8 no mirror
 };
 
@@ -427,33 +428,26 @@ __device__ __forceinline__ void write_quarter(const DenseArgs &a,
     }
 }
 
-template <int MF, int BK, int NST, int WPE, int XABL = 0, bool PRIO = false, int IL = 0>
-__global__ __launch_bounds__(256, WPE) void gram_dense_mfma_kernel(DenseArgs a) {
+// One wave's part of tile `tile` over the k range [kb, ke): its quarter (rows qr.., cols qc..), whether it
+// lies below the diagonal, and the accumulators (zeroed here).
+struct Quarter {
+    int64_t qr, qc;
+    bool diag, below;
+};
+
+template <int MF, int BK, int NST, int XABL, bool PRIO, int IL>
+__device__ __forceinline__ Quarter tile_compute(const DenseArgs &a, float *lds, int64_t tile, int64_t kb, int64_t ke,
+                                                int wave, int lane,
+                                                typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK]
+                                                                                   [Layout<MF, BK>::NBLK]) {
     using L = Layout<MF, BK>;
     using St = Stage<BK>;
     constexpr int NB = L::NBLK;
-    __shared__ __attribute__((aligned(16))) float lds[NST * 2 * St::F];  // (one array: the DMA ring)
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int wm = wave >> 1, wn = wave & 1;
-
-    // work item -> (tile, k slice)
-    const int64_t w = blockIdx.x;
-    int64_t tile, slice = 0, pieces = 1;
-    if (w < a.n_whole) {
-        tile = w;
-    } else {
-        tile = a.n_whole + (w - a.n_whole) / a.n_split;
-        slice = (w - a.n_whole) % a.n_split;
-        pieces = a.n_split;
-    }
     int64_t bi, bj;
     tile_coords(tile, a.nt, bi, bj);
     const int64_t m0 = bi * kTile, n0 = bj * kTile;
     const bool diag = bi == bj;
-    const int64_t kb = pieces > 1 ? slice * a.k_split : 0;
-    const int64_t ke = pieces > 1 ? (kb + a.k_split < a.kpad ? kb + a.k_split : a.kpad) : a.kpad;
-
     // per-lane DMA sources: piece j of this wave covers LDS chunks p = (wave * PW + j) * 64 + lane,
     // i.e. row p / C, stored chunk p % C, which holds logical chunk (p % C) ^ swz(row)
     const float *srcA[St::PW], *srcB[St::PW];
@@ -473,13 +467,9 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_mfma_kernel(DenseArgs a) 
         aoff[g] = L::off(wm * 64, 0, g, lane);
         boff[g] = L::off(wn * 64, 0, g, lane);
     }
-    // this wave's quarter: rows m0 + wm*64 .., cols n0 + wn*64 ..; no MFMAs when it lies wholly below the
-    // diagonal or past n
-    const int64_t qr = m0 + wm * 64, qc = n0 + wn * 64;
-    const bool below = diag && wn < wm;
-    const bool live = !below && qr < a.n && qc < a.n;
-
-    typename L::acc_t c[NB][NB];
+    // this wave's quarter: no MFMAs when it lies wholly below the diagonal or past n
+    Quarter q{m0 + wm * 64, n0 + wn * 64, diag, diag && wn < wm};
+    const bool live = !q.below && q.qr < a.n && q.qc < a.n;
 #pragma unroll
     for (int x = 0; x < NB; ++x)
 #pragma unroll
@@ -491,44 +481,129 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_mfma_kernel(DenseArgs a) 
         if (live) kloop<MF, BK, NST, false, true, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
         else kloop<MF, BK, NST, false, false, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
     }
+    return q;
+}
 
-    if (pieces > 1) {
-        // partial tile -> slab; the last of the tile's pieces sums the slabs in slice order
-        const int64_t u = tile - a.n_whole;
-        f32x4v *slab = reinterpret_cast<f32x4v *>(a.slabs) + ((u * pieces + slice) * 4 + wave) * 16 * 64 + lane;
+// A piece of a split tile: its partial tile goes to slab slab_of(me) (16-B stores, register layout); the
+// piece that draws the last of `pieces` tickets sums slab_of(0 .. pieces - 1) in that order (its own from
+// registers) into c and returns true.  Hand-off: slab stores -> every wave vmcnt(0) -> barrier -> agent
+// release -> ticket fetch_add; the last arriver resets the ticket, then agent acquire -> barrier -> loads.
+// `flag` is LDS the ring no longer uses (every wave is past its k-loop).
+template <int MF, int BK, typename SlabOf>
+__device__ __forceinline__ bool split_combine(const DenseArgs &a,
+                                              typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK]
+                                                                                 [Layout<MF, BK>::NBLK],
+                                              int32_t *ticket, int64_t pieces, int64_t me, SlabOf slab_of,
+                                              int32_t *flag, int wave, int lane) {
+    using L = Layout<MF, BK>;
+    constexpr int64_t kSlab = 4 * 16 * 64;  // float4 per piece: [4 waves][16 float4][64 lanes]
+    f32x4v *mine = reinterpret_cast<f32x4v *>(a.slabs) + slab_of(me) * kSlab + wave * 16 * 64 + lane;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) slab[j * 64] = L::get(c, j);
+    for (int j = 0; j < 16; ++j) mine[j * 64] = L::get(c, j);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int32_t *flag = reinterpret_cast<int32_t *>(lds);  // (the ring is idle: every wave is past its k-loop)
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int32_t old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t last = old == pieces - 1;
+        if (last) {
+            __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int32_t old = __hip_atomic_fetch_add(a.tickets + u, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int32_t last = old == pieces - 1;
-            if (last) {
-                __hip_atomic_store(a.tickets + u, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            *flag = last;
         }
-        __syncthreads();
-        if (!*flag) return;
-        const f32x4v *base = reinterpret_cast<const f32x4v *>(a.slabs) + (u * pieces * 4 + wave) * 16 * 64 + lane;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const f32x4v own = L::get(c, j);
-            f32x4v acc = slice == 0 ? own : base[j * 64];
-            for (int64_t s = 1; s < pieces; ++s) acc += s == slice ? own : base[(s * 4 * 16 + j) * 64];
-            L::set(c, j, acc);
-        }
+        *flag = last;
     }
-    if (qr >= a.n || qc >= a.n) return;
-    if (a.upper_only) {
-        write_quarter<MF, BK>(a, c, qr, qc, false, true, lane);
-    } else if (!below) {
-        write_quarter<MF, BK>(a, c, qr, qc, diag && wm == wn, false, lane);
+    __syncthreads();
+    if (!*flag) return false;
+    const f32x4v *slabs = reinterpret_cast<const f32x4v *>(a.slabs) + wave * 16 * 64 + lane;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const f32x4v own = L::get(c, j);
+        f32x4v acc = me == 0 ? own : slabs[slab_of(0) * kSlab + j * 64];
+        for (int64_t s = 1; s < pieces; ++s) acc += s == me ? own : slabs[slab_of(s) * kSlab + j * 64];
+        L::set(c, j, acc);
+    }
+    return true;
+}
+
+template <int MF, int BK>
+__device__ __forceinline__ void tile_write(const DenseArgs &a,
+                                           const typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK]
+                                                                                    [Layout<MF, BK>::NBLK],
+                                           const Quarter &q, int wave, int lane) {
+    if (q.qr >= a.n || q.qc >= a.n) return;
+    if (a.upper_only) write_quarter<MF, BK>(a, c, q.qr, q.qc, false, true, lane);
+    else if (!q.below) write_quarter<MF, BK>(a, c, q.qr, q.qc, q.diag && (wave >> 1) == (wave & 1), false, lane);
+}
+
+// One work item per workgroup: a whole tile, or a k-slice of one of the split tiles.
+template <int MF, int BK, int NST, int WPE, int XABL = 0, bool PRIO = false, int IL = 0>
+__global__ __launch_bounds__(256, WPE) void gram_dense_mfma_kernel(DenseArgs a) {
+    using L = Layout<MF, BK>;
+    using St = Stage<BK>;
+    constexpr int NB = L::NBLK;
+    __shared__ __attribute__((aligned(16))) float lds[NST * 2 * St::F];  // (one array: the DMA ring)
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t w = blockIdx.x;
+    int64_t tile, slice = 0, pieces = 1;
+    if (w < a.n_whole) {
+        tile = w;
+    } else {
+        tile = a.n_whole + (w - a.n_whole) / a.n_split;
+        slice = (w - a.n_whole) % a.n_split;
+        pieces = a.n_split;
+    }
+    const int64_t kb = pieces > 1 ? slice * a.k_split : 0;
+    const int64_t ke = pieces > 1 ? (kb + a.k_split < a.kpad ? kb + a.k_split : a.kpad) : a.kpad;
+    typename L::acc_t c[NB][NB];
+    const Quarter q = tile_compute<MF, BK, NST, XABL, PRIO, IL>(a, lds, tile, kb, ke, wave, lane, c);
+    if (pieces > 1) {
+        const int64_t u = tile - a.n_whole;
+        if (!split_combine<MF, BK>(a, c, a.tickets + u, pieces, slice, [&](int64_t s) { return u * pieces + s; },
+                                   reinterpret_cast<int32_t *>(lds), wave, lane))
+            return;
+    }
+    tile_write<MF, BK>(a, c, q, wave, lane);
+}
+
+// Stream-K: slot (workgroup) s takes the k-tile units [s U, (s + 1) U) of the tiles laid end to end (tile t
+// = units [t KT, (t + 1) KT)), so every slot does the same MFMA work and the split tiles' hand-offs fall at
+// different times instead of in one burst at the end.  A tile wholly inside a slot is written directly; a
+// tile cut by slot boundaries has pieces in slots s0 .. s1, piece j's slab being slot (s0 + j)'s first
+// segment (j >= 1) -- slab 2 slot -- or, for j = 0, slot s0's last segment (slab 2 s0 + 1) unless the tile
+// starts exactly at s0's start (slab 2 s0).  Each slot has at most one first and one last segment, so the
+// slabs and the tickets (indexed by piece 0's slab) are private to one tile per launch.
+template <int MF, int BK, int NST, int WPE, int IL>
+__global__ __launch_bounds__(256, WPE) void gram_dense_sk_kernel(DenseArgs a) {
+    using L = Layout<MF, BK>;
+    using St = Stage<BK>;
+    constexpr int NB = L::NBLK;
+    __shared__ __attribute__((aligned(16))) float lds[NST * 2 * St::F];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t U = a.sk_units, KT = a.sk_kt;
+    const int64_t u0 = (int64_t)blockIdx.x * U;
+    const int64_t u1 = u0 + U < a.sk_total ? u0 + U : a.sk_total;
+    for (int64_t u = u0; u < u1;) {
+        const int64_t tile = u / KT, tb = tile * KT, te = tb + KT;
+        const int64_t se = u1 < te ? u1 : te;
+        __syncthreads();  // (the previous segment's ring reads and hand-off flag are done)
+        typename L::acc_t c[NB][NB];
+        const Quarter q =
+            tile_compute<MF, BK, NST, 0, false, IL>(a, lds, tile, (u - tb) * BK, (se - tb) * BK, wave, lane, c);
+        bool write = true;
+        if (u != tb || se != te) {
+            const int64_t s0 = tb / U, s1 = (te - 1) / U;
+            const int64_t first = 2 * s0 + (tb == s0 * U ? 0 : 1);
+            write = split_combine<MF, BK>(
+                a, c, a.tickets + first, s1 - s0 + 1, blockIdx.x - s0,
+                [&](int64_t j) { return j == 0 ? first : 2 * (s0 + j); }, reinterpret_cast<int32_t *>(lds), wave,
+                lane);
+        }
+        if (write) tile_write<MF, BK>(a, c, q, wave, lane);
+        u = se;
     }
 }
 
@@ -591,12 +666,29 @@ DensePlan dense_plan(int64_t n, int64_t k_dim, int bk) {
     return p;
 }
 
+// Stream-K plan (GRF_DENSE_SK=1): slots = 2 workgroups per CU, U k-tile units each.
+struct SkPlan {
+    int64_t kt, total, units, grid;
+    size_t ws_bytes;
+};
+SkPlan sk_plan(int64_t n, int64_t k_dim, int bk) {
+    SkPlan p{};
+    const int64_t nt = cdiv<int64_t>(n, kTile);
+    p.kt = cdiv<int64_t>(k_dim, bk);
+    p.total = nt * (nt + 1) / 2 * p.kt;
+    const int64_t slots = std::min<int64_t>(2 * kCUs, std::max<int64_t>(p.total, 1));
+    p.units = std::max<int64_t>(1, cdiv<int64_t>(p.total, slots));
+    p.grid = cdiv<int64_t>(p.total, p.units);
+    p.ws_bytes = kTicketBytes + (size_t)(2 * p.grid) * kTile * kTile * sizeof(float);
+    return p;
+}
+
 }  // namespace
 
 size_t dense_gram_workspace_bytes(int64_t n, int64_t k_dim) {
     if (n <= 0) return 16;
     const DensePlan p = dense_plan(n, k_dim, 16);
-    return std::max<size_t>(16, p.ws_bytes);
+    return std::max<size_t>(16, std::max(p.ws_bytes, sk_plan(n, k_dim, 16).ws_bytes));
 }
 
 int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk, void *workspace,
@@ -612,6 +704,37 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
     const int BK = variant / 100 % 100 == 32 ? 32 : 16;
     DensePlan p = dense_plan(n, k_dim, BK);
     GRF_REQUIRE(p.kpad <= lda, GRF_EINVAL, "grf_gram_dense: lda must cover k_dim rounded up to %d", BK);
+    // stream-K when the tiles fill at least half the slots (every slot then takes >= half a tile of k, so a
+    // split tile has <= 3 pieces): n = 4096 0.68 -> 0.78, C2 0.83 -> 0.86 of the MFMA peak; at C3 (253 tiles)
+    // even, below it the per-tile splits win (profiles/r04_dense_ab.txt).  GRF_DENSE_SK: 0 never, 1 always.
+    static const int sk_env = env_int("GRF_DENSE_SK", -1);
+    const bool sk = sk_env == 1 || (sk_env != 0 && p.tiles >= kCUs);
+    if (sk && BK == 16) {
+        const SkPlan q = sk_plan(n, k_dim, BK);
+        if (workspace && workspace_bytes >= q.ws_bytes && ((uintptr_t)workspace & 255) == 0) {
+            GRF_REQUIRE_GRID(q.grid, 256, "gram_dense_sk_kernel");
+            DenseArgs a{};
+            a.A = A;
+            a.K = K;
+            a.tickets = reinterpret_cast<int32_t *>(workspace);
+            a.slabs = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes);
+            a.n = n;
+            a.nt = p.nt;
+            a.lda = lda;
+            a.ldk = ldk;
+            a.kpad = p.kpad;
+            a.upper_only = upper_only ? 1 : 0;
+            a.sk_units = q.units;
+            a.sk_kt = q.kt;
+            a.sk_total = q.total;
+            hipStream_t st = S(stream);
+            static const int il_sk = env_int("GRF_DENSE_IL", 2);
+            if (il_sk == 1) gram_dense_sk_kernel<32, 16, 4, 2, 1><<<(unsigned)q.grid, 256, 0, st>>>(a);
+            else gram_dense_sk_kernel<32, 16, 4, 2, 2><<<(unsigned)q.grid, 256, 0, st>>>(a);
+            GRF_CHECK_LAUNCH("gram_dense_sk_kernel");
+            return GRF_OK;
+        }
+    }
     if (p.ws_bytes > 0 && (!workspace || workspace_bytes < p.ws_bytes || ((uintptr_t)workspace & 255))) {
         // no (or too small) workspace: whole tiles only
         p.n_split = 1;
@@ -640,7 +763,7 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
     const unsigned grid = (unsigned)items;
     hipStream_t st = S(stream);
     static const bool prio = env_int("GRF_DENSE_PRIO", 0) == 1;
-    static const int il = env_int("GRF_DENSE_IL", 1);
+    static const int il = env_int("GRF_DENSE_IL", 2);
     switch ((variant ? variant : 321642) + (prio ? 1000000 : 0) + il * 2000000) {  // A/B (GRF_DENSE_VARIANT): MF * 10000 + BK * 100 + stages * 10 + waves per SIMD
         case 321642: gram_dense_mfma_kernel<32, 16, 4, 2><<<grid, 256, 0, st>>>(a); break;
         case 321652: gram_dense_mfma_kernel<32, 16, 5, 2><<<grid, 256, 0, st>>>(a); break;
@@ -655,7 +778,7 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
         case 6321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 3><<<grid, 256, 0, st>>>(a); break;
         case 4161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, false, 2><<<grid, 256, 0, st>>>(a); break;
         case 6161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, false, 3><<<grid, 256, 0, st>>>(a); break;
-        default: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 1><<<grid, 256, 0, st>>>(a); break;
+        default: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 2><<<grid, 256, 0, st>>>(a); break;
     }
     GRF_CHECK_LAUNCH("gram_dense_mfma_kernel");
     return GRF_OK;

@@ -15,7 +15,9 @@ __device__ inline void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
         const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        // (three-input XOR in one v_bitop3_b32, truth table 0x96, the key from its SGPR)
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32(hi1, c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32(hi0, c3, k1, 0x96);
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
@@ -38,7 +40,18 @@ __device__ __noinline__ uint64_t philox_lemire_retry(uint32_t d, uint32_t thr, u
     }
 }
 
-__device__ inline double load_update(int rule, double load, int64_t deg, double w, double p) {
+// The halt test h < p of the 53-bit double h = (x0:x1 >> 11) 2^-53 as an integer compare: h < p <=> t < p 2^53
+// <=> t < ceil(p 2^53) for the integer t (p 2^53 is exact); 0 when p <= 0 or NaN (never halts).
+__device__ inline uint64_t halt_threshold(double p) {
+    const double y = ceil(p * 9007199254740992.0);
+    return y > 0.0 ? (y < 9007199254740992.0 ? (uint64_t)y : (1ull << 53)) : 0ull;
+}
+__device__ inline bool halts(uint32_t x0, uint32_t x1, uint64_t thr) {
+    return ((((uint64_t)x0 << 32) | x1) >> 11) < thr;
+}
+
+template <typename Deg>
+__device__ inline double load_update(int rule, double load, Deg deg, double w, double p) {
     const double f = ((double)deg * w) / (1.0 - p);
     if (rule == GRF_LOAD_CUMULATIVE) return load * f;
     if (rule == GRF_LOAD_NONCUMULATIVE) return f;
@@ -56,6 +69,7 @@ __device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const i
                                       int32_t rule, uint32_t k0, uint32_t k1, Visit visit) {
     int64_t cur = s;
     double load = 1.0;
+    const uint64_t hthr = halt_threshold(p);
     int32_t l = 0;
     for (; l < L; ++l) {
         visit(l, (int32_t)cur, load);
@@ -63,8 +77,7 @@ __device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const i
         if (deg == 0) return l + 1;
         uint32_t x0, x1, x2, x3;
         philox4x32_10((uint32_t)l, w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
-        const double h = (double)((((uint64_t)x0 << 32) | x1) >> 11) * (1.0 / 9007199254740992.0);
-        if (h < p) return l + 1;
+        if (halts(x0, x1, hthr)) return l + 1;
         const uint32_t d = (uint32_t)deg;
         uint32_t k = 0;
         if (d > 1) {
@@ -114,6 +127,7 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
     const unsigned char *recs = aug + kAugHeader;
     int64_t cur = s;
     double load = 1.0;
+    const uint64_t hthr = halt_threshold(p);
     int64_t rs = g_ptr[s];
     int64_t deg = g_ptr[s + 1] - rs;
     int32_t l = 0;
@@ -122,8 +136,7 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
         if (deg == 0) return l + 1;
         uint32_t x0, x1, x2, x3;
         philox4x32_10((uint32_t)l, w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
-        const double h = (double)((((uint64_t)x0 << 32) | x1) >> 11) * (1.0 / 9007199254740992.0);
-        if (h < p) return l + 1;
+        if (halts(x0, x1, hthr)) return l + 1;
         const uint32_t d = (uint32_t)deg;
         uint32_t k = 0;
         if (d > 1) {
@@ -138,7 +151,7 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
             const int4 a = *reinterpret_cast<const int4 *>(recs + (size_t)(rs + k) * sizeof(AugRec16));
             const uint64_t pk = ((uint64_t)(uint32_t)a.y << 32) | (uint32_t)a.x;
             const double wt = __hiloint2double(a.w, a.z);
-            load = load_update(rule, load, deg, wt, p);
+            load = load_update(rule, load, (uint32_t)deg, wt, p);  // (a row length < n < 2^31: exact either way)
             cur = (int64_t)(pk & tmask);
             rs = (int64_t)((pk >> tb) & rmask);
             deg = (int64_t)(pk >> (tb + rb));
@@ -146,7 +159,7 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
             const AugRec *rec = reinterpret_cast<const AugRec *>(recs) + rs + k;
             const int4 a = *reinterpret_cast<const int4 *>(rec);
             const double wt = rec->w;
-            load = load_update(rule, load, deg, wt, p);
+            load = load_update(rule, load, (uint32_t)deg, wt, p);
             cur = a.x;
             rs = (int64_t)(uint32_t)a.y;
             deg = a.z;

@@ -433,10 +433,12 @@ def test_gram_dense_asymmetric_layout(eng):
     np.testing.assert_allclose(K, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("n,k", [(300, 900), (2708, 2708), (1500, 4000)])
+@pytest.mark.parametrize("n,k", [(300, 900), (2708, 2708), (1500, 4000), (4200, 1000), (4200, 20), (5000, 4999)])
 def test_gram_dense_split_k(eng, n, k):
-    """Split-K dense Gram (small n: slices of k summed in order by the combine pass that writes both
-    triangles) against fp64 and against the unsplit kernel; exactly symmetric, run-to-run identical."""
+    """Split-K dense Gram against fp64 and against the unsplit kernel (no workspace); exactly symmetric,
+    run-to-run identical.  Small n: every tile cut into k-slices summed in order by the last piece; from
+    256 tiles on (n >= 4200 here) the stream-K slots, whose pieces span slot boundaries -- k = 20 gives
+    tiles of 2 k-tiles over slots of 3, so most tiles are cut."""
     import torch
     from grf_amd import _lib as C
     lda = -(-k // 64) * 64

@@ -17,4 +17,7 @@ for w in c3 c2 c5; do
   echo $w ok; tail -c 300 $O/bench_$w.json
 done
 PASSES=sq timeout -k 10 500 $R/tools/pmc_passes.sh $O/pmc_c4 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-mfma-leg || exit 1
-echo done
+
+bash tools/r04_ab11.sh || exit 1
+timeout -k 10 400 python3 -u tools/c5_hub_model.py > $O/c5_hub_model.txt 2>&1 || { echo c5 model failed; tail $O/c5_hub_model.txt; exit 1; }
+tail -9 $O/c5_hub_model.txt

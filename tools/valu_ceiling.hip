@@ -47,7 +47,15 @@ __global__ void valu_kernel(unsigned long long *stamps, float *out, int iters, f
 #define OP(i) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(d[i]) : "v"(da), "v"(db));
                 REP8(OP)
 #undef OP
-            } else {  // v_rcp_f64 (the fp64 divide's seed: transcendental rate)
+            } else if constexpr (KIND == 5) {  // v_mad_u64_u32 (Philox's 32 x 32 -> 64 products)
+#define OP(i) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(d[i]) : "v"(u[i]), "v"(m) : "vcc");
+                REP8(OP)
+#undef OP
+            } else if constexpr (KIND == 6) {  // v_med3_u32 (the sort network's keep)
+#define OP(i) asm volatile("v_med3_u32 %0, %0, %1, %2" : "+v"(u[i]) : "v"(m), "v"(u[(i + 1) & 7]));
+                REP8(OP)
+#undef OP
+            } else if constexpr (KIND == 4) {  // v_rcp_f64 (the fp64 divide's seed: transcendental rate)
 #define OP(i) asm volatile("v_rcp_f64 %0, %0" : "+v"(d[i]));
                 REP8(OP)
 #undef OP
@@ -64,7 +72,7 @@ __global__ void valu_kernel(unsigned long long *stamps, float *out, int iters, f
 
 int main() {
     const int cus = 256, iters = 2000;
-    const char *names[] = {"v_fma_f32", "v_xad_u32", "v_mul_hi_u32", "v_fma_f64", "v_rcp_f64"};
+    const char *names[] = {"v_fma_f32", "v_xad_u32", "v_mul_hi_u32", "v_fma_f64", "v_rcp_f64", "v_mad_u64_u32", "v_med3_u32"};
     float *out;
     unsigned long long *stamps;
     hipMalloc(&out, cus * 1024 * sizeof(float));
@@ -74,7 +82,7 @@ int main() {
     hipEventCreate(&e1);
     std::vector<unsigned long long> h(cus * 16);
     printf("kind wps  cyc_per_inst_per_SIMD(median WG)  insts_per_SIMD_cycle  wall_ms  clock_GHz(from stamps)\n");
-    for (int kind = 0; kind < 5; ++kind) {
+    for (int kind = 0; kind < 7; ++kind) {
         for (int wps = 1; wps <= 4; wps *= 2) {
             const int threads = 256 * wps;
             for (int rep = 0; rep < 2; ++rep) {
@@ -84,7 +92,9 @@ int main() {
                     case 1: valu_kernel<1><<<cus, threads>>>(stamps, out, iters, 1e-3f); break;
                     case 2: valu_kernel<2><<<cus, threads>>>(stamps, out, iters, 1e-3f); break;
                     case 3: valu_kernel<3><<<cus, threads>>>(stamps, out, iters, 1e-3f); break;
-                    default: valu_kernel<4><<<cus, threads>>>(stamps, out, iters, 1e-3f); break;
+                    case 4: valu_kernel<4><<<cus, threads>>>(stamps, out, iters, 1e-3f); break;
+                    case 5: valu_kernel<5><<<cus, threads>>>(stamps, out, iters, 1e-3f); break;
+                    default: valu_kernel<6><<<cus, threads>>>(stamps, out, iters, 1e-3f); break;
                 }
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);
