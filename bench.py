@@ -36,7 +36,7 @@ from grf_amd.graphs import er_graph_exact_edges, powerlaw_graph, snap_graph  # n
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh -> tools/pmc_summary.py), committed
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_summary.json")
 DEFAULT_WORKLOAD = (100_000, 1_000_000, 128, 8, 0.1)
 
 
@@ -1013,7 +1013,7 @@ def mfma_leg(eng, args, steps: int = 20, workload: str = "c3"):
     flops = 1.0 * n * (n + 1) * n
     tfs = flops / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "gram_dense_kernel (v_mfma_f32_32x32x2f32) + its combine/mirror",
+            "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "gram_dense_mfma_kernel / gram_dense_sk_kernel (LDS-DMA staged 128x128 upper tiles, v_mfma_f32_32x32x2f32, both triangles written)",
             "kernel_ms": ms, "algorithmic_flops": flops,
             "workload": f"{wdesc} dense path, m={m}, L={L}: K = Phi Phi^T of the dense fp32 Phi "
                         f"(N (N+1) N flops: the unique entries of the symmetric product)"}

@@ -50,9 +50,24 @@ __device__ inline bool halts(uint32_t x0, uint32_t x1, uint64_t thr) {
     return ((((uint64_t)x0 << 32) | x1) >> 11) < thr;
 }
 
+// x / c correctly rounded without the IEEE divide sequence (v_div_scale x2, v_rcp_f64, 5 FMAs, v_div_fmas,
+// v_div_fixup per call): with y = RN(1 / c) (loop-invariant: computed once per walk) the quotient
+// q = RN(x y) is faithful, the remainder x - c q is exact in one FMA, and RN(q + (x - c q) y) is RN(x / c)
+// (Markstein's theorem; finite normal x and c, as the loads and 1 - p_halt are).  Same bits as x / c.
+__device__ inline double div_by(double x, double c, double y) {
+    const double q = x * y;
+    return __builtin_fma(__builtin_fma(-q, c, x), y, q);
+}
+
+// The importance weight deg w / (1 - p) applied by the load rule; keep = 1 - p and its reciprocal
+// (LoadKeep, once per walk).
+struct LoadKeep {
+    double c, y;
+    __device__ explicit LoadKeep(double p) : c(1.0 - p), y(1.0 / (1.0 - p)) {}
+};
 template <typename Deg>
-__device__ inline double load_update(int rule, double load, Deg deg, double w, double p) {
-    const double f = ((double)deg * w) / (1.0 - p);
+__device__ inline double load_update(int rule, double load, Deg deg, double w, const LoadKeep &keep) {
+    const double f = div_by((double)deg * w, keep.c, keep.y);
     if (rule == GRF_LOAD_CUMULATIVE) return load * f;
     if (rule == GRF_LOAD_NONCUMULATIVE) return f;
     return w;
@@ -70,6 +85,7 @@ __device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const i
     int64_t cur = s;
     double load = 1.0;
     const uint64_t hthr = halt_threshold(p);
+    const LoadKeep keep(p);
     int32_t l = 0;
     for (; l < L; ++l) {
         visit(l, (int32_t)cur, load);
@@ -89,7 +105,7 @@ __device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const i
             k = (uint32_t)(mm >> 32);
         }
         const double wt = g_val[rs + k];
-        load = load_update(rule, load, deg, wt, p);
+        load = load_update(rule, load, deg, wt, keep);
         cur = g_idx[rs + k];
     }
     return L;
@@ -128,6 +144,7 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
     int64_t cur = s;
     double load = 1.0;
     const uint64_t hthr = halt_threshold(p);
+    const LoadKeep keep(p);
     int64_t rs = g_ptr[s];
     int64_t deg = g_ptr[s + 1] - rs;
     int32_t l = 0;
@@ -151,7 +168,7 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
             const int4 a = *reinterpret_cast<const int4 *>(recs + (size_t)(rs + k) * sizeof(AugRec16));
             const uint64_t pk = ((uint64_t)(uint32_t)a.y << 32) | (uint32_t)a.x;
             const double wt = __hiloint2double(a.w, a.z);
-            load = load_update(rule, load, (uint32_t)deg, wt, p);  // (a row length < n < 2^31: exact either way)
+            load = load_update(rule, load, (uint32_t)deg, wt, keep);  // (a row length < n < 2^31: exact either way)
             cur = (int64_t)(pk & tmask);
             rs = (int64_t)((pk >> tb) & rmask);
             deg = (int64_t)(pk >> (tb + rb));
@@ -159,7 +176,7 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
             const AugRec *rec = reinterpret_cast<const AugRec *>(recs) + rs + k;
             const int4 a = *reinterpret_cast<const int4 *>(rec);
             const double wt = rec->w;
-            load = load_update(rule, load, (uint32_t)deg, wt, p);
+            load = load_update(rule, load, (uint32_t)deg, wt, keep);
             cur = a.x;
             rs = (int64_t)(uint32_t)a.y;
             deg = a.z;

@@ -24,6 +24,14 @@ namespace grf {
 __device__ inline double normalise(double acc, int32_t norm, int64_t m) {
     return norm == GRF_NORM_DIV ? acc / (double)m : acc * (1.0 / (double)m);
 }
+// The same with 1 / m computed once per workgroup: NORM_DIV divides through div_by (grf_philox.h: the
+// correctly rounded quotient, same bits as acc / m), NORM_MUL_RECIP multiplies by the rounded reciprocal
+struct Norm {
+    double m, inv;
+    int32_t norm;
+    __device__ Norm(int32_t norm_, int64_t m_) : m((double)m_), inv(1.0 / (double)m_), norm(norm_) {}
+    __device__ double operator()(double acc) const { return norm == GRF_NORM_DIV ? div_by(acc, m, inv) : acc * inv; }
+};
 
 // --------------------------------------------------------------- grf_steps
 // one workgroup per (source, step) group of m slots; P = next_pow2(m) keys in LDS
@@ -165,6 +173,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     KT *key = reinterpret_cast<KT *>(scratch + 32);             // [P]
     const KT kNone = (KT)~(KT)0;
     const int64_t s = blockIdx.x;
+    const Norm nrm(norm, m);
     const int sh = wbits + lbits;
     const KT wmask = (KT)(((KT)1 << wbits) - 1), lmask = (KT)(((KT)1 << lbits) - 1);
     auto make_key = [&](int32_t node, int l, int64_t w) {
@@ -280,7 +289,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
             }
         }
         hk_[q] = run_k;  // (static register indexing: q is the unrolled position)
-        hv_[q] = normalise(acc, norm, m);
+        hv_[q] = nrm(acc);
         owned = false;
         ++c;
     }

@@ -153,6 +153,7 @@ __global__ __launch_bounds__(64) void walk_pcg64_kernel(int64_t n, const int64_t
         recs = g_aug + kAugHeader;
     }
     const uint64_t tmask = (1ull << tb) - 1, rmask = (1ull << rb) - 1;
+    const LoadKeep keep(p);
     for (int64_t s = b; s < e; ++s) {
         const int64_t sl = s - src_begin;
         const int64_t rs0 = g_ptr[s], deg0 = g_ptr[s + 1] - rs0;
@@ -173,19 +174,19 @@ __global__ __launch_bounds__(64) void walk_pcg64_kernel(int64_t n, const int64_t
                 const uint32_t k = g.integers((uint32_t)deg);
                 if (!kAug) {
                     const double wt = g_val[rs + k];
-                    load = load_update(rule, load, deg, wt, p);
+                    load = load_update(rule, load, deg, wt, keep);
                     cur = g_idx[rs + k];
                 } else if (compact) {
                     const int4 a = *reinterpret_cast<const int4 *>(recs + (size_t)(rs + k) * sizeof(AugRec16));
                     const uint64_t pk = ((uint64_t)(uint32_t)a.y << 32) | (uint32_t)a.x;
-                    load = load_update(rule, load, deg, __hiloint2double(a.w, a.z), p);
+                    load = load_update(rule, load, deg, __hiloint2double(a.w, a.z), keep);
                     cur = (int64_t)(pk & tmask);
                     rs = (int64_t)((pk >> tb) & rmask);
                     deg = (int64_t)(pk >> (tb + rb));
                 } else {
                     const AugRec *rec = reinterpret_cast<const AugRec *>(recs) + rs + k;
                     const int4 a = *reinterpret_cast<const int4 *>(rec);
-                    load = load_update(rule, load, deg, rec->w, p);
+                    load = load_update(rule, load, deg, rec->w, keep);
                     cur = a.x;
                     rs = (int64_t)(uint32_t)a.y;
                     deg = a.z;

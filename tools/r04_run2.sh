@@ -5,6 +5,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/r04_run2
 mkdir -p $O
 cd $R
+bash tools/gpu_tests.sh r04_run2_tests "gram_dense" 300 || exit 1
 timeout -k 10 120 ./tools/valu_ceiling > $O/valu_ceiling.txt 2>&1 || { echo valu failed; exit 1; }
 cat $O/valu_ceiling.txt
 (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
