@@ -5,35 +5,38 @@
 //
 // Tiles.  K is symmetric, so only the 128 x 128 tiles on and above the diagonal are computed
 // (n^2 k flops instead of 2 n^2 k); every tile writes its entries to both triangles, so there is no
-// mirror pass.  A workgroup of 4 waves (2 x 2) owns one tile, each wave a 64 x 64 quarter: 4 x 4 blocks
-// of v_mfma_f32_16x16x4f32 (MF = 16) or 2 x 2 blocks of v_mfma_f32_32x32x2f32 (MF = 32), 64 accumulator
-// VGPRs either way.  A wave whose quarter lies wholly below the diagonal (diagonal tiles) or past n
-// (edge tiles) issues no MFMAs.
+// mirror pass.  A workgroup of 4 waves (2 x 2) owns one tile, each wave a 64 x 64 quarter of 2 x 2 blocks
+// of v_mfma_f32_32x32x2f32 (64 accumulator VGPRs).  A wave whose quarter lies wholly below the diagonal
+// (diagonal tiles) or past n (edge tiles) issues no MFMAs.
 //
 // Staging.  Both operands are rows of A (k contiguous), so the k-tiles go global -> LDS by LDS-DMA
-// (global_load_lds_dwordx4: no VGPR round trip, no transposing LDS writes) into a ring of NST stages with
-// ONE barrier per k-tile and NST - 2 k-tiles in flight behind a counted `s_waitcnt vmcnt` (never 0 in the
-// loop).  The loop is software-pipelined across the k-tile boundary: the next fragments are read from
-// LDS before the current MFMAs, and the boundary (retire k-tile t + 1, barrier, DMA of k-tile
-// t + NST - 1, read of t + 1's first fragments) sits before the MFMAs of tile t's last fragment group,
-// so no MFMA waits on a read issued after a barrier.  WAR: the DMA issued at boundary t -> t + 1 refills
-// the stage of tile t - 1, which every wave has consumed before reaching that barrier.  A diagonal tile
-// stages one operand (B = A).  The LDS image of a k-tile is row-major, BK floats a row; one DMA piece
-// (64 lanes x 16 B) is lane-linear, so the bank swizzle (16-B chunk c of row r stored at c ^ swz(r)) is
-// applied on the per-lane SOURCE address and on the fragment read (conflict-free ds_read_b128).
+// (global_load_lds_dwordx4: no VGPR round trip, no transposing LDS writes) into a ring of NST = 4 stages
+// with ONE barrier per k-tile and 2 k-tiles in flight behind a counted `s_waitcnt vmcnt` (never 0 in the
+// loop).  The loop is software-pipelined across the k-tile boundary: each step's MFMAs go in four chunks,
+// each preceded by a quarter of the NEXT fragments' reads and followed by a quarter of the boundary's DMA
+// pieces; the boundary (retire k-tile t + 1, barrier, DMA of k-tile t + 3) sits before the MFMAs of tile
+// t's last fragment group, so no MFMA waits on a read issued after a barrier.  WAR: the DMA issued at
+// boundary t -> t + 1 refills the stage of tile t - 1, which every wave has consumed before that barrier.
+// A diagonal tile stages one operand (B = A).  The LDS image of a k-tile is row-major, BK floats a row; one
+// DMA piece (64 lanes x 16 B) is lane-linear, so the bank swizzle (16-B chunk c of row r stored at
+// c ^ swz(r)) is applied on the per-lane SOURCE address and on the fragment read (conflict-free
+// ds_read_b128).  Measured alternatives (16 x 16 x 4 blocks, 3 / 5 stages, MFMA-first chunks, wave
+// priority, operands straight to registers, 3 workgroups per CU): profiles/r04_dense_ab.txt.
 //
-// k order.  MF = 32: lane (r, h) holds k = h BK/2 + 4 g + s at step (g, s); MF = 16: lane (r, q) holds
-// k = 4 q + s at step s (BK = 16): one ds_read_b128 gives a lane the operands of four MFMA steps.  Each K
-// entry is a fixed chain of exact f32 FMAs over that order (bitwise reproducible run to run); diagonal
-// tiles write each entry computed at (i, j >= i) to both (i, j) and (j, i), so K is exactly symmetric.
+// k order.  Lane (r, h) holds k = h BK/2 + 4 g + s at step (g, s): one ds_read_b128 gives a lane the
+// operands of four MFMA steps.  Each K entry is a fixed chain of exact f32 FMAs over that order (bitwise
+// reproducible run to run); diagonal tiles write each entry computed at (i, j >= i) to both (i, j) and
+// (j, i), so K is exactly symmetric.
 //
-// Split-K (small n: too few tiles for the CUs; large n: the last `tail` tiles, so that the last partial
-// round of workgroups is cut finer): a tile's pieces are k-slices; each writes its partial tile (16-B
-// stores, register layout) to a slab, and the piece that draws the last ticket sums the slabs in slice
+// Work decomposition.  From 256 tiles on, stream-K (gram_dense_sk_kernel): 512 slots (2 workgroups per
+// CU) take equal runs of k-tile units of the tiles laid end to end, so no slot idles in a last partial
+// round and the hand-offs of the tiles cut by slot boundaries fall at different times.  Below that every
+// tile is cut into 2-4 k-slices (gram_dense_mfma_kernel).  A cut tile's pieces write their partial tiles
+// (16-B stores, register layout) to slabs, and the piece that draws the last ticket sums them in piece
 // order (its own from registers) and writes the tile.  Hand-off (cdna_hip_programming.md, "Projection
 // GEMM" item 2): slab stores -> every wave vmcnt(0) -> barrier -> agent release -> ticket fetch_add; the
 // last arriver: agent acquire -> barrier -> plain loads.  The last arriver resets its ticket, so the
-// ticket array stays zero between launches (it must be zero on first use).
+// ticket block stays zero between launches (it must be zero on first use).
 #include "grf_common.h"
 
 namespace grf {
@@ -56,7 +59,6 @@ struct DenseArgs {
     int32_t n_split;   // pieces per split tile (the tiles from n_whole on)
     int32_t upper_only;  // write only K[row][col] of the computed tiles (the hub panel's seed)
     int64_t sk_units, sk_kt, sk_total;  // stream-K: k-tile units per slot, per tile, in all
-    int32_t abl;       // A/B ablations (GRF_DENSE_ABL; timing only): 1 no DMA, 4 no barrier, 8 no mirror
 };
 
 // Fragment layout of one wave's 64 x 64 quarter.
@@ -92,29 +94,6 @@ struct Layout<32, BK> {  // 2 x 2 blocks of 32 x 32; lane (r = lane & 31, h = la
     }
     static __device__ __forceinline__ int row0(int j, int lane) { return 32 * (j >> 3) + 8 * (j & 3) + 4 * (lane >> 5); }
     static __device__ __forceinline__ int col(int j, int lane) { return 32 * ((j >> 2) & 1) + (lane & 31); }
-};
-
-template <int BK>
-struct Layout<16, BK> {  // 4 x 4 blocks of 16 x 16; lane (r = lane & 15, q = lane >> 4)
-    static_assert(BK == 16, "the 16 x 16 layout stages k-tiles of 16");
-    static constexpr int NBLK = 4, GG = 1;
-    typedef f32x4v acc_t;
-    static constexpr int C = 4;
-    // (row / 4) & 2: the four lanes of a ds_read_b128 lane group that share row % 4 get distinct chunks
-    static __device__ __forceinline__ int swz(int row) { return (row >> 2) & 2; }
-    static __device__ __forceinline__ int off(int q0, int x, int, int lane) {
-        const int row = q0 + x * 16 + (lane & 15), chunk = (lane >> 4) ^ swz(row);
-        return (row * C + chunk) * 4;
-    }
-    static constexpr int XSTRIDE = 16 * C * 16;
-    static __device__ __forceinline__ acc_t mfma(float a, float b, acc_t c) {
-        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-    }
-    // float4 j: block (x, y) = (j >> 2, j & 3), rows 16 x + 4 q + 0..3, column 16 y + (lane & 15)
-    static __device__ __forceinline__ f32x4v get(const acc_t (&c)[4][4], int j) { return c[j >> 2][j & 3]; }
-    static __device__ __forceinline__ void set(acc_t (&c)[4][4], int j, f32x4v v) { c[j >> 2][j & 3] = v; }
-    static __device__ __forceinline__ int row0(int j, int lane) { return 16 * (j >> 2) + 4 * (lane >> 4); }
-    static __device__ __forceinline__ int col(int j, int lane) { return 16 * (j & 3) + (lane & 15); }
 };
 
 template <int BK>
@@ -162,34 +141,33 @@ __device__ __forceinline__ void tile_coords(int64_t b, int64_t nt, int64_t &bi, 
 }
 
 // The k-loop over [kb, ke) of one tile.  DIAG: B = A (one operand staged).  LIVE: this wave computes
-// (a dead wave still stages its share of the DMA and joins the barriers).  XABL (timing-only builds):
-// 16 = no fragment reads after the first.
-template <int MF, int BK, int NST, bool DIAG, bool LIVE, int XABL, bool PRIO, int IL>
+// (a dead wave still stages its share of the DMA and joins the barriers).
+template <int MF, int BK, int NST, bool DIAG, bool LIVE>
 __device__ __forceinline__ void kloop(float *lds, const float *const *srcA, const float *const *srcB, int64_t kb,
                                       int64_t ke, int wave, const int *aoff, const int *boff,
-                                      typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK][Layout<MF, BK>::NBLK],
-                                      int abl) {
+                                      typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK][Layout<MF, BK>::NBLK]) {
     using L = Layout<MF, BK>;
     using St = Stage<BK>;
     constexpr int NB = L::NBLK, GG = L::GG;
+    static_assert(NB == 2 && GG == 2, "the step sequence below is written for 2 x 2 blocks and 2 groups per k-tile");
     constexpr int D = NST - 2;  // k-tiles in flight behind the one being published
-    static_assert(D >= 1, "the pipelined k-loop needs NST >= 3");
+    static_assert(D >= 1 && D <= 3, "the pipelined k-loop needs 3 <= NST <= 5");
     constexpr int G = DIAG ? St::PW : 2 * St::PW;  // DMA instructions per wave per k-tile
     const int64_t nk = (ke - kb) / BK;
-    auto issue = [&](int64_t t) {
-        if (abl & 1) return;
+    const uint32_t lds0 = lds_addr(lds);
+    // DMA pieces q, q + 4, ... of k-tile t (all of them: issue(t, -1))
+    auto issue = [&](int64_t t, int q) {
         float *base = lds + (int)(t % NST) * 2 * St::F + wave * St::PW * 256;
         const int64_t k0 = kb + t * BK;
 #pragma unroll
-        for (int j = 0; j < St::PW; ++j) dma16(srcA[j] + k0, base + j * 256);
-        if (!DIAG) {
-#pragma unroll
-            for (int j = 0; j < St::PW; ++j) dma16(srcB[j] + k0, base + St::F + j * 256);
+        for (int j = 0; j < G; ++j) {
+            if (q >= 0 && (j & 3) != q) continue;
+            if (j < St::PW) dma16(srcA[j] + k0, base + j * 256);
+            else dma16(srcB[j - St::PW] + k0, base + St::F + (j - St::PW) * 256);
         }
     };
     // retire the oldest k-tile in flight (`ahead` younger ones may stay in flight) and publish it
     auto retire = [&](int64_t ahead) {  // (ahead <= D - 1)
-        static_assert(D <= 3, "add the vmcnt cases for D > 3");
         if constexpr (D == 3) {
             if (ahead >= 2) wait_vm<2 * G>();
             else if (ahead == 1) wait_vm<G>();
@@ -200,94 +178,27 @@ __device__ __forceinline__ void kloop(float *lds, const float *const *srcA, cons
         } else {
             wait_vm<0>();
         }
-        if (!(abl & 4)) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
     struct Frag { f32x4v a[NB], b[NB]; };
-    Frag fixed{};
-    const uint32_t lds0 = lds_addr(lds);
-    auto read = [&](int64_t t, int g) {
-        if constexpr ((XABL & 16) != 0) {
-            if (t > 0 || g > 0) return fixed;
-        }
-        const uint32_t As = lds0 + (uint32_t)(t % NST) * (2 * St::F * 4);
-        const uint32_t Bs = DIAG ? As : As + St::F * 4;
-        const uint32_t ab = As + (uint32_t)aoff[g] * 4, bb = Bs + (uint32_t)boff[g] * 4;
-        Frag f;
-        f.a[0] = ds_read16<0>(ab);
-        f.b[0] = ds_read16<0>(bb);
-        f.a[1] = ds_read16<L::XSTRIDE>(ab);
-        f.b[1] = ds_read16<L::XSTRIDE>(bb);
-        if constexpr (NB == 4) {
-            f.a[2] = ds_read16<2 * L::XSTRIDE>(ab);
-            f.b[2] = ds_read16<2 * L::XSTRIDE>(bb);
-            f.a[3] = ds_read16<3 * L::XSTRIDE>(ab);
-            f.b[3] = ds_read16<3 * L::XSTRIDE>(bb);
-        }
-        return f;
-    };
-    // every read issued so far has landed; f's registers are redefined here (nothing reads them earlier)
-    auto lgkm_done = [&](Frag &f) {
-        if constexpr (NB == 4)
-            asm volatile("s_waitcnt lgkmcnt(0)"
-                         : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.b[0]), "+v"(f.b[1]),
-                           "+v"(f.b[2]), "+v"(f.b[3])::"memory");
-        else
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.b[0]), "+v"(f.b[1])::"memory");
-    };
-    auto mfma = [&](const Frag &f) {
-        if constexpr (LIVE) {
-            if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int x = 0; x < NB; ++x)
-#pragma unroll
-                    for (int y = 0; y < NB; ++y) c[x][y] = L::mfma(f.a[x][s], f.b[y][s], c[x][y]);
-            if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-        }
-    };
-    if (nk <= 0) return;
-#pragma unroll
-    for (int t = 0; t < D; ++t)
-        if (t < nk) issue(t);
-    retire(D - 1 < nk - 1 ? D - 1 : nk - 1);
-    if (D < nk) issue(D);
-    // one step = the MFMAs of fragment group g of k-tile t, with the next group's reads in flight; the
-    // two fragment sets alternate by name (no register copies between steps)
-    // interleaved form (IL): the MFMAs of one step in four chunks (one k-step s each), each followed by a
-    // quarter of the next fragments' reads and of the boundary's DMA pieces
+    // read q (0..3) of fragment group g of k-tile t: a0, b0, a1, b1
     auto read_q = [&](int64_t t, int g, int q, Frag &f) {
         const uint32_t As = lds0 + (uint32_t)(t % NST) * (2 * St::F * 4);
         const uint32_t Bs = DIAG ? As : As + St::F * 4;
         const uint32_t ab = As + (uint32_t)aoff[g] * 4, bb = Bs + (uint32_t)boff[g] * 4;
-        if constexpr (NB == 4) {
-            switch (q) {
-                case 0: f.a[0] = ds_read16<0>(ab); f.b[0] = ds_read16<0>(bb); break;
-                case 1: f.a[1] = ds_read16<L::XSTRIDE>(ab); f.b[1] = ds_read16<L::XSTRIDE>(bb); break;
-                case 2: f.a[2] = ds_read16<2 * L::XSTRIDE>(ab); f.b[2] = ds_read16<2 * L::XSTRIDE>(bb); break;
-                default: f.a[3] = ds_read16<3 * L::XSTRIDE>(ab); f.b[3] = ds_read16<3 * L::XSTRIDE>(bb); break;
-            }
-        } else {
-            switch (q) {
-                case 0: f.a[0] = ds_read16<0>(ab); break;
-                case 1: f.b[0] = ds_read16<0>(bb); break;
-                case 2: f.a[1] = ds_read16<L::XSTRIDE>(ab); break;
-                default: f.b[1] = ds_read16<L::XSTRIDE>(bb); break;
-            }
+        switch (q) {
+            case 0: f.a[0] = ds_read16<0>(ab); break;
+            case 1: f.b[0] = ds_read16<0>(bb); break;
+            case 2: f.a[1] = ds_read16<L::XSTRIDE>(ab); break;
+            default: f.b[1] = ds_read16<L::XSTRIDE>(bb); break;
         }
     };
-    auto issue_q = [&](int64_t t, int q) {  // pieces q, q + 4, ... of the tile's G
-        if (abl & 1) return;
-        float *base = lds + (int)(t % NST) * 2 * St::F + wave * St::PW * 256;
-        const int64_t k0 = kb + t * BK;
-#pragma unroll
-        for (int j = q; j < G; j += 4) {
-            if (j < St::PW) dma16(srcA[j] + k0, base + j * 256);
-            else dma16(srcB[j - St::PW] + k0, base + St::F + (j - St::PW) * 256);
-        }
+    // every read issued so far has landed; f's registers are redefined here (nothing reads them earlier)
+    auto lgkm_done = [&](Frag &f) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.b[0]), "+v"(f.b[1])::"memory");
     };
-    auto mfma_q = [&](const Frag &f, int s) {
+    auto mfma_q = [&](const Frag &f, int s) {  // k-step s of the group: the 2 x 2 blocks
         if constexpr (LIVE) {
 #pragma unroll
             for (int x = 0; x < NB; ++x)
@@ -295,99 +206,50 @@ __device__ __forceinline__ void kloop(float *lds, const float *const *srcA, cons
                 for (int y = 0; y < NB; ++y) c[x][y] = L::mfma(f.a[x][s], f.b[y][s], c[x][y]);
         }
     };
-    auto step_il = [&](int64_t t, int g, const Frag &cur, Frag &nxt) {
+    if (nk <= 0) return;
+#pragma unroll
+    for (int t = 0; t < D; ++t)
+        if (t < nk) issue(t, -1);
+    retire(D - 1 < nk - 1 ? D - 1 : nk - 1);
+    if (D < nk) issue(D, -1);
+    // One step = the MFMAs of fragment group g of k-tile t in four chunks (one k-step each); ahead of chunk q
+    // go read q of the NEXT group's fragments (so the last read still has 4 MFMAs behind it), after it a
+    // quarter of the boundary's DMA pieces.  The two fragment sets alternate by name (no register copies).
+    // Boundary t -> t + 1 (g = 1): k-tiles up to min(t + D, nk - 1) are issued; the DMA refills the stage of
+    // tile t - 1, which every wave has consumed before this barrier.
+    auto step = [&](int64_t t, int g, const Frag &cur, Frag &nxt) {
         const bool boundary = g + 1 == GG;
         const int64_t tn = boundary ? t + 1 : t;
         const int gn = boundary ? 0 : g + 1;
         const bool dma = boundary && t + 1 + D < nk;
         if (boundary) retire((t + D < nk - 1 ? t + D : nk - 1) - (t + 1));
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-        if constexpr (IL == 1) {  // chunk q: MFMAs, then a quarter of the reads and of the DMA
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                __builtin_amdgcn_sched_barrier(0);
-                mfma_q(cur, q);
-                __builtin_amdgcn_sched_barrier(0);
-                read_q(tn, gn, q, nxt);
-                if (dma) issue_q(t + 1 + D, q);
-            }
-        } else if constexpr (IL == 2) {  // reads ahead of each chunk's MFMAs: the last read has 4 MFMAs behind it
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                __builtin_amdgcn_sched_barrier(0);
-                read_q(tn, gn, q, nxt);
-                __builtin_amdgcn_sched_barrier(0);
-                mfma_q(cur, q);
-                __builtin_amdgcn_sched_barrier(0);
-                if (dma) issue_q(t + 1 + D, q);
-            }
-        } else {  // all reads in the first two chunks, the DMA in the last two
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                __builtin_amdgcn_sched_barrier(0);
-                if (q < 2) {
-                    read_q(tn, gn, 2 * q, nxt);
-                    read_q(tn, gn, 2 * q + 1, nxt);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                mfma_q(cur, q);
-                __builtin_amdgcn_sched_barrier(0);
-                if (dma && q >= 2) {
-                    issue_q(t + 1 + D, 2 * (q - 2));
-                    issue_q(t + 1 + D, 2 * (q - 2) + 1);
-                }
-            }
+        for (int q = 0; q < 4; ++q) {
+            __builtin_amdgcn_sched_barrier(0);
+            read_q(tn, gn, q, nxt);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_q(cur, q);
+            __builtin_amdgcn_sched_barrier(0);
+            if (dma) issue(t + 1 + D, q);
         }
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         lgkm_done(nxt);
     };
-    auto step = [&](int64_t t, int g, const Frag &cur, Frag &nxt) {
-        if constexpr (IL != 0) {
-            step_il(t, g, cur, nxt);
-            return;
-        }
-        if (g + 1 < GG) {
-            nxt = read(t, g + 1);
-        } else {
-            // boundary t -> t + 1: k-tiles up to min(t + D, nk - 1) are issued
-            retire((t + D < nk - 1 ? t + D : nk - 1) - (t + 1));
-            nxt = read(t + 1, 0);
-            if (t + 1 + D < nk) issue(t + 1 + D);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // (the next fragments' reads go out before these MFMAs)
-        mfma(cur);
-        __builtin_amdgcn_sched_barrier(0);
-        lgkm_done(nxt);  // (landed during the MFMAs)
-    };
-    auto last = [&](const Frag &cur) {  // the last step: no reads after it
-        __builtin_amdgcn_sched_barrier(0);
-        mfma(cur);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    Frag fa = read(0, 0), fb;
+    Frag fa, fb;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) read_q(0, 0, q, fa);
     lgkm_done(fa);
-    fixed = fa;
-    if constexpr (GG == 2) {
-        for (int64_t t = 0; t + 1 < nk; ++t) {
-            step(t, 0, fa, fb);
-            step(t, 1, fb, fa);
-        }
-        step(nk - 1, 0, fa, fb);  // (g = 0 of the last k-tile reads g = 1: no boundary)
-        last(fb);
-    } else {
-        int64_t t = 0;
-        for (; t + 2 < nk; t += 2) {
-            step(t, 0, fa, fb);
-            step(t + 1, 0, fb, fa);
-        }
-        if (t + 1 < nk) {
-            step(t, 0, fa, fb);
-            last(fb);
-        } else {
-            last(fa);
-        }
+    for (int64_t t = 0; t + 1 < nk; ++t) {
+        step(t, 0, fa, fb);
+        step(t, 1, fb, fa);
     }
+    step(nk - 1, 0, fa, fb);  // (g = 0 of the last k-tile reads g = 1: no boundary)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // the last step: no reads after it
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_q(fb, q);
+    }
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // Writes the wave's 64 x 64 quarter (rows r0.., cols c0.. of K) to K[row][col] and, mirrored,
@@ -414,7 +276,7 @@ __device__ __forceinline__ void write_quarter(const DenseArgs &a,
         } else if (!diag && row + 3 < n) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) K[(row + s) * ldk + col] = v[s];
-            if (!(a.abl & 8)) *reinterpret_cast<f32x4v *>(K + col * ldk + row) = v;  // the mirrored entries
+            *reinterpret_cast<f32x4v *>(K + col * ldk + row) = v;  // the mirrored entries
         } else {
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
@@ -435,7 +297,7 @@ struct Quarter {
     bool diag, below;
 };
 
-template <int MF, int BK, int NST, int XABL, bool PRIO, int IL>
+template <int MF, int BK, int NST>
 __device__ __forceinline__ Quarter tile_compute(const DenseArgs &a, float *lds, int64_t tile, int64_t kb, int64_t ke,
                                                 int wave, int lane,
                                                 typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK]
@@ -475,11 +337,11 @@ __device__ __forceinline__ Quarter tile_compute(const DenseArgs &a, float *lds, 
 #pragma unroll
         for (int y = 0; y < NB; ++y) c[x][y] = typename L::acc_t{};
     if (diag) {
-        if (live) kloop<MF, BK, NST, true, true, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
-        else kloop<MF, BK, NST, true, false, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
+        if (live) kloop<MF, BK, NST, true, true>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c);
+        else kloop<MF, BK, NST, true, false>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c);
     } else {
-        if (live) kloop<MF, BK, NST, false, true, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
-        else kloop<MF, BK, NST, false, false, XABL, PRIO, IL>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c, a.abl);
+        if (live) kloop<MF, BK, NST, false, true>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c);
+        else kloop<MF, BK, NST, false, false>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c);
     }
     return q;
 }
@@ -538,7 +400,7 @@ __device__ __forceinline__ void tile_write(const DenseArgs &a,
 }
 
 // One work item per workgroup: a whole tile, or a k-slice of one of the split tiles.
-template <int MF, int BK, int NST, int WPE, int XABL = 0, bool PRIO = false, int IL = 0>
+template <int MF, int BK, int NST, int WPE>
 __global__ __launch_bounds__(256, WPE) void gram_dense_mfma_kernel(DenseArgs a) {
     using L = Layout<MF, BK>;
     using St = Stage<BK>;
@@ -558,7 +420,7 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_mfma_kernel(DenseArgs a) 
     const int64_t kb = pieces > 1 ? slice * a.k_split : 0;
     const int64_t ke = pieces > 1 ? (kb + a.k_split < a.kpad ? kb + a.k_split : a.kpad) : a.kpad;
     typename L::acc_t c[NB][NB];
-    const Quarter q = tile_compute<MF, BK, NST, XABL, PRIO, IL>(a, lds, tile, kb, ke, wave, lane, c);
+    const Quarter q = tile_compute<MF, BK, NST>(a, lds, tile, kb, ke, wave, lane, c);
     if (pieces > 1) {
         const int64_t u = tile - a.n_whole;
         if (!split_combine<MF, BK>(a, c, a.tickets + u, pieces, slice, [&](int64_t s) { return u * pieces + s; },
@@ -575,7 +437,7 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_mfma_kernel(DenseArgs a) 
 // segment (j >= 1) -- slab 2 slot -- or, for j = 0, slot s0's last segment (slab 2 s0 + 1) unless the tile
 // starts exactly at s0's start (slab 2 s0).  Each slot has at most one first and one last segment, so the
 // slabs and the tickets (indexed by piece 0's slab) are private to one tile per launch.
-template <int MF, int BK, int NST, int WPE, int IL>
+template <int MF, int BK, int NST, int WPE>
 __global__ __launch_bounds__(256, WPE) void gram_dense_sk_kernel(DenseArgs a) {
     using L = Layout<MF, BK>;
     using St = Stage<BK>;
@@ -592,7 +454,7 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_sk_kernel(DenseArgs a) {
         __syncthreads();  // (the previous segment's ring reads and hand-off flag are done)
         typename L::acc_t c[NB][NB];
         const Quarter q =
-            tile_compute<MF, BK, NST, 0, false, IL>(a, lds, tile, (u - tb) * BK, (se - tb) * BK, wave, lane, c);
+            tile_compute<MF, BK, NST>(a, lds, tile, (u - tb) * BK, (se - tb) * BK, wave, lane, c);
         bool write = true;
         if (u != tb || se != te) {
             const int64_t s0 = tb / U, s1 = (te - 1) / U;
@@ -700,37 +562,34 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
     GRF_REQUIRE(upper_only || (ldk % 4 == 0 && ((uintptr_t)K & 15) == 0), GRF_EINVAL,
                 "grf_gram_dense: ldk must be a multiple of 4 and K 16-byte aligned");
     if (n == 0) return GRF_OK;
-    static const int variant = env_int("GRF_DENSE_VARIANT", 0);
-    const int BK = variant / 100 % 100 == 32 ? 32 : 16;
+    constexpr int BK = 16;
     DensePlan p = dense_plan(n, k_dim, BK);
     GRF_REQUIRE(p.kpad <= lda, GRF_EINVAL, "grf_gram_dense: lda must cover k_dim rounded up to %d", BK);
+    DenseArgs a{};
+    a.A = A;
+    a.K = K;
+    a.n = n;
+    a.nt = p.nt;
+    a.lda = lda;
+    a.ldk = ldk;
+    a.kpad = p.kpad;
+    a.upper_only = upper_only ? 1 : 0;
+    hipStream_t st = S(stream);
     // stream-K when the tiles fill at least half the slots (every slot then takes >= half a tile of k, so a
     // split tile has <= 3 pieces): n = 4096 0.68 -> 0.78, C2 0.83 -> 0.86 of the MFMA peak; at C3 (253 tiles)
     // even, below it the per-tile splits win (profiles/r04_dense_ab.txt).  GRF_DENSE_SK: 0 never, 1 always.
     static const int sk_env = env_int("GRF_DENSE_SK", -1);
     const bool sk = sk_env == 1 || (sk_env != 0 && p.tiles >= kCUs);
-    if (sk && BK == 16) {
+    if (sk) {
         const SkPlan q = sk_plan(n, k_dim, BK);
         if (workspace && workspace_bytes >= q.ws_bytes && ((uintptr_t)workspace & 255) == 0) {
             GRF_REQUIRE_GRID(q.grid, 256, "gram_dense_sk_kernel");
-            DenseArgs a{};
-            a.A = A;
-            a.K = K;
             a.tickets = reinterpret_cast<int32_t *>(workspace);
             a.slabs = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes);
-            a.n = n;
-            a.nt = p.nt;
-            a.lda = lda;
-            a.ldk = ldk;
-            a.kpad = p.kpad;
-            a.upper_only = upper_only ? 1 : 0;
             a.sk_units = q.units;
             a.sk_kt = q.kt;
             a.sk_total = q.total;
-            hipStream_t st = S(stream);
-            static const int il_sk = env_int("GRF_DENSE_IL", 2);
-            if (il_sk == 1) gram_dense_sk_kernel<32, 16, 4, 2, 1><<<(unsigned)q.grid, 256, 0, st>>>(a);
-            else gram_dense_sk_kernel<32, 16, 4, 2, 2><<<(unsigned)q.grid, 256, 0, st>>>(a);
+            gram_dense_sk_kernel<32, BK, 4, 2><<<(unsigned)q.grid, 256, 0, st>>>(a);
             GRF_CHECK_LAUNCH("gram_dense_sk_kernel");
             return GRF_OK;
         }
@@ -744,42 +603,12 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
     const int64_t split_tiles = p.tiles - p.n_whole;
     const int64_t items = p.n_whole + split_tiles * p.n_split;
     GRF_REQUIRE_GRID(items, 256, "gram_dense_mfma_kernel");
-    DenseArgs a{};
-    a.A = A;
-    a.K = K;
     a.tickets = split_tiles > 0 ? reinterpret_cast<int32_t *>(workspace) : nullptr;
     a.slabs = split_tiles > 0 ? reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes) : nullptr;
-    a.n = n;
-    a.nt = p.nt;
-    a.lda = lda;
-    a.ldk = ldk;
-    a.kpad = p.kpad;
     a.n_whole = p.n_whole;
     a.k_split = p.k_split;
     a.n_split = p.n_split;
-    a.upper_only = upper_only ? 1 : 0;
-    static const int abl = env_int("GRF_DENSE_ABL", 0);
-    a.abl = abl;
-    const unsigned grid = (unsigned)items;
-    hipStream_t st = S(stream);
-    static const bool prio = env_int("GRF_DENSE_PRIO", 0) == 1;
-    static const int il = env_int("GRF_DENSE_IL", 2);
-    switch ((variant ? variant : 321642) + (prio ? 1000000 : 0) + il * 2000000) {  // A/B (GRF_DENSE_VARIANT): MF * 10000 + BK * 100 + stages * 10 + waves per SIMD
-        case 321642: gram_dense_mfma_kernel<32, 16, 4, 2><<<grid, 256, 0, st>>>(a); break;
-        case 321652: gram_dense_mfma_kernel<32, 16, 5, 2><<<grid, 256, 0, st>>>(a); break;
-        case 161652: gram_dense_mfma_kernel<16, 16, 5, 2><<<grid, 256, 0, st>>>(a); break;
-        case 1321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, true><<<grid, 256, 0, st>>>(a); break;
-        case 1161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, true><<<grid, 256, 0, st>>>(a); break;
-        case 2161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, false, 1><<<grid, 256, 0, st>>>(a); break;
-        case 2321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 1><<<grid, 256, 0, st>>>(a); break;
-        case 3161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, true, 1><<<grid, 256, 0, st>>>(a); break;
-        case 3321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, true, 1><<<grid, 256, 0, st>>>(a); break;
-        case 4321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 2><<<grid, 256, 0, st>>>(a); break;
-        case 6321642: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 3><<<grid, 256, 0, st>>>(a); break;
-        case 4161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, false, 2><<<grid, 256, 0, st>>>(a); break;
-        case 6161642: gram_dense_mfma_kernel<16, 16, 4, 2, 0, false, 3><<<grid, 256, 0, st>>>(a); break;
-        default: gram_dense_mfma_kernel<32, 16, 4, 2, 0, false, 2><<<grid, 256, 0, st>>>(a); break;
-    }
+    gram_dense_mfma_kernel<32, BK, 4, 2><<<(unsigned)items, 256, 0, st>>>(a);
     GRF_CHECK_LAUNCH("gram_dense_mfma_kernel");
     return GRF_OK;
 }

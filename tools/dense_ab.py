@@ -1,7 +1,7 @@
 """Dense MFMA Gram A/B harness: time grf_gram_dense_ws (HIP events, `reps` launches back to back) at
 several n on random sparse-ish fp32 operands, check it against fp64 (|dK| <= 1e-5 (|A||A|^T)), exact
 symmetry and run-to-run bit identity, and print one JSON line per n.  Knobs are the library's env
-variables (GRF_DENSE_*), read once per process: run one process per arm.
+variables (GRF_DENSE_SK, GRF_DENSE_SPLIT, GRF_DENSE_TAIL), read once per process: run one process per arm.
 usage: python tools/dense_ab.py [--label L] [--zeros-frac F] n [n ...]"""
 import argparse
 import hashlib
