@@ -596,12 +596,20 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
     };
     for (int i = tid; i < nbk_r * kS; i += 256) lcur[i] = 0u;
     __syncthreads();
-    // pass 1: the region's bucket (and sub-band) counts
+    // pass 1: the region's bucket (and sub-band) counts (four loads in flight per thread)
     for (int64_t w = w0 + tid; w < w1; w += 256) {
         const int32_t *trow = tab + w * (nreg + 1);
         const int32_t o0 = trow[g], o1 = trow[g + 1];
         const uint2 *run = staging + ptr[w * kBinRows];
-        for (int32_t o = o0; o < o1; ++o) atomicAdd(&lcur[slot(run[o].x)], 1u);
+        int32_t o = o0;
+        for (; o + 4 <= o1; o += 4) {
+            uint32_t x[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[r] = run[o + r].x;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomicAdd(&lcur[slot(x[r])], 1u);
+        }
+        for (; o < o1; ++o) atomicAdd(&lcur[slot(run[o].x)], 1u);
     }
     __syncthreads();
     auto bucket_count = [&](int i) -> uint32_t {
@@ -645,6 +653,51 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
     __syncthreads();
     const int64_t img = (int64_t)total * unit;
     if (img == 0) return;
+    if (!lds && !kSplit) {
+        // oversized region (hub columns: 12 % of Enron's regions exceed the LDS image cap, up to ~500 KB):
+        // the bucket cursors stay in LDS and every record is stored straight to its place in t_rec --
+        // one global atomic per entry in a dependent chain per thread took ~1 ms per launch on Enron
+        for (int i = tid; i < nbk_r; i += 256) {  // the odd buckets' padding record (0, +0.0)
+            const uint32_t c = lcur[i];
+            if (c & 1) {
+                unsigned char *pair = t_rec + (U0 * unit + lline[i]) + (int64_t)kPairBytes * (c >> 1);
+                reinterpret_cast<uint16_t *>(pair)[1] = 0;
+                reinterpret_cast<float *>(pair + 4)[1] = 0.f;
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < nbk_r; i += 256) lcur[i] = 0u;
+        __syncthreads();
+        unsigned char *region = t_rec + U0 * unit;
+        for (int64_t w = w0 + tid; w < w1; w += 256) {
+            const int32_t *trow = tab + w * (nreg + 1);
+            const int32_t o0 = trow[g], o1 = trow[g + 1];
+            const uint2 *run = staging + ptr[w * kBinRows];
+            int32_t o = o0;
+            for (; o + 4 <= o1; o += 4) {  // (four loads in flight per thread)
+                uint2 x[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[r] = run[o + r];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t kk = x[r].x >> 16;
+                    const uint32_t sl = atomicAdd(&lcur[kk], 1u);
+                    unsigned char *pair = region + lline[kk] + kPairBytes * (sl >> 1);
+                    reinterpret_cast<uint16_t *>(pair)[sl & 1] = (uint16_t)(x[r].x & 0xffffu);
+                    reinterpret_cast<uint32_t *>(pair + 4)[sl & 1] = x[r].y;
+                }
+            }
+            for (; o < o1; ++o) {
+                const uint2 x = run[o];
+                const uint32_t kk = x.x >> 16;
+                const uint32_t sl = atomicAdd(&lcur[kk], 1u);
+                unsigned char *pair = region + lline[kk] + kPairBytes * (sl >> 1);
+                reinterpret_cast<uint16_t *>(pair)[sl & 1] = (uint16_t)(x.x & 0xffffu);
+                reinterpret_cast<uint32_t *>(pair + 4)[sl & 1] = x.y;
+            }
+        }
+        return;
+    }
     if (lds) {
         for (int64_t i = tid; i < (img + 15) / 16; i += 256) reinterpret_cast<uint4 *>(image)[i] = make_uint4(0u, 0u, 0u, 0u);
     } else {  // oversized region: global cursors of its own buckets, odd buckets padded below
@@ -667,7 +720,22 @@ __global__ __launch_bounds__(256) void tr_place_self_kernel(int64_t n_rows, int6
         const int32_t *trow = tab + w * (nreg + 1);
         const int32_t o0 = trow[g], o1 = trow[g + 1];
         const uint2 *run = staging + ptr[w * kBinRows];
-        for (int32_t o = o0; o < o1; ++o) {
+        int32_t o = o0;
+        if (lds) {
+            for (; o + 4 <= o1; o += 4) {  // (four loads in flight per thread)
+                uint2 x[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[r] = run[o + r];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t s = atomicAdd(&lcur[slot(x[r].x)], 1u);
+                    unsigned char *pair = image + lline[x[r].x >> 16] + kPairBytes * (s >> 1);
+                    reinterpret_cast<uint16_t *>(pair)[s & 1] = (uint16_t)(x[r].x & 0xffffu);
+                    reinterpret_cast<uint32_t *>(pair + 4)[s & 1] = x[r].y;
+                }
+            }
+        }
+        for (; o < o1; ++o) {
             const uint2 x = run[o];
             const uint32_t kk = x.x >> 16;
             if (lds) {
