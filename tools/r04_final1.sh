@@ -3,5 +3,5 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R
-bash tools/gpu_tests.sh r04_final_tests "" 600 || exit 1
-bash tools/gpu_profile.sh r04_prof || exit 1
+bash tools/gpu_tests.sh r04_final2_tests "" 600 || exit 1
+bash tools/gpu_profile.sh r04_prof2 || exit 1
