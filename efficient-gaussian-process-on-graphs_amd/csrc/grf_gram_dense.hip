@@ -609,9 +609,10 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
     a.k_split = p.k_split;
     a.n_split = p.n_split;
     // the hub panel (upper_only, k of a few k-tiles): each tile is a short k-loop then a 64 KB write, so a
-    // third workgroup per CU (3-stage ring, 48 KB) overlaps one tile's stores with the others' MFMAs.
-    // GRF_DENSE_HUB_NST: 3 or 4 (the ring of the other launches).
-    static const int hub_nst = env_int("GRF_DENSE_HUB_NST", 4);
+    // third workgroup per CU (3-stage ring, 48 KB) overlaps one tile's stores with the others' MFMAs: Enron's
+    // panel 1.67 -> 1.49 ms, step 7.84-7.87 -> 7.62-7.71 ms (profiles/r04_hub_ring_ab.txt).
+    // GRF_DENSE_HUB_NST: 3 (default) or 4 (the ring of the other launches).
+    static const int hub_nst = env_int("GRF_DENSE_HUB_NST", 3);
     if (upper_only && split_tiles == 0 && hub_nst == 3) {
         gram_dense_mfma_kernel<32, BK, 3, 3><<<(unsigned)items, 256, 0, st>>>(a);
         GRF_CHECK_LAUNCH("gram_dense_mfma_kernel");

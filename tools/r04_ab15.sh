@@ -17,6 +17,12 @@ for g in enron facebook; do
   done
 done
 export GRF_DENSE_HUB_NST=3
+for h in 128 160; do  # (a faster panel may pay for more hub columns)
+  timeout -k 10 240 python3 $R/bench.py --graph enron --hubs $h --steps 10 --warmup 2 --no-cpu-baseline --no-mfma-leg \
+      > $O/enron_nst3_h$h.json 2> $O/enron_nst3_h$h.err || { echo "hubs $h failed"; tail $O/enron_nst3_h$h.err; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'])" \
+      $O/enron_nst3_h$h.json "enron nst=3 hubs=$h"
+done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
     python3 $R/bench.py --graph enron --steps 10 --warmup 2 --no-cpu-baseline --no-mfma-leg > $O/trace.log 2>&1 || { echo "trace failed"; tail $O/trace.log; exit 1; }
 echo trace ok
