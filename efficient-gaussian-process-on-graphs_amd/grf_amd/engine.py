@@ -780,13 +780,21 @@ class GRFEngine:
         ldk = self.leading_dim(n)
         out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
         # split-K partial tiles (small n, or the last tiles of a large n) and their tickets: a cached
-        # workspace, zeroed once (the kernel leaves the tickets zero after every launch)
+        # workspace per stream, ZEROED when allocated (the kernel leaves the tickets zero after every
+        # launch; an uninitialised block gave round 4's NaN, profiles/AB_LOG.md "dense-Gram NaN"), dropped
+        # after a failed call so that no ticket a broken launch may have left is read again
         need = int(self.lib.grf_gram_dense_workspace_bytes(n, k_dim))
-        ws = getattr(self, "_dense_ws", None)
+        stream = self.stream
+        cache = self.__dict__.setdefault("_dense_ws", {})
+        ws = cache.get(stream.value)
         if ws is None or ws.numel() < need:
-            ws = self._dense_ws = torch.zeros(max(need, 16), dtype=torch.uint8, device=self.device)
-        C.check(self.lib.grf_gram_dense_ws(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, _p(ws),
-                                           ws.numel(), self.stream), "grf_gram_dense_ws")
+            ws = cache[stream.value] = torch.zeros(max(need, 16), dtype=torch.uint8, device=self.device)
+        try:
+            C.check(self.lib.grf_gram_dense_ws(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, _p(ws),
+                                               ws.numel(), stream), "grf_gram_dense_ws")
+        except Exception:
+            cache.pop(stream.value, None)
+            raise
         return out[:, :n]
 
     @staticmethod

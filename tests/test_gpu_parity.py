@@ -480,6 +480,47 @@ def test_gram_dense_workspace_reused_across_sizes(eng):
         assert np.array_equal(K, fresh) and np.isfinite(K).all()
 
 
+@pytest.mark.parametrize("n", [2708, 4500])
+def test_gram_dense_first_call_on_dirty_allocator_block(eng, n):
+    """Round 4's NaN (profiles/AB_LOG.md, "dense-Gram NaN"): the split-K tickets live in the caller's
+    workspace and must be zero on first use; the engine once took it uninitialised from the caching
+    allocator, whose block had held other data.  Here the allocator's free block is filled with 0xFF
+    (every ticket -1) before a FRESH engine's first call at n = 2708 (the per-tile split: 253 tiles x
+    2 pieces) and n = 4500 (stream-K): K must be finite, exactly symmetric and within the fp64 bound,
+    the tickets must come back zero, and a second call must repeat the bits."""
+    import torch
+    from grf_amd import _lib as C
+    from grf_amd.engine import GRFEngine
+    k = n
+    lda = -(-k // 64) * 64
+    r = np.random.default_rng(n + 3)
+    Ad = np.zeros((n, lda), np.float32)
+    Ad[:, :k] = (r.standard_normal((n, k)) * (r.random((n, k)) < 0.05)).astype(np.float32)
+    At = torch.from_numpy(Ad).to(eng.device)
+    need = int(eng.lib.grf_gram_dense_workspace_bytes(n, k))
+    assert need > 4096  # (tickets + slabs: the split path runs)
+    torch.cuda.synchronize()
+    dirty = torch.full((need + (1 << 20),), 0xFF, dtype=torch.uint8, device=eng.device)
+    torch.cuda.synchronize()
+    del dirty  # (the block stays in the caching allocator, 0xFF-filled, for the next allocation)
+    fresh = GRFEngine(eng.device)
+    K = fresh.gram_dense(At, k).cpu().numpy()
+    assert np.isfinite(K).all() and np.array_equal(K, K.T)
+    ref = Ad.astype(np.float64) @ Ad.astype(np.float64).T
+    bound = np.abs(Ad).astype(np.float64) @ np.abs(Ad).astype(np.float64).T
+    assert np.all(np.abs(K - ref) <= 1e-5 * bound + 1e-30)
+    # the cached workspace came back with every ticket zero: a second call gives the same bits
+    ws = next(iter(fresh._dense_ws.values()))
+    assert int(ws[:4096].view(torch.int32).abs().sum()) == 0
+    assert np.array_equal(fresh.gram_dense(At, k).cpu().numpy(), K)
+    # the hub panel's upper-only launch takes no workspace (whole tiles only): same upper triangle
+    Ku = torch.zeros((n, eng.leading_dim(n)), dtype=torch.float32, device=eng.device)
+    C.check(eng.lib.grf_gram_dense_upper(n, k, At.data_ptr(), lda, Ku.data_ptr(), Ku.stride(0), eng.stream),
+            "grf_gram_dense_upper")
+    Ku = np.triu(Ku[:, :n].cpu().numpy())
+    assert np.all(np.abs(Ku - np.triu(ref)) <= 1e-5 * np.triu(bound) + 1e-30)
+
+
 def test_full_pipeline_c2_scale(eng):
     """ER N=10k (C2-like) -- Philox walks vs oracle on a source sample, K rows vs oracle, symmetry."""
     n = 10000
