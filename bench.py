@@ -544,6 +544,13 @@ def main():
     ap.add_argument("--path", choices=["dense", "sparse"], default="dense",
                     help="c2: the reference's dense path (dense adjacency, MFMA Gram; default) or its sparse path "
                          "as BASELINE config 2 names it (CSR adjacency, fused walks, transpose, symmetric sparse Gram)")
+    ap.add_argument("--rank-turns", action="store_true",
+                    help="N > 1: after the timed steps, re-run each rank's K assembly alone (ranks take turns between "
+                         "barriers) and report gram_ms_alone_per_rank (the per-rank time of an unshared GPU when the "
+                         "ranks share one GPU under GRF_DIST_BACKEND=gloo)")
+    ap.add_argument("--fingerprint-dir", default=None,
+                    help="write a bit-level fingerprint of every rank's K block (tools/gram_hash.py) to "
+                         "DIR/rank<r>.json after the run (the multi-rank at-size parity test)")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
     ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
@@ -745,6 +752,16 @@ def main():
     args.overlap = ov
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
     walk_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in walk_ev]))
+    gram_alone = rank_turns_gram_ms(eng, last[0], pl, K, coll, rank, world) if args.rank_turns else None
+    if args.fingerprint_dir:
+        # bit-level fingerprint of this rank's K block (tools/gram_hash.py), for the at-size multi-rank test
+        from tools.gram_hash import fingerprint
+        torch.cuda.synchronize()
+        h, s_ = fingerprint(P.k_view(K, pl))
+        os.makedirs(args.fingerprint_dir, exist_ok=True)
+        with open(os.path.join(args.fingerprint_dir, f"rank{rank}.json"), "w") as fh:
+            json.dump({"rank": rank, "world": world, "mode": pl.mode, "shard": [b, e], "cols_sym": pl.cols_sym,
+                       "k_rows": args.k_rows, "hash": h, "sum": s_}, fh)
     coll_ms = float(np.mean([a.elapsed_time(b_) for a, b_, _, _ in gather_stats])) if gather_stats else 0.0
     coll_sent = float(np.mean([x for _, _, x, _ in gather_stats])) if gather_stats else 0.0
     coll_recv = float(np.mean([x for _, _, _, x in gather_stats])) if gather_stats else 0.0
@@ -754,7 +771,7 @@ def main():
         t, gram_avg, walk_ms = (float(x) for x in tt.tolist())
         # every rank's Gram time, collective time and volume, and parity ratio (rank order)
         mine = torch.tensor([float(np.mean(gram_ms)), coll_ms, coll_sent, coll_recv, parity["max_ratio"],
-                             float(pl.e - pl.b)], dtype=torch.float64, device=dev)
+                             float(pl.e - pl.b), gram_alone or 0.0], dtype=torch.float64, device=dev)
         allr = torch.zeros(world * mine.numel(), dtype=torch.float64, device=dev)
         allr[rank * mine.numel():(rank + 1) * mine.numel()] = mine
         dist_all_reduce(allr)
@@ -770,6 +787,12 @@ def main():
                      "gather_bytes_received_per_rank": [int(x) for x in per_rank[:, 3]],
                      "gather_note": "HIP events on the issuing stream around each step's Phi all-gather "
                                     "(the transfer + the wait for the slowest rank), mean over the timed steps"}
+        if args.rank_turns:
+            dist_info["gram_ms_alone_per_rank"] = [float(x) for x in per_rank[:, 6]]
+            dist_info["gram_alone_note"] = ("each rank's K assembly (its column / row block from the last front) "
+                                            "re-run alone on the GPU, ranks taking turns between barriers, HIP events "
+                                            "over 3 launches: the per-rank Gram time of an unshared GPU (under gloo "
+                                            "the ranks share one GPU, so gram_ms_per_rank includes the others' work)")
     else:
         gram_avg = float(np.mean(gram_ms))
         dist_info = None
@@ -908,6 +931,34 @@ def main():
         print(json.dumps(out), flush=True)
     if coll:
         dist.destroy_process_group()
+
+
+def rank_turns_gram_ms(eng, fr, pl, K, coll: bool, rank: int, world: int, reps: int = 3) -> float:
+    """This rank's K assembly (from front `fr`) timed alone: the ranks take turns between barriers, so
+    on a shared GPU (gloo rehearsal) no other rank's kernels run beside it.  The all-reduce mode's
+    collective needs every rank and is not re-run (0).  HIP events on this rank's stream."""
+    import torch
+    import torch.distributed as dist
+
+    from grf_amd import pipeline as P
+
+    ms = 0.0
+    for turn in range(world):
+        if coll:
+            dist.barrier()
+        if turn == rank and pl.mode != "allreduce":
+            P.k_assembly(eng, fr, pl, K)  # (warm)
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            for _ in range(reps):
+                P.k_assembly(eng, fr, pl, K)
+            ev[1].record()
+            ev[1].synchronize()
+            ms = ev[0].elapsed_time(ev[1]) / reps
+        torch.cuda.synchronize()
+    if coll:
+        dist.barrier()
+    return ms
 
 
 def time_transfers(A, K, pl, dev, ms_per_step: float, reps: int = 3) -> dict:

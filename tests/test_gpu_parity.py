@@ -1160,6 +1160,101 @@ def test_bench_line_n2_reports_parity_and_collectives_gloo(mode, world):
     assert line["parity"]["ok"] and line["parity"]["max_ratio"] <= 1.0 and len(line["parity"]["per_rank"]) == world
 
 
+_C4_REF_PRINTS = {}  # (b, e, cols_sym) -> fingerprint of the one-GPU K's columns [b, e)
+
+
+def _c4_reference_prints(eng, worlds=(2, 4, 8)):
+    """Fingerprints (tools/gram_hash.py) of the one-GPU K's column blocks K[:, R_r] for every rank of the
+    given world sizes at the headline size (C4: ER N = 100k, 1M edges, m = 128, L = 8, p = 0.1, Philox
+    seed 42).  The one-GPU K is the row-mode Gram of the setup walk's Phi (every entry from its own row,
+    as a rank's column block computes it; the block's own square symmetrised from its upper triangle
+    when the bench does, 4 |R_r| >= n).  Computed once per session (40 GB of K), then freed."""
+    import torch
+    from grf_amd.dist import setup_phi, shard_range
+    from grf_amd.engine import DeviceCSR
+    from grf_amd.graphs import er_graph_exact_edges
+    from tools.gram_hash import fingerprint
+    import bench
+    if _C4_REF_PRINTS:
+        return _C4_REF_PRINTS
+    n, m, L, p = 100_000, 128, 8, 0.1
+    A = DeviceCSR.from_scipy(er_graph_exact_edges(n, 1_000_000, seed=0), eng.device)
+    phi = setup_phi(eng, A, m, p, L, bench.diffusion_modulator(L, 1.0), seed=42)
+    K = eng.gram_sparse(phi, eng.transpose_banded(phi, 8192))
+    del phi, A
+    for w in worlds:
+        for r in range(w):
+            b, e = shard_range(n, r, w)
+            sym = 4 * (e - b) >= n
+            if (b, e, sym) in _C4_REF_PRINTS:
+                continue
+            blk = K[:, b:e].clone()
+            if sym:
+                sq = blk[b:e].clone()
+                blk[b:e] = torch.triu(sq) + torch.triu(sq, 1).T
+                del sq
+            _C4_REF_PRINTS[(b, e, sym)] = fingerprint(blk)
+            del blk
+    del K
+    torch.cuda.empty_cache()
+    return _C4_REF_PRINTS
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_cols_at_headline_size_gloo(eng, world):
+    """the N > 1 column-block step at the HEADLINE size (C4: N = 100k, 1M edges,
+    m = 128), `world` gloo ranks sharing the one GPU: bench.py --gpus W under torch.distributed.run
+    (the real 43.5 M-entry Phi all-gather with its exact bound, 100k / W-column blocks and their band
+    widths; world 8 without the mirrored own square).  Every rank's K[:, R_r] must be bit-identical to
+    the same columns of the one-GPU K (fingerprints, tools/gram_hash.py), the in-run K check passes,
+    and the line reports every rank's Gram time re-run alone (--rank-turns).  GRF_TEST_OUT=<dir> keeps
+    the line (profiles/r05_bench_gloo_n<W>.json)."""
+    import json
+    import os
+    import shutil
+    import socket
+    import subprocess
+    import sys
+    import tempfile
+    from grf_amd.dist import shard_range
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    fp_dir = tempfile.mkdtemp(prefix="grf_fp_")
+    try:
+        env = dict(os.environ, GRF_DIST_BACKEND="gloo")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+               "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--rank-turns",
+               "--fingerprint-dir", fp_dir]
+        r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=800)
+        assert r.returncode == 0, r.stderr[-3000:]
+        line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+        out_dir = os.environ.get("GRF_TEST_OUT")
+        if out_dir:
+            os.makedirs(out_dir, exist_ok=True)
+            with open(os.path.join(out_dir, f"r05_bench_gloo_n{world}.json"), "w") as fh:
+                fh.write(json.dumps(line) + "\n")
+        d = line["distributed"]
+        assert line["n_gpus"] == world and d["backend"] == "gloo" and d["world_size"] == world
+        assert line["config"]["n_nodes"] == 100_000 and line["config"]["walks_per_node"] == 128
+        assert line["parity"]["ok"] and len(line["parity"]["per_rank"]) == world
+        assert all(x > 0 for x in d["gram_ms_alone_per_rank"]) and all(x > 0 for x in d["gather_bytes_sent_per_rank"])
+        prints = [json.load(open(os.path.join(fp_dir, f"rank{q}.json"))) for q in range(world)]
+    finally:
+        shutil.rmtree(fp_dir, ignore_errors=True)
+    ref = _c4_reference_prints(eng)
+    for q, fp in enumerate(prints):
+        b, e = shard_range(100_000, q, world)
+        assert fp["mode"] == "cols" and fp["shard"] == [b, e] and fp["cols_sym"] == (4 * (e - b) >= 100_000)
+        h, sm = ref[(b, e, fp["cols_sym"])]
+        assert fp["hash"] == h, f"rank {q} of {world}: K block bits differ from the one-GPU K"
+        assert abs(fp["sum"] - sm) <= 1e-12 * abs(sm), (q, fp["sum"], sm)
+
+
 @pytest.mark.parametrize("mode", ["cols", "rows", "allreduce"])
 def test_bench_multi_gpu_path_on_rccl_one_rank(mode):
     """The N > 1 bench step on RCCL itself (backend "nccl"), one rank on the one-GPU box
