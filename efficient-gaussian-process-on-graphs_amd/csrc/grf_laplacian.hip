@@ -457,13 +457,27 @@ __global__ __launch_bounds__(256) void lap_row_group_kernel(int64_t n, const int
 }
 
 // ------------------------------------------------------------------- dense
-// Dense rows all have the same length n, so numpy's pairwise recursion over a row has the same
-// leaves and the same combining order for every row: the host lists them once (PwPlan, a kernel
-// argument) and the kernel sums leaf l with the 8 lanes of group l % 8 (lane j owns numpy's
-// accumulator r_j: a[j], a[j + 8], ... -- 64 contiguous bytes per group and load), folds the 8
-// accumulators in numpy's order ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), adds the leaf's
-// tail, and lane 0 combines the leaf sums with the recorded post-order program.  Bit-identical to
-// wave_np_pairwise (lane-0 leaf listing, one lane per leaf walking 128 strided loads).
+// Two launches, one HBM read of W (was three full passes: degrees, counts, fill).
+//
+//  lapd_stage_kernel -- one wave per row, 16-B loads with 8 per lane in flight: the degree (numpy's
+//    pairwise sum: rows of integer values take the exact strided sum, any other row the recursion's
+//    plan below), D^-1/2, and the row's structural nonzeros (w != 0) in column order, the first
+//    kLapdCap of them staged as (column, w) pairs.  It also zeroes the next launch's look-back words.
+//  lapd_emit_kernel -- one wave per row in ticket order: the Laplacian row's nonzeros from the staged
+//    pairs and the diagonal (a row with more than kLapdCap structural nonzeros re-reads W), its count
+//    published for a decoupled look-back (CUB-style: each wave sums its predecessors' aggregates until
+//    an inclusive prefix), so the row pointer and the CSR come out of the one launch with no scan pass.
+//    Waves take rows by an atomic ticket, so every predecessor a wave waits on is already running.
+//
+// Values: lapd_value below, the reference's elementwise arithmetic; an entry with w = 0 off the
+// diagonal is exactly zero in every mode (D^-1/2 is finite), so only the structural nonzeros and the
+// diagonal can be stored -- the CSR is the np.flatnonzero order of the dense L (sampler.py:22-28).
+constexpr int kLapdCap = 127;  // staged structural nonzeros per row (+ the diagonal: two 64-lane rounds)
+
+// numpy's pairwise sum of a dense row, leaves and combine order from the host-built plan (all rows
+// have the same length): the 8 lanes of group l % 8 sum leaf l with numpy's accumulators r_j = a[j],
+// a[j + 8], ..., folded ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) plus the leaf's tail; lane 0
+// combines the leaf sums with the recorded post-order program.  Every lane returns the sum.
 constexpr int kPwPlanLeaves = 64;  // rows of up to 64 leaves: n <= 8192
 struct PwPlan {
     int32_t nl;                      // leaves
@@ -476,8 +490,7 @@ struct PwPlan {
 static bool pw_plan_build(int64_t n, PwPlan &p) {
     p.nl = 0;
     p.nprog = 0;
-    if (n <= 128) return false;  // (one leaf: the plain per-row path)
-    // the recursion of pairwise_sum: leaves in order, then the post-order combine program
+    if (n <= 128) return false;  // (one leaf: wave_np_pairwise's own path)
     struct F { int64_t o, m; int state; };
     F st[64];
     int sp = 0;
@@ -511,13 +524,8 @@ static bool pw_plan_build(int64_t n, PwPlan &p) {
     return true;
 }
 
-__global__ __launch_bounds__(256) void lapd_deg_plan_kernel(int64_t n, const double *W, int32_t mode, PwPlan plan,
-                                                            double *deg, double *dinv) {
-    __shared__ double sums[4][kPwPlanLeaves];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
-    const int64_t i = (int64_t)blockIdx.x * 4 + wave;  // one wave per row
-    if (i >= n) return;
-    const double *a = W + i * n;
+__device__ double plan_row_sum(const double *a, const PwPlan &plan, double *sums, int lane) {
+    const int g = lane >> 3, j = lane & 7;
     for (int l0 = 0; l0 < plan.nl; l0 += 8) {
         const int l = l0 + g;
         double r = 0.0;
@@ -529,49 +537,35 @@ __global__ __launch_bounds__(256) void lapd_deg_plan_kernel(int64_t n, const dou
             r = a[off + j];
             for (int32_t q = 8 + j; q < nb; q += 8) r += a[off + q];
         }
-        // numpy's fold of the 8 accumulators, then the leaf's tail in order
         const double r1 = __shfl_xor(r, 1, 64);
-        const double p01 = (j & 1) ? r1 + r : r + r1;                  // (r0 + r1), (r2 + r3), ...
+        const double p01 = (j & 1) ? r1 + r : r + r1;       // (r0 + r1), (r2 + r3), ...
         const double p23 = __shfl_xor(p01, 2, 64);
-        const double q = (j & 2) ? p23 + p01 : p01 + p23;             // ((r0 + r1) + (r2 + r3)), ...
+        const double q = (j & 2) ? p23 + p01 : p01 + p23;  // ((r0 + r1) + (r2 + r3)), ...
         const double q4 = __shfl_xor(q, 4, 64);
         double res = (j & 4) ? q4 + q : q + q4;
         if (j == 0 && l < plan.nl) {
             for (int32_t t = nb; t < len; ++t) res += a[off + t];
-            sums[wave][l] = res;
+            sums[l] = res;
         }
     }
     __builtin_amdgcn_wave_barrier();
+    double d = 0.0;
     if (lane == 0) {
         double stk[32];
         int sp = -1;
         for (int t = 0; t < plan.nprog; ++t) {
             const int tok = plan.prog[t];
             if (tok >= 0) {
-                stk[++sp] = sums[wave][tok];
+                stk[++sp] = sums[tok];
             } else {
                 const double rgt = stk[sp--];
                 stk[sp] = stk[sp] + rgt;
             }
         }
-        const double d = stk[0];
-        deg[i] = d;
-        if (mode == GRF_LAP_NUMPY) dinv[i] = d > 0.0 ? 1.0 / sqrt(d) : 0.0;
-        else dinv[i] = 1.0 / sqrt(d > 0.0 ? d : 1.0);
+        d = stk[0];
     }
-}
-
-__global__ __launch_bounds__(256) void lapd_deg_kernel(int64_t n, const double *W, int32_t mode, double *deg,
-                                                       double *dinv) {
-    __shared__ PwLeaf leaves[4][kPwLeaves];
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per row
-    if (i >= n) return;
-    const double d = wave_np_pairwise(W + i * n, n, leaves[threadIdx.x >> 6]);
-    if ((threadIdx.x & 63) == 0) {
-        deg[i] = d;
-        if (mode == GRF_LAP_NUMPY) dinv[i] = d > 0.0 ? 1.0 / sqrt(d) : 0.0;
-        else dinv[i] = 1.0 / sqrt(d > 0.0 ? d : 1.0);
-    }
+    __builtin_amdgcn_wave_barrier();
+    return __shfl(d, 0, 64);
 }
 
 __device__ inline double lapd_value(int32_t mode, int64_t i, int64_t j, double w, const double *deg,
@@ -583,41 +577,237 @@ __device__ inline double lapd_value(int32_t mode, int64_t i, int64_t j, double w
     }
 }
 
-// one wave per row; EMIT=false counts nonzeros, EMIT=true writes them in column order
-template <bool EMIT>
-__global__ __launch_bounds__(256) void lapd_row_kernel(int64_t n, const double *W, int32_t mode, const double *deg,
-                                                       const double *dinv, int32_t *cnt, const int64_t *l_ptr,
-                                                       int32_t *l_idx, double *l_val, int64_t l_cap) {
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+// the row's elements in column order, up to two per lane per round: lane-ordered positions by ballots
+struct RowStager {
+    int32_t *col;
+    double *val;
+    int32_t cnt;  // wave-uniform running count
+    __device__ void put(bool nz0, int64_t c0, double v0, bool nz1, int64_t c1, double v1, int lane) {
+        const uint64_t m0 = __ballot(nz0), m1 = __ballot(nz1);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        int32_t p = cnt + __popcll(m0 & lt) + __popcll(m1 & lt);
+        if (nz0) {
+            if (p < kLapdCap) { col[p] = (int32_t)c0; val[p] = v0; }
+            ++p;
+        }
+        if (nz1 && p < kLapdCap) { col[p] = (int32_t)c1; val[p] = v1; }
+        cnt += __popcll(m0) + __popcll(m1);
+    }
+};
+
+struct IntSum {  // per-lane exact-integer-sum state of numpy's shortcut (wave_np_pairwise)
+    bool integral = true, nonzero = false;
+    double s = 0.0;
+    __device__ void add(double v) {
+        integral = integral && v == rint(v) && fabs(v) <= 1048576.0;
+        nonzero = nonzero || v != 0.0;
+        s += v;
+    }
+};
+
+__global__ __launch_bounds__(256) void lapd_stage_kernel(int64_t n, const double *W, int32_t mode, PwPlan plan,
+                                                         double *deg, double *dinv, int32_t *scnt, int32_t *scol,
+                                                         double *sval, uint64_t *flags, uint32_t *ticket,
+                                                         int32_t *err) {
+    __shared__ double sums[4][kPwPlanLeaves];
+    __shared__ PwLeaf leaves[4][kPwLeaves];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + wave;  // one wave per row
     if (i >= n) return;
-    const int lane = threadIdx.x & 63;
-    int64_t out = EMIT ? l_ptr[i] : 0;
-    int32_t c = 0;
-    constexpr int kU = 4;  // 64-column chunks in flight per step (all loads issued before the ballots)
-    for (int64_t j0 = 0; j0 < n; j0 += 64 * kU) {
-        double v[kU];
+    const double *a = W + i * n;
+    const int h = (int)(((uintptr_t)a >> 3) & 1);  // the row starts mid-16-B: element 0 alone
+    const int64_t npair = (n - h) >> 1;
+    const bool tail = ((n - h) & 1) != 0;
+    const double2 *pa = reinterpret_cast<const double2 *>(a + h);
+    RowStager st{scol + i * kLapdCap, sval + i * kLapdCap, 0};
+    IntSum is;
+    if (h) {
+        const double v = lane == 0 ? a[0] : 0.0;
+        if (lane == 0) is.add(v);
+        st.put(lane == 0 && v != 0.0, 0, v, false, 0, 0.0, lane);
+    }
+    constexpr int kU = 8;  // 16-B loads in flight per lane
+    for (int64_t p0 = 0; p0 < npair; p0 += 64 * kU) {
+        double2 v[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const int64_t j = j0 + u * 64 + lane;
-            v[u] = j < n ? lapd_value(mode, i, j, W[i * n + j], deg, dinv) : 0.0;
+            const int64_t p = p0 + u * 64 + lane;
+            v[u] = p < npair ? pa[p] : double2{0.0, 0.0};
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const int64_t j = j0 + u * 64 + lane;
-            const bool nz = j < n && v[u] != 0.0;
-            const uint64_t mask = __ballot(nz);
-            if (EMIT) {
-                if (nz) {
-                    const int64_t pos = out + __popcll(mask & ((1ull << lane) - 1ull));
-                    if (pos < l_cap) { l_idx[pos] = (int32_t)j; l_val[pos] = v[u]; }
-                }
-                out += __popcll(mask);
-            } else {
-                c += __popcll(mask);
-            }
+            if (p0 + u * 64 >= npair) break;  // (uniform)
+            const int64_t c0 = h + 2 * (p0 + u * 64 + lane);
+            is.add(v[u].x);
+            is.add(v[u].y);
+            st.put(v[u].x != 0.0, c0, v[u].x, v[u].y != 0.0, c0 + 1, v[u].y, lane);
         }
     }
-    if (!EMIT && lane == 0) cnt[i] = c;
+    if (tail) {
+        const double v = lane == 0 ? a[n - 1] : 0.0;
+        if (lane == 0) is.add(v);
+        st.put(lane == 0 && v != 0.0, n - 1, v, false, 0, 0.0, lane);
+    }
+    double d;
+    if (__all(is.integral) && __any(is.nonzero)) {
+        // every partial sum of any order is an exact integer (< 2^53): the recursion's result, bit for bit
+        d = wave_sum(is.s);
+    } else {
+        d = plan.nl > 0 ? plan_row_sum(a, plan, sums[wave], lane) : wave_np_pairwise(a, n, leaves[wave]);
+    }
+    if (lane == 0) {
+        deg[i] = d;
+        if (mode == GRF_LAP_NUMPY) dinv[i] = d > 0.0 ? 1.0 / sqrt(d) : 0.0;
+        else dinv[i] = 1.0 / sqrt(d > 0.0 ? d : 1.0);
+        scnt[i] = st.cnt;
+        flags[i] = 0;
+        if (i == 0) {
+            *ticket = 0u;
+            *err = 0;
+        }
+    }
+}
+
+typedef __attribute__((address_space(1))) uint64_t gu64_t;
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1ull;
+
+// Decoupled look-back (R2 granules: the 8-byte word {status, value} is the whole hand-off, written and
+// polled by relaxed agent-scope atomics; cdna_hip_programming.md Guideline 16).  Publishes this row's
+// count, returns the exclusive prefix of the counts before it.  Bounded spins: after ~2^20 polls of an
+// unpublished word (a predecessor that never ran: impossible under the ticket order) *err is set and the
+// wave goes on (its row pointer is then wrong; the word is left for a debugger, the launch still ends).
+__device__ int64_t lookback(uint64_t *flags, int64_t i, int64_t c, int lane, int32_t *err) {
+    gu64_t *f = (gu64_t *)flags;
+    if (lane == 0) __hip_atomic_store(f + i, (i == 0 ? kLbIncl : kLbAgg) | (uint64_t)c, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    if (i == 0) return 0;
+    int64_t excl = 0, pos = i - 1;
+    for (;;) {
+        const int64_t idx = pos - lane;
+        uint64_t w = kLbIncl;  // (before row 0: an inclusive zero)
+        if (idx >= 0) {
+            for (uint32_t spin = 0;; ++spin) {
+                w = __hip_atomic_load(f + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((w >> 62) != 0) break;
+                if (spin > (1u << 20)) {
+                    *err = 1;
+                    w = kLbIncl;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        const uint64_t incl = __ballot((w >> 62) == 2);
+        const int64_t v = (int64_t)(w & kLbVal);
+        if (incl) {
+            const int k = __ffsll((long long)incl) - 1;
+            excl += wave_sum<int64_t>(lane <= k ? v : 0);
+            break;
+        }
+        excl += wave_sum<int64_t>(v);
+        pos -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(f + i, kLbIncl | (uint64_t)(excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+__global__ __launch_bounds__(256) void lapd_emit_kernel(int64_t n, const double *W, int32_t mode, const double *deg,
+                                                        const double *dinv, const int32_t *scnt, const int32_t *scol,
+                                                        const double *sval, uint64_t *flags, uint32_t *ticket,
+                                                        int32_t *err, int64_t *l_ptr, int32_t *l_idx, double *l_val,
+                                                        int64_t l_cap) {
+    const int lane = threadIdx.x & 63;
+    uint32_t t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t i = (int64_t)__shfl(t, 0, 64);
+    if (i >= n) return;
+    const int32_t c = scnt[i];
+    if (c <= kLapdCap) {
+        // staged: k < c pairs (ascending columns) merged with the diagonal (an element even when w_ii = 0)
+        const int32_t *rc = scol + i * kLapdCap;
+        const double *rv = sval + i * kLapdCap;
+        const int32_t k0 = lane, k1 = lane + 64;
+        const int32_t c0 = k0 < c ? rc[k0] : INT32_MAX, c1 = k1 < c ? rc[k1] : INT32_MAX;
+        const int32_t q = __popcll(__ballot(c0 < i)) + __popcll(__ballot(c1 < i));  // staged columns before i
+        const bool expl = __any(c0 == i || c1 == i);
+        const int32_t T = c + (expl ? 0 : 1);
+        int64_t col[2];
+        double u[2];
+        bool keep[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int32_t m = r * 64 + lane;
+            keep[r] = false;
+            col[r] = 0;
+            u[r] = 0.0;
+            if (m < T) {
+                double w = 0.0;
+                if (!expl && m == q) {
+                    col[r] = i;
+                } else {
+                    const int32_t k = (!expl && m > q) ? m - 1 : m;
+                    col[r] = rc[k];
+                    w = rv[k];
+                }
+                u[r] = lapd_value(mode, i, col[r], w, deg, dinv);
+                keep[r] = u[r] != 0.0;
+            }
+        }
+        const uint64_t b0 = __ballot(keep[0]), b1 = __ballot(keep[1]);
+        const int64_t cnt = __popcll(b0) + __popcll(b1);
+        const int64_t o = lookback(flags, i, cnt, lane, err);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        const int64_t p0 = o + __popcll(b0 & lt), p1 = o + __popcll(b0) + __popcll(b1 & lt);
+        if (keep[0] && p0 < l_cap) { l_idx[p0] = (int32_t)col[0]; l_val[p0] = u[0]; }
+        if (keep[1] && p1 < l_cap) { l_idx[p1] = (int32_t)col[1]; l_val[p1] = u[1]; }
+        if (lane == 0) {
+            l_ptr[i] = o;
+            if (i == n - 1) l_ptr[n] = o + cnt;
+        }
+        return;
+    }
+    // a row with more structural nonzeros than the stage holds: count over W's row, look back, then fill
+    const double *a = W + i * n;
+    constexpr int kU = 4;
+    int64_t cnt = 0;
+    for (int64_t j0 = 0; j0 < n; j0 += 64 * kU) {
+        double w[kU];
+#pragma unroll
+        for (int r = 0; r < kU; ++r) {
+            const int64_t j = j0 + r * 64 + lane;
+            w[r] = j < n ? a[j] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < kU; ++r) {
+            const int64_t j = j0 + r * 64 + lane;
+            const bool nz = j < n && (w[r] != 0.0 || j == i) && lapd_value(mode, i, j, w[r], deg, dinv) != 0.0;
+            cnt += __popcll(__ballot(nz));
+        }
+    }
+    const int64_t o = lookback(flags, i, cnt, lane, err);
+    int64_t out = o;
+    for (int64_t j0 = 0; j0 < n; j0 += 64 * kU) {
+        double w[kU];
+#pragma unroll
+        for (int r = 0; r < kU; ++r) {
+            const int64_t j = j0 + r * 64 + lane;
+            w[r] = j < n ? a[j] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < kU; ++r) {
+            const int64_t j = j0 + r * 64 + lane;
+            const double v = j < n && (w[r] != 0.0 || j == i) ? lapd_value(mode, i, j, w[r], deg, dinv) : 0.0;
+            const bool nz = v != 0.0;
+            const uint64_t m = __ballot(nz);
+            const int64_t pos = out + __popcll(m & ((1ull << lane) - 1ull));
+            if (nz && pos < l_cap) { l_idx[pos] = (int32_t)j; l_val[pos] = v; }
+            out += __popcll(m);
+        }
+    }
+    if (lane == 0) {
+        l_ptr[i] = o;
+        if (i == n - 1) l_ptr[n] = o + cnt;
+    }
 }
 
 }  // namespace grf
@@ -632,10 +822,13 @@ size_t grf_laplacian_csr_workspace_bytes(int64_t n) {
     return cnt_bytes + scan_ws_bytes(n);
 }
 
+// dense workspace: dinv [n] f64 | staged counts [n] i32 | staged columns [n x cap] i32 | staged values
+// [n x cap] f64 | look-back words [n] u64 | ticket + error word (256 B)
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 size_t grf_laplacian_dense_workspace_bytes(int64_t n) {
     const size_t nn = (size_t)(n > 0 ? n : 1);
-    return ((nn * sizeof(double) + 255) & ~(size_t)255) + ((nn * sizeof(int32_t) + 255) & ~(size_t)255) +
-           scan_ws_bytes(n);
+    return al256(nn * sizeof(double)) + al256(nn * sizeof(int32_t)) + al256(nn * kLapdCap * sizeof(int32_t)) +
+           al256(nn * kLapdCap * sizeof(double)) + al256(nn * sizeof(uint64_t)) + 256;
 }
 
 int32_t grf_laplacian_csr(int64_t n, const int64_t *a_ptr, const int32_t *a_idx, const double *a_val, int32_t mode,
@@ -686,36 +879,38 @@ int32_t grf_laplacian_dense(int64_t n, const double *W, int32_t mode, int64_t *l
     GRF_REQUIRE(mode == GRF_LAP_NUMPY || mode == GRF_LAP_NUMPY_SAFE || mode == GRF_LAP_COMBINATORIAL ||
                     mode == GRF_LAP_NONE,
                 GRF_EINVAL, "grf_laplacian_dense: bad mode %d", mode);
-    const size_t nn = (size_t)(n > 0 ? n : 1);
-    const size_t dinv_bytes = (nn * sizeof(double) + 255) & ~(size_t)255;
-    const size_t cnt_bytes = (nn * sizeof(int32_t) + 255) & ~(size_t)255;
-    GRF_REQUIRE(workspace_bytes >= dinv_bytes + cnt_bytes + scan_ws_bytes(n), GRF_EINVAL,
-                "grf_laplacian_dense: workspace too small");
+    GRF_REQUIRE(((uintptr_t)W & 7) == 0, GRF_EINVAL, "grf_laplacian_dense: W must be 8-byte aligned");
+    GRF_REQUIRE(n < INT32_MAX, GRF_EINVAL, "grf_laplacian_dense: n must fit int32 column indices");
+    GRF_REQUIRE(workspace_bytes >= grf_laplacian_dense_workspace_bytes(n) && ((uintptr_t)workspace & 255) == 0,
+                GRF_EINVAL, "grf_laplacian_dense: workspace too small or not 256-byte aligned");
     hipStream_t st = S(stream);
     if (n == 0) {
         GRF_CHECK_HIP(hipMemsetAsync(l_ptr, 0, sizeof(int64_t), st));
         return GRF_OK;
     }
-    double *dinv = (double *)workspace;
-    int32_t *cnt = (int32_t *)((char *)workspace + dinv_bytes);
-    void *scan_ws = (char *)workspace + dinv_bytes + cnt_bytes;
-    GRF_REQUIRE_GRID(cdiv<int64_t>(n, 4), 256, "lapd_deg_kernel");
+    const size_t nn = (size_t)n;
+    char *w = (char *)workspace;
+    double *dinv = (double *)w;
+    w += al256(nn * sizeof(double));
+    int32_t *scnt = (int32_t *)w;
+    w += al256(nn * sizeof(int32_t));
+    int32_t *scol = (int32_t *)w;
+    w += al256(nn * kLapdCap * sizeof(int32_t));
+    double *sval = (double *)w;
+    w += al256(nn * kLapdCap * sizeof(double));
+    uint64_t *flags = (uint64_t *)w;
+    w += al256(nn * sizeof(uint64_t));
+    uint32_t *ticket = (uint32_t *)w;
+    int32_t *err = (int32_t *)(w + 16);
     PwPlan plan;
-    if (pw_plan_build(n, plan)) {
-        lapd_deg_plan_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, st>>>(n, W, mode, plan, deg, dinv);
-    } else {
-        lapd_deg_kernel<<<(unsigned)cdiv<int64_t>(n, 4), 256, 0, st>>>(n, W, mode, deg, dinv);
-    }
-    GRF_CHECK_LAUNCH("lapd_deg_kernel");
+    if (!pw_plan_build(n, plan)) plan.nl = 0;
     const unsigned g = (unsigned)cdiv<int64_t>(n, 4);
-    GRF_REQUIRE_GRID(g, 256, "lapd_row_kernel");
-    lapd_row_kernel<false><<<g, 256, 0, st>>>(n, W, mode, deg, dinv, cnt, nullptr, nullptr, nullptr, 0);
-    GRF_CHECK_LAUNCH("lapd_row_kernel<count>");
-    int32_t rc = scan_counts_i32(n, cnt, l_ptr, scan_ws, workspace_bytes - dinv_bytes - cnt_bytes, st);
-    if (rc != GRF_OK) return rc;
-    GRF_REQUIRE_GRID(g, 256, "lapd_row_kernel");
-    lapd_row_kernel<true><<<g, 256, 0, st>>>(n, W, mode, deg, dinv, nullptr, l_ptr, l_idx, l_val, l_cap);
-    GRF_CHECK_LAUNCH("lapd_row_kernel<fill>");
+    GRF_REQUIRE_GRID(g, 256, "lapd_stage_kernel");
+    lapd_stage_kernel<<<g, 256, 0, st>>>(n, W, mode, plan, deg, dinv, scnt, scol, sval, flags, ticket, err);
+    GRF_CHECK_LAUNCH("lapd_stage_kernel");
+    lapd_emit_kernel<<<g, 256, 0, st>>>(n, W, mode, deg, dinv, scnt, scol, sval, flags, ticket, err, l_ptr, l_idx,
+                                        l_val, l_cap);
+    GRF_CHECK_LAUNCH("lapd_emit_kernel");
     return GRF_OK;
 }
 

@@ -53,10 +53,17 @@ __device__ inline bool halts(uint32_t x0, uint32_t x1, uint64_t thr) {
 // x / c correctly rounded without the IEEE divide sequence (v_div_scale x2, v_rcp_f64, 5 FMAs, v_div_fmas,
 // v_div_fixup per call): with y = RN(1 / c) (loop-invariant: computed once per walk) the quotient
 // q = RN(x y) is faithful, the remainder x - c q is exact in one FMA, and RN(q + (x - c q) y) is RN(x / c)
-// (Markstein's theorem; finite normal x and c, as the loads and 1 - p_halt are).  Same bits as x / c.
+// (Markstein's theorem; it needs x, the quotient and the remainder normal and c q free of overflow, which
+// holds for magnitudes in [2^-960, 2^960] with c the normal 1 - p_halt or m).  Anything else -- zero,
+// subnormal, huge, inf or NaN operands or quotients, e.g. cumulative loads that overflowed -- takes the
+// IEEE divide (a branch no lane takes on the benchmarked graphs), so the bits are x / c's everywhere
+// (tools/div_check.c checks both ranges).
 __device__ inline double div_by(double x, double c, double y) {
     const double q = x * y;
-    return __builtin_fma(__builtin_fma(-q, c, x), y, q);
+    const double r = __builtin_fma(__builtin_fma(-q, c, x), y, q);
+    const double ax = fabs(x), ar = fabs(r);
+    if (!(ax >= 0x1p-960 && ax <= 0x1p960 && ar >= 0x1p-960 && ar <= 0x1p960)) return x / c;
+    return r;
 }
 
 // The importance weight deg w / (1 - p) applied by the load rule; keep = 1 - p and its reciprocal

@@ -89,6 +89,10 @@ class GraphDiffusionFastGRFKernel(torch.nn.Module):
         i2 = i1 if X2 is None else _indices(X2).to(Kf.device)
         return Kf[i1][:, i2]
 
+    def invalidate(self) -> None:
+        """Drop the cached K (the calls here key it by the host value of beta; K_torch by tensor)."""
+        self._steps.invalidate()
+
     def _cached(self) -> torch.Tensor:
         b = float(self.beta.detach())
         return float(self.sigma_f.detach()) ** 2 * self._steps.gram(self.modulator(b), key=("beta", b))

@@ -91,16 +91,27 @@ class GraphGeneralFastGRFKernel(torch.nn.Module):
         i2 = i1 if X2 is None else _indices(X2).to(Kf.device)
         return Kf[i1][:, i2]
 
+    def _gram_host_keyed(self) -> torch.Tensor:
+        """The cached K keyed by the modulator's VALUES (these calls return host arrays, so reading the
+        L values back costs nothing extra): a write through ``.data`` is seen too."""
+        fv = self.modulator_vector.detach().to("cpu", torch.float64).numpy()
+        return self._steps.gram(self.modulator_vector, key=("f", fv.tobytes()))
+
+    def invalidate(self) -> None:
+        """Drop the cached K (needed only by ``K_torch`` after a modulator write that bypasses its version
+        counter, e.g. ``modulator_vector.data.copy_(...)``)."""
+        self._steps.invalidate()
+
     def K(self, X1, X2=None) -> np.ndarray:
         """K[X1, X2] (reference :61-67): a gather from the cached K of the current modulator."""
-        Kf = self._steps.gram(self.modulator_vector)
+        Kf = self._gram_host_keyed()
         i1 = _indices(X1).to(Kf.device)
         i2 = i1 if X2 is None else _indices(X2).to(Kf.device)
         return Kf[i1][:, i2].cpu().numpy().astype(np.float64)
 
     def K_diag(self, X) -> np.ndarray:
         """diag(K)[X] (reference :69-72), from the same cached K."""
-        Kf = self._steps.gram(self.modulator_vector)
+        Kf = self._gram_host_keyed()
         i = _indices(X).to(Kf.device)
         return Kf.diagonal()[i].cpu().numpy().astype(np.float64)
 

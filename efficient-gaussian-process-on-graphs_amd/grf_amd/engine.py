@@ -70,6 +70,24 @@ class DeviceCSR:
             self._nnz = int(self.ptr[-1].item())
         return self._nnz
 
+    # a row selection's entry buffers are sized by rows x row_bound only while that stays within this factor
+    # of the matrix's own entries (repeats allowed) or ROWS_BOUND_FLOOR entries; past it (a hub row makes
+    # row_bound ~ n_cols) the exact count is read back instead
+    ROWS_BOUND_FACTOR = 4
+    ROWS_BOUND_FLOOR = 1 << 22
+
+    def rows_entry_bound(self, n_sel: int) -> Optional[int]:
+        """An upper bound of the entries of n_sel selected rows that is known without a host read and
+        not wasteful (None: count them exactly)."""
+        if self.row_bound is None:
+            return None
+        bound = n_sel * self.row_bound
+        total = self.nnz_or_bound() if (self._nnz is not None or self.nnz_bound is not None) else None
+        if total is None:
+            return None
+        reps = -(-max(n_sel, 1) // max(self.n_rows, 1))  # (a selection longer than the matrix repeats rows)
+        return bound if bound <= max(self.ROWS_BOUND_FACTOR * reps * total, self.ROWS_BOUND_FLOOR) else None
+
     def nnz_or_bound(self) -> int:
         """nnz when it is known on the host, else the bound (no device->host read), else nnz (read)."""
         if self._nnz is not None:
@@ -858,8 +876,8 @@ class GRFEngine:
         if rmap is None:
             nnz = phi.nnz_or_bound()
             exact = phi._nnz is not None
-        elif phi.row_bound is not None:
-            nnz, exact = n_sel * phi.row_bound, False
+        elif phi.rows_entry_bound(n_sel) is not None:
+            nnz, exact = phi.rows_entry_bound(n_sel), False
         else:
             rl = rmap.long()
             nnz = int((phi.ptr[rl + 1] - phi.ptr[rl]).sum().item()) if n_sel else 0

@@ -120,8 +120,9 @@ def gather_rows(eng: GRFEngine, A: DeviceCSR, rows: torch.Tensor) -> DeviceCSR:
     ptr = eng._empty(n_sel + 1, torch.int64)
     ws = eng._ws(eng.lib.grf_scan_workspace_bytes(n_sel))
     C.check(eng.lib.grf_scan_counts(n_sel, _p(cnt), _p(ptr), _p(ws), ws.numel(), eng.stream), "grf_scan_counts")
-    if A.row_bound is not None:
-        nnz, bound = None, n_sel * A.row_bound
+    bound = A.rows_entry_bound(n_sel)
+    if bound is not None:
+        nnz = None
     else:
         nnz = int(ptr[-1].item()) if n_sel else 0
         bound = nnz
@@ -130,6 +131,17 @@ def gather_rows(eng: GRFEngine, A: DeviceCSR, rows: torch.Tensor) -> DeviceCSR:
     C.check(eng.lib.grf_csr_gather_rows(n_sel, _p(A.ptr), _p(A.idx), _p(A.val32), _p(rmap), _p(ptr), _p(idx),
                                         _p(val), eng.stream), "grf_csr_gather_rows")
     return DeviceCSR(n_sel, A.n_cols, ptr, idx, None, val, nnz, nnz_bound=bound, row_bound=A.row_bound)
+
+
+def _square_symmetrised(K: torch.Tensor, i1: Optional[torch.Tensor], i2: Optional[torch.Tensor]) -> torch.Tensor:
+    """K(x1, x2) for equal-length index tensors that are different objects: where x1 and x2 hold the
+    same values (decided on the device, no host read), the block is K(x, x) and is returned exactly
+    symmetric as (K + K^T) / 2 -- what the symmetric path's mirrored tiles give up to the K tolerance;
+    otherwise K unchanged."""
+    if i1 is None or i2 is None or K.dim() != 2 or K.shape[0] != K.shape[1] or i1.shape != i2.shape:
+        return K
+    same = torch.eq(i1, i2).all()
+    return torch.where(same, 0.5 * (K + K.t()), K)
 
 
 def rowdot(eng: GRFEngine, A: DeviceCSR, rows_a: Optional[torch.Tensor], B: DeviceCSR,
@@ -202,6 +214,8 @@ class GRFKernelFunction(torch.autograd.Function):
             out = rowdot(eng, phi, i1, phi, i2, n1).to(f.dtype)
         else:
             out = kernel_block(eng, phi, i1, i2, same)
+            if not same:
+                out = _square_symmetrised(out, i1, i2)
             out = out.to(f.dtype) if out.dtype != f.dtype else out
         ctx.steps, ctx.phi, ctx.i1, ctx.i2, ctx.diag, ctx.n_f = steps, phi, i1, i2, diag, f.numel()
         ctx.f_dtype, ctx.f_device = f.dtype, f.device
@@ -286,22 +300,35 @@ class DenseSteps:
         return self._phi_both(f)[0]
 
     def gram(self, f: torch.Tensor, key=None) -> torch.Tensor:
-        """K = Phi Phi^T (fp32, N x N) on the MFMA Gram, cached.  The cache key: ``key`` when the caller
-        has a host-side one (the modulator's own parameters, e.g. ("beta", b)), else the modulator
-        TENSOR -- the same memory at the same version counter (an in-place update such as an optimiser
-        step bumps it; a tensor autograd saved for the backward shares both; the cache holds the tensor,
-        so its memory cannot be reused by another).  Neither reads f back to the host."""
+        """K = Phi Phi^T (fp32, N x N) on the MFMA Gram, cached.  The cache key:
+        * ``key`` when the caller has a host-side one (the modulator's own parameters, e.g. ("beta", b));
+        * a modulator on the HOST (a CPU tensor, numpy-backed or not): its values (exact bytes), so a write
+          through numpy or ``.data`` is seen;
+        * a device modulator: the same memory at the same version counter (an in-place update such as an
+          optimiser step bumps it; a tensor autograd saved for the backward shares both) -- no host read
+          of f.  A write that bypasses the counter (``p.data.copy_(...)``: ``.data`` has a counter of its
+          own) is not seen: call ``invalidate()`` after one.
+        The cached K and Phi are dropped by ``invalidate()``."""
         k = self._key
         if key is not None:
-            hit = k is not None and k[0] == "host" and k[1] == key
+            new_key = ("host", key)
+            hit = k == new_key
+        elif f.device.type == "cpu":
+            new_key = ("value", tuple(f.shape), f.detach().to(torch.float64).contiguous().numpy().tobytes())
+            hit = k == new_key
         else:
+            new_key = ("tensor", f, f._version)
             hit = k is not None and k[0] == "tensor" and f.data_ptr() == k[1].data_ptr() and \
                 f._version == k[2] and f.shape == k[1].shape and f.dtype == k[1].dtype and f.stride() == k[1].stride()
         if not hit:
             self._phi64, phi32 = self._phi_both(f)
             self._K = self.engine.gram_dense(phi32, self.n)
-            self._key = ("host", key) if key is not None else ("tensor", f, f._version)
+            self._key = new_key
         return self._K
+
+    def invalidate(self) -> None:
+        """Drop the cached K (and Phi): the next ``gram`` recomputes whatever the modulator's key says."""
+        self._key, self._K, self._phi64 = None, None, None
 
     def grad(self, f: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
         """dL/df_l = <F_l, (G + G^T) Phi> for the upstream gradient G of K (fp64, length L)."""

@@ -266,3 +266,80 @@ def test_dense_gram_cache_keyed_without_host_copy():
         torch.cuda.set_sync_debug_mode("default")
     assert K2 is not K1
     torch.testing.assert_close(K2, 4.0 * K1, rtol=1e-5, atol=1e-6)
+
+
+def test_dense_gram_cache_sees_writes_that_bypass_the_version_counter():
+    """a CPU modulator is keyed by value (a numpy write into a torch.from_numpy tensor is
+    seen); the GPflow wrapper's host-returning K / K_diag key by the modulator's values (a write
+    through ``.data`` is seen); the device path (K_torch) is sync-free and keyed by the version counter,
+    and ``invalidate()`` drops the cache after a ``.data`` write."""
+    from efficient_graph_gp.gpflow_kernels import GraphGeneralFastGRFKernel
+    from grf_amd.features import DenseSteps
+    torch.manual_seed(0)
+    F = torch.rand(48, 48, 3, dtype=torch.float64) * (torch.rand(48, 48, 3, dtype=torch.float64) < 0.3)
+    ds = DenseSteps(F)
+    arr = np.array([1.0, -0.5, 0.25])
+    fh = torch.from_numpy(arr)
+    K1 = ds.gram(fh).clone()
+    arr *= 2.0  # (no version bump: numpy writes the shared memory)
+    torch.testing.assert_close(ds.gram(fh), 4.0 * K1, rtol=1e-5, atol=1e-6)
+    # the GPflow-style wrapper
+    r = np.random.default_rng(2)
+    A = (r.random((40, 40)) < 0.15).astype(np.float64)
+    A = np.maximum(A, A.T)
+    np.fill_diagonal(A, 0.0)
+    kern = GraphGeneralFastGRFKernel(A, walks_per_node=16, p_halt=0.2, max_walk_length=3, random_walk_seed=1)
+    X = np.arange(40)
+    Ka = kern.K(X)
+    with torch.no_grad():
+        kern.modulator_vector.data.copy_(2.0 * kern.modulator_vector.detach())  # (bypasses _version)
+    np.testing.assert_allclose(kern.K(X), 4.0 * Ka, rtol=1e-5, atol=1e-6)
+    Kt1 = kern.K_torch(X).detach().clone()
+    kern.modulator_vector.data.mul_(0.5)
+    kern.invalidate()
+    np.testing.assert_allclose(kern.K_torch(X).detach().cpu().numpy(), Kt1.cpu().numpy() / 4.0, rtol=1e-5, atol=1e-6)
+
+
+def test_row_selection_bounds_fall_back_to_exact_counts_on_hub_rows():
+    """a row selection's buffers use rows x row_bound only while that stays near the
+    matrix's own entries; one dense (hub) row makes row_bound ~ n_cols, and the exact count is used."""
+    from grf_amd.engine import DeviceCSR, GRFEngine
+    from grf_amd.features import gather_rows
+    eng = GRFEngine("cuda:0")
+    n = 20000
+    r = np.random.default_rng(3)
+    rows = np.repeat(np.arange(n), 3)
+    cols = r.integers(0, n, rows.size)
+    A = sp.csr_matrix((np.ones(rows.size), (rows, cols)), shape=(n, n))
+    A = A + sp.csr_matrix((np.ones(n), (np.zeros(n, int), np.arange(n))), shape=(n, n))  # row 0: dense
+    A = sp.csr_matrix(A)
+    Ad = DeviceCSR.from_scipy(A, eng.device)
+    Ad.val32 = Ad.val.float()
+    Ad.row_bound = int(np.diff(A.indptr).max())
+    sel = torch.arange(0, n, 2, device=eng.device)
+    assert Ad.rows_entry_bound(sel.numel()) is None  # (10k x 20k entries would be 200 M)
+    G = gather_rows(eng, Ad, sel)
+    want = A[np.arange(0, n, 2)]
+    assert G.nnz_bound == want.nnz
+    assert same_csr(G.to_scipy().astype(np.float64), want.astype(np.float32).astype(np.float64))
+    small = torch.arange(1, 200, device=eng.device)  # (199 rows x the bound: within the floor)
+    assert Ad.rows_entry_bound(small.numel()) == small.numel() * Ad.row_bound
+
+
+def test_kernel_block_equal_valued_indices_is_exactly_symmetric(golden):
+    """K(x1, x2) with x1, x2 equal-valued but different tensors (a caller that clones
+    the inputs) comes out exactly symmetric (decided on the device, no host read); different values of
+    the same length are left as computed."""
+    from efficient_graph_gp_sparse.gptorch_kernels_sparse import SparseGRFKernel
+    d = golden("small_graphs")
+    steps = [csr(d, f"er40_sp_n3_s7_l{l}", 40) for l in range(4)]
+    torch.manual_seed(0)
+    kern = SparseGRFKernel(4, _ops(steps)).cuda()
+    x = torch.tensor([0, 3, 5, 17, 39, 8, 21], device="cuda")
+    K = kern(x, x.clone()).detach()
+    assert torch.equal(K, K.t())
+    torch.testing.assert_close(K, kern(x, x).detach(), rtol=1e-6, atol=1e-7)
+    y = torch.tensor([1, 3, 5, 17, 39, 8, 22], device="cuda")
+    Ky = kern(x, y).detach()
+    Kxy = kern(x, y.clone()).detach()
+    assert torch.equal(Ky, Kxy)

@@ -112,6 +112,55 @@ def test_laplacian_dense_modes(eng, golden):
         assert np.array_equal(G.indices, ix) and bit_equal(G.data, dx), mode
 
 
+def _dense_laplacian_cases():
+    """Dense adjacencies that reach every branch of the stage / emit kernels (grf_laplacian.hip)."""
+    r = np.random.default_rng(11)
+    cases = {}
+    # fully dense weighted rows: > 127 structural nonzeros (emit re-reads W), non-integral degrees
+    # (numpy's plan), n odd (rows alternately start mid-16-B)
+    W = r.random((301, 301))
+    cases["dense_weighted_odd"] = W + W.T
+    # sparse 0/1, odd n: the exact integer degree, staged rows, the diagonal inserted
+    A = (r.random((1001, 1001)) < 0.004).astype(np.float64)
+    A = np.maximum(A, A.T)
+    np.fill_diagonal(A, 0.0)
+    cases["unit_sparse_odd"] = A
+    # asymmetric with zero rows, negative weights (degrees <= 0: D^-1/2 = 0 or the safe 1), explicit
+    # diagonal entries and -0.0 entries
+    B = (r.random((257, 257)) < 0.03) * r.uniform(-1.0, 2.0, (257, 257))
+    B[5] = 0.0
+    B[7] = -0.0
+    B[9, 9] = 3.0
+    B[10, :12] = -1.0
+    cases["asym_signed"] = B
+    # rows of mixed lengths around the stage's cap (127 staged + the diagonal)
+    C = np.zeros((400, 400))
+    for i in range(400):
+        k = [0, 1, 126, 127, 128, 200][i % 6]
+        C[i, r.choice(400, k, replace=False)] = 1.0
+    cases["cap_edges"] = C
+    # n > 8192 with weighted rows: the degree recursion beyond the host plan (wave_np_pairwise)
+    D = np.zeros((8300, 8300))
+    idx = r.integers(0, 8300, (8300, 12))
+    D[np.arange(8300)[:, None], idx] = r.uniform(0.1, 2.0, (8300, 12))
+    cases["large_weighted"] = D
+    return cases
+
+
+@pytest.mark.parametrize("name", ["dense_weighted_odd", "unit_sparse_odd", "asym_signed", "cap_edges", "large_weighted"])
+def test_laplacian_dense_stage_emit_branches(eng, name):
+    """The one-read dense Laplacian (stage + look-back emit) bit-exact against the oracle in every mode,
+    row pointer included, on inputs that take each branch: exact-integer and recursion degrees, the
+    host plan and wave_np_pairwise, staged rows and rows re-read from W, rows at the stage's cap,
+    unaligned rows, zero / negative degrees, explicit and inserted diagonals."""
+    W = _dense_laplacian_cases()[name]
+    for mode, ref_mode in ((1, 0), (2, 1), (3, 2), (4, None)):
+        G = eng.walk_matrix_dense(W, mode).to_scipy()
+        ip, ix, dx = O.dense_to_walk_csr(W if ref_mode is None else O.laplacian_dense(W, ref_mode))
+        assert np.array_equal(G.indptr, ip), (name, mode)
+        assert np.array_equal(G.indices, ix) and bit_equal(G.data, dx), (name, mode)
+
+
 # ---------------------------------------------------------------------- walks
 @pytest.mark.parametrize("rule", [0, 1, 2])
 def test_walk_philox_matches_oracle(eng, rule):
