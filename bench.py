@@ -762,6 +762,9 @@ def main():
         with open(os.path.join(args.fingerprint_dir, f"rank{rank}.json"), "w") as fh:
             json.dump({"rank": rank, "world": world, "mode": pl.mode, "shard": [b, e], "cols_sym": pl.cols_sym,
                        "k_rows": args.k_rows, "hash": h, "sum": s_}, fh)
+    # the sparse Gram tiles' gather roofline (whole-K mode): their bucket-line gathers against the
+    # guide's indexed-row rates (after the fingerprint: the timing launches rewrite K's upper tiles)
+    gather_rl = gather_roofline(eng, last[0], pl, K) if pl.mode == "sym" else None
     coll_ms = float(np.mean([a.elapsed_time(b_) for a, b_, _, _ in gather_stats])) if gather_stats else 0.0
     coll_sent = float(np.mean([x for _, _, x, _ in gather_stats])) if gather_stats else 0.0
     coll_recv = float(np.mean([x for _, _, _, x in gather_stats])) if gather_stats else 0.0
@@ -901,6 +904,7 @@ def main():
         "nnz_phi": nnz_phi,
         "parity": parity,
         "parity_note": "the last timed (pipelined) step's K block, checked after the timed region",
+        "roofline_gather": gather_rl,
         "pipelined": bool(ov),
         "front_at": args.front_at,
         "serial_ms_per_step": serial_ms,
@@ -931,6 +935,84 @@ def main():
         print(json.dumps(out), flush=True)
     if coll:
         dist.destroy_process_group()
+
+
+# MI355X_MICROARCH.md "Indexed rows": chip-wide rates of rows gathered by index, by where they are served
+GATHER_PEAK_IC_TBS = 8.6      # 38 MB table, uniformly random rows (Infinity Cache)
+GATHER_PEAK_BEYOND_TBS = 7.4  # 151 MB table (7.4-7.9); past 256 MiB 3-9 % slower again (lower bound taken)
+IC_BYTES = 256 << 20
+
+
+def gather_model(phi, tr, sym: bool = True):
+    """Bucket gathers of the sparse Gram tiles (gram_sparse_kernel), counted from the transpose's
+    descriptors and Phi's entries, no PMC: the tile of row i gathers, for every nonzero Phi[i, k], the
+    bucket (band b, column k) of every band b of its tiles (symmetric mode: b >= band(i)), so bucket
+    (b, k) is read by the entries of column k in bands <= b.  Returns (128-B lines gathered, record
+    bytes gathered, table bytes), or None for the slot layout (its buckets are not in t_desc)."""
+    import torch
+
+    from grf_amd import _lib as C
+
+    if tr.rec_unit == C.REC_SLOT or phi.nnz == 0:
+        return None
+    n, ncol, W = tr.n_rows, tr.n_cols, tr.band_width
+    nb = -(-n // W)
+    desc = tr.t_desc[:2 * nb * ncol].view(nb, ncol, 2).long()
+    first, pairs = desc[..., 0], desc[..., 1]
+    if tr.rec_unit == C.REC_LINE:
+        lines = (12 * pairs + 127) // 128
+    else:  # packed: the lines a bucket's bytes span from its start
+        start = first * tr.rec_unit
+        lines = torch.where(pairs > 0, (start + 12 * pairs - 1) // 128 - start // 128 + 1, torch.zeros_like(pairs))
+    nnz = phi.nnz
+    rows = torch.repeat_interleave(torch.arange(phi.n_rows, device=phi.ptr.device), phi.ptr.diff())
+    ent = torch.bincount((rows // W) * ncol + phi.idx[:nnz].long(), minlength=nb * ncol).view(nb, ncol)
+    del rows
+    visits = ent.cumsum(0) if sym else ent.sum(0, keepdim=True).expand(nb, ncol)
+    line_visits = int((visits * lines).sum())
+    rec_bytes = int((visits * pairs).sum()) * 12
+    table = int(((first + (lines if tr.rec_unit == C.REC_LINE else 0)).max() * tr.rec_unit)) \
+        if tr.rec_unit == C.REC_LINE else int((first * tr.rec_unit + 12 * pairs).max())
+    return line_visits, rec_bytes, table
+
+
+def gather_roofline(eng, fr, pl, K, reps: int = 3) -> dict:
+    """roofline_gather: the sparse Gram tiles alone (no mirror, no hub panel; the
+    hub columns, when split off, are already dropped from this front's transpose) timed with HIP events,
+    their gathered 128-B bucket lines (gather_model) per launch / that time, against the guide's
+    indexed-row rate for where the transpose is served from (Infinity Cache when it fits, else the
+    larger-table rate).  HBM bytes stay in `roofline`."""
+    import torch
+
+    try:
+        model = gather_model(fr.phi, fr.tr, sym=True)
+        if model is None:
+            return None
+        lines, rec_bytes, table = model
+        cuts = getattr(fr, "cuts", None)
+        if cuts is None and pl.hubs > 0:
+            cuts = eng.row_cuts(fr.phi, fr.tr, pl.skewed)
+        eng.gram_sparse_upper(fr.phi, fr.tr, out=K, cuts=cuts)  # (warm)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        for _ in range(reps):
+            eng.gram_sparse_upper(fr.phi, fr.tr, out=K, cuts=cuts)
+        ev[1].record()
+        ev[1].synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / reps
+        peak = GATHER_PEAK_IC_TBS if table <= IC_BYTES else GATHER_PEAK_BEYOND_TBS
+        ach = 128.0 * lines / (ms * 1e-3) / 1e12
+        return {"bound": "gather", "achieved": ach, "peak": peak, "unit": "TB/s", "frac": ach / peak,
+                "kernel": "gram_sparse_kernel (upper tiles alone)", "kernel_ms": ms,
+                "lines_gathered": lines, "line_bytes_gathered": 128 * lines, "record_bytes_gathered": rec_bytes,
+                "record_TBps": rec_bytes / (ms * 1e-3) / 1e12, "table_bytes": table,
+                "peak_source": ("MI355X_MICROARCH.md 'Indexed rows': " +
+                                ("38 MB table, uniformly random rows, Infinity Cache: 8.6 TB/s" if table <= IC_BYTES else
+                                 "151 MB table 7.4-7.9 TB/s, past 256 MiB 3-9 % slower: 7.4 TB/s taken")),
+                "model": "bucket (band b, column k) read by the entries of column k in bands <= b; 128-B lines "
+                         "of its 12-B record pairs (line-aligned buckets, or the lines a packed bucket spans)"}
+    except Exception as exc:  # noqa: BLE001  (a side leg: reported, never at the cost of the line)
+        return {"error": f"{type(exc).__name__}: {exc}"}
 
 
 def rank_turns_gram_ms(eng, fr, pl, K, coll: bool, rank: int, world: int, reps: int = 3) -> float:

@@ -463,11 +463,14 @@ __global__ __launch_bounds__(256) void lap_row_group_kernel(int64_t n, const int
 //    pairwise sum: rows of integer values take the exact strided sum, any other row the recursion's
 //    plan below), D^-1/2, and the row's structural nonzeros (w != 0) in column order, the first
 //    kLapdCap of them staged as (column, w) pairs.  It also zeroes the next launch's look-back words.
-//  lapd_emit_kernel -- one wave per row in ticket order: the Laplacian row's nonzeros from the staged
-//    pairs and the diagonal (a row with more than kLapdCap structural nonzeros re-reads W), its count
-//    published for a decoupled look-back (CUB-style: each wave sums its predecessors' aggregates until
-//    an inclusive prefix), so the row pointer and the CSR come out of the one launch with no scan pass.
-//    Waves take rows by an atomic ticket, so every predecessor a wave waits on is already running.
+//  lapd_emit_kernel -- tiles of 256 rows in ticket order: each row's Laplacian nonzeros from its staged
+//    pairs and the diagonal (one thread per row; a row with more than kLapdCap structural nonzeros is
+//    re-read from W by the whole workgroup), a block scan, and the tile's count published for a
+//    decoupled look-back over the tiles (CUB-style: wave 0 sums its predecessors' aggregates until an
+//    inclusive prefix), so the row pointer and the CSR come out of the one launch with no scan pass.
+//    Workgroups take tiles by an atomic ticket, so every tile a workgroup waits on is already running.
+//    (One wave per row with the look-back over rows took 124 us at C3: the chain of inclusive prefixes
+//    advanced 64 rows per round trip.)
 //
 // Values: lapd_value below, the reference's elementwise arithmetic; an entry with w = 0 off the
 // diagonal is exactly zero in every mode (D^-1/2 is finite), so only the structural nonzeros and the
@@ -711,102 +714,130 @@ __device__ int64_t lookback(uint64_t *flags, int64_t i, int64_t c, int lane, int
     return excl;
 }
 
+// One row of the emit pass from its staged pairs (c <= kLapdCap structural nonzeros, ascending columns)
+// merged with the diagonal, by one thread: counts its nonzeros (EMIT = false) or writes them from `o`.
+template <bool EMIT>
+__device__ int32_t lapd_staged_row(int64_t i, int32_t c, int32_t mode, const int32_t *rc, const double *rv,
+                                   const double *deg, const double *dinv, int64_t o, int32_t *l_idx, double *l_val,
+                                   int64_t l_cap) {
+    int32_t cnt = 0;
+    bool diag_done = false;
+    auto put = [&](int64_t col, double w) {
+        const double u = lapd_value(mode, i, col, w, deg, dinv);
+        if (u != 0.0) {
+            if (EMIT && o + cnt < l_cap) {
+                l_idx[o + cnt] = (int32_t)col;
+                l_val[o + cnt] = u;
+            }
+            ++cnt;
+        }
+    };
+    for (int32_t k = 0; k < c; ++k) {
+        const int64_t col = rc[k];
+        if (!diag_done && col >= i) {
+            if (col > i) put(i, 0.0);  // (the diagonal, w_ii = 0, before the first column past it)
+            diag_done = true;
+        }
+        put(col, rv[k]);
+    }
+    if (!diag_done) put(i, 0.0);
+    return cnt;
+}
+
+// A row with more structural nonzeros than the stage holds, by the whole workgroup (256 threads) over W's
+// row: counts (EMIT = false, the total in every thread) or writes from `o` in column order (chunks of 256
+// columns: wave ballots, then the waves' counts through LDS).
+template <bool EMIT>
+__device__ int64_t lapd_dense_row(int64_t i, int64_t n, int32_t mode, const double *W, const double *deg,
+                                  const double *dinv, int64_t o, int32_t *l_idx, double *l_val, int64_t l_cap,
+                                  int32_t *wcnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const double *a = W + i * n;
+    int64_t total = 0;
+    for (int64_t j0 = 0; j0 < n; j0 += 256) {
+        const int64_t j = j0 + tid;
+        const double w = j < n ? a[j] : 0.0;
+        const double v = j < n && (w != 0.0 || j == i) ? lapd_value(mode, i, j, w, deg, dinv) : 0.0;
+        const uint64_t m = __ballot(v != 0.0);
+        __syncthreads();  // (the previous chunk's counts are read)
+        if (lane == 0) wcnt[wave] = __popcll(m);
+        __syncthreads();
+        int64_t before = 0, chunk = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            before += q < wave ? wcnt[q] : 0;
+            chunk += wcnt[q];
+        }
+        if (EMIT && v != 0.0) {
+            const int64_t pos = o + total + before + __popcll(m & ((1ull << lane) - 1ull));
+            if (pos < l_cap) {
+                l_idx[pos] = (int32_t)j;
+                l_val[pos] = v;
+            }
+        }
+        total += chunk;
+    }
+    return total;
+}
+
+// Tiles of 256 rows in ticket order: counts (one thread per staged row; the workgroup per long row), a
+// block scan, the look-back over the tiles' counts (wave 0), then the fill.  2708 rows (C3) are 11 tiles.
+constexpr int kLapdTileRows = 256;
+
 __global__ __launch_bounds__(256) void lapd_emit_kernel(int64_t n, const double *W, int32_t mode, const double *deg,
                                                         const double *dinv, const int32_t *scnt, const int32_t *scol,
                                                         const double *sval, uint64_t *flags, uint32_t *ticket,
                                                         int32_t *err, int64_t *l_ptr, int32_t *l_idx, double *l_val,
                                                         int64_t l_cap) {
-    const int lane = threadIdx.x & 63;
-    uint32_t t = 0;
-    if (lane == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t i = (int64_t)__shfl(t, 0, 64);
-    if (i >= n) return;
-    const int32_t c = scnt[i];
-    if (c <= kLapdCap) {
-        // staged: k < c pairs (ascending columns) merged with the diagonal (an element even when w_ii = 0)
-        const int32_t *rc = scol + i * kLapdCap;
-        const double *rv = sval + i * kLapdCap;
-        const int32_t k0 = lane, k1 = lane + 64;
-        const int32_t c0 = k0 < c ? rc[k0] : INT32_MAX, c1 = k1 < c ? rc[k1] : INT32_MAX;
-        const int32_t q = __popcll(__ballot(c0 < i)) + __popcll(__ballot(c1 < i));  // staged columns before i
-        const bool expl = __any(c0 == i || c1 == i);
-        const int32_t T = c + (expl ? 0 : 1);
-        int64_t col[2];
-        double u[2];
-        bool keep[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int32_t m = r * 64 + lane;
-            keep[r] = false;
-            col[r] = 0;
-            u[r] = 0.0;
-            if (m < T) {
-                double w = 0.0;
-                if (!expl && m == q) {
-                    col[r] = i;
-                } else {
-                    const int32_t k = (!expl && m > q) ? m - 1 : m;
-                    col[r] = rc[k];
-                    w = rv[k];
-                }
-                u[r] = lapd_value(mode, i, col[r], w, deg, dinv);
-                keep[r] = u[r] != 0.0;
-            }
-        }
-        const uint64_t b0 = __ballot(keep[0]), b1 = __ballot(keep[1]);
-        const int64_t cnt = __popcll(b0) + __popcll(b1);
-        const int64_t o = lookback(flags, i, cnt, lane, err);
-        const uint64_t lt = (1ull << lane) - 1ull;
-        const int64_t p0 = o + __popcll(b0 & lt), p1 = o + __popcll(b0) + __popcll(b1 & lt);
-        if (keep[0] && p0 < l_cap) { l_idx[p0] = (int32_t)col[0]; l_val[p0] = u[0]; }
-        if (keep[1] && p1 < l_cap) { l_idx[p1] = (int32_t)col[1]; l_val[p1] = u[1]; }
-        if (lane == 0) {
-            l_ptr[i] = o;
-            if (i == n - 1) l_ptr[n] = o + cnt;
-        }
-        return;
-    }
-    // a row with more structural nonzeros than the stage holds: count over W's row, look back, then fill
-    const double *a = W + i * n;
-    constexpr int kU = 4;
-    int64_t cnt = 0;
-    for (int64_t j0 = 0; j0 < n; j0 += 64 * kU) {
-        double w[kU];
-#pragma unroll
-        for (int r = 0; r < kU; ++r) {
-            const int64_t j = j0 + r * 64 + lane;
-            w[r] = j < n ? a[j] : 0.0;
-        }
-#pragma unroll
-        for (int r = 0; r < kU; ++r) {
-            const int64_t j = j0 + r * 64 + lane;
-            const bool nz = j < n && (w[r] != 0.0 || j == i) && lapd_value(mode, i, j, w[r], deg, dinv) != 0.0;
-            cnt += __popcll(__ballot(nz));
+    __shared__ int64_t s_scan[5];
+    __shared__ int32_t s_wcnt[4];
+    __shared__ int64_t s_excl;
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_long[kLapdTileRows / 64];  // rows of this tile past the stage (a bit per row)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int64_t tile = s_tile, r0 = tile * kLapdTileRows;
+    if (r0 >= n) return;
+    const int64_t i = r0 + tid;
+    const bool valid = i < n;
+    const int32_t c = valid ? scnt[i] : 0;
+    const bool lng = valid && c > kLapdCap;
+    const int32_t *rc = scol + (valid ? i : 0) * kLapdCap;
+    const double *rv = sval + (valid ? i : 0) * kLapdCap;
+    int64_t cnt = (valid && !lng) ? lapd_staged_row<false>(i, c, mode, rc, rv, deg, dinv, 0, nullptr, nullptr, 0) : 0;
+    const uint64_t lm = __ballot(lng);
+    if (lane == 0) s_long[wave] = lm;
+    __syncthreads();
+    for (int q = 0; q < 4; ++q) {  // (uniform: every thread walks the same list)
+        for (uint64_t m = s_long[q]; m; m &= m - 1) {
+            const int r = q * 64 + __ffsll((long long)m) - 1;
+            const int64_t t = lapd_dense_row<false>(r0 + r, n, mode, W, deg, dinv, 0, nullptr, nullptr, 0, s_wcnt);
+            if (tid == r) cnt = t;
         }
     }
-    const int64_t o = lookback(flags, i, cnt, lane, err);
-    int64_t out = o;
-    for (int64_t j0 = 0; j0 < n; j0 += 64 * kU) {
-        double w[kU];
-#pragma unroll
-        for (int r = 0; r < kU; ++r) {
-            const int64_t j = j0 + r * 64 + lane;
-            w[r] = j < n ? a[j] : 0.0;
-        }
-#pragma unroll
-        for (int r = 0; r < kU; ++r) {
-            const int64_t j = j0 + r * 64 + lane;
-            const double v = j < n && (w[r] != 0.0 || j == i) ? lapd_value(mode, i, j, w[r], deg, dinv) : 0.0;
-            const bool nz = v != 0.0;
-            const uint64_t m = __ballot(nz);
-            const int64_t pos = out + __popcll(m & ((1ull << lane) - 1ull));
-            if (nz && pos < l_cap) { l_idx[pos] = (int32_t)j; l_val[pos] = v; }
-            out += __popcll(m);
-        }
+    int64_t total;
+    const int64_t pre = block_exclusive_scan<int64_t>(cnt, s_scan, &total);
+    if (wave == 0) {
+        const int64_t ex = lookback(flags, tile, total, lane, err);
+        if (lane == 0) s_excl = ex;
     }
-    if (lane == 0) {
+    __syncthreads();
+    const int64_t o = s_excl + pre;
+    if (valid) {
         l_ptr[i] = o;
         if (i == n - 1) l_ptr[n] = o + cnt;
+        if (!lng) lapd_staged_row<true>(i, c, mode, rc, rv, deg, dinv, o, l_idx, l_val, l_cap);
+    }
+    for (int q = 0; q < 4; ++q) {
+        for (uint64_t m = s_long[q]; m; m &= m - 1) {
+            const int r = q * 64 + __ffsll((long long)m) - 1;
+            __shared__ int64_t s_o;
+            __syncthreads();
+            if (tid == r) s_o = o;
+            __syncthreads();
+            lapd_dense_row<true>(r0 + r, n, mode, W, deg, dinv, s_o, l_idx, l_val, l_cap, s_wcnt);
+        }
     }
 }
 
@@ -908,7 +939,8 @@ int32_t grf_laplacian_dense(int64_t n, const double *W, int32_t mode, int64_t *l
     GRF_REQUIRE_GRID(g, 256, "lapd_stage_kernel");
     lapd_stage_kernel<<<g, 256, 0, st>>>(n, W, mode, plan, deg, dinv, scnt, scol, sval, flags, ticket, err);
     GRF_CHECK_LAUNCH("lapd_stage_kernel");
-    lapd_emit_kernel<<<g, 256, 0, st>>>(n, W, mode, deg, dinv, scnt, scol, sval, flags, ticket, err, l_ptr, l_idx,
+    const unsigned gt = (unsigned)cdiv<int64_t>(n, kLapdTileRows);
+    lapd_emit_kernel<<<gt, 256, 0, st>>>(n, W, mode, deg, dinv, scnt, scol, sval, flags, ticket, err, l_ptr, l_idx,
                                         l_val, l_cap);
     GRF_CHECK_LAUNCH("lapd_emit_kernel");
     return GRF_OK;

@@ -392,3 +392,52 @@ def _empty_shard_gather_worker(rank, world, port, q):
 
 def test_gather_phi_empty_shard_same_path_gloo():
     assert _spawn(_empty_shard_gather_worker, 3) == [(r, True) for r in range(3)]
+
+
+def test_gather_model_counts_bucket_line_visits():
+    """bench.gather_model (roofline_gather): bucket (band b, column k) is read once per entry of column
+    k in bands <= b (symmetric tiles) or in any band (row tiles); lines from the descriptors' pairs
+    (line-aligned) or the span of a packed bucket.  Checked against a brute-force count."""
+    import types
+
+    import scipy.sparse as sp
+    import torch
+
+    import bench
+    from grf_amd import _lib as C
+    r = np.random.default_rng(5)
+    n, W = 37, 8
+    nb = -(-n // W)
+    dense = (r.random((n, n)) < 0.3) * r.standard_normal((n, n))
+    A = sp.csr_matrix(dense)
+    phi = types.SimpleNamespace(nnz=A.nnz, n_rows=n, ptr=torch.from_numpy(A.indptr.astype(np.int64)),
+                                idx=torch.from_numpy(A.indices.astype(np.int32)))
+    ent = np.zeros((nb, n), np.int64)
+    for i in range(n):
+        for k in A.indices[A.indptr[i]:A.indptr[i + 1]]:
+            ent[i // W, k] += 1
+    pairs = (ent + 1) // 2
+    for unit in (C.REC_LINE, C.REC_PACKED):
+        first = np.zeros((nb, n), np.int64)
+        pos = 0
+        for b in range(nb):
+            for k in range(n):
+                first[b, k] = pos
+                pos += -(-12 * pairs[b, k] // 128) if unit == C.REC_LINE else pairs[b, k]
+        desc = np.stack([first, pairs], -1).reshape(-1).astype(np.int32)
+        tr = types.SimpleNamespace(n_rows=n, n_cols=n, band_width=W, rec_unit=unit,
+                                   t_desc=torch.from_numpy(np.concatenate([desc, [0, 0]]).astype(np.int32)))
+        for sym in (True, False):
+            want_lines = want_rec = 0
+            for b in range(nb):
+                for k in range(n):
+                    visits = ent[:b + 1, k].sum() if sym else ent[:, k].sum()
+                    if unit == C.REC_LINE:
+                        lines = -(-12 * pairs[b, k] // 128)
+                    else:
+                        s0 = first[b, k] * 12
+                        lines = (s0 + 12 * pairs[b, k] - 1) // 128 - s0 // 128 + 1 if pairs[b, k] else 0
+                    want_lines += visits * lines
+                    want_rec += visits * pairs[b, k] * 12
+            got = bench.gather_model(phi, tr, sym=sym)
+            assert got[0] == want_lines and got[1] == want_rec, (unit, sym)
