@@ -714,36 +714,6 @@ __device__ int64_t lookback(uint64_t *flags, int64_t i, int64_t c, int lane, int
     return excl;
 }
 
-// One row of the emit pass from its staged pairs (c <= kLapdCap structural nonzeros, ascending columns)
-// merged with the diagonal, by one thread: counts its nonzeros (EMIT = false) or writes them from `o`.
-template <bool EMIT>
-__device__ int32_t lapd_staged_row(int64_t i, int32_t c, int32_t mode, const int32_t *rc, const double *rv,
-                                   const double *deg, const double *dinv, int64_t o, int32_t *l_idx, double *l_val,
-                                   int64_t l_cap) {
-    int32_t cnt = 0;
-    bool diag_done = false;
-    auto put = [&](int64_t col, double w) {
-        const double u = lapd_value(mode, i, col, w, deg, dinv);
-        if (u != 0.0) {
-            if (EMIT && o + cnt < l_cap) {
-                l_idx[o + cnt] = (int32_t)col;
-                l_val[o + cnt] = u;
-            }
-            ++cnt;
-        }
-    };
-    for (int32_t k = 0; k < c; ++k) {
-        const int64_t col = rc[k];
-        if (!diag_done && col >= i) {
-            if (col > i) put(i, 0.0);  // (the diagonal, w_ii = 0, before the first column past it)
-            diag_done = true;
-        }
-        put(col, rv[k]);
-    }
-    if (!diag_done) put(i, 0.0);
-    return cnt;
-}
-
 // A row with more structural nonzeros than the stage holds, by the whole workgroup (256 threads) over W's
 // row: counts (EMIT = false, the total in every thread) or writes from `o` in column order (chunks of 256
 // columns: wave ballots, then the waves' counts through LDS).
@@ -780,64 +750,180 @@ __device__ int64_t lapd_dense_row(int64_t i, int64_t n, int32_t mode, const doub
     return total;
 }
 
-// Tiles of 256 rows in ticket order: counts (one thread per staged row; the workgroup per long row), a
-// block scan, the look-back over the tiles' counts (wave 0), then the fill.  2708 rows (C3) are 11 tiles.
-constexpr int kLapdTileRows = 256;
+// Tiles of 64 rows in ticket order, 256 threads: every staged pair of the tile's rows is one work item
+// (rows laid end to end, each followed by one item for its diagonal), so the items' dependent loads
+// (pair -> D^-1/2 of its column) run side by side instead of row after row.  Pass 1: values, per-row
+// counts (LDS adds of integers), rows past the stage by the whole workgroup; a block scan of the counts;
+// the tile total published for the look-back over tiles (wave 0); pass 2: the items again, their places
+// from a running scan of the nonzero flags in item order.  An inserted diagonal (no explicit w_ii) goes
+// after the row's pairs with columns < i, which is where the items of columns > i are shifted by one.
+// (Measured: one wave per row with the look-back over rows took 124 us at C3, the chain of inclusive
+// prefixes advancing 64 rows per round trip; one thread per row of a 256-row tile 169 us, a hub row's
+// pairs walked by one thread.)
+constexpr int kLapdTileRows = 64;
 
 __global__ __launch_bounds__(256) void lapd_emit_kernel(int64_t n, const double *W, int32_t mode, const double *deg,
                                                         const double *dinv, const int32_t *scnt, const int32_t *scol,
                                                         const double *sval, uint64_t *flags, uint32_t *ticket,
                                                         int32_t *err, int64_t *l_ptr, int32_t *l_idx, double *l_val,
                                                         int64_t l_cap) {
-    __shared__ int64_t s_scan[5];
+    constexpr int R = kLapdTileRows;
+    __shared__ int32_t s_seg[R + 1];  // items before row r (pairs + 1 diagonal item per staged row)
+    __shared__ int32_t s_cnt[R];      // nonzeros of row r
+    __shared__ int32_t s_expl[R];     // row r has an explicit diagonal pair
+    __shared__ int32_t s_dnz[R];      // row r's inserted diagonal is a nonzero
+    __shared__ int32_t s_off[R + 1];  // nonzeros of the tile before row r
+    __shared__ int32_t s_lt[R];       // nonzero pairs of row r with columns < r0 + r
+    __shared__ int32_t s_nzp[R + 1];  // nonzero pairs (diagonal items excluded) of the tile before row r
+    __shared__ int32_t s_wsum[4];
     __shared__ int32_t s_wcnt[4];
     __shared__ int64_t s_excl;
     __shared__ uint32_t s_tile;
-    __shared__ uint64_t s_long[kLapdTileRows / 64];  // rows of this tile past the stage (a bit per row)
+    __shared__ uint64_t s_long;  // rows past the stage (bit r)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) s_tile = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < R) {
+        s_cnt[tid] = 0;
+        s_expl[tid] = 0;
+        s_lt[tid] = 0;
+    }
     __syncthreads();
-    const int64_t tile = s_tile, r0 = tile * kLapdTileRows;
+    const int64_t tile = s_tile, r0 = tile * R;
     if (r0 >= n) return;
-    const int64_t i = r0 + tid;
-    const bool valid = i < n;
-    const int32_t c = valid ? scnt[i] : 0;
-    const bool lng = valid && c > kLapdCap;
-    const int32_t *rc = scol + (valid ? i : 0) * kLapdCap;
-    const double *rv = sval + (valid ? i : 0) * kLapdCap;
-    int64_t cnt = (valid && !lng) ? lapd_staged_row<false>(i, c, mode, rc, rv, deg, dinv, 0, nullptr, nullptr, 0) : 0;
-    const uint64_t lm = __ballot(lng);
-    if (lane == 0) s_long[wave] = lm;
+    // rows -> item segments (wave 0, one lane per row)
+    if (wave == 0) {
+        const int64_t i = r0 + lane;
+        const int32_t c = i < n ? scnt[i] : 0;
+        const bool lng = i < n && c > kLapdCap;
+        const int32_t seg = (i < n && !lng) ? c + 1 : 0;
+        const int32_t inc = wave_inclusive_scan<int32_t>(seg);
+        s_seg[lane + 1] = inc;
+        if (lane == 0) s_seg[0] = 0;
+        const uint64_t lm = __ballot(lng);
+        if (lane == 0) s_long = lm;
+    }
     __syncthreads();
-    for (int q = 0; q < 4; ++q) {  // (uniform: every thread walks the same list)
-        for (uint64_t m = s_long[q]; m; m &= m - 1) {
-            const int r = q * 64 + __ffsll((long long)m) - 1;
-            const int64_t t = lapd_dense_row<false>(r0 + r, n, mode, W, deg, dinv, 0, nullptr, nullptr, 0, s_wcnt);
-            if (tid == r) cnt = t;
+    const int32_t E = s_seg[R];
+    // the item e -> (row r, position k in the row's segment): upper bound in s_seg
+    auto locate = [&](int32_t e, int &r, int32_t &k) {
+        int lo = 0, hi = R;  // s_seg[lo] <= e < s_seg[hi]
+#pragma unroll
+        for (int st = 0; st < 6; ++st) {
+            const int mid = (lo + hi) >> 1;
+            if (s_seg[mid] <= e) lo = mid;
+            else hi = mid;
+        }
+        r = lo;
+        k = e - s_seg[lo];
+    };
+    // pass 1a: the pairs (explicit diagonals flagged, nonzeros counted)
+    for (int32_t e = tid; e < E; e += 256) {
+        int r;
+        int32_t k;
+        locate(e, r, k);
+        const int64_t i = r0 + r;
+        const int32_t c = s_seg[r + 1] - s_seg[r] - 1;
+        if (k < c) {
+            const int64_t col = scol[i * kLapdCap + k];
+            const double u = lapd_value(mode, i, col, sval[i * kLapdCap + k], deg, dinv);
+            if (col == i) s_expl[r] = 1;
+            if (u != 0.0) {
+                atomicAdd(&s_cnt[r], 1);
+                if (col < i) atomicAdd(&s_lt[r], 1);
+            }
         }
     }
-    int64_t total;
-    const int64_t pre = block_exclusive_scan<int64_t>(cnt, s_scan, &total);
+    __syncthreads();
+    // pass 1b: the inserted diagonals (w_ii = 0) of rows with no explicit one
+    if (tid < R) {
+        const int64_t i = r0 + tid;
+        const bool staged = s_seg[tid + 1] > s_seg[tid];
+        const bool dnz = staged && !s_expl[tid] && lapd_value(mode, i, i, 0.0, deg, dinv) != 0.0;
+        s_dnz[tid] = dnz ? 1 : 0;
+        if (dnz) s_cnt[tid] += 1;
+    }
+    // rows past the stage: the whole workgroup over W's row (uniform loop)
+    for (uint64_t m = s_long; m; m &= m - 1) {
+        const int r = __ffsll((long long)m) - 1;
+        const int64_t t = lapd_dense_row<false>(r0 + r, n, mode, W, deg, dinv, 0, nullptr, nullptr, 0, s_wcnt);
+        if (tid == 0) s_cnt[r] = (int32_t)t;
+    }
+    __syncthreads();
     if (wave == 0) {
+        const int32_t cr = s_cnt[lane];
+        const int32_t inc = wave_inclusive_scan<int32_t>(cr);
+        s_off[lane + 1] = inc;
+        if (lane == 0) s_off[0] = 0;
+        const bool lng = (s_long >> lane) & 1;
+        const int32_t pz = wave_inclusive_scan<int32_t>(lng ? 0 : cr - s_dnz[lane]);
+        s_nzp[lane + 1] = pz;
+        if (lane == 0) s_nzp[0] = 0;
+        const int64_t total = __shfl(inc, 63, 64);
         const int64_t ex = lookback(flags, tile, total, lane, err);
         if (lane == 0) s_excl = ex;
     }
     __syncthreads();
-    const int64_t o = s_excl + pre;
-    if (valid) {
-        l_ptr[i] = o;
-        if (i == n - 1) l_ptr[n] = o + cnt;
-        if (!lng) lapd_staged_row<true>(i, c, mode, rc, rv, deg, dinv, o, l_idx, l_val, l_cap);
+    const int64_t base = s_excl;
+    if (tid < R && r0 + tid < n) {
+        const int64_t i = r0 + tid;
+        l_ptr[i] = base + s_off[tid];
+        if (i == n - 1) l_ptr[n] = base + s_off[tid + 1];
     }
-    for (int q = 0; q < 4; ++q) {
-        for (uint64_t m = s_long[q]; m; m &= m - 1) {
-            const int r = q * 64 + __ffsll((long long)m) - 1;
-            __shared__ int64_t s_o;
-            __syncthreads();
-            if (tid == r) s_o = o;
-            __syncthreads();
-            lapd_dense_row<true>(r0 + r, n, mode, W, deg, dinv, s_o, l_idx, l_val, l_cap, s_wcnt);
+    // pass 2: places by a running scan of the pairs' nonzero flags in item order (diagonal items: 0)
+    int32_t run = 0;  // nonzero pairs before this chunk
+    for (int32_t e0 = 0; e0 < E; e0 += 256) {
+        const int32_t e = e0 + tid;
+        int r = 0;
+        int32_t k = 0;
+        bool nz = false;
+        int64_t col = 0;
+        double u = 0.0;
+        if (e < E) {
+            locate(e, r, k);
+            const int32_t c = s_seg[r + 1] - s_seg[r] - 1;
+            if (k < c) {
+                const int64_t i = r0 + r;
+                col = scol[i * kLapdCap + k];
+                u = lapd_value(mode, i, col, sval[i * kLapdCap + k], deg, dinv);
+                nz = u != 0.0;
+            }
         }
+        const uint64_t m = __ballot(nz);
+        __syncthreads();  // (the previous chunk's wave sums are read)
+        if (lane == 0) s_wsum[wave] = __popcll(m);
+        __syncthreads();
+        int32_t before = run, chunk = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            before += q < wave ? s_wsum[q] : 0;
+            chunk += s_wsum[q];
+        }
+        if (nz) {
+            const int64_t i = r0 + r;
+            // this pair's rank among the tile's nonzero pairs, made row-local, placed after the row's own
+            // offset and after the inserted diagonal when its column is past i
+            const int32_t rank = before + __popcll(m & ((1ull << lane) - 1ull));
+            const int64_t pos = base + s_off[r] + (rank - s_nzp[r]) + ((s_dnz[r] && col > i) ? 1 : 0);
+            if (pos < l_cap) {
+                l_idx[pos] = (int32_t)col;
+                l_val[pos] = u;
+            }
+        }
+        run += chunk;
+    }
+    // the inserted diagonals: after the row's nonzero pairs with columns < i
+    if (tid < R && s_dnz[tid]) {
+        const int64_t i = r0 + tid;
+        const int64_t pos = base + s_off[tid] + s_lt[tid];
+        if (pos < l_cap) {
+            l_idx[pos] = (int32_t)i;
+            l_val[pos] = lapd_value(mode, i, i, 0.0, deg, dinv);
+        }
+    }
+    // rows past the stage: the whole workgroup fills from the row's offset
+    for (uint64_t m = s_long; m; m &= m - 1) {
+        const int r = __ffsll((long long)m) - 1;
+        lapd_dense_row<true>(r0 + r, n, mode, W, deg, dinv, base + s_off[r], l_idx, l_val, l_cap, s_wcnt);
     }
 }
 
