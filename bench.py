@@ -360,11 +360,9 @@ def main_c3(args):
 
     def front():
         G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY)
-        # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule (sync-free compaction:
-        # no host read inside the step)
-        phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False,
-                          sync_free=True)
-        return eng.densify(phi)
+        # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule, written straight into
+        # the dense fp32 Phi the Gram reads (no compaction, no memset: grf_densify_padded)
+        return eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False))
 
     def front_on_side():
         # independent of `main`: a front reads only the resident adjacency and writes fresh buffers
@@ -1132,8 +1130,7 @@ def mfma_leg(eng, args, steps: int = 20, workload: str = "c3"):
     n, m, L, p = W.shape[0], args.walks, args.length, args.p_halt
     f = diffusion_modulator(L, 1.0)
     G = eng.walk_matrix_dense(torch.from_numpy(W).to(eng.device), C.LAP_NUMPY)
-    phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False)
-    dense = eng.densify(phi)
+    dense = eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False))
     del G, W
     for _ in range(3):
         eng.gram_dense(dense, n)

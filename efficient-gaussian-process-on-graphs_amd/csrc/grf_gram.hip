@@ -587,6 +587,27 @@ __global__ __launch_bounds__(256) void densify_kernel(int64_t n_rows, const int6
     for (int64_t e = ptr[row] + lane; e < ptr[row + 1]; e += 64) out[row * lda + idx[e]] = val[e];
 }
 
+// The dense path's Phi straight from the walk's padded rows (no compaction): one workgroup per row builds the
+// zero-padded fp32 row in LDS (zero, scatter the row's entries, copy out with 16-B loads and stores), so the
+// row is written once, whole, with no separate memset pass over the matrix.
+__global__ __launch_bounds__(256) void densify_padded_kernel(int64_t cap, const int32_t *__restrict__ cnt,
+                                                             const int32_t *__restrict__ idx,
+                                                             const float *__restrict__ val, float *__restrict__ out,
+                                                             int64_t lda) {
+    extern __shared__ __attribute__((aligned(16))) float row[];  // [lda]
+    const int64_t r = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int q4 = (int)(lda >> 2);
+    for (int t = tid; t < q4; t += 256) reinterpret_cast<float4 *>(row)[t] = float4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    const int64_t b = r * cap;
+    const int c = cnt[r];
+    for (int e = tid; e < c; e += 256) row[idx[b + e]] = val[b + e];
+    __syncthreads();
+    float4 *o = reinterpret_cast<float4 *>(out + r * lda);
+    for (int t = tid; t < q4; t += 256) o[t] = reinterpret_cast<const float4 *>(row)[t];
+}
+
 // grf_gram_dense.hip: the dense path's MFMA Gram
 size_t dense_gram_workspace_bytes(int64_t n, int64_t k_dim);
 int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk, void *workspace,
@@ -972,6 +993,22 @@ int32_t grf_gram_dense_upper(int64_t n, int64_t k_dim, const float *A, int64_t l
 int32_t grf_gram_dense(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                        grf_stream_t stream) {
     return grf_gram_dense_ws(n, k_dim, A, lda, K, ldk, nullptr, 0, stream);
+}
+
+int32_t grf_densify_padded(int64_t n_rows, int64_t cap, int64_t n_cols, const int32_t *cnt, const int32_t *idx,
+                           const float *val, float *out, int64_t lda, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && cap >= 1 && n_cols >= 0 && cnt && idx && val && out && lda >= n_cols, GRF_EINVAL,
+                "grf_densify_padded: bad arguments");
+    GRF_REQUIRE(lda % 4 == 0 && ((uintptr_t)out & 15) == 0, GRF_EINVAL,
+                "grf_densify_padded: lda must be a multiple of 4 and out 16-byte aligned");
+    GRF_REQUIRE(lda * (int64_t)sizeof(float) <= 160 * 1024, GRF_EUNSUPPORTED,
+                "grf_densify_padded: a row of %lld floats does not fit one CU's LDS (use grf_densify)", (long long)lda);
+    if (n_rows == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(n_rows, 256, "densify_padded_kernel");
+    densify_padded_kernel<<<(unsigned)n_rows, 256, (size_t)lda * sizeof(float), S(stream)>>>(cap, cnt, idx, val, out,
+                                                                                           lda);
+    GRF_CHECK_LAUNCH("densify_padded_kernel");
+    return GRF_OK;
 }
 
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,

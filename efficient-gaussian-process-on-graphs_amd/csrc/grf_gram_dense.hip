@@ -37,6 +37,9 @@
 // GEMM" item 2): slab stores -> every wave vmcnt(0) -> barrier -> agent release -> ticket fetch_add; the
 // last arriver: agent acquire -> barrier -> plain loads.  The last arriver resets its ticket, so the
 // ticket block stays zero between launches (it must be zero on first use).
+// One wave per 128 x 128 tile (4 x 4 blocks, AccVGPR accumulators, one wave per SIMD) was built and measured in
+// round 5: half the fragment reads, but the LDS-DMA pieces per MFMA unchanged and their issue cost exposed
+// without a second wave per SIMD -- 0.645 vs 0.859 at C2 (profiles/r05_dense_w1_ab.txt); removed.
 #include "grf_common.h"
 
 namespace grf {
@@ -469,282 +472,6 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_sk_kernel(DenseArgs a) {
     }
 }
 
-// ------------------------------------------------------- one wave, a whole 128 x 128 tile (stream-K)
-// the 2 x 2-block wave tile reads one fragment per MFMA from LDS (8 ds_read_b128 per
-// 32 MFMAs) and its four waves meet at a barrier every k-tile; without those reads C2 ran 0.90.  Here ONE
-// wave owns a whole 128 x 128 tile as 4 x 4 blocks of v_mfma_f32_32x32x2f32 (256 accumulators: the
-// AccVGPR half of the register file, one wave per SIMD), so a k-step's 16 MFMAs take 8 fragments -- half
-// the reads per MFMA -- and the workgroup is that one wave: its LDS ring (4 stages x 8 KB, four
-// workgroups per CU) is filled by its own LDS-DMA and read by its own ds_reads, so no barrier at all, only
-// counted vmcnt / lgkmcnt waits.  A k-tile is 8 k (a 32-byte row segment: 1 KiB DMA piece = 32 rows);
-// chunk c of row r is stored at c ^ ((r >> 3) & 1) (conflict-free ds_read_b128 over the b128 lane
-// groups of MI355X_MICROARCH.md "LDS").  Diagonal tiles stage one operand and skip the 6 blocks below the
-// diagonal.  Same gfx950 hand-off as gram_dense_sk_kernel for tiles cut by slot boundaries.
-// k order: lane (r, h) holds k = 4h + s of a k-tile at step s; each entry is a fixed chain of exact f32
-// FMAs (run-to-run identical bits); diagonal tiles write entry (i, j >= i) to both places.
-constexpr int kW1BK = 8;
-constexpr int kW1NST = 4;
-constexpr int kW1StageF = 2 * kTile * kW1BK;  // floats per ring stage (A, then B)
-
-struct W1Frag {
-    f32x4v a[4], b[4];
-};
-
-template <bool DIAG>
-__device__ __forceinline__ void w1_kloop(float *lds, const float *const *srcA, const float *const *srcB, int64_t kb,
-                                         int64_t ke, uint32_t roff, f32x16 (&c)[4][4]) {
-    constexpr int G = DIAG ? 4 : 8;  // DMA pieces (1 KiB) per k-tile
-    const int64_t nk = (ke - kb) / kW1BK;
-    if (nk <= 0) return;
-    const uint32_t lds0 = lds_addr(lds);
-    auto piece = [&](int64_t t, int j) {
-        float *base = lds + (int)(t % kW1NST) * kW1StageF;
-        const int64_t k0 = kb + t * kW1BK;
-        if (j < 4) dma16(srcA[j] + k0, base + j * 256);
-        else dma16(srcB[j - 4] + k0, base + kTile * kW1BK + (j - 4) * 256);
-    };
-    auto issue = [&](int64_t t) {
-#pragma unroll
-        for (int j = 0; j < G; ++j) piece(t, j);
-    };
-    // fragment q (0..7: a0..a3, b0..b3) of k-tile t
-    auto read_q = [&](int64_t t, int q, W1Frag &f) {
-        const uint32_t As = lds0 + (uint32_t)(t % kW1NST) * (kW1StageF * 4) + roff;
-        const uint32_t Bs = DIAG ? As : As + kTile * kW1BK * 4;
-        switch (q) {
-            case 0: f.a[0] = ds_read16<0>(As); break;
-            case 1: f.a[1] = ds_read16<1024>(As); break;
-            case 2: f.a[2] = ds_read16<2048>(As); break;
-            case 3: f.a[3] = ds_read16<3072>(As); break;
-            case 4: if (!DIAG) f.b[0] = ds_read16<0>(Bs); break;
-            case 5: if (!DIAG) f.b[1] = ds_read16<1024>(Bs); break;
-            case 6: if (!DIAG) f.b[2] = ds_read16<2048>(Bs); break;
-            default: if (!DIAG) f.b[3] = ds_read16<3072>(Bs); break;
-        }
-    };
-    auto lgkm_done = [&](W1Frag &f) {
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.b[0]), "+v"(f.b[1]),
-                       "+v"(f.b[2]), "+v"(f.b[3])::"memory");
-    };
-    // the blocks of k-step s, the q-th quarter of them (4 MFMAs; diagonal tiles: the x <= y ones only)
-    auto mfma_q = [&](const W1Frag &f, int s, int q) {
-        const int x = q;
-#pragma unroll
-        for (int y = 0; y < 4; ++y) {
-            if (DIAG && y < x) continue;
-            const float av = f.a[x][s], bv = DIAG ? f.a[y][s] : f.b[y][s];
-            c[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, c[x][y], 0, 0, 0);
-        }
-    };
-    // k-tile t+1 landed: the pieces issued after it (k-tiles t+2, t+3 when they exist) may stay in flight
-    auto wait_next = [&](int64_t t) {
-        const int64_t after = (t + 2 < nk ? 1 : 0) + (t + 3 < nk ? 1 : 0);
-        if (after == 2) wait_vm<2 * G>();
-        else if (after == 1) wait_vm<G>();
-        else wait_vm<0>();
-    };
-    // One k-tile: k-steps 0 and 1 with k-tile t+3's DMA pieces between the MFMA quarters, the wait for
-    // k-tile t+1, k-step 2 with its 8 fragment reads, k-step 3 (1024+ MFMA cycles cover the reads).
-    auto tile_step = [&](int64_t t, const W1Frag &cur, W1Frag &nxt) {
-        const bool dma = t + 3 < nk;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                __builtin_amdgcn_sched_barrier(0);
-                mfma_q(cur, s, q);
-                __builtin_amdgcn_sched_barrier(0);
-                if (dma && (DIAG ? (q < 2) : true)) piece(t + 3, DIAG ? s * 2 + q : s * 4 + q);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < nk) wait_next(t);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (t + 1 < nk) {
-                read_q(t + 1, 2 * q, nxt);
-                read_q(t + 1, 2 * q + 1, nxt);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            mfma_q(cur, 2, q);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            __builtin_amdgcn_sched_barrier(0);
-            mfma_q(cur, 3, q);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < nk) lgkm_done(nxt);
-    };
-    // prologue: k-tiles 0 .. 2 in flight, k-tile 0 read
-    issue(0);
-    if (1 < nk) issue(1);
-    if (2 < nk) issue(2);
-    {
-        const int64_t after = (1 < nk ? 1 : 0) + (2 < nk ? 1 : 0);
-        if (after == 2) wait_vm<2 * G>();
-        else if (after == 1) wait_vm<G>();
-        else wait_vm<0>();
-    }
-    W1Frag fa, fb;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) read_q(0, q, fa);
-    lgkm_done(fa);
-    int64_t t = 0;
-    for (; t + 1 < nk; t += 2) {
-        tile_step(t, fa, fb);
-        tile_step(t + 1, fb, fa);
-    }
-    if (t < nk) tile_step(t, fa, fb);
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// the tile's entries to K: block (x, y), float4 group g of lane (r, h) = rows 32 x + 8 g + 4 h + 0..3,
-// column 32 y + r; each written to K[row][col] and mirrored to K[col][row] (diagonal blocks: col >= row).
-// get(x, y, g): the float4 (the accumulators, or the pieces of a split tile summed from their slabs).
-template <bool DIAG, typename Get>
-__device__ __forceinline__ void w1_write(const DenseArgs &a, Get get, int64_t m0, int64_t n0, int lane) {
-    const int64_t n = a.n, ldk = a.ldk;
-    float *K = a.K;
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-#pragma unroll
-        for (int y = 0; y < 4; ++y) {
-            if (DIAG && y < x) continue;
-            const bool dblk = DIAG && x == y;
-            __builtin_amdgcn_sched_barrier(0);  // (one block at a time: no register blow-up)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4v v = get(x, y, g);
-                const int64_t row = m0 + 32 * x + 8 * g + 4 * (lane >> 5), col = n0 + 32 * y + (lane & 31);
-                if (col >= n) continue;
-                if (!dblk && row + 3 < n) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) K[(row + q) * ldk + col] = v[q];
-                    *reinterpret_cast<f32x4v *>(K + col * ldk + row) = v;
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int64_t rr = row + q;
-                        if (rr < n && (!dblk || col >= rr)) {
-                            K[rr * ldk + col] = v[q];
-                            K[col * ldk + rr] = v[q];
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-constexpr int64_t kW1Slab = 64 * 64;  // float4 per piece: [16 blocks x 4 groups][64 lanes] (64 KiB)
-
-// A piece of a split tile: its accumulators to its slab, then the release / ticket / acquire protocol of
-// split_combine; returns true for the last arriver, which then writes the tile summed from the slabs in
-// piece order (w1_write with w1_slab_sum: its own piece is read back from its slab, the same bits).
-template <typename SlabOf>
-__device__ __forceinline__ bool w1_split_arrive(const DenseArgs &a, const f32x16 (&c)[4][4], int32_t *ticket,
-                                                int64_t pieces, int64_t me, SlabOf slab_of, int lane) {
-    f32x4v *mine = reinterpret_cast<f32x4v *>(a.slabs) + slab_of(me) * kW1Slab + lane;
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) {
-            __builtin_amdgcn_sched_barrier(0);
-            f32x4v *blk = mine + (x * 4 + y) * 4 * 64;
-            asm volatile("" : "+v"(blk));  // (computed here: 16 hoisted 64-bit addresses would cost 32 VGPRs)
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                blk[g * 64] = f32x4v{c[x][y][4 * g], c[x][y][4 * g + 1], c[x][y][4 * g + 2], c[x][y][4 * g + 3]};
-        }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int32_t last = 0;
-    if (lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int32_t old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old == pieces - 1;
-        if (last) {
-            __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    return __shfl(last, 0, 64) != 0;
-}
-
-// Stream-K over one-wave slots (4 per CU): slot s takes k-tile units [s U, (s + 1) U) of the 128-tiles laid
-// end to end, as gram_dense_sk_kernel (slabs 2 s / 2 s + 1, tickets by piece 0's slab).
-__global__ __launch_bounds__(64, 1) void gram_dense_w1_kernel(DenseArgs a) {
-    __shared__ __attribute__((aligned(16))) float lds[kW1NST * kW1StageF];
-    const int lane = threadIdx.x;
-    const int64_t U = a.sk_units, KT = a.sk_kt;
-    const int64_t u0 = (int64_t)blockIdx.x * U;
-    const int64_t u1 = u0 + U < a.sk_total ? u0 + U : a.sk_total;
-    // lane constants: DMA (row lane >> 1 of each 32-row piece, stored chunk lane & 1 = logical chunk kc)
-    // and the fragment read offset (row lane & 31, logical chunk lane >> 5, stored swizzled)
-    const int kc = (lane & 1) ^ ((lane >> 4) & 1);
-    const int rr = lane & 31;
-    const uint32_t roff = (uint32_t)((rr * kW1BK + 4 * ((lane >> 5) ^ ((rr >> 3) & 1))) * 4);
-    for (int64_t u = u0; u < u1;) {
-        const int64_t tile = u / KT, tb = tile * KT, te = tb + KT;
-        const int64_t se = u1 < te ? u1 : te;
-        int64_t bi, bj;
-        tile_coords(tile, a.nt, bi, bj);
-        const int64_t m0 = bi * kTile, n0 = bj * kTile;
-        const bool diag = bi == bj;
-        const float *srcA[4], *srcB[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int64_t ra = m0 + 32 * j + (lane >> 1), rb = n0 + 32 * j + (lane >> 1);
-            ra = ra < a.n ? ra : a.n - 1;  // (rows past n: valid rows, their products are never written)
-            rb = rb < a.n ? rb : a.n - 1;
-            srcA[j] = a.A + ra * a.lda + 4 * kc;
-            srcB[j] = a.A + rb * a.lda + 4 * kc;
-        }
-        f32x16 c[4][4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) c[x][y] = f32x16{};
-        const int64_t kb = (u - tb) * kW1BK, ke = (se - tb) * kW1BK;
-        if (diag) w1_kloop<true>(lds, srcA, srcB, kb, ke, roff, c);
-        else w1_kloop<false>(lds, srcA, srcB, kb, ke, roff, c);
-        if (u == tb && se == te) {  // a whole tile: written from the accumulators
-            auto from_acc = [&](int x, int y, int g) {
-                return f32x4v{c[x][y][4 * g], c[x][y][4 * g + 1], c[x][y][4 * g + 2], c[x][y][4 * g + 3]};
-            };
-            if (diag) w1_write<true>(a, from_acc, m0, n0, lane);
-            else w1_write<false>(a, from_acc, m0, n0, lane);
-        } else {
-            const int64_t s0 = tb / U, s1 = (te - 1) / U, pieces = s1 - s0 + 1;
-            const int64_t first = 2 * s0 + (tb == s0 * U ? 0 : 1);
-            auto slab_of = [&](int64_t j) { return j == 0 ? first : 2 * (s0 + j); };
-            if (w1_split_arrive(a, c, a.tickets + first, pieces, (int64_t)blockIdx.x - s0, slab_of, lane)) {
-                const f32x4v *slabs = reinterpret_cast<const f32x4v *>(a.slabs) + lane;
-                auto summed = [&](int x, int y, int g) {  // the pieces in order, from their slabs
-                    const int64_t o = ((x * 4 + y) * 4 + g) * 64;
-                    const f32x4v *p0 = slabs + slab_of(0) * kW1Slab + o;
-                    asm volatile("" : "+v"(p0));  // (no hoisted per-entry addresses)
-                    f32x4v acc = *p0;
-                    for (int64_t q = 1; q < pieces; ++q) {
-                        const f32x4v *pq = slabs + slab_of(q) * kW1Slab + o;
-                        asm volatile("" : "+v"(pq));
-                        acc += *pq;
-                    }
-                    return acc;
-                };
-                if (diag) w1_write<true>(a, summed, m0, n0, lane);
-                else w1_write<false>(a, summed, m0, n0, lane);
-            }
-        }
-        u = se;
-    }
-}
-
 constexpr int kCUs = 256;
 
 int env_int(const char *name, int dflt) {
@@ -755,7 +482,7 @@ int env_int(const char *name, int dflt) {
 // Workspace layout, the same for every (n, k): kMaxSplitTiles tickets at a fixed place, then the slabs.
 // A ticket is zero between launches (the last arriver resets it) and slabs never overlap the ticket
 // block, so one workspace, zeroed once, serves calls of any size in any order on its stream.
-constexpr int64_t kMaxSplitTiles = 4096;  // (tiles < 512 when all split; the tail is < 1024; w1 tickets < 2 x 1024)
+constexpr int64_t kMaxSplitTiles = 1024;  // (tiles < 512 when all split; the tail is < 1024)
 constexpr size_t kTicketBytes = kMaxSplitTiles * sizeof(int32_t);
 
 struct DensePlan {
@@ -821,25 +548,12 @@ SkPlan sk_plan(int64_t n, int64_t k_dim, int bk) {
     return p;
 }
 
-// The one-wave stream-K plan (gram_dense_w1_kernel): 1024 slots (one wave per SIMD), k-tiles of 8.
-SkPlan w1_plan(int64_t n, int64_t k_dim) {
-    SkPlan p{};
-    const int64_t nt = cdiv<int64_t>(n, kTile);
-    p.kt = cdiv<int64_t>(k_dim, kW1BK);
-    p.total = nt * (nt + 1) / 2 * p.kt;
-    const int64_t slots = std::min<int64_t>(4 * kCUs, std::max<int64_t>(p.total, 1));
-    p.units = std::max<int64_t>(1, cdiv<int64_t>(p.total, slots));
-    p.grid = cdiv<int64_t>(p.total, p.units);
-    p.ws_bytes = kTicketBytes + (size_t)(2 * p.grid) * kTile * kTile * sizeof(float);
-    return p;
-}
-
 }  // namespace
 
 size_t dense_gram_workspace_bytes(int64_t n, int64_t k_dim) {
     if (n <= 0) return 16;
     const DensePlan p = dense_plan(n, k_dim, 16);
-    return std::max<size_t>(16, std::max(std::max(p.ws_bytes, sk_plan(n, k_dim, 16).ws_bytes), w1_plan(n, k_dim).ws_bytes));
+    return std::max<size_t>(16, std::max(p.ws_bytes, sk_plan(n, k_dim, 16).ws_bytes));
 }
 
 int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk, void *workspace,
@@ -869,23 +583,6 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
     // even, below it the per-tile splits win (profiles/r04_dense_ab.txt).  GRF_DENSE_SK: 0 never, 1 always.
     static const int sk_env = env_int("GRF_DENSE_SK", -1);
     const bool sk = sk_env == 1 || (sk_env != 0 && p.tiles >= kCUs);
-    // GRF_DENSE_W1: 1 = the one-wave 128 x 128 tiles for the stream-K range, 0 = the four-wave tiles (read per
-    // call: tests run both)
-    const int w1_env = env_int("GRF_DENSE_W1", 0);
-    if (sk && w1_env == 1 && !upper_only) {
-        const SkPlan q = w1_plan(n, k_dim);
-        if (workspace && workspace_bytes >= q.ws_bytes && ((uintptr_t)workspace & 255) == 0 && q.kt * kW1BK <= lda) {
-            GRF_REQUIRE_GRID(q.grid, 64, "gram_dense_w1_kernel");
-            a.tickets = reinterpret_cast<int32_t *>(workspace);
-            a.slabs = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes);
-            a.sk_units = q.units;
-            a.sk_kt = q.kt;
-            a.sk_total = q.total;
-            gram_dense_w1_kernel<<<(unsigned)q.grid, 64, 0, st>>>(a);
-            GRF_CHECK_LAUNCH("gram_dense_w1_kernel");
-            return GRF_OK;
-        }
-    }
     if (sk) {
         const SkPlan q = sk_plan(n, k_dim, BK);
         if (workspace && workspace_bytes >= q.ws_bytes && ((uintptr_t)workspace & 255) == 0) {

@@ -629,7 +629,7 @@ __global__ __launch_bounds__(256) void lapd_stage_kernel(int64_t n, const double
         if (lane == 0) is.add(v);
         st.put(lane == 0 && v != 0.0, 0, v, false, 0, 0.0, lane);
     }
-    constexpr int kU = 8;  // 16-B loads in flight per lane
+    constexpr int kU = 16;  // 16-B loads in flight per lane (C3: a row in two rounds)
     for (int64_t p0 = 0; p0 < npair; p0 += 64 * kU) {
         double2 v[kU];
 #pragma unroll
@@ -715,34 +715,42 @@ __device__ int64_t lookback(uint64_t *flags, int64_t i, int64_t c, int lane, int
 }
 
 // A row with more structural nonzeros than the stage holds, by the whole workgroup (256 threads) over W's
-// row: counts (EMIT = false, the total in every thread) or writes from `o` in column order (chunks of 256
-// columns: wave ballots, then the waves' counts through LDS).
+// row: counts (EMIT = false, the total in every thread) or writes from `o` in column order.  A pass takes
+// 2048 columns, 8 consecutive ones per thread (four 16-B loads in flight), places by a block scan of the
+// threads' counts: Cora's 168-neighbour rows are 2 passes (were 11 chunks of 256 with two barriers each).
+constexpr int kLapdRowPer = 8;
+
 template <bool EMIT>
 __device__ int64_t lapd_dense_row(int64_t i, int64_t n, int32_t mode, const double *W, const double *deg,
                                   const double *dinv, int64_t o, int32_t *l_idx, double *l_val, int64_t l_cap,
-                                  int32_t *wcnt) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                  int64_t *scan) {
+    const int tid = threadIdx.x;
     const double *a = W + i * n;
     int64_t total = 0;
-    for (int64_t j0 = 0; j0 < n; j0 += 256) {
-        const int64_t j = j0 + tid;
-        const double w = j < n ? a[j] : 0.0;
-        const double v = j < n && (w != 0.0 || j == i) ? lapd_value(mode, i, j, w, deg, dinv) : 0.0;
-        const uint64_t m = __ballot(v != 0.0);
-        __syncthreads();  // (the previous chunk's counts are read)
-        if (lane == 0) wcnt[wave] = __popcll(m);
-        __syncthreads();
-        int64_t before = 0, chunk = 0;
+    for (int64_t j0 = 0; j0 < n; j0 += 256 * kLapdRowPer) {
+        const int64_t jb = j0 + (int64_t)tid * kLapdRowPer;
+        double v[kLapdRowPer];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            before += q < wave ? wcnt[q] : 0;
-            chunk += wcnt[q];
+        for (int q = 0; q < kLapdRowPer; ++q) {
+            const int64_t j = jb + q;
+            const double w = j < n ? a[j] : 0.0;
+            v[q] = j < n && (w != 0.0 || j == i) ? lapd_value(mode, i, j, w, deg, dinv) : 0.0;
         }
-        if (EMIT && v != 0.0) {
-            const int64_t pos = o + total + before + __popcll(m & ((1ull << lane) - 1ull));
-            if (pos < l_cap) {
-                l_idx[pos] = (int32_t)j;
-                l_val[pos] = v;
+        int64_t c = 0;
+#pragma unroll
+        for (int q = 0; q < kLapdRowPer; ++q) c += v[q] != 0.0 ? 1 : 0;
+        int64_t chunk;
+        int64_t pos = o + total + block_exclusive_scan<int64_t>(c, scan, &chunk);
+        if (EMIT) {
+#pragma unroll
+            for (int q = 0; q < kLapdRowPer; ++q) {
+                if (v[q] != 0.0) {
+                    if (pos < l_cap) {
+                        l_idx[pos] = (int32_t)(jb + q);
+                        l_val[pos] = v[q];
+                    }
+                    ++pos;
+                }
             }
         }
         total += chunk;
@@ -776,7 +784,7 @@ __global__ __launch_bounds__(256) void lapd_emit_kernel(int64_t n, const double 
     __shared__ int32_t s_lt[R];       // nonzero pairs of row r with columns < r0 + r
     __shared__ int32_t s_nzp[R + 1];  // nonzero pairs (diagonal items excluded) of the tile before row r
     __shared__ int32_t s_wsum[4];
-    __shared__ int32_t s_wcnt[4];
+    __shared__ int64_t s_rscan[5];
     __shared__ int64_t s_excl;
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_long;  // rows past the stage (bit r)
@@ -845,7 +853,7 @@ __global__ __launch_bounds__(256) void lapd_emit_kernel(int64_t n, const double 
     // rows past the stage: the whole workgroup over W's row (uniform loop)
     for (uint64_t m = s_long; m; m &= m - 1) {
         const int r = __ffsll((long long)m) - 1;
-        const int64_t t = lapd_dense_row<false>(r0 + r, n, mode, W, deg, dinv, 0, nullptr, nullptr, 0, s_wcnt);
+        const int64_t t = lapd_dense_row<false>(r0 + r, n, mode, W, deg, dinv, 0, nullptr, nullptr, 0, s_rscan);
         if (tid == 0) s_cnt[r] = (int32_t)t;
     }
     __syncthreads();
@@ -923,7 +931,7 @@ __global__ __launch_bounds__(256) void lapd_emit_kernel(int64_t n, const double 
     // rows past the stage: the whole workgroup fills from the row's offset
     for (uint64_t m = s_long; m; m &= m - 1) {
         const int r = __ffsll((long long)m) - 1;
-        lapd_dense_row<true>(r0 + r, n, mode, W, deg, dinv, base + s_off[r], l_idx, l_val, l_cap, s_wcnt);
+        lapd_dense_row<true>(r0 + r, n, mode, W, deg, dinv, base + s_off[r], l_idx, l_val, l_cap, s_rscan);
     }
 }
 

@@ -793,6 +793,18 @@ class GRFEngine:
                 "grf_densify")
         return out
 
+    def densify_padded(self, rows: PaddedRows) -> torch.Tensor:
+        """The dense fp32 Phi (zero-padded lda, as ``densify``) straight from the walk's padded rows, no
+        compaction (grf_densify_padded); rows too wide for one CU's LDS take compact + densify."""
+        n = rows.n_rows
+        lda = max(64, -(-rows.n_cols // 64) * 64)
+        if rows.val32 is None or lda * 4 > 160 * 1024:
+            return self.densify(self.compact(rows, want64=False, sync_free=True))
+        out = torch.empty((n, lda), dtype=torch.float32, device=self.device)
+        C.check(self.lib.grf_densify_padded(n, rows.cap, rows.n_cols, _p(rows.cnt), _p(rows.idx), _p(rows.val32),
+                                            _p(out), lda, self.stream), "grf_densify_padded")
+        return out
+
     def gram_dense(self, dense_phi: torch.Tensor, k_dim: int) -> torch.Tensor:
         n = dense_phi.shape[0]
         ldk = self.leading_dim(n)

@@ -70,7 +70,7 @@ enum grf_norm {
 
 /* The ABI revision of this header: grf_version() returns it, and a binding must refuse a library whose
  * revision differs (argument lists change between revisions). */
-#define GRF_ABI_VERSION 4
+#define GRF_ABI_VERSION 5
 
 const char *grf_last_error(void);
 int32_t grf_version(void);
@@ -422,6 +422,13 @@ int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda,
 /* CSR (float32) -> dense float32 [n_rows x lda], zero filled. */
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,
                     int64_t lda, grf_stream_t stream);
+/* The same from padded rows (grf_walk_phi's output: row r's cnt[r] entries at idx / val [r * cap, ...),
+ * columns < n_cols), with no compaction: every row written whole once (zeros included) through LDS.
+ * lda % 4 == 0, lda >= n_cols, lda * 4 <= 160 KiB (one CU's LDS), out 16-byte aligned.  ABI v5.
+ * Replaces the dense path's Phi = F f (efficient_graph_gp/graph_kernels/fast_grf_kernel_general.py:38)
+ * handed to the Gram as a dense matrix. */
+int32_t grf_densify_padded(int64_t n_rows, int64_t cap, int64_t n_cols, const int32_t *cnt, const int32_t *idx,
+                           const float *val, float *out, int64_t lda, grf_stream_t stream);
 
 /* -------------------------------------- GPflow surface: a dense (N, N, L) step tensor F
  * Replaces efficient_graph_gp/gpflow_kernels/general_kernel_fast_grf.py:74-77 and

@@ -206,7 +206,9 @@ def test_c5_column_block_path(eng):
 def test_c3_dense_leg_cora(eng):
     """C3: Cora through the dense path exactly as bench.py (--workload c3 / the MFMA leg) runs it:
     numpy-semantics dense Laplacian -> fused Philox walks -> Phi (dense sampler's divide-by-m rule)
-    -> densify -> MFMA Gram.  Oracle: the dense Laplacian, the same walks, NORM_DIV steps, Phi, K."""
+    -> the padded rows straight to the dense Phi (grf_densify_padded, the bench's front) -> MFMA Gram; the
+    dense Phi also equals compact + densify bit for bit.  Oracle: the dense Laplacian, the same walks,
+    NORM_DIV steps, Phi, K."""
     import torch
     from grf_amd import _lib as C
     from bench import cora_adjacency
@@ -215,8 +217,11 @@ def test_c3_dense_leg_cora(eng):
     n, m, L, p = W.shape[0], 128, 8, 0.1
     f = _diffusion(L)
     G = eng.walk_matrix_dense(torch.from_numpy(W).to(eng.device), C.LAP_NUMPY)
-    phi = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False), want64=False)
-    K = eng.gram_dense(eng.densify(phi), n).cpu().numpy()
+    rows = eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False)
+    phi = eng.compact(rows, want64=False)
+    dense = eng.densify_padded(rows)
+    assert torch.equal(dense, eng.densify(phi))
+    K = eng.gram_dense(dense, n).cpu().numpy()
     ip, ix, dx = O.dense_to_walk_csr(O.laplacian_dense(W, 0))
     node, load = O.walk_slots(ip, ix, dx, m, p, L, rng=O.RNG_PHILOX, seed=42, n_threads=N_THREADS)
     ref = O.phi_sparse(O.reduce_steps(node, load, O.NORM_DIV), f)

@@ -482,16 +482,8 @@ def test_gram_dense_asymmetric_layout(eng):
     np.testing.assert_allclose(K, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.fixture(params=["w4", "w1"])
-def dense_variant(request, monkeypatch):
-    """The stream-K range's two tile kernels: four waves per 128-tile (gram_dense_sk_kernel) and one wave
-    per 128-tile (gram_dense_w1_kernel, GRF_DENSE_W1=1, read by the library per call)."""
-    monkeypatch.setenv("GRF_DENSE_W1", "1" if request.param == "w1" else "0")
-    return request.param
-
-
 @pytest.mark.parametrize("n,k", [(300, 900), (2708, 2708), (1500, 4000), (4200, 1000), (4200, 20), (5000, 4999)])
-def test_gram_dense_split_k(eng, n, k, dense_variant):
+def test_gram_dense_split_k(eng, n, k):
     """Split-K dense Gram against fp64 and against the unsplit kernel (no workspace); exactly symmetric,
     run-to-run identical.  Small n: every tile cut into k-slices summed in order by the last piece; from
     256 tiles on (n >= 4200 here) the stream-K slots, whose pieces span slot boundaries -- k = 20 gives
@@ -517,9 +509,9 @@ def test_gram_dense_split_k(eng, n, k, dense_variant):
     assert np.array_equal(eng.gram_dense(At, k).cpu().numpy(), Ksn)
 
 
-def test_gram_dense_c2_size_stream_k(eng, dense_variant):
-    """the stream-K path at the bench's C2 size (n = k = 10 000, 3160 tiles; the one-wave
-    kernel's 1024 slots cut tiles at most k-tile boundaries) against fp64 on sampled rows, exactly
+def test_gram_dense_c2_size_stream_k(eng):
+    """the stream-K path at the bench's C2 size (n = k = 10 000, 3160 tiles over 512
+    slots: tiles cut at slot boundaries and summed through slabs) against fp64 on sampled rows, exactly
     symmetric, run-to-run identical bits."""
     import torch
     n = k = 10000
@@ -559,7 +551,7 @@ def test_gram_dense_workspace_reused_across_sizes(eng):
 
 
 @pytest.mark.parametrize("n", [2708, 4500])
-def test_gram_dense_first_call_on_dirty_allocator_block(eng, n, dense_variant):
+def test_gram_dense_first_call_on_dirty_allocator_block(eng, n):
     """Round 4's NaN (profiles/AB_LOG.md, "dense-Gram NaN"): the split-K tickets live in the caller's
     workspace and must be zero on first use; the engine once took it uninitialised from the caching
     allocator, whose block had held other data.  Here the allocator's free block is filled with 0xFF
