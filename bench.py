@@ -355,7 +355,9 @@ def main_c3(args):
     Wt = torch.from_numpy(W).to(eng.device)
     gram_ev = []        # the Gram in the timed (pipelined) steps
     gram_ev_alone = []  # the Gram in the serial steps (nothing beside it): the roofline's time
-    side = torch.cuda.Stream(eng.device)  # the next step's front runs here beside this step's Gram
+    # the next step's front runs here beside this step's Gram (--side-priority high: the stream's workgroups
+    # are dispatched ahead of the Gram's when both wait for a CU slot)
+    side = torch.cuda.Stream(eng.device, priority=-1 if args.side_priority == "high" else 0)
     main = torch.cuda.current_stream(eng.device)
 
     def front():
@@ -549,6 +551,8 @@ def main():
     ap.add_argument("--fingerprint-dir", default=None,
                     help="write a bit-level fingerprint of every rank's K block (tools/gram_hash.py) to "
                          "DIR/rank<r>.json after the run (the multi-rank at-size parity test)")
+    ap.add_argument("--side-priority", choices=["normal", "high"], default="normal",
+                    help="pipelined steps: the HIP priority of the stream the next front runs on")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
     ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
@@ -620,7 +624,8 @@ def main():
     walk_ev = []  # (start, end) events around walk_phi in the serial-latency steps (kernel alone)
     last = [None]
 
-    side = torch.cuda.Stream(dev)  # the next step's front runs here while the Gram runs on `main`
+    # the next step's front runs here while the Gram runs on `main` (--side-priority: see main_c3)
+    side = torch.cuda.Stream(dev, priority=-1 if args.side_priority == "high" else 0)
     main = torch.cuda.current_stream(dev)
 
     if args.front_at is None:
