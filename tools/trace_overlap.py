@@ -10,7 +10,7 @@ ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"
 keys = sys.argv[2:]
 alone, shared = defaultdict(list), defaultdict(list)
 for i, (s, e, name) in enumerate(ev):
-    short = name.split("(")[0].replace("void ", "")[:70]
+    short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[:70]
     if keys and not any(k in name for k in keys):
         continue
     ov = any(s2 < e and e2 > s for j, (s2, e2, _) in enumerate(ev) if j != i and abs(j - i) < 64)
