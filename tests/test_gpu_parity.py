@@ -670,7 +670,8 @@ def test_walk_phi_csr_matches_padded_plus_compaction(eng, n, deg, m, L, p, rule)
         assert torch.equal(got.idx[:nnz], ref.idx[:nnz]) and torch.equal(got.val32[:nnz], ref.val32[:nnz])
         assert torch.equal(got.val[:nnz], ref.val[:nnz])
         assert torch.equal(eng.phi_row_shifts(got), eng.phi_row_shifts(ref)), (b, e)
-        assert torch.equal(got.row_stats, ref.row_stats), (b, e)
+        rows = e - b  # (the statistics: row max |Phi| as float32 at the blob's start; padding bytes differ)
+        assert torch.equal(got.row_stats[:4 * rows], ref.row_stats[:4 * rows]), (b, e)
     # the kernel's bucket counts for the transpose of its own rows
     bw = 128
     ws1, ws2 = eng.transpose_workspace(n, n, bw), eng.transpose_workspace(n, n, bw)
