@@ -671,6 +671,49 @@ __global__ __launch_bounds__(256) void lapd_stage_kernel(int64_t n, const double
     }
 }
 
+typedef __attribute__((address_space(1))) uint64_t gu64_t;
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1ull;
+
+// Decoupled look-back (R2 granules: the 8-byte word {status, value} is the whole hand-off, written and
+// polled by relaxed agent-scope atomics; cdna_hip_programming.md Guideline 16).  Publishes this row's
+// count, returns the exclusive prefix of the counts before it.  Bounded spins: after ~2^20 polls of an
+// unpublished word (a predecessor that never ran: impossible under the ticket order) *err is set and the
+// wave goes on (its row pointer is then wrong; the word is left for a debugger, the launch still ends).
+__device__ int64_t lookback(uint64_t *flags, int64_t i, int64_t c, int lane, int32_t *err) {
+    gu64_t *f = (gu64_t *)flags;
+    if (lane == 0) __hip_atomic_store(f + i, (i == 0 ? kLbIncl : kLbAgg) | (uint64_t)c, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    if (i == 0) return 0;
+    int64_t excl = 0, pos = i - 1;
+    for (;;) {
+        const int64_t idx = pos - lane;
+        uint64_t w = kLbIncl;  // (before row 0: an inclusive zero)
+        if (idx >= 0) {
+            for (uint32_t spin = 0;; ++spin) {
+                w = __hip_atomic_load(f + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((w >> 62) != 0) break;
+                if (spin > (1u << 20)) {
+                    *err = 1;
+                    w = kLbIncl;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        const uint64_t incl = __ballot((w >> 62) == 2);
+        const int64_t v = (int64_t)(w & kLbVal);
+        if (incl) {
+            const int k = __ffsll((long long)incl) - 1;
+            excl += wave_sum<int64_t>(lane <= k ? v : 0);
+            break;
+        }
+        excl += wave_sum<int64_t>(v);
+        pos -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(f + i, kLbIncl | (uint64_t)(excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 // A row with more structural nonzeros than the stage holds, by the whole workgroup (256 threads) over W's
 // row: counts (EMIT = false, the total in every thread) or writes from `o` in column order.  A pass takes
 // 2048 columns, 8 consecutive ones per thread (four 16-B loads in flight), places by a block scan of the

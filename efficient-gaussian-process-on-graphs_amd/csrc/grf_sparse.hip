@@ -1192,16 +1192,6 @@ static void row_stats_layout(void *workspace, int64_t n_rows, float *&row_max, d
     row_sum = (double *)(w + tr_align((size_t)n_rows * 4));
     wg_max = (float *)(w + tr_align((size_t)n_rows * 4) + tr_align((size_t)n_rows * 8));
 }
-}  // extern "C"
-#pragma GCC visibility push(hidden)
-namespace grf {
-// (for grf_steps.hip: the walk kernel's compact output leaves the same statistics)
-void row_stats_layout_ext(void *workspace, int64_t n_rows, float *&row_max, double *&row_sum, float *&wg_max) {
-    row_stats_layout(workspace, n_rows, row_max, row_sum, wg_max);
-}
-}  // namespace grf
-#pragma GCC visibility pop
-extern "C" {
 
 int32_t grf_compact_rows_stats(int64_t n_rows, int64_t cap, const int32_t *cnt, const int64_t *out_ptr,
                                const int32_t *in_idx, const double *in_val, const float *in_val32, int32_t *out_idx,

@@ -21,8 +21,6 @@
 
 namespace grf {
 
-void row_stats_layout_ext(void *workspace, int64_t n_rows, float *&row_max, double *&row_sum, float *&wg_max);
-
 __device__ inline double normalise(double acc, int32_t norm, int64_t m) {
     return norm == GRF_NORM_DIV ? acc / (double)m : acc * (1.0 / (double)m);
 }
@@ -162,11 +160,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
                                                         double *__restrict__ phi_val, float *__restrict__ phi_val32,
                                                         int32_t *__restrict__ t_count, int64_t band_width,
-                                                        int64_t n_cols, int64_t count_row0, int32_t sort_lds,
-                                                        int64_t *__restrict__ phi_ptr, uint64_t *lb_flags,
-                                                        uint32_t *lb_ticket, int32_t *lb_err, int64_t n_src,
-                                                        float *__restrict__ st_row_max, double *__restrict__ st_row_sum,
-                                                        float *st_wg_max) {
+                                                        int64_t n_cols, int64_t count_row0, int32_t sort_lds) {
     // LDS: ld [E] loads by slot (later the compacted step values), fl [Lf] the modulator,
     // scratch (2 x 16 ints), key [P] the sorted keys (later the compacted step keys).  32-bit
     // keys when (node, step, walk) fits 32 bits (C4 / C5): half the sort's LDS traffic and a
@@ -178,16 +172,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     int32_t *scratch = reinterpret_cast<int32_t *>(fl + ((Lf + 1) & ~1));  // [32]
     KT *key = reinterpret_cast<KT *>(scratch + 32);             // [P]
     const KT kNone = (KT)~(KT)0;
-    // compact output (phi_ptr != NULL): sources in ticket order, so the look-back below only waits on
-    // workgroups that are already running
-    __shared__ uint32_t s_ticket;
-    __shared__ int64_t s_base;
-    int64_t s = blockIdx.x;
-    if (phi_ptr) {
-        if (tid == 0) s_ticket = __hip_atomic_fetch_add(lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        s = s_ticket;
-    }
+    const int64_t s = blockIdx.x;
     const Norm nrm(norm, m);
     const int sh = wbits + lbits;
     const KT wmask = (KT)(((KT)1 << wbits) - 1), lmask = (KT)(((KT)1 << lbits) - 1);
@@ -354,25 +339,11 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     }
     int32_t total;
     int32_t rank = block_exclusive_scan_fast<int32_t>(emit, scratch + 16, &total);
-    int64_t obase = s * cap;
-    if (phi_ptr) {  // the row's place in the compact CSR: decoupled look-back over the sources (wave 0)
-        if (tid < 64) {
-            const int64_t b = lookback(lb_flags, s, total, tid, lb_err);
-            if (tid == 0) s_base = b;
-        }
-        __syncthreads();
-        obase = s_base;
-        if (tid == 0) {
-            phi_ptr[s] = obase;
-            if (s == n_src - 1) phi_ptr[n_src] = obase + total;
-        }
-    }
-    float *stage = reinterpret_cast<float *>(ld);  // (|Phi| in row order for the stats; ld is consumed)
+    const int64_t obase = s * cap;
 #pragma unroll
     for (int qq = 0; qq < kPer; ++qq) {
         if (pn_[qq] >= 0) {
             if (rank < cap) {
-                if (st_row_max) stage[rank] = fabsf((float)pv_[qq]);
                 phi_idx[obase + rank] = pn_[qq];
                 if (phi_val) phi_val[obase + rank] = pv_[qq];  // (NULL: the caller keeps the f32 copy only)
                 if (phi_val32) phi_val32[obase + rank] = (float)pv_[qq];
@@ -382,29 +353,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
             ++rank;
         }
     }
-    if (tid == 0 && phi_cnt) phi_cnt[s] = total < cap ? total : (int32_t)cap;
-    if (st_row_max) {
-        // the Gram shift statistics of the row, in compact_rows_stats_kernel's order (lane-strided fp64 sum,
-        // butterfly max): the same bits as grf_compact_rows_stats
-        __syncthreads();
-        if (tid < 64) {
-            float mx = 0.f;
-            double sm = 0.0;
-            for (int e = tid; e < total; e += 64) {
-                const float a = stage[e];
-                mx = fmaxf(mx, a);
-                sm += (double)a;
-            }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-            sm = wave_sum<double>(sm);
-            if (tid == 0) {
-                st_row_max[s] = mx;
-                st_row_sum[s] = sm;
-                atomicMax(reinterpret_cast<int32_t *>(st_wg_max) + (s >> 2), __float_as_int(mx));  // (mx >= 0)
-            }
-        }
-    }
+    if (tid == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
 }
 
 // ---------------------------------------------- augmented walk matrix (philox_walk_aug)
@@ -468,8 +417,6 @@ using namespace grf;
 extern "C" {
 #pragma GCC visibility push(default)
 
-size_t grf_phi_row_shifts_workspace_bytes(int64_t n_rows);
-
 int32_t grf_steps(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
                   const double *slot_load, int32_t *step_cnt, int32_t *step_idx, double *step_val,
                   grf_stream_t stream) {
@@ -522,10 +469,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
                                 int32_t rule, uint64_t seed,
                                 int64_t src_begin, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
                                 int32_t *phi_idx, double *phi_val, float *phi_val32, int32_t *t_count,
-                                int64_t band_width, int64_t n_cols, hipStream_t st, int64_t count_row0 = 0,
-                                int64_t *phi_ptr = nullptr, uint64_t *lb_flags = nullptr, uint32_t *lb_ticket = nullptr,
-                                int32_t *lb_err = nullptr, float *st_row_max = nullptr, double *st_row_sum = nullptr,
-                                float *st_wg_max = nullptr) {
+                                int64_t band_width, int64_t n_cols, hipStream_t st, int64_t count_row0 = 0) {
     GRF_REQUIRE(norm == GRF_NORM_DIV || norm == GRF_NORM_MUL_RECIP, GRF_EINVAL, "grf_phi_fused: bad norm");
     GRF_REQUIRE(n_f >= 0 && (n_f == 0 || f), GRF_EINVAL, "grf_phi_fused: bad modulator");
     GRF_REQUIRE(m * (int64_t)L <= 4096, GRF_EUNSUPPORTED, "grf_phi_fused: needs walks_per_node * L <= 4096");
@@ -569,8 +513,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val,                                   \
         reinterpret_cast<const unsigned char *>(g_aug), p_halt, rule, (uint32_t)seed,                               \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
-        n_cols, count_row0, sort_lds, phi_ptr, lb_flags, lb_ticket, lb_err, n_src, st_row_max, st_row_sum,           \
-        st_wg_max)
+        n_cols, count_row0, sort_lds)
 #define GRF_PHI_LAUNCH_KT(W, K, KT) GRF_PHI_LAUNCH_KTT(W, K, KT, 0)
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
     do {                                                                                                          \
@@ -634,57 +577,6 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
     return phi_fused_launch(true, src_end - src_begin, P.walks_per_node, P.max_walk_length, norm, nullptr, nullptr,
                             g_ptr, g_idx, g_val, g_aug, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, phi_cnt,
                             phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream), count_row0);
-}
-
-size_t grf_walk_phi_csr_workspace_bytes(int64_t n_src) {
-    return (((size_t)(n_src > 0 ? n_src : 1) * sizeof(uint64_t) + 255) & ~(size_t)255) + 256;
-}
-
-int32_t grf_walk_phi_csr(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
-                         const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm,
-                         const double *f, int32_t n_f, int64_t phi_cap, int64_t *phi_ptr, int32_t *phi_idx,
-                         double *phi_val, float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
-                         void *stats, size_t stats_bytes, void *workspace, size_t workspace_bytes,
-                         grf_stream_t stream) {
-    GRF_REQUIRE(params != nullptr, GRF_EINVAL, "grf_walk_phi_csr: params is NULL");
-    const grf_walk_params P = *params;
-    GRF_REQUIRE(n >= 0 && g_ptr && phi_ptr && phi_idx && (phi_val || phi_val32), GRF_EINVAL,
-                "grf_walk_phi_csr: bad arguments");
-    GRF_REQUIRE(0 <= src_begin && src_begin <= src_end && src_end <= n, GRF_EINVAL, "grf_walk_phi_csr: bad source range");
-    const int64_t ns = src_end - src_begin;
-    GRF_REQUIRE(phi_cap >= std::min<int64_t>(P.walks_per_node * (int64_t)P.max_walk_length, n), GRF_EINVAL,
-                "grf_walk_phi_csr: phi_cap must hold a whole row (min(walks_per_node * max_walk_length, n))");
-    GRF_REQUIRE(workspace && workspace_bytes >= grf_walk_phi_csr_workspace_bytes(ns) && ((uintptr_t)workspace & 255) == 0,
-                GRF_EINVAL, "grf_walk_phi_csr: workspace too small or not 256-byte aligned");
-    GRF_REQUIRE(!stats || (stats_bytes >= grf_phi_row_shifts_workspace_bytes(ns) && phi_val32), GRF_EINVAL,
-                "grf_walk_phi_csr: stats needs grf_phi_row_shifts_workspace_bytes(rows) bytes and fp32 values");
-    GRF_REQUIRE(P.rng == GRF_RNG_PHILOX, GRF_EUNSUPPORTED, "grf_walk_phi_csr: Philox walks only");
-    hipStream_t st = S(stream);
-    GRF_CHECK_HIP(hipMemsetAsync(workspace, 0, grf_walk_phi_csr_workspace_bytes(ns), st));
-    if (ns == 0) {
-        GRF_CHECK_HIP(hipMemsetAsync(phi_ptr, 0, sizeof(int64_t), st));
-        return GRF_OK;
-    }
-    const size_t fl_bytes = ((size_t)ns * sizeof(uint64_t) + 255) & ~(size_t)255;
-    uint64_t *flags = (uint64_t *)workspace;
-    uint32_t *ticket = (uint32_t *)((char *)workspace + fl_bytes);
-    int32_t *err = (int32_t *)((char *)workspace + fl_bytes + 16);
-    float *row_max = nullptr, *wg_max = nullptr;
-    double *row_sum = nullptr;
-    if (stats) {
-        row_stats_layout_ext(stats, ns, row_max, row_sum, wg_max);
-        GRF_CHECK_HIP(hipMemsetAsync(wg_max, 0, (size_t)cdiv<int64_t>(ns, 4) * sizeof(float), st));
-    }
-    GRF_REQUIRE(P.walks_per_node >= 1 && P.max_walk_length >= 1 && P.p_halt >= 0.0 && P.p_halt < 1.0 &&
-                    P.load_rule >= 0 && P.load_rule <= 2 && n <= 0x7fffffffLL,
-                GRF_EINVAL, "grf_walk_phi_csr: bad walk parameters");
-    GRF_REQUIRE(!t_count || (band_width >= 1 && 0 <= count_row0 && count_row0 <= src_begin), GRF_EINVAL,
-                "grf_walk_phi_csr: counting needs band_width >= 1 and count_row0 in [0, src_begin]");
-    GRF_REQUIRE(!g_aug || ((uintptr_t)g_aug & 31) == 0, GRF_EINVAL, "grf_walk_phi_csr: g_aug must be 32-byte aligned");
-    return phi_fused_launch(true, ns, P.walks_per_node, P.max_walk_length, norm, nullptr, nullptr, g_ptr, g_idx, g_val,
-                            g_aug, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, nullptr, phi_idx, phi_val,
-                            phi_val32, t_count, band_width, n, st, count_row0, phi_ptr, flags, ticket, err, row_max,
-                            row_sum, wg_max);
 }
 
 size_t grf_walk_aug_bytes(int64_t nnz) { return kAugHeader + (size_t)(nnz > 0 ? nnz : 0) * sizeof(AugRec); }

@@ -65,10 +65,6 @@ SIGNATURES = {
     "grf_walk_aug_bytes": (_sz, [_i64]),
     "grf_walk_phi": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32, _i64,
                              _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
-    "grf_walk_phi_csr_workspace_bytes": (_sz, [_i64]),
-    "grf_walk_phi_csr": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32,
-                                _i64, _vp, _vp, _vp, _vp, _vp,
-                                _i64, _i64, _vp, _sz, _vp, _sz, _vp]),
     "grf_phi_fused": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_scan_workspace_bytes": (_sz, [_i64]),

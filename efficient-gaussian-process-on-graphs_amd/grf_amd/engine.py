@@ -362,43 +362,6 @@ class GRFEngine:
                 "grf_walk_phi")
         return PaddedRows(cnt, idx, val, v32, cap, n)
 
-    def walk_phi_csr(self, G: DeviceCSR, walks_per_node: int, p_halt: float, max_walk_length: int, f, *,
-                     seed: int = 42, load_rule: int = C.LOAD_CUMULATIVE, norm: int = C.NORM_MUL_RECIP,
-                     src_begin: int = 0, src_end: Optional[int] = None, count_ws: Optional[torch.Tensor] = None,
-                     band_width: int = 0, count_origin: int = 0, want64: bool = False,
-                     stats: bool = False) -> DeviceCSR:
-        """``compact(walk_phi(...), sync_free=True)`` in ONE kernel (grf_walk_phi_csr): every source's row is
-        placed after its predecessors' by a decoupled look-back, so there is no padded buffer pass and no
-        compaction launch.  Same entries and bits; fp32 values always (fp64 too with want64); stats: the
-        rows' Gram shift statistics (as compact(..., stats=True))."""
-        n = G.n_rows
-        src_end = n if src_end is None else src_end
-        m, L = int(walks_per_node), int(max_walk_length)
-        if m < 1 or L < 1:
-            raise ValueError("walks_per_node and max_walk_length must be >= 1")
-        ft = self._f(f)
-        ns = src_end - src_begin
-        cap = max(1, min(m * L, n))
-        bound = max(ns * cap, 1)
-        ptr = self._empty(ns + 1, torch.int64)
-        idx = self._empty(bound, torch.int32)
-        v64 = self._empty(bound, torch.float64) if want64 else None
-        v32 = self._empty(bound, torch.float32)
-        st = None
-        if stats:
-            st = torch.empty(int(self.lib.grf_phi_row_shifts_workspace_bytes(ns)), dtype=torch.uint8, device=self.device)
-        ws = self._ws(self.lib.grf_walk_phi_csr_workspace_bytes(ns))
-        prm = C.GrfWalkParams(m, float(p_halt), L, int(load_rule), C.RNG_PHILOX, 0, 1, int(seed) & 0xFFFFFFFFFFFFFFFF)
-        aug = self.walk_aug(G)
-        C.check(self.lib.grf_walk_phi_csr(n, _p(G.ptr), _p(G.idx), _p(G.val), _p(aug), ctypes.byref(prm), src_begin,
-                                          src_end, norm, _p(ft), ft.numel(), cap, _p(ptr), _p(idx), _p(v64), _p(v32),
-                                          _p(count_ws), int(band_width), int(count_origin), _p(st),
-                                          0 if st is None else st.numel(), _p(ws), ws.numel(), self.stream),
-                "grf_walk_phi_csr")
-        out = DeviceCSR(ns, n, ptr, idx, v64, v32, None, nnz_bound=bound)
-        out.row_stats = st
-        return out
-
     def walk_aug(self, G: DeviceCSR) -> Optional[torch.Tensor]:
         """The augmented walk matrix of G (grf_walk_aug), built once per DeviceCSR; None when
         nnz >= 2^32 (the walk then reads the row bounds per step)."""

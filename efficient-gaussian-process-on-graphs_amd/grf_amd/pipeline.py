@@ -35,9 +35,6 @@ COMPACT_STATS = os.environ.get("GRF_COMPACT_STATS", "1") == "1"
 # not at the mirror (Enron 8.66-8.68 -> 8.13-8.23 ms per K, profiles/r03_hub_early_front_ab.txt;
 # GRF_HUB_EARLY_FRONT=0: at the mirror)
 HUB_EARLY_FRONT = os.environ.get("GRF_HUB_EARLY_FRONT", "1") == "1"
-# the walk writes Phi's rows compact (grf_walk_phi_csr: look-back placement, no padded buffer pass, no
-# compaction launch); GRF_WALK_CSR=0: padded rows + compact_rows (A/B)
-WALK_CSR = os.environ.get("GRF_WALK_CSR", "1") == "1"
 
 
 @dataclass
@@ -154,16 +151,10 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
         # walk counts its buckets when the block is all of the rank's rows
         fused = pl.kr_end == e and not SELF_COUNT_TRANSPOSE
         tws = eng.transpose_workspace(pl.block_rows, n, pl.band_width) if fused else None
-        stats = COMPACT_STATS and not pl.collective
-        if WALK_CSR:
-            local = eng.walk_phi_csr(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
-                                     count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
-                                     stats=stats)
-        else:
-            local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
-                                             count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
-                                             want64=False),
-                                want64=False, want32=True, sync_free=True, stats=stats)
+        local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
+                                         count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
+                                         want64=False),
+                            want64=False, want32=True, sync_free=True, stats=COMPACT_STATS and not pl.collective)
         phi = gather_phi(eng, local, group=pl.group, shards=pl.shards, entries_bound=pl.gather_bound or None,
                          row_cap=pl.rows_cap, always=True) if pl.collective else local
         blk = local if fused else DeviceCSR(pl.block_rows, n, local.ptr[:pl.block_rows + 1], local.idx, None,
@@ -184,14 +175,10 @@ def front_walk(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan, G: Optional[Devic
     G = eng.laplacian(A_dev) if G is None else G
     # (the transpose counts its own buckets unless GRF_TRANSPOSE_SELF=0: then the walk counts them)
     tws = None if SELF_COUNT_TRANSPOSE else eng.transpose_workspace(n, n, pl.band_width)
-    if WALK_CSR:
-        local = eng.walk_phi_csr(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
-                                 count_ws=tws, band_width=pl.band_width if tws is not None else 0)
-    else:
-        local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
-                                         count_ws=tws, band_width=pl.band_width if tws is not None else 0,
-                                         want64=False),
-                            want64=False, want32=True, sync_free=True)
+    local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
+                                     count_ws=tws, band_width=pl.band_width if tws is not None else 0,
+                                     want64=False),
+                        want64=False, want32=True, sync_free=True)
     phi = gather_phi(eng, local, tws, group=pl.group, band_width=pl.band_width, shards=pl.shards,
                      entries_bound=pl.gather_bound or None, row_cap=pl.rows_cap, always=True) if pl.collective else local
     fr = Front(phi, None, local)

@@ -182,21 +182,6 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
                      int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
                      float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
                      grf_stream_t stream);
-
-/* grf_walk_phi with the rows written COMPACT (CSR) instead of padded: phi_ptr [n_src + 1] int64 is filled by
- * the kernel itself (each source's workgroup places its row after its predecessors' by a decoupled look-back
- * over the sources, in ticket order), so no compaction pass follows; phi_idx / phi_val / phi_val32 need room
- * for n_src * phi_cap entries (the bound; the rows are packed from 0).  Same entries, same order, same bits as
- * grf_walk_phi + grf_compact_rows.  stats (optional, grf_phi_row_shifts_workspace_bytes(n_src) bytes): the
- * rows' Gram shift statistics exactly as grf_compact_rows_stats leaves them, for grf_phi_row_shifts_stats.
- * workspace: grf_walk_phi_csr_workspace_bytes(n_src) bytes, 256-byte aligned (zeroed by the call).  ABI v5. */
-size_t grf_walk_phi_csr_workspace_bytes(int64_t n_src);
-int32_t grf_walk_phi_csr(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
-                         const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm,
-                         const double *f, int32_t n_f, int64_t phi_cap, int64_t *phi_ptr, int32_t *phi_idx,
-                         double *phi_val, float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
-                         void *stats, size_t stats_bytes, void *workspace, size_t workspace_bytes,
-                         grf_stream_t stream);
 /* The augmented walk matrix of grf_walk_phi (opaque to the caller): a 32-byte header, then one
  * record per entry e of the CSR walk matrix (g_ptr, g_idx, g_val) holding the target v, the row
  * start and row length of v and the weight g_val[e] -- 16 bytes ({v, row start, length} packed

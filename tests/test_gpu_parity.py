@@ -647,42 +647,6 @@ def test_walk_phi_fused_bitexact(eng, n, deg, m, L, p, rule):
     assert np.array_equal(K1, K2)
 
 
-@pytest.mark.parametrize("n,deg,m,L,p,rule", [(3000, 8, 128, 8, 0.1, 0), (500, 3, 16, 5, 0.3, 1), (300, 4, 7, 6, 0.2, 0),
-                                             (2000, 10, 64, 8, 0.1, 0), (70, 2, 32, 8, 0.5, 2)])
-def test_walk_phi_csr_matches_padded_plus_compaction(eng, n, deg, m, L, p, rule):
-    """grf_walk_phi_csr (rows placed compact by the walk kernel's look-back over the sources) == grf_walk_phi +
-    grf_compact_rows bit for bit: row pointer, columns, fp32 and fp64 values, the transpose bucket counts the
-    kernel leaves, and the Gram shift statistics (== compact_rows_stats: the shifts and K of the column-block
-    Gram); on a graph with isolated nodes (empty rows) and on source ranges."""
-    import torch
-    A = er_graph(n, deg, n + m + 1).tolil()
-    A[3, :] = 0
-    A[:, 3] = 0
-    A = A.tocsr()
-    A.eliminate_zeros()
-    G = eng.laplacian(A)
-    f = [(-0.6) ** l for l in range(L)]
-    for b, e in [(0, n), (n // 5, n - n // 7), (n - 1, n)]:
-        ref = eng.compact(eng.walk_phi(G, m, p, L, f, seed=3, load_rule=rule, src_begin=b, src_end=e), stats=True)
-        got = eng.walk_phi_csr(G, m, p, L, f, seed=3, load_rule=rule, src_begin=b, src_end=e, want64=True, stats=True)
-        nnz = ref.nnz
-        assert torch.equal(got.ptr, ref.ptr), (b, e)
-        assert torch.equal(got.idx[:nnz], ref.idx[:nnz]) and torch.equal(got.val32[:nnz], ref.val32[:nnz])
-        assert torch.equal(got.val[:nnz], ref.val[:nnz])
-        assert torch.equal(eng.phi_row_shifts(got), eng.phi_row_shifts(ref)), (b, e)
-        rows = e - b  # (the statistics: row max |Phi| as float32 at the blob's start; padding bytes differ)
-        assert torch.equal(got.row_stats[:4 * rows], ref.row_stats[:4 * rows]), (b, e)
-    # the kernel's bucket counts for the transpose of its own rows
-    bw = 128
-    ws1, ws2 = eng.transpose_workspace(n, n, bw), eng.transpose_workspace(n, n, bw)
-    ref = eng.compact(eng.walk_phi(G, m, p, L, f, seed=3, load_rule=rule, count_ws=ws1, band_width=bw, want64=False),
-                      want64=False, sync_free=True)
-    got = eng.walk_phi_csr(G, m, p, L, f, seed=3, load_rule=rule, count_ws=ws2, band_width=bw)
-    K1 = eng.gram_sparse(ref, eng.transpose_banded(ref, bw, counted_ws=ws1)).cpu().numpy()
-    K2 = eng.gram_sparse(got, eng.transpose_banded(got, bw, counted_ws=ws2)).cpu().numpy()
-    assert np.array_equal(K1, K2)
-
-
 # ------------------------------------------------- real graphs (SURVEY.md §8d)
 def _diffusion(L):
     return np.array([(-1.0) ** l / (2.0 ** l * float(np.prod(np.arange(1, l + 1)))) for l in range(L)])
