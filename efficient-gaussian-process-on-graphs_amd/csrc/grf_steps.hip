@@ -227,8 +227,9 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         }
     }
     __syncthreads();
-    if (sort_lds) block_bitonic_sort<KT>(key, P);
-    else block_bitonic_sort_regs<KT, kPer, kT * kPer>(key, P);  // (P == kPer * blockDim.x)
+    if (sort_lds == 1) block_bitonic_sort<KT>(key, P);
+    else if (sort_lds == 0) block_bitonic_sort_regs<KT, kPer, kT * kPer>(key, P);  // (P == kPer * blockDim.x)
+    // (sort_lds == 2: no sort -- a TIMING-ONLY ablation, GRF_PHI_SORT_LDS=2; Phi is then wrong)
 
     // ---- step values of the (node, step) runs, kept in registers: loads in walk order from 0.0.
     //      Thread t owns the sorted positions [t kPer, (t + 1) kPer) and the runs whose first visit
@@ -483,9 +484,9 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
     // needs the node-id bound n_cols, known for the walking kernel (the slots path stays 64-bit)
     const bool key32 = walk && n_cols > 0 && ((uint64_t)n_cols << (wbits + lbits)) <= 0xffffffffull;
     const int32_t Lf_ = n_f < L ? n_f : L;
-    static const int32_t sort_lds = [] {  // (experiments: GRF_PHI_SORT_LDS=1, the all-LDS bitonic sort)
-        const char *e = getenv("GRF_PHI_SORT_LDS");
-        return (int32_t)(e && atoi(e) != 0);
+    static const int32_t sort_lds = [] {  // (experiments: GRF_PHI_SORT_LDS=1, the all-LDS bitonic sort;
+        const char *e = getenv("GRF_PHI_SORT_LDS");  //  2, no sort at all: timing-only)
+        return (int32_t)(e ? atoi(e) : 0);
     }();
     static const size_t lds_pad = [] {  // (experiments: extra LDS per source, GRF_PHI_LDS_PAD bytes)
         const char *e = getenv("GRF_PHI_LDS_PAD");
