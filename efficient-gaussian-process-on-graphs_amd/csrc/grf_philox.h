@@ -53,28 +53,38 @@ __device__ inline bool halts(uint32_t x0, uint32_t x1, uint64_t thr) {
 // x / c correctly rounded without the IEEE divide sequence (v_div_scale x2, v_rcp_f64, 5 FMAs, v_div_fmas,
 // v_div_fixup per call): with y = RN(1 / c) (loop-invariant: computed once per walk) the quotient
 // q = RN(x y) is faithful, the remainder x - c q is exact in one FMA, and RN(q + (x - c q) y) is RN(x / c)
-// (Markstein's theorem; it needs x, the quotient and the remainder normal and c q free of overflow, which
-// holds for magnitudes in [2^-960, 2^960] with c the normal 1 - p_halt or m).  Anything else -- zero,
-// subnormal, huge, inf or NaN operands or quotients, e.g. cumulative loads that overflowed -- takes the
-// IEEE divide (a branch no lane takes on the benchmarked graphs), so the bits are x / c's everywhere
-// (tools/div_check.c checks both ranges).
-__device__ inline double div_by(double x, double c, double y) {
-    const double q = x * y;
-    const double r = __builtin_fma(__builtin_fma(-q, c, x), y, q);
-    const double ax = fabs(x), ar = fabs(r);
-    if (!(ax >= 0x1p-960 && ax <= 0x1p960 && ar >= 0x1p-960 && ar <= 0x1p960)) return x / c;
-    return r;
-}
-
-// The importance weight deg w / (1 - p) applied by the load rule; keep = 1 - p and its reciprocal
-// (LoadKeep, once per walk).
-struct LoadKeep {
+// (Markstein's theorem; it needs x, the quotient and the remainder normal and c q free of overflow).
+// Divisor precomputes, once per walk, the window of x's biased exponent for which both |x| and |x / c|
+// lie in [2^-959, 2^961): there the fast path is exact; anything else -- zero, subnormal, huge, inf or
+// NaN operands or quotients, e.g. cumulative loads that overflowed -- takes the IEEE divide (a branch no
+// lane takes on the benchmarked graphs), so the bits are x / c's everywhere (tools/div_check.c checks
+// both ranges).  The window test is one bit-field extract and one unsigned compare on x's high word.
+struct Divisor {
     double c, y;
-    __device__ explicit LoadKeep(double p) : c(1.0 - p), y(1.0 / (1.0 - p)) {}
+    uint32_t lo, span;  // fast path iff (exponent(x) - lo) <= span, unsigned
+    __device__ explicit Divisor(double c_) : c(c_), y(1.0 / c_) {
+        const int32_t ec = (int32_t)((__double2hiint(c_) >> 20) & 0x7ff);
+        const int32_t l = ec - 958 > 64 ? ec - 958 : 64, h = ec + 959 < 1983 ? ec + 959 : 1983;
+        lo = (uint32_t)l;
+        span = h >= l ? (uint32_t)(h - l) : 0u;
+        if (h < l) lo = 0xffffffffu;  // (an empty window: always the IEEE divide)
+    }
+    __device__ double operator()(double x) const {
+        const uint32_t ex = ((uint32_t)__double2hiint(x) >> 20) & 0x7ffu;
+        if (ex - lo > span) return x / c;
+        const double q = x * y;
+        return __builtin_fma(__builtin_fma(-q, c, x), y, q);
+    }
+};
+
+// The importance weight deg w / (1 - p) applied by the load rule; keep = the divisor 1 - p (once per walk).
+struct LoadKeep {
+    Divisor d;
+    __device__ explicit LoadKeep(double p) : d(1.0 - p) {}
 };
 template <typename Deg>
 __device__ inline double load_update(int rule, double load, Deg deg, double w, const LoadKeep &keep) {
-    const double f = div_by((double)deg * w, keep.c, keep.y);
+    const double f = keep.d((double)deg * w);
     if (rule == GRF_LOAD_CUMULATIVE) return load * f;
     if (rule == GRF_LOAD_NONCUMULATIVE) return f;
     return w;

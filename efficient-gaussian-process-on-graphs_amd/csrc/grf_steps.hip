@@ -24,13 +24,14 @@ namespace grf {
 __device__ inline double normalise(double acc, int32_t norm, int64_t m) {
     return norm == GRF_NORM_DIV ? acc / (double)m : acc * (1.0 / (double)m);
 }
-// The same with 1 / m computed once per workgroup: NORM_DIV divides through div_by (grf_philox.h: the
+// The same with 1 / m computed once per workgroup: NORM_DIV divides through Divisor (grf_philox.h: the
 // correctly rounded quotient, same bits as acc / m), NORM_MUL_RECIP multiplies by the rounded reciprocal
 struct Norm {
-    double m, inv;
+    Divisor d;
+    double inv;
     int32_t norm;
-    __device__ Norm(int32_t norm_, int64_t m_) : m((double)m_), inv(1.0 / (double)m_), norm(norm_) {}
-    __device__ double operator()(double acc) const { return norm == GRF_NORM_DIV ? div_by(acc, m, inv) : acc * inv; }
+    __device__ Norm(int32_t norm_, int64_t m_) : d((double)m_), inv(1.0 / (double)m_), norm(norm_) {}
+    __device__ double operator()(double acc) const { return norm == GRF_NORM_DIV ? d(acc) : acc * inv; }
 };
 
 // --------------------------------------------------------------- grf_steps

@@ -245,9 +245,10 @@ class GRFEngine:
         n = Wt.shape[0]
         if Wt.dim() != 2 or Wt.shape[1] != n:
             raise ValueError("Adjacency matrix must be square.")
-        # walk-matrix capacity: nnz(W) + n; the bound n^2 up to 64 M entries avoids counting
-        # (a reduction and a host round trip per call)
-        cap = n * n if n * n <= (1 << 26) else int(torch.count_nonzero(Wt).item()) + n
+        # walk-matrix capacity: nnz(W) + n; the bound n^2 up to 256 M entries (3 GB of CSR: capacity only,
+        # the kernels write the real entries) avoids counting -- a torch reduction over W and a host round
+        # trip per call, 0.64 ms of C2's 10k x 10k front (profiles/r05_c2_kernel_alone.txt)
+        cap = n * n if n * n <= (1 << 28) else int(torch.count_nonzero(Wt).item()) + n
         lp, li, lv = self._empty(n + 1, torch.int64), self._empty(cap, torch.int32), self._empty(cap, torch.float64)
         deg = self._empty(n, torch.float64)
         ws = self._ws(self.lib.grf_laplacian_dense_workspace_bytes(n))
