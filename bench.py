@@ -401,7 +401,10 @@ def main_c3(args):
             cur = front_on_side() if s_ + 1 < steps else None
             back(dense, record)
 
-    pipelined = args.overlap is not False
+    # pipelined by default only while the front is a real share of the step: at C3 (the Gram 0.205 ms, the front
+    # ~0.09 ms alone) 0.291-0.301 vs 0.295-0.298 serial; at C2 the front's 800 MB read of W slows the 7.4 ms MFMA
+    # Gram more than it hides (8.13-8.79 vs 7.76-8.48 serial; profiles/r05_dense_overlap_ab.txt)
+    pipelined = args.overlap if args.overlap is not None else n < 4096
     run(args.warmup, False, pipelined)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -551,8 +554,10 @@ def main():
     ap.add_argument("--fingerprint-dir", default=None,
                     help="write a bit-level fingerprint of every rank's K block (tools/gram_hash.py) to "
                          "DIR/rank<r>.json after the run (the multi-rank at-size parity test)")
-    ap.add_argument("--side-priority", choices=["normal", "high"], default="normal",
-                    help="pipelined steps: the HIP priority of the stream the next front runs on")
+    ap.add_argument("--side-priority", choices=["normal", "high"], default="high",
+                    help="pipelined steps: the HIP priority of the stream the next front runs on (high: its workgroups "
+                         "are dispatched ahead of the Gram's; C3 0.295-0.301 vs 0.306-0.313 ms, C4 equal: "
+                         "profiles/r05_dense_overlap_ab.txt)")
     ap.add_argument("--samples", type=int, default=64, help="predict: n_samples")
     ap.add_argument("--cg-dtype", choices=["f64", "f32"], default="f64", help="predict: CG vector precision")
     args = ap.parse_args()
