@@ -36,7 +36,7 @@ from grf_amd.graphs import er_graph_exact_edges, powerlaw_graph, snap_graph  # n
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh -> tools/pmc_summary.py), committed
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_summary.json")
 DEFAULT_WORKLOAD = (100_000, 1_000_000, 128, 8, 0.1)
 
 
