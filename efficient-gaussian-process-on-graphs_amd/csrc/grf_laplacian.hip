@@ -281,33 +281,17 @@ __global__ __launch_bounds__(256) void lap_row_kernel(int64_t n, const int64_t *
 // ---------------------------------------------- scipy, eight rows per wave
 // Most rows of a sparse graph are short (C5: mean degree ~10): a wave per row leaves 50+ lanes
 // idle.  These kernels give each row a group of 8 lanes (8 rows per wave); rows too long for a
-// group (degree sums over more than one numpy leaf, or more than kGroupRowMax entries) are done
-// afterwards by the whole wave with the one-row-per-wave code.  Same arithmetic, same bits.
+// group (degree sums over more than one numpy leaf, or 64 entries and more) are done afterwards by
+// the whole wave.  Same arithmetic, same bits.  Each lane issues ALL its loads of a row at once
+// (then the neighbours' D^-1/2 at once): a row costs three dependent round trips (row bounds,
+// entries, neighbour scales) instead of one per entry tail element and per binary-search step
+// (C5, 1M rows: 627 us for the three launches, latency-bound at ~0.1 TB/s).
 constexpr int kGroupRowMax = 64;
+constexpr int kLeafPer = 16;  // 128 (one numpy leaf) / 8 lanes
 
-// numpy pairwise sum of a[0 .. m), m <= 128 (one leaf), by the 8 lanes of a group (lane j owns
-// accumulator r_j); every lane of the wave must call it.  The group's lane 0 gets the sum.
-__device__ __forceinline__ double group_pw_leaf(const double *a, int64_t m, int j) {
-    const int64_t nb = m >= 8 ? m - (m % 8) : 0;
-    double r = 0.0;
-    if (m >= 8) {
-        r = a[j];
-        for (int64_t q = 8 + j; q < nb; q += 8) r += a[q];
-    }
-    const double r1 = __shfl_xor(r, 1, 64);
-    const double p01 = (j & 1) ? r1 + r : r + r1;
-    const double p23 = __shfl_xor(p01, 2, 64);
-    const double q = (j & 2) ? p23 + p01 : p01 + p23;
-    const double q4 = __shfl_xor(q, 4, 64);
-    double res = (j & 4) ? q4 + q : q + q4;
-    if (m < 8) res = 0.0;  // (numpy: res = 0; res += a[i] for short inputs)
-    if (j == 0)
-        for (int64_t t = nb; t < m; ++t) res += a[t];
-    return res;
-}
-
-__global__ __launch_bounds__(256) void lap_deg_group_kernel(int64_t n, const int64_t *ptr, const double *val,
-                                                            double *deg, double *dinv) {
+__global__ __launch_bounds__(256) void lap_deg_group_kernel(int64_t n, const int64_t *__restrict__ ptr,
+                                                            const double *__restrict__ val, double *__restrict__ deg,
+                                                            double *__restrict__ dinv) {
     __shared__ PwLeaf leaves[4][kPwLeaves];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
     const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 8;
@@ -318,11 +302,50 @@ __global__ __launch_bounds__(256) void lap_deg_group_kernel(int64_t n, const int
         b = ptr[i];
         e = ptr[i + 1];
     }
-    const int64_t m = e - b > 1 ? e - b - 1 : 0;
+    const int64_t m = e - b > 1 ? e - b - 1 : 0;  // deg = a0 + pairwise(a[1 ..])
     const bool lng = m > 128;
-    const double rest = group_pw_leaf(val + b + 1, lng ? 0 : m, j);
+    const int64_t mm = lng ? 0 : m;
+    const double *a = val + b + 1;
+    // numpy's leaf: accumulator r_j = a[j] + a[j + 8] + ... over the first nb = mm - mm % 8 values,
+    // the fixed tree over r_0..r_7, then the tail a[nb ..) added in order (mm < 8: the tail alone from 0)
+    // (loads past the wave's longest row are skipped by a scalar branch: ER rows of ~20 entries issue 3)
+    int64_t mw = mm;
+#pragma unroll
+    for (int off = 8; off < 64; off <<= 1) mw = max(mw, (int64_t)__shfl_xor(mw, off, 64));
+    const int qmax = __builtin_amdgcn_readfirstlane((int)((mw + 7) >> 3));
+    double x[kLeafPer];
+#pragma unroll
+    for (int q = 0; q < kLeafPer; ++q) {
+        x[q] = 0.0;
+        if (q < qmax && 8 * q + j < mm) x[q] = a[8 * q + j];
+    }
+    const double a0 = (j == 0 && e > b) ? val[b] : 0.0;
+    const int64_t nb = mm >= 8 ? mm - (mm % 8) : 0;
+    double r = x[0];
+#pragma unroll
+    for (int q = 1; q < kLeafPer; ++q)
+        if (q < qmax && 8 * q + j < nb) r += x[q];
+    const double r1 = __shfl_xor(r, 1, 64);
+    const double p01 = (j & 1) ? r1 + r : r + r1;
+    const double p23 = __shfl_xor(p01, 2, 64);
+    const double qq = (j & 2) ? p23 + p01 : p01 + p23;
+    const double q4 = __shfl_xor(qq, 4, 64);
+    double res = (j & 4) ? q4 + qq : qq + q4;
+    if (mm < 8) res = 0.0;  // (numpy: res = 0; res += a[i] for short inputs)
+    // the tail value a[nb + j] is this lane's x[nb / 8]
+    const int qt = (int)(nb >> 3);
+    double tv = 0.0;
+#pragma unroll
+    for (int q = 0; q < kLeafPer; ++q)
+        if (q < qmax && q == qt) tv = x[q];
+    const int64_t ntail = mm - nb;  // <= 7
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const double t = __shfl(tv, (lane & ~7) + k, 64);
+        if (k < ntail) res += t;
+    }
     if (j == 0 && i < n && !lng) {
-        const double d = e > b ? val[b] + rest : 0.0;
+        const double d = e > b ? a0 + res : 0.0;
         deg[i] = d;
         const double v = 1.0 / sqrt(d);
         dinv[i] = isinf(v) ? 0.0 : v;
@@ -342,7 +365,28 @@ __global__ __launch_bounds__(256) void lap_deg_group_kernel(int64_t n, const int
     }
 }
 
-// the row's virtual sequence (lap_row_kernel): element k -> (column, scaled value, kept)
+// One element of row i of D^-1/2 (D - A) D^-1/2 with the serial code's exact arithmetic, in two
+// halves so that the neighbour's D^-1/2 loads of several elements are in flight together:
+// lap_pre gives the scaled value t = di v and whether D^-1/2[col] is needed (else dropped),
+// lap_post the element u = t dj and whether it is kept (u != 0).  v = d - a_ii for an explicit
+// diagonal when d != 0, else 0 - a (sp.diags drops a zero diagonal); the inserted diagonal has v = d.
+__device__ __forceinline__ bool lap_pre(double v, double di, double &t) {
+    if (v != 0.0 && di != 0.0) {
+        t = di * v;
+        return t != 0.0;
+    }
+    return false;
+}
+__device__ __forceinline__ bool lap_post(bool need, double t, double dj, double &u) {
+    u = 0.0;
+    if (need && dj != 0.0) {
+        u = t * dj;
+        return u != 0.0;
+    }
+    return false;
+}
+
+// the row's virtual sequence (long rows, the whole wave): element k -> (column, scaled value, kept)
 struct LapRow {
     int64_t i, b, e, pd, total;
     double d, di;
@@ -365,94 +409,155 @@ struct LapRow {
         insert = has_diag && !expl;
         total = (e - b) + (insert ? 1 : 0);
     }
-    __device__ bool element(int64_t k, const int32_t *idx, const double *val, const double *dinv, int64_t &col,
-                            double &u) const {
-        double v;
+    // element k's column and value before the neighbour scale (k < total)
+    __device__ void raw(int64_t k, const int32_t *idx, const double *val, int32_t &col, double &v) const {
         if (insert && k == pd) {
-            col = i;
+            col = (int32_t)i;
             v = d;
         } else {
             const int64_t a = b + ((insert && k > pd) ? k - 1 : k);
             col = idx[a];
-            v = (has_diag && col == i) ? d - val[a] : 0.0 - val[a];
+            const double w = val[a];
+            v = (has_diag && col == i) ? d - w : 0.0 - w;
         }
-        if (v != 0.0 && di != 0.0) {
-            const double t = di * v;
-            if (t != 0.0) {
-                const double dj = dinv[col];
-                if (dj != 0.0) {
-                    u = t * dj;
-                    return u != 0.0;
-                }
-            }
-        }
-        return false;
     }
 };
 
 template <bool EMIT>
-__global__ __launch_bounds__(256) void lap_row_group_kernel(int64_t n, const int64_t *ptr, const int32_t *idx,
-                                                            const double *val, const double *deg, const double *dinv,
-                                                            int32_t *cnt, const int64_t *l_ptr, int32_t *l_idx,
-                                                            double *l_val, int64_t l_cap) {
+__global__ __launch_bounds__(256) void lap_row_group_kernel(int64_t n, const int64_t *__restrict__ ptr,
+                                                            const int32_t *__restrict__ idx,
+                                                            const double *__restrict__ val,
+                                                            const double *__restrict__ deg,
+                                                            const double *__restrict__ dinv, int32_t *__restrict__ cnt,
+                                                            const int64_t *__restrict__ l_ptr,
+                                                            int32_t *__restrict__ l_idx, double *__restrict__ l_val,
+                                                            int64_t l_cap) {
+    constexpr int kQ = kGroupRowMax / 8;  // entries per lane of a group row
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
     const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 8;
     if (r0 >= n) return;
     const int64_t i = r0 + g;
-    LapRow R;
-    R.total = 0;
-    if (i < n) R.init(i, ptr, idx, deg, dinv);
-    const bool lng = R.total > kGroupRowMax;
-    const int64_t mine = lng ? 0 : R.total;
-    int64_t it = (mine + 7) / 8;  // iterations of this group; the wave runs the max
+    const bool valid = i < n;
+    int64_t b = 0, e = 0, out = 0;
+    double d = 0.0, di = 0.0;
+    if (valid) {
+        b = ptr[i];
+        e = ptr[i + 1];
+        d = deg[i];
+        di = dinv[i];
+        if (EMIT) out = l_ptr[i];
+    }
+    const bool lng = e - b >= kGroupRowMax;  // (with an inserted diagonal: more than kGroupRowMax elements)
+    const int64_t len = lng ? 0 : e - b;
+    const int sh = 8 * g;
+    // round trip 2: the row's entries, all at once (entry 8 q + j in lane j; rounds past the wave's
+    // longest group row are skipped by a scalar branch)
+    int64_t lw = len;
 #pragma unroll
-    for (int off = 8; off < 64; off <<= 1) it = max(it, (int64_t)__shfl_xor(it, off, 64));
-    int64_t out = (EMIT && i < n && !lng) ? l_ptr[i] : 0;
-    int32_t c = 0;
-    for (int64_t t = 0; t < it; ++t) {
-        const int64_t k = t * 8 + j;
-        int64_t col = 0;
-        double u = 0.0;
-        const bool keep = k < mine && R.element(k, idx, val, dinv, col, u);
-        const uint32_t gm = (uint32_t)(__ballot(keep) >> (8 * g)) & 0xffu;
-        if (EMIT) {
-            const int64_t o = out + __popc(gm & ((1u << j) - 1u));
-            if (keep && o < l_cap) {
-                l_idx[o] = (int32_t)col;
-                l_val[o] = u;
-            }
-            out += __popc(gm);
-        } else {
-            c += __popc(gm);
+    for (int off = 8; off < 64; off <<= 1) lw = max(lw, (int64_t)__shfl_xor(lw, off, 64));
+    const int qmax = __builtin_amdgcn_readfirstlane((int)((lw + 7) >> 3));
+    int32_t col[kQ];
+    double w[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+        col[q] = -1;
+        w[q] = 0.0;
+        if (q < qmax && 8 * q + j < len) {
+            col[q] = idx[b + 8 * q + j];
+            w[q] = val[b + 8 * q + j];
         }
     }
-    if (!EMIT && j == 0 && i < n && !lng) cnt[i] = c;
-    uint64_t todo = __ballot(lng && j == 0);
-    while (todo) {  // long rows: the whole wave, 64 elements per step
+    const bool has_diag = d != 0.0;
+    bool expl = false;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q)
+        if (q < qmax) expl = expl || ((__ballot(col[q] == i) >> sh) & 0xffu) != 0;
+    const bool insert = has_diag && !expl;
+    // round trip 3: the neighbours' D^-1/2 (a dropped element reads its own row's, a valid address)
+    double t[kQ], dj[kQ];
+    bool need[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+        need[q] = false;
+        t[q] = 0.0;
+        dj[q] = 0.0;
+        if (q < qmax) {
+            const bool in = 8 * q + j < len;
+            const double v = (has_diag && col[q] == i) ? d - w[q] : 0.0 - w[q];
+            need[q] = in && lap_pre(v, di, t[q]);
+            dj[q] = dinv[need[q] ? col[q] : (valid ? i : 0)];
+        }
+    }
+    double ti;
+    const bool need_i = insert && lap_pre(d, di, ti);
+    double ui;
+    const bool keep_i = lap_post(need_i, ti, di, ui);  // (dinv[i] is di)
+    int64_t run = out;  // EMIT: the next place; else the count
+    int32_t klt = 0;    // kept entries with columns < i: the inserted diagonal goes after them
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+        if (q >= qmax) break;
+        double u;
+        const bool keep = lap_post(need[q], t[q], dj[q], u);
+        const uint32_t gm = (uint32_t)(__ballot(keep) >> sh) & 0xffu;
+        klt += __popc((uint32_t)(__ballot(keep && col[q] < i) >> sh) & 0xffu);
+        if (EMIT) {
+            const int64_t o = run + __popc(gm & ((1u << j) - 1u)) + ((keep_i && col[q] > i) ? 1 : 0);
+            if (keep && o < l_cap) {
+                l_idx[o] = col[q];
+                l_val[o] = u;
+            }
+        }
+        run += __popc(gm);
+    }
+    if (j == 0 && valid && !lng) {
+        if (EMIT) {
+            const int64_t o = out + klt;
+            if (keep_i && o < l_cap) {
+                l_idx[o] = (int32_t)i;
+                l_val[o] = ui;
+            }
+        } else {
+            cnt[i] = (int32_t)(run + (keep_i ? 1 : 0));
+        }
+    }
+    uint64_t todo = __ballot(lng && j == 0 && valid);
+    while (todo) {  // long rows: the whole wave, 4 x 64 elements in flight per round
         const int gg = (__ffsll((long long)todo) - 1) >> 3;
         todo &= todo - 1;
         LapRow W;
         W.init(r0 + gg, ptr, idx, deg, dinv);
         int64_t o0 = EMIT ? l_ptr[W.i] : 0;
-        int32_t cc = 0;
-        for (int64_t base = 0; base < W.total; base += 64) {
-            const int64_t k = base + lane;
-            int64_t col = 0;
-            double u = 0.0;
-            const bool keep = k < W.total && W.element(k, idx, val, dinv, col, u);
-            const uint64_t m = __ballot(keep);
-            if (EMIT) {
-                const int64_t o = o0 + __popcll(m & ((1ull << lane) - 1ull));
-                if (keep && o < l_cap) {
-                    l_idx[o] = (int32_t)col;
-                    l_val[o] = u;
+        for (int64_t base = 0; base < W.total; base += 256) {
+            int32_t c4[4];
+            double t4[4], dj4[4];
+            bool n4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t k = base + 64 * u + lane;
+                double v = 0.0;
+                c4[u] = (int32_t)W.i;
+                if (k < W.total) W.raw(k, idx, val, c4[u], v);
+                n4[u] = k < W.total && lap_pre(v, W.di, t4[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) dj4[u] = dinv[n4[u] ? c4[u] : (int32_t)W.i];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                double uu;
+                const bool keep = lap_post(n4[u], t4[u], dj4[u], uu);
+                const uint64_t m = __ballot(keep);
+                if (EMIT) {
+                    const int64_t o = o0 + __popcll(m & ((1ull << lane) - 1ull));
+                    if (keep && o < l_cap) {
+                        l_idx[o] = c4[u];
+                        l_val[o] = uu;
+                    }
                 }
                 o0 += __popcll(m);
-            } else {
-                cc += __popcll(m);
             }
         }
-        if (!EMIT && lane == 0) cnt[W.i] = cc;
+        if (!EMIT && lane == 0) cnt[W.i] = (int32_t)o0;
     }
 }
 

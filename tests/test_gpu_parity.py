@@ -94,6 +94,61 @@ def test_laplacian_sparse_random(eng):
         assert same_csr(got, ref), seed
 
 
+def _sparse_laplacian_cases():
+    """CSR adjacencies (sorted columns, explicit entries kept as given) that reach every branch of the
+    eight-rows-per-wave Laplacian kernels (grf_laplacian.hip): group rows of every length 0..63 and the
+    leaf's tail sizes, whole-wave rows (>= 64 entries) and degree sums past one numpy leaf (> 129 entries),
+    integral and non-integral weights, explicit / inserted / cancelling diagonals, zero and negative
+    degrees, explicit zeros and -0.0 entries."""
+    r = np.random.default_rng(17)
+    lengths = [0, 1, 2, 5, 7, 8, 9, 15, 16, 17, 31, 62, 63, 64, 65, 127, 128, 129, 130, 131, 200, 300, 700]
+    cases = {}
+    for name, unit in (("mixed_weighted", False), ("mixed_unit", True)):
+        n = 2300
+        ptr, idx = [0], []
+        for i in range(n):
+            k = lengths[(i * 7) % len(lengths)]
+            idx.extend(np.sort(r.choice(n, k, replace=False)).tolist())
+            ptr.append(len(idx))
+        val = np.ones(len(idx)) if unit else r.uniform(0.1, 2.0, len(idx))
+        cases[name] = sp.csr_matrix((val, np.asarray(idx, np.int32), np.asarray(ptr, np.int64)), shape=(n, n))
+    n = 600
+    ptr, idx, val = [0], [], []
+    for i in range(n):
+        kind = i % 8
+        cols = np.sort(r.choice(n, int(r.integers(1, 90)), replace=False))
+        v = r.uniform(-1.0, 2.0, len(cols))
+        if kind == 0:  # the diagonal alone: d - a_ii = 0 (dropped)
+            cols, v = np.array([i]), np.array([2.5])
+        elif kind == 1:  # +1 / -1: degree 0 (D^-1/2 = 0, nothing inserted)
+            cols = np.array(sorted({(i + 1) % n, (i + 2) % n}))
+            v = np.array([1.0, -1.0])
+        elif kind == 2:  # explicit zeros and -0.0 among the entries
+            v[::3] = 0.0
+            v[1::5] = -0.0
+        elif kind == 3:  # negative degree (D^-1/2 NaN)
+            v = -np.abs(v) - 0.1
+        elif kind == 4:  # an explicit diagonal inside the row
+            cols = np.unique(np.append(cols, i))
+            v = r.uniform(0.1, 2.0, len(cols))
+        idx.extend(cols.tolist())
+        val.extend(np.asarray(v, np.float64).tolist())
+        ptr.append(len(idx))
+    cases["signed_diag"] = sp.csr_matrix((np.asarray(val), np.asarray(idx, np.int32), np.asarray(ptr, np.int64)),
+                                         shape=(n, n))
+    return cases
+
+
+@pytest.mark.parametrize("name", ["mixed_weighted", "mixed_unit", "signed_diag"])
+def test_laplacian_sparse_group_branches(eng, name):
+    """The sparse (scipy-semantics) Laplacian bit-exact against the oracle, row pointer included, on rows
+    of every length class and the diagonal / zero / sign cases above."""
+    A = _sparse_laplacian_cases()[name]
+    ref, _ = O.laplacian_sparse(A)
+    got = eng.laplacian(A).to_scipy()
+    assert same_csr(got, ref), name
+
+
 def test_laplacian_dense_modes(eng, golden):
     d = golden("small_graphs")
     for name in d["names"]:
@@ -1388,11 +1443,12 @@ def test_gram_row_cuts_bit_identical(eng, hubs):
 
 def test_compaction_row_stats_give_same_shifts(eng):
     """compact(..., stats=True) leaves the rows' Gram shift statistics; phi_row_shifts from them equals
-    the separate pass over the values bit for bit (power-law graph, rows of very different norms)."""
+    the separate pass over the values bit for bit (power-law graph, rows of very different norms; a row
+    count that leaves the last wave's group of four rows partial)."""
     import torch
 
     from grf_amd.graphs import powerlaw_graph
-    A = powerlaw_graph(30000, 10.0, 2.5, seed=4)
+    A = powerlaw_graph(30003, 10.0, 2.5, seed=4)
     G = eng.laplacian(A)
     rows = eng.walk_phi(G, 64, 0.1, 8, [1.0, 0.5, 0.25, 0.125, 0.06, 0.03, 0.015, 0.008], seed=9, want64=False)
     a = eng.compact(rows, want64=False, want32=True, sync_free=True, stats=True)
