@@ -311,6 +311,27 @@ def main_predict(args):
 
 
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (v_mfma_f32_32x32x16_bf16 = 16x the fp32 rate)
+SPLIT_PRODUCTS = 6  # grf_gram_dense_split: bf16 plane products per fp32 multiply-add (p + q <= 2 of 3 x 3)
+
+
+def dense_gram_roofline(precision: str, flops: float, ms: float) -> dict:
+    """The dense Gram's roofline for the arithmetic it ran on: 'fp32' = v_mfma_f32_32x32x2_f32 against the
+    fp32 matrix peak; 'split' = the bf16 three-plane split (SPLIT_PRODUCTS bf16 products per fp32 term on
+    v_mfma_f32_32x32x16_bf16) against the bf16 peak, with the fp32-equivalent rate beside it."""
+    tfs = flops / (ms * 1e-3) / 1e12
+    if precision == "split":
+        return {"bound": "mfma", "achieved": SPLIT_PRODUCTS * tfs, "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": SPLIT_PRODUCTS * tfs / MFMA_BF16_PEAK_TFS, "traffic": None,
+                "kernel": "gram_split_mfma_kernel / gram_split_sk_kernel (fp32 LDS-DMA staging, exact three-plane "
+                          "bf16 split in registers, v_mfma_f32_32x32x16_bf16, 6 products per term)",
+                "kernel_ms": ms, "algorithmic_flops": flops, "bf16_flops": SPLIT_PRODUCTS * flops,
+                "fp32_equivalent_tflops": tfs, "fp32_equivalent_vs_fp32_peak": tfs / MFMA_F32_PEAK_TFS}
+    return {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": tfs / MFMA_F32_PEAK_TFS, "traffic": None,
+            "kernel": "gram_dense_mfma_kernel / gram_dense_sk_kernel (LDS-DMA staged 128x128 upper tiles, "
+                      "v_mfma_f32_32x32x2f32, both triangles written)",
+            "kernel_ms": ms, "algorithmic_flops": flops}
 
 
 def cora_adjacency() -> np.ndarray:
@@ -378,7 +399,7 @@ def main_c3(args):
         if record:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        K = eng.gram_dense(dense, n)
+        K = eng.gram_dense(dense, n, precision=args.gram_precision or None)
         if record:
             ev[1].record()
             (gram_ev if record is True else gram_ev_alone).append(ev)
@@ -425,7 +446,12 @@ def main_c3(args):
     # above the diagonal and mirrors them; counting 2 n^2 k would credit work it does not do; k = n,
     # the zero padding of the k range is not counted either)
     flops = 1.0 * n * (n + 1) * n
-    tfs = flops / (gram_ms * 1e-3) / 1e12
+    prec = args.gram_precision or eng.dense_precision
+    split = prec == "split"
+    roof = dense_gram_roofline(prec, flops, gram_ms)
+    roof.update({"kernel_ms": gram_ms,
+                 "kernel_ms_note": "HIP events around the Gram in the serial steps (alone on the GPU)",
+                 "kernel_ms_pipelined": gram_ms_pipe})
     out = {
         "metric": (f"GRF kernel-matrices/sec ({'Cora N=2708' if args.workload == 'c3' else f'ER N={n}'}, dense path, "
                    f"m={m} walks; MFMA utilisation of the Gram)"),
@@ -438,16 +464,13 @@ def main_c3(args):
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "fp64 walk loads, fp32 Phi, fp32 MFMA Gram",
+        "dtype": ("fp64 walk loads, fp32 Phi, fp32 Gram on the bf16 MFMA (exact three-plane split, fp32 accumulation)"
+                  if split else "fp64 walk loads, fp32 Phi, fp32 MFMA Gram"),
         "data": wdata,
         "config": {"workload": f"{wdesc} resident in HBM, dense numpy-semantics Laplacian, "
                                f"walks_per_node={m}, max_walk_length={L}, p_halt={p}, diffusion modulator beta=1, "
                                f"Philox seed 42, dense fp32 Phi and K", "n_nodes": n},
-        "roofline": {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": tfs / MFMA_F32_PEAK_TFS, "traffic": None, "kernel": "gram_dense_kernel",
-                     "kernel_ms": gram_ms, "algorithmic_flops": flops,
-                     "kernel_ms_note": "HIP events around the Gram in the serial steps (alone on the GPU)",
-                     "kernel_ms_pipelined": gram_ms_pipe},
+        "roofline": roof,
         "pipelined": pipelined,
         "serial_ms_per_step": serial_ms,
     }
@@ -554,6 +577,10 @@ def main():
     ap.add_argument("--fingerprint-dir", default=None,
                     help="write a bit-level fingerprint of every rank's K block (tools/gram_hash.py) to "
                          "DIR/rank<r>.json after the run (the multi-rank at-size parity test)")
+    ap.add_argument("--gram-precision", choices=["fp32", "split"], default=None,
+                    help="dense-path Gram (c3 / c2 and the MFMA legs): the fp32 MFMA, or the same product on the bf16 "
+                         "MFMA from an exact three-plane bf16 split of Phi (grf_gram_dense_split); default: the "
+                         "engine's (GRF_GRAM_DENSE_PRECISION, 'split')")
     ap.add_argument("--side-priority", choices=["normal", "high"], default="high",
                     help="pipelined steps: the HIP priority of the stream the next front runs on (high: its workgroups "
                          "are dispatched ahead of the Gram's; C3 0.295-0.301 vs 0.306-0.313 ms, C4 equal: "
@@ -1142,22 +1169,28 @@ def mfma_leg(eng, args, steps: int = 20, workload: str = "c3"):
     G = eng.walk_matrix_dense(torch.from_numpy(W).to(eng.device), C.LAP_NUMPY)
     dense = eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False))
     del G, W
-    for _ in range(3):
-        eng.gram_dense(dense, n)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev[0].record()
-    for _ in range(steps):
-        eng.gram_dense(dense, n)
-    ev[1].record()
-    ev[1].synchronize()
-    ms = ev[0].elapsed_time(ev[1]) / steps
     flops = 1.0 * n * (n + 1) * n
-    tfs = flops / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "gram_dense_mfma_kernel / gram_dense_sk_kernel (LDS-DMA staged 128x128 upper tiles, v_mfma_f32_32x32x2f32, both triangles written)",
-            "kernel_ms": ms, "algorithmic_flops": flops,
-            "workload": f"{wdesc} dense path, m={m}, L={L}: K = Phi Phi^T of the dense fp32 Phi "
-                        f"(N (N+1) N flops: the unique entries of the symmetric product)"}
+
+    def time_gram(prec):
+        for _ in range(3):
+            eng.gram_dense(dense, n, precision=prec)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(steps):
+            eng.gram_dense(dense, n, precision=prec)
+        ev[1].record()
+        ev[1].synchronize()
+        return ev[0].elapsed_time(ev[1]) / steps
+
+    prec = args.gram_precision or eng.dense_precision
+    out = dense_gram_roofline(prec, flops, time_gram(prec))
+    out["workload"] = (f"{wdesc} dense path, m={m}, L={L}: K = Phi Phi^T of the dense fp32 Phi "
+                       f"(N (N+1) N flops: the unique entries of the symmetric product)")
+    if prec != "fp32":
+        # the fp32 matrix instruction's kernel on the same operand, for comparison
+        f32 = dense_gram_roofline("fp32", flops, time_gram("fp32"))
+        out["fp32_path"] = {k: f32[k] for k in ("kernel_ms", "achieved", "peak", "frac", "kernel")}
+    return out
 
 
 if __name__ == "__main__":

@@ -472,6 +472,211 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_sk_kernel(DenseArgs a) {
     }
 }
 
+// ------------------------------------------------------------ fp32 on the bf16 matrix cores
+// The fp32 Gram by exact three-way bf16 splits (grf_gram_dense_split).  Every fp32 value a is the exact sum
+// of three bf16 values: a0 = bf16(a), a1 = bf16(a - a0), a2 = a - a0 - a1 (round to nearest: a has 24
+// significant bits, a0 and a1 take 8 each, so the last remainder has at most 8 and is a bf16 exactly;
+// values below ~2^-100 lose their last plane to the bf16 subnormal range).  a b = sum over p, q of a_p b_q;
+// the six products with p + q <= 2 are kept (the dropped three are below 2^-23 |a b| together), each exact
+// in the MFMA's fp32 arithmetic, summed on v_mfma_f32_32x32x16_bf16 -- 16x the fp32 MFMA's rate per clock,
+// so six of them cost 3/8 of the fp32 instruction's cycles per k.  The leading product a0 b0 is
+// accumulated on its own (c0) and the five corrections together (c1, 2^-8 of the magnitude), c0 + c1 at
+// the end: c0's rounding is the fp32 chain's, c1's 2^-8 of that, so the error bound stays the fp32 MFMA
+// path's plus 2^-23 sum |a_k b_k| for the dropped products.
+//
+// Staging is the fp32 path's (the same LDS-DMA pieces, swizzled k-tiles of BK = 16 floats, 4-stage ring,
+// two workgroups per CU): the split is done in registers after the fragment reads, so the bytes staged
+// per k are the fp32 kernel's.  (Staging three bf16 planes instead, 1.5x the bytes, measured slower:
+// profiles/AB_LOG.md "split Gram".)  A lane's operand of one bf16 MFMA is 8 consecutive k of its row --
+// the two 16-B chunks the fp32 kernel reads for fragment groups 0 and 1 (Layout<32, 16>::off).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// 8 floats -> their three bf16 planes (round to nearest; every step exact)
+__device__ __forceinline__ void split3(f32x4v lo, f32x4v hi, bf16x8 &p0, bf16x8 &p1, bf16x8 &p2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float v = e < 4 ? lo[e] : hi[e - 4];
+        const __bf16 a0 = (__bf16)v;
+        const float r1 = v - (float)a0;
+        const __bf16 a1 = (__bf16)r1;
+        p0[e] = a0;
+        p1[e] = a1;
+        p2[e] = (__bf16)(r1 - (float)a1);
+    }
+}
+
+// The k-loop of one tile over [kb, ke) with the split products.  The ring, the DMA pieces (issue: all of
+// k-tile t's) and the retire/publish step are kloop's; per k-tile a wave reads its 2 + 2 blocks' two chunks,
+// splits them and issues 4 blocks x 6 MFMAs.
+template <int NST, bool DIAG, bool LIVE>
+__device__ __forceinline__ void kloop_split(float *lds, const float *const *srcA, const float *const *srcB, int64_t kb,
+                                            int64_t ke, int wave, const int *aoff, const int *boff,
+                                            f32x16 (&c0)[2][2], f32x16 (&c1)[2][2]) {
+    using L = Layout<32, 16>;
+    using St = Stage<16>;
+    constexpr int G = DIAG ? St::PW : 2 * St::PW;  // DMA pieces per wave per k-tile
+    const int64_t nk = (ke - kb) / 16;
+    auto issue = [&](int64_t t) {
+        float *base = lds + (int)(t % NST) * 2 * St::F + wave * St::PW * 256;
+        const int64_t k0 = kb + t * 16;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            if (j < St::PW) dma16(srcA[j] + k0, base + j * 256);
+            else dma16(srcB[j - St::PW] + k0, base + St::F + (j - St::PW) * 256);
+        }
+    };
+    if (nk <= 0) return;
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+        if (t < nk) issue(t);
+    for (int64_t t = 0; t < nk; ++t) {
+        // k-tile t landed (the younger ones issued so far may stay in flight), then published
+        const int64_t younger = (t + NST - 2 < nk - 1 ? t + NST - 2 : nk - 1) - t;
+        if (younger >= 2) wait_vm<2 * G>();
+        else if (younger == 1) wait_vm<G>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();  // (also: every wave is done with k-tile t - 1, whose stage refills now)
+        asm volatile("" ::: "memory");
+        if (t + NST - 1 < nk) issue(t + NST - 1);
+        if constexpr (LIVE) {
+            const float *As = lds + (int)(t % NST) * 2 * St::F;
+            const float *Bs = DIAG ? As : As + St::F;
+            bf16x8 a[2][3], b[2][3];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const char *pa = reinterpret_cast<const char *>(As) + aoff[0] * 4 + x * L::XSTRIDE;
+                const char *pa1 = reinterpret_cast<const char *>(As) + aoff[1] * 4 + x * L::XSTRIDE;
+                split3(*reinterpret_cast<const f32x4v *>(pa), *reinterpret_cast<const f32x4v *>(pa1), a[x][0], a[x][1],
+                       a[x][2]);
+                const char *pb = reinterpret_cast<const char *>(Bs) + boff[0] * 4 + x * L::XSTRIDE;
+                const char *pb1 = reinterpret_cast<const char *>(Bs) + boff[1] * 4 + x * L::XSTRIDE;
+                split3(*reinterpret_cast<const f32x4v *>(pb), *reinterpret_cast<const f32x4v *>(pb1), b[x][0], b[x][1],
+                       b[x][2]);
+            }
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y) {
+                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][0], c0[x][y], 0, 0, 0);
+                    f32x16 d = c1[x][y];
+                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][1], d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][1], b[y][0], d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][2], d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][1], b[y][1], d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][2], b[y][0], d, 0, 0, 0);
+                    c1[x][y] = d;
+                }
+        }
+    }
+}
+
+constexpr int kSplitNST = 4;
+
+__device__ __forceinline__ Quarter tile_compute_split(const DenseArgs &a, float *lds, int64_t tile, int64_t kb,
+                                                      int64_t ke, int wave, int lane, f32x16 (&c)[2][2]) {
+    using L = Layout<32, 16>;
+    using St = Stage<16>;
+    const int wm = wave >> 1, wn = wave & 1;
+    int64_t bi, bj;
+    tile_coords(tile, a.nt, bi, bj);
+    const int64_t m0 = bi * kTile, n0 = bj * kTile;
+    const bool diag = bi == bj;
+    // the fp32 path's DMA sources (tile_compute)
+    const float *srcA[St::PW], *srcB[St::PW];
+#pragma unroll
+    for (int j = 0; j < St::PW; ++j) {
+        const int p = (wave * St::PW + j) * 64 + lane;
+        const int row = p / L::C, kc = (p % L::C) ^ L::swz(row);
+        int64_t ra = m0 + row, rb = n0 + row;
+        ra = ra < a.n ? ra : a.n - 1;
+        rb = rb < a.n ? rb : a.n - 1;
+        srcA[j] = a.A + ra * a.lda + 4 * kc;
+        srcB[j] = a.A + rb * a.lda + 4 * kc;
+    }
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        aoff[g] = L::off(wm * 64, 0, g, lane);
+        boff[g] = L::off(wn * 64, 0, g, lane);
+    }
+    Quarter q{m0 + wm * 64, n0 + wn * 64, diag, diag && wn < wm};
+    const bool live = !q.below && q.qr < a.n && q.qc < a.n;
+    f32x16 c0[2][2], c1[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            c0[x][y] = f32x16{};
+            c1[x][y] = f32x16{};
+        }
+    if (diag) {
+        if (live) kloop_split<kSplitNST, true, true>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c0, c1);
+        else kloop_split<kSplitNST, true, false>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c0, c1);
+    } else {
+        if (live) kloop_split<kSplitNST, false, true>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c0, c1);
+        else kloop_split<kSplitNST, false, false>(lds, srcA, srcB, kb, ke, wave, aoff, boff, c0, c1);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) c[x][y] = c0[x][y] + c1[x][y];
+    return q;
+}
+
+// the split path's kernels: the same work items as gram_dense_mfma_kernel / gram_dense_sk_kernel
+__global__ __launch_bounds__(256, 2) void gram_split_mfma_kernel(DenseArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[kSplitNST * 2 * Stage<16>::F];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t w = blockIdx.x;
+    int64_t tile, slice = 0, pieces = 1;
+    if (w < a.n_whole) {
+        tile = w;
+    } else {
+        tile = a.n_whole + (w - a.n_whole) / a.n_split;
+        slice = (w - a.n_whole) % a.n_split;
+        pieces = a.n_split;
+    }
+    const int64_t kb = pieces > 1 ? slice * a.k_split : 0;
+    const int64_t ke = pieces > 1 ? (kb + a.k_split < a.kpad ? kb + a.k_split : a.kpad) : a.kpad;
+    f32x16 c[2][2];
+    const Quarter q = tile_compute_split(a, lds, tile, kb, ke, wave, lane, c);
+    if (pieces > 1) {
+        const int64_t u = tile - a.n_whole;
+        if (!split_combine<32, 16>(a, c, a.tickets + u, pieces, slice, [&](int64_t s) { return u * pieces + s; },
+                                   reinterpret_cast<int32_t *>(lds), wave, lane))
+            return;
+    }
+    tile_write<32, 16>(a, c, q, wave, lane);
+}
+
+__global__ __launch_bounds__(256, 2) void gram_split_sk_kernel(DenseArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[kSplitNST * 2 * Stage<16>::F];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t U = a.sk_units, KT = a.sk_kt;
+    const int64_t u0 = (int64_t)blockIdx.x * U;
+    const int64_t u1 = u0 + U < a.sk_total ? u0 + U : a.sk_total;
+    for (int64_t u = u0; u < u1;) {
+        const int64_t tile = u / KT, tb = tile * KT, te = tb + KT;
+        const int64_t se = u1 < te ? u1 : te;
+        __syncthreads();  // (the previous segment's ring reads and hand-off flag are done)
+        f32x16 c[2][2];
+        const Quarter q = tile_compute_split(a, lds, tile, (u - tb) * 16, (se - tb) * 16, wave, lane, c);
+        bool write = true;
+        if (u != tb || se != te) {
+            const int64_t s0 = tb / U, s1 = (te - 1) / U;
+            const int64_t first = 2 * s0 + (tb == s0 * U ? 0 : 1);
+            write = split_combine<32, 16>(
+                a, c, a.tickets + first, s1 - s0 + 1, blockIdx.x - s0,
+                [&](int64_t j) { return j == 0 ? first : 2 * (s0 + j); }, reinterpret_cast<int32_t *>(lds), wave,
+                lane);
+        }
+        if (write) tile_write<32, 16>(a, c, q, wave, lane);
+        u = se;
+    }
+}
+
 constexpr int kCUs = 256;
 
 int env_int(const char *name, int dflt) {
@@ -623,6 +828,61 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
     }
     gram_dense_mfma_kernel<32, BK, 4, 2><<<(unsigned)items, 256, 0, st>>>(a);
     GRF_CHECK_LAUNCH("gram_dense_mfma_kernel");
+    return GRF_OK;
+}
+
+
+// The split path: the fp32 path's workspace (tickets and slabs; the ticket block must be zero on first use)
+size_t dense_gram_split_workspace_bytes(int64_t n, int64_t k_dim) { return dense_gram_workspace_bytes(n, k_dim); }
+
+int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                         void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && k_dim >= 0 && A && K && ldk >= n && lda >= k_dim, GRF_EINVAL,
+                "grf_gram_dense_split: bad arguments");
+    GRF_REQUIRE(lda % 16 == 0 && ((uintptr_t)A & 15) == 0, GRF_EINVAL,
+                "grf_gram_dense_split: lda must be a multiple of 16 and A 16-byte aligned");
+    GRF_REQUIRE(ldk % 4 == 0 && ((uintptr_t)K & 15) == 0, GRF_EINVAL,
+                "grf_gram_dense_split: ldk must be a multiple of 4 and K 16-byte aligned");
+    if (n == 0) return GRF_OK;
+    GRF_REQUIRE(workspace && ((uintptr_t)workspace & 255) == 0 &&
+                    workspace_bytes >= dense_gram_split_workspace_bytes(n, k_dim),
+                GRF_EINVAL, "grf_gram_dense_split: workspace missing, too small or not 256-byte aligned");
+    constexpr int BK = 16;
+    DensePlan p = dense_plan(n, k_dim, BK);
+    GRF_REQUIRE(p.kpad <= lda, GRF_EINVAL, "grf_gram_dense_split: lda must cover k_dim rounded up to %d", BK);
+    hipStream_t st = S(stream);
+    DenseArgs a{};
+    a.A = A;
+    a.K = K;
+    a.n = n;
+    a.nt = p.nt;
+    a.lda = lda;
+    a.ldk = ldk;
+    a.kpad = p.kpad;
+    static const int sk_env = env_int("GRF_DENSE_SK", -1);
+    const bool sk = sk_env == 1 || (sk_env != 0 && p.tiles >= kCUs);
+    if (sk) {
+        const SkPlan q = sk_plan(n, k_dim, BK);
+        GRF_REQUIRE_GRID(q.grid, 256, "gram_split_sk_kernel");
+        a.tickets = reinterpret_cast<int32_t *>(workspace);
+        a.slabs = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes);
+        a.sk_units = q.units;
+        a.sk_kt = q.kt;
+        a.sk_total = q.total;
+        gram_split_sk_kernel<<<(unsigned)q.grid, 256, 0, st>>>(a);
+        GRF_CHECK_LAUNCH("gram_split_sk_kernel");
+        return GRF_OK;
+    }
+    const int64_t split_tiles = p.tiles - p.n_whole;
+    const int64_t items = p.n_whole + split_tiles * p.n_split;
+    GRF_REQUIRE_GRID(items, 256, "gram_split_mfma_kernel");
+    a.tickets = split_tiles > 0 ? reinterpret_cast<int32_t *>(workspace) : nullptr;
+    a.slabs = split_tiles > 0 ? reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes) : nullptr;
+    a.n_whole = p.n_whole;
+    a.k_split = p.k_split;
+    a.n_split = p.n_split;
+    gram_split_mfma_kernel<<<(unsigned)items, 256, 0, st>>>(a);
+    GRF_CHECK_LAUNCH("gram_split_mfma_kernel");
     return GRF_OK;
 }
 

@@ -4,7 +4,7 @@ The (N, N, L) step tensor is sampled once at construction on the GPU (Laplacian 
 degrees as in preprocessing/laplacian_np.py, or the raw adjacency with the ablation rule) and
 stays on the device.  ``modulator_vector`` is a learnable parameter (``torch.nn.Parameter``, fp64:
 the reference's ``gpflow.Parameter(tf.float64)``, :31-41); K = (F f)(F f)^T runs on the MFMA Gram
-(fp32, ``grf_gram_dense``) once per modulator value and is cached, so ``K`` / ``K_diag`` only gather
+(fp32 result, ``GRFEngine.gram_dense``) once per modulator value and is cached, so ``K`` / ``K_diag`` only gather
 from it.  ``K_torch`` returns the same block as a torch tensor that is differentiable w.r.t. the
 modulator (``grf_amd.features.DenseGramFunction``).  GPflow / TensorFlow are not installed here:
 the class is a ``torch.nn.Module`` and ``K`` / ``K_diag`` return numpy arrays.

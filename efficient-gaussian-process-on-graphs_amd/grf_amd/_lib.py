@@ -26,7 +26,7 @@ RNG_PCG64, RNG_PHILOX = 0, 1
 LOAD_CUMULATIVE, LOAD_NONCUMULATIVE, LOAD_ABLATION = 0, 1, 2
 NORM_DIV, NORM_MUL_RECIP = 0, 1
 REC_LINE, REC_PACKED, REC_SLOT = 128, 12, 32
-ABI_VERSION = 5  # include/grf.h GRF_ABI_VERSION: argument lists change between revisions
+ABI_VERSION = 6  # include/grf.h GRF_ABI_VERSION: argument lists change between revisions
 
 
 class GrfWalkParams(ctypes.Structure):
@@ -115,6 +115,8 @@ SIGNATURES = {
     "grf_gram_dense": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_gram_dense_workspace_bytes": (_sz, [_i64, _i64]),
     "grf_gram_dense_ws": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
+    "grf_gram_dense_split_workspace_bytes": (_sz, [_i64, _i64]),
+    "grf_gram_dense_split": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
     "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "grf_densify_padded": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     # the GPyTorch surface's feature algebra (step_* are host arrays of device pointers)

@@ -202,6 +202,10 @@ class GRFEngine:
         C.check(self.lib.grf_set_device(self.device.index), "grf_set_device")
         # the Gram kernels' tile work counter (calls on this engine's stream are ordered)
         self._gram_ws = self._ws(self.lib.grf_gram_workspace_bytes())
+        # the dense Gram's arithmetic (gram_dense): the exact three-plane bf16 'split' on the bf16 matrix
+        # cores (fp32-class error, 1.3-1.4x faster: profiles/r05_split_gram_error.txt, AB_LOG "split Gram") or
+        # the 'fp32' matrix instruction
+        self.dense_precision = os.environ.get("GRF_GRAM_DENSE_PRECISION", "split")
 
     # ------------------------------------------------------------ utilities
     @property
@@ -806,23 +810,34 @@ class GRFEngine:
                                             _p(out), lda, self.stream), "grf_densify_padded")
         return out
 
-    def gram_dense(self, dense_phi: torch.Tensor, k_dim: int) -> torch.Tensor:
+    def gram_dense(self, dense_phi: torch.Tensor, k_dim: int, precision: Optional[str] = None) -> torch.Tensor:
+        """K = A A^T of the dense fp32 Phi on the MFMA.  precision 'fp32': the fp32 matrix instruction
+        (grf_gram_dense_ws); 'split': the same product on the bf16 matrix cores from an exact three-plane
+        split of A (grf_gram_dense_split, error bound the fp32 path's + 2^-23 sum |a b|); None: the engine's
+        ``dense_precision`` (GRF_GRAM_DENSE_PRECISION, default 'split')."""
+        precision = precision or self.dense_precision
+        if precision not in ("fp32", "split"):
+            raise ValueError(f"unknown dense Gram precision {precision!r}")
+        split = precision == "split"
         n = dense_phi.shape[0]
         ldk = self.leading_dim(n)
         out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
         # split-K partial tiles (small n, or the last tiles of a large n) and their tickets: a cached
         # workspace per stream, ZEROED when allocated (the kernel leaves the tickets zero after every
         # launch; an uninitialised block gave round 4's NaN, profiles/AB_LOG.md "dense-Gram NaN"), dropped
-        # after a failed call so that no ticket a broken launch may have left is read again
-        need = int(self.lib.grf_gram_dense_workspace_bytes(n, k_dim))
+        # after a failed call so that no ticket a broken launch may have left is read again.  The split
+        # path's planes follow the ticket block and slabs in the same workspace.
+        need = int(self.lib.grf_gram_dense_split_workspace_bytes(n, k_dim) if split
+                   else self.lib.grf_gram_dense_workspace_bytes(n, k_dim))
         stream = self.stream
         cache = self.__dict__.setdefault("_dense_ws", {})
         ws = cache.get(stream.value)
         if ws is None or ws.numel() < need:
             ws = cache[stream.value] = torch.zeros(max(need, 16), dtype=torch.uint8, device=self.device)
+        fn = self.lib.grf_gram_dense_split if split else self.lib.grf_gram_dense_ws
         try:
-            C.check(self.lib.grf_gram_dense_ws(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, _p(ws),
-                                               ws.numel(), stream), "grf_gram_dense_ws")
+            C.check(fn(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, _p(ws), ws.numel(), stream),
+                    "grf_gram_dense_split" if split else "grf_gram_dense_ws")
         except Exception:
             cache.pop(stream.value, None)
             raise

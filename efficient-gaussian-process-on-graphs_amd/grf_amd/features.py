@@ -266,7 +266,8 @@ class DenseSteps:
     """A dense (N, N, L) step tensor F resident on the device once (the GPflow wrappers'
     ``feature_matrices_tf``, gpflow_kernels/general_kernel_fast_grf.py:44-59).  Per modulator value:
     Phi = F f on ``grf_dense_steps_phi`` (fp64, plus the fp32 image of the Gram), K = Phi Phi^T on the
-    MFMA Gram (``grf_gram_dense_ws``), cached; the modulator gradient on ``grf_dense_steps_grad``."""
+    MFMA Gram (``GRFEngine.gram_dense``: the engine's dense precision, by default the exact bf16 split
+    ``grf_gram_dense_split``), cached; the modulator gradient on ``grf_dense_steps_grad``."""
 
     def __init__(self, F, engine: Optional[GRFEngine] = None):
         self.engine = engine or get_engine()

@@ -70,7 +70,7 @@ enum grf_norm {
 
 /* The ABI revision of this header: grf_version() returns it, and a binding must refuse a library whose
  * revision differs (argument lists change between revisions). */
-#define GRF_ABI_VERSION 5
+#define GRF_ABI_VERSION 6
 
 const char *grf_last_error(void);
 int32_t grf_version(void);
@@ -418,6 +418,17 @@ int32_t grf_gram_dense_upper(int64_t n, int64_t k_dim, const float *A, int64_t l
 size_t grf_gram_dense_workspace_bytes(int64_t n, int64_t k_dim);
 int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                           void *workspace, size_t workspace_bytes, grf_stream_t stream);
+/* The same K on the bf16 matrix cores (ABI 6): A is split exactly into three bf16 planes (a = a0 + a1 +
+ * a2), K = sum over the six plane products a_p b_q with p + q <= 2 on v_mfma_f32_32x32x16_bf16 (16x the
+ * fp32 MFMA's rate), a0 b0 and the five corrections accumulated apart in fp32.  The dropped products are
+ * below 2^-23 |a b| per term, so the error bound is the fp32 path's plus 2^-23 sum_k |A_ik A_jk|
+ * (measured against fp64: tests/test_gpu_parity.py test_gram_dense_split_*).  Same tiles, stream-K /
+ * split-K decomposition, symmetry and determinism as grf_gram_dense_ws.  workspace (required):
+ * grf_gram_dense_split_workspace_bytes(n, k_dim) bytes, 256-byte aligned, ZERO on first use (the first
+ * part is grf_gram_dense_ws's ticket block and slabs, the rest the planes). */
+size_t grf_gram_dense_split_workspace_bytes(int64_t n, int64_t k_dim);
+int32_t grf_gram_dense_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                             void *workspace, size_t workspace_bytes, grf_stream_t stream);
 
 /* CSR (float32) -> dense float32 [n_rows x lda], zero filled. */
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,

@@ -231,6 +231,37 @@ def test_c3_dense_leg_cora(eng):
     assert np.array_equal(K, K.T)
 
 
+def test_c3_dense_leg_cora_split_gram(eng):
+    """C3's Gram on the bf16 three-plane split (grf_gram_dense_split, bench.py --gram-precision split):
+    the same Cora operand as test_c3_dense_leg_cora, K against the oracle's Phi within the same bound
+    as the fp32 path, its error against fp64 beside the fp32 path's, exactly symmetric."""
+    import torch
+    from grf_amd import _lib as C
+    from bench import cora_adjacency
+
+    W = cora_adjacency()
+    n, m, L, p = W.shape[0], 128, 8, 0.1
+    f = _diffusion(L)
+    G = eng.walk_matrix_dense(torch.from_numpy(W).to(eng.device), C.LAP_NUMPY)
+    dense = eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False))
+    Ks = eng.gram_dense(dense, n, precision="split")
+    Kf = eng.gram_dense(dense, n, precision="fp32")
+    P = dense[:, :n].double()
+    ref = P @ P.t()
+    bound = P.abs() @ P.abs().t() + 1e-30
+    es = float(((Ks.double() - ref).abs() / bound).max())
+    ef = float(((Kf.double() - ref).abs() / bound).max())
+    print(f"[c3 split] max err / sum|ab|: split {es:.3e}, fp32 {ef:.3e}", flush=True)
+    assert es <= 1e-5 and es <= 8.0 * ef + 1e-9, (es, ef)
+    ip, ix, dx = O.dense_to_walk_csr(O.laplacian_dense(W, 0))
+    node, load = O.walk_slots(ip, ix, dx, m, p, L, rng=O.RNG_PHILOX, seed=42, n_threads=N_THREADS)
+    ref_phi = O.phi_sparse(O.reduce_steps(node, load, O.NORM_DIV), f)
+    Kn = Ks.cpu().numpy()
+    ok, e, nbad = _rows_close(Kn, ref_phi, np.arange(n))
+    assert ok, (e, nbad)
+    assert np.array_equal(Kn, Kn.T)
+
+
 def test_dense_path_bench_pipelined_line():
     """bench.py's dense-path workload (C3) pipelined: the next step's front on a side stream beside this
     step's MFMA Gram.  The line keeps the contract fields, reports the pipelining, the serial latency

@@ -564,6 +564,34 @@ def test_gram_dense_split_k(eng, n, k):
     assert np.array_equal(eng.gram_dense(At, k).cpu().numpy(), Ksn)
 
 
+@pytest.mark.parametrize("n,k", [(160, 150), (300, 900), (2708, 2708), (4200, 1000), (4200, 20), (5000, 4999)])
+def test_gram_dense_split_vs_fp64_and_fp32(eng, n, k):
+    """The bf16 three-plane split Gram (grf_gram_dense_split) against fp64: within the fp32 path's test bound
+    (1e-5 of sum |a b|), its typical error within a small factor of the fp32 MFMA path's (fp32-class, not a
+    reduced precision), exactly symmetric, run-to-run identical; every decomposition (whole tiles, per-tile
+    split-K below 256 tiles, stream-K from 256 on, k of one stage)."""
+    import torch
+    lda = -(-k // 64) * 64
+    Ad = np.zeros((n, lda), np.float32)
+    r = np.random.default_rng(n + k)
+    # Phi-like: nonnegative entries spread over four decades, and signed ones in every other row
+    v = (r.random((n, k)) * 10.0 ** r.uniform(-3, 1, (n, k))) * (r.random((n, k)) < 0.2)
+    v[::2] *= np.sign(r.standard_normal((n // 2 + n % 2, k)))
+    Ad[:, :k] = v.astype(np.float32)
+    At = torch.from_numpy(Ad).to(eng.device)
+    Ks = eng.gram_dense(At, k, precision="split")
+    Kf = eng.gram_dense(At, k, precision="fp32")
+    ref = Ad.astype(np.float64) @ Ad.astype(np.float64).T
+    bound = np.abs(Ad).astype(np.float64) @ np.abs(Ad).astype(np.float64).T + 1e-30
+    es = np.abs(Ks.cpu().numpy() - ref) / bound
+    ef = np.abs(Kf.cpu().numpy() - ref) / bound
+    assert es.max() <= 1e-5, es.max()
+    assert np.sqrt((es ** 2).mean()) <= 4.0 * np.sqrt((ef ** 2).mean()) + 1e-9, (es.max(), ef.max())
+    Ksn = Ks.cpu().numpy()
+    assert np.array_equal(Ksn, Ksn.T) and np.isfinite(Ksn).all()
+    assert np.array_equal(eng.gram_dense(At, k, precision="split").cpu().numpy(), Ksn)
+
+
 def test_gram_dense_c2_size_stream_k(eng):
     """the stream-K path at the bench's C2 size (n = k = 10 000, 3160 tiles over 512
     slots: tiles cut at slot boundaries and summed through slabs) against fp64 on sampled rows, exactly
