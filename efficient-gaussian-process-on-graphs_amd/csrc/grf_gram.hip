@@ -612,7 +612,7 @@ __global__ __launch_bounds__(256) void densify_padded_kernel(int64_t cap, const 
 size_t dense_gram_workspace_bytes(int64_t n, int64_t k_dim);
 size_t dense_gram_split_workspace_bytes(int64_t n, int64_t k_dim);
 int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
-                         void *workspace, size_t workspace_bytes, grf_stream_t stream);
+                         void *workspace, size_t workspace_bytes, bool upper_only, grf_stream_t stream);
 int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk, void *workspace,
                    size_t workspace_bytes, bool upper_only, grf_stream_t stream);
 
@@ -1005,7 +1005,14 @@ size_t grf_gram_dense_split_workspace_bytes(int64_t n, int64_t k_dim) {
 // the same K on the bf16 matrix cores: A split exactly into three bf16 planes, six products per term
 int32_t grf_gram_dense_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                              void *workspace, size_t workspace_bytes, grf_stream_t stream) {
-    return grf::dense_gram_split(n, k_dim, A, lda, K, ldk, workspace, workspace_bytes, stream);
+    GRF_REQUIRE(workspace, GRF_EINVAL, "grf_gram_dense_split: workspace required");
+    return grf::dense_gram_split(n, k_dim, A, lda, K, ldk, workspace, workspace_bytes, false, stream);
+}
+
+// grf_gram_dense_upper on the split products (the hub-column split's panel)
+int32_t grf_gram_dense_split_upper(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                                   grf_stream_t stream) {
+    return grf::dense_gram_split(n, k_dim, A, lda, K, ldk, nullptr, 0, true, stream);
 }
 
 int32_t grf_densify_padded(int64_t n_rows, int64_t cap, int64_t n_cols, const int32_t *cnt, const int32_t *idx,

@@ -835,18 +835,19 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
 // The split path: the fp32 path's workspace (tickets and slabs; the ticket block must be zero on first use)
 size_t dense_gram_split_workspace_bytes(int64_t n, int64_t k_dim) { return dense_gram_workspace_bytes(n, k_dim); }
 
+// workspace NULL (the hub panel's upper_only call): whole tiles only, as dense_gram without one
 int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
-                         void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+                         void *workspace, size_t workspace_bytes, bool upper_only, grf_stream_t stream) {
     GRF_REQUIRE(n >= 0 && k_dim >= 0 && A && K && ldk >= n && lda >= k_dim, GRF_EINVAL,
                 "grf_gram_dense_split: bad arguments");
     GRF_REQUIRE(lda % 16 == 0 && ((uintptr_t)A & 15) == 0, GRF_EINVAL,
                 "grf_gram_dense_split: lda must be a multiple of 16 and A 16-byte aligned");
-    GRF_REQUIRE(ldk % 4 == 0 && ((uintptr_t)K & 15) == 0, GRF_EINVAL,
+    GRF_REQUIRE(upper_only || (ldk % 4 == 0 && ((uintptr_t)K & 15) == 0), GRF_EINVAL,
                 "grf_gram_dense_split: ldk must be a multiple of 4 and K 16-byte aligned");
     if (n == 0) return GRF_OK;
-    GRF_REQUIRE(workspace && ((uintptr_t)workspace & 255) == 0 &&
-                    workspace_bytes >= dense_gram_split_workspace_bytes(n, k_dim),
-                GRF_EINVAL, "grf_gram_dense_split: workspace missing, too small or not 256-byte aligned");
+    GRF_REQUIRE(!workspace || (((uintptr_t)workspace & 255) == 0 &&
+                               workspace_bytes >= dense_gram_split_workspace_bytes(n, k_dim)),
+                GRF_EINVAL, "grf_gram_dense_split: workspace too small or not 256-byte aligned");
     constexpr int BK = 16;
     DensePlan p = dense_plan(n, k_dim, BK);
     GRF_REQUIRE(p.kpad <= lda, GRF_EINVAL, "grf_gram_dense_split: lda must cover k_dim rounded up to %d", BK);
@@ -859,8 +860,13 @@ int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, 
     a.lda = lda;
     a.ldk = ldk;
     a.kpad = p.kpad;
+    a.upper_only = upper_only ? 1 : 0;
     static const int sk_env = env_int("GRF_DENSE_SK", -1);
-    const bool sk = sk_env == 1 || (sk_env != 0 && p.tiles >= kCUs);
+    const bool sk = workspace && (sk_env == 1 || (sk_env != 0 && p.tiles >= kCUs));
+    if (!workspace) {
+        p.n_split = 1;
+        p.n_whole = p.tiles;
+    }
     if (sk) {
         const SkPlan q = sk_plan(n, k_dim, BK);
         GRF_REQUIRE_GRID(q.grid, 256, "gram_split_sk_kernel");

@@ -117,6 +117,7 @@ SIGNATURES = {
     "grf_gram_dense_ws": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_dense_split_workspace_bytes": (_sz, [_i64, _i64]),
     "grf_gram_dense_split": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
+    "grf_gram_dense_split_upper": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "grf_densify_padded": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     # the GPyTorch surface's feature algebra (step_* are host arrays of device pointers)

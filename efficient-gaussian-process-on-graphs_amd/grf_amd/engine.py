@@ -765,8 +765,8 @@ class GRFEngine:
             ev.record(torch.cuda.current_stream(self.device))
             after_tiles(ev)
             after_tiles = None
-        C.check(self.lib.grf_gram_dense_upper(n, h, _p(P), P.stride(0), _p(out), out.stride(0), self.stream),
-                "grf_gram_dense_upper")
+        upper = self.lib.grf_gram_dense_split_upper if self.dense_precision == "split" else self.lib.grf_gram_dense_upper
+        C.check(upper(n, h, _p(P), P.stride(0), _p(out), out.stride(0), self.stream), "grf_gram_dense_upper")
         cuts = self.row_cuts(phi, tr, skewed)  # (after the hub drop: the weights of the columns left)
         if cuts is not None:
             self._gram_upper_cuts(phi, tr, out, cuts, (0, 1, 1), True)

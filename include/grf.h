@@ -429,6 +429,9 @@ int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda,
 size_t grf_gram_dense_split_workspace_bytes(int64_t n, int64_t k_dim);
 int32_t grf_gram_dense_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                              void *workspace, size_t workspace_bytes, grf_stream_t stream);
+/* grf_gram_dense_upper on the split products (ABI 6): the hub-column split's panel. */
+int32_t grf_gram_dense_split_upper(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
+                                   grf_stream_t stream);
 
 /* CSR (float32) -> dense float32 [n_rows x lda], zero filled. */
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,
