@@ -505,6 +505,21 @@ __device__ __forceinline__ void split3(f32x4v lo, f32x4v hi, bf16x8 &p0, bf16x8 
     }
 }
 
+// elements 2 i, 2 i + 1 of split3 (the same operations): a slice of one operand's split to place between MFMAs
+template <int I>
+__device__ __forceinline__ void split_pair(f32x4v lo, f32x4v hi, bf16x8 &p0, bf16x8 &p1, bf16x8 &p2) {
+#pragma unroll
+    for (int e = 2 * I; e < 2 * I + 2; ++e) {
+        const float v = e < 4 ? lo[e] : hi[e - 4];
+        const __bf16 a0 = (__bf16)v;
+        const float r1 = v - (float)a0;
+        const __bf16 a1 = (__bf16)r1;
+        p0[e] = a0;
+        p1[e] = a1;
+        p2[e] = (__bf16)(r1 - (float)a1);
+    }
+}
+
 // The k-loop of one tile over [kb, ke) with the split products.  The ring, the DMA pieces (issue: all of
 // k-tile t's) and the retire/publish step are kloop's; per k-tile a wave reads its 2 + 2 blocks' two chunks,
 // splits them and issues 4 blocks x 6 MFMAs.
@@ -516,56 +531,77 @@ __device__ __forceinline__ void kloop_split(float *lds, const float *const *srcA
     using St = Stage<16>;
     constexpr int G = DIAG ? St::PW : 2 * St::PW;  // DMA pieces per wave per k-tile
     const int64_t nk = (ke - kb) / 16;
+    // k-tile t's pieces into stage t % NST.  Issued unconditionally, the k-tiles past the last re-load the last
+    // one into a stage nothing reads again (no branch in the MFMA region; every wait is the same count)
     auto issue = [&](int64_t t) {
         float *base = lds + (int)(t % NST) * 2 * St::F + wave * St::PW * 256;
-        const int64_t k0 = kb + t * 16;
+        const int64_t k0 = kb + (t < nk ? t : nk - 1) * 16;
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             if (j < St::PW) dma16(srcA[j] + k0, base + j * 256);
             else dma16(srcB[j - St::PW] + k0, base + St::F + (j - St::PW) * 256);
         }
     };
+    auto issue_part = [&](int64_t t, int q) {  // piece q of k-tile t's G (<= 4) pieces
+        if (q >= G) return;
+        float *base = lds + (int)(t % NST) * 2 * St::F + wave * St::PW * 256;
+        const int64_t k0 = kb + (t < nk ? t : nk - 1) * 16;
+        if (q < St::PW) dma16(srcA[q] + k0, base + q * 256);
+        else dma16(srcB[q - St::PW] + k0, base + St::F + (q - St::PW) * 256);
+    };
     if (nk <= 0) return;
 #pragma unroll
-    for (int t = 0; t < NST - 1; ++t)
-        if (t < nk) issue(t);
+    for (int t = 0; t < NST - 1; ++t) issue(t);
     for (int64_t t = 0; t < nk; ++t) {
-        // k-tile t landed (the younger ones issued so far may stay in flight), then published
-        const int64_t younger = (t + NST - 2 < nk - 1 ? t + NST - 2 : nk - 1) - t;
-        if (younger >= 2) wait_vm<2 * G>();
-        else if (younger == 1) wait_vm<G>();
-        else wait_vm<0>();
+        wait_vm<(NST - 2) * G>();  // k-tile t landed (the NST - 2 younger ones may stay in flight), then published
         __builtin_amdgcn_s_barrier();  // (also: every wave is done with k-tile t - 1, whose stage refills now)
         asm volatile("" ::: "memory");
-        if (t + NST - 1 < nk) issue(t + NST - 1);
-        if constexpr (LIVE) {
+        if constexpr (!LIVE) {
+            issue(t + NST - 1);
+        } else {
             const float *As = lds + (int)(t % NST) * 2 * St::F;
             const float *Bs = DIAG ? As : As + St::F;
-            bf16x8 a[2][3], b[2][3];
-#pragma unroll
-            for (int x = 0; x < 2; ++x) {
-                const char *pa = reinterpret_cast<const char *>(As) + aoff[0] * 4 + x * L::XSTRIDE;
-                const char *pa1 = reinterpret_cast<const char *>(As) + aoff[1] * 4 + x * L::XSTRIDE;
-                split3(*reinterpret_cast<const f32x4v *>(pa), *reinterpret_cast<const f32x4v *>(pa1), a[x][0], a[x][1],
-                       a[x][2]);
-                const char *pb = reinterpret_cast<const char *>(Bs) + boff[0] * 4 + x * L::XSTRIDE;
-                const char *pb1 = reinterpret_cast<const char *>(Bs) + boff[1] * 4 + x * L::XSTRIDE;
-                split3(*reinterpret_cast<const f32x4v *>(pb), *reinterpret_cast<const f32x4v *>(pb1), b[x][0], b[x][1],
-                       b[x][2]);
-            }
+            const char *pa = reinterpret_cast<const char *>(As), *pb = reinterpret_cast<const char *>(Bs);
+            f32x4v ra[2][2], rb[2][2];
 #pragma unroll
             for (int x = 0; x < 2; ++x)
 #pragma unroll
-                for (int y = 0; y < 2; ++y) {
-                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][0], c0[x][y], 0, 0, 0);
-                    f32x16 d = c1[x][y];
-                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][1], d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][1], b[y][0], d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][2], d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][1], b[y][1], d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][2], b[y][0], d, 0, 0, 0);
-                    c1[x][y] = d;
+                for (int g = 0; g < 2; ++g) {
+                    ra[x][g] = *reinterpret_cast<const f32x4v *>(pa + aoff[g] * 4 + x * L::XSTRIDE);
+                    rb[x][g] = *reinterpret_cast<const f32x4v *>(pb + boff[g] * 4 + x * L::XSTRIDE);
                 }
+            bf16x8 a[2][3], b[2][3];
+            // block (0, 0) needs A0 and B0 split; B1's and A1's splits (a pair of elements per MFMA) and the next
+            // k-tile's DMA pieces go between the MFMAs of the blocks before them, in this order (sched_barrier
+            // fences): VALU and VMEM issue in the MFMA shadows instead of ~110 VALU ahead of the first MFMA
+            split3(ra[0][0], ra[0][1], a[0][0], a[0][1], a[0][2]);
+            split3(rb[0][0], rb[0][1], b[0][0], b[0][1], b[0][2]);
+            __builtin_amdgcn_sched_barrier(0);
+            auto mf = [&](int x, int y, int s) {
+                if (s == 0) {
+                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][0], c0[x][y], 0, 0, 0);
+                    return;
+                }
+                constexpr int P[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
+                c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][P[s][0]], b[y][P[s][1]], c1[x][y], 0, 0, 0);
+            };
+            auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+            mf(0, 0, 0); split_pair<0>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
+            mf(0, 0, 1); split_pair<1>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
+            mf(0, 0, 2); split_pair<2>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
+            mf(0, 0, 3); split_pair<3>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
+            mf(0, 0, 4); issue_part(t + NST - 1, 0); fence();
+            mf(0, 0, 5); issue_part(t + NST - 1, 1); fence();
+            mf(0, 1, 0); split_pair<0>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
+            mf(0, 1, 1); split_pair<1>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
+            mf(0, 1, 2); split_pair<2>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
+            mf(0, 1, 3); split_pair<3>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
+            mf(0, 1, 4); issue_part(t + NST - 1, 2); fence();
+            mf(0, 1, 5); issue_part(t + NST - 1, 3); fence();
+#pragma unroll
+            for (int s = 0; s < 6; ++s) mf(1, 0, s);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) mf(1, 1, s);
         }
     }
 }
