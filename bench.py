@@ -80,11 +80,12 @@ def auto_hubs(eng, A_dev, m, p, L, f, share: float = 0.13):
     """(hub columns worth a dense panel, skewed) from one setup walk (untimed): a column in c of the n rows
     saves ~c^2 / 2 gathered records and costs n^2 / 2 MFMA multiply-adds, ~60x cheaper each, so it pays from
     c / n ~ 1 / sqrt(60) = 0.13 (measured: Enron's best split is 128 columns, whose c reaches 13 % of n;
-    Facebook's 64th column is in 9 % of the rows and the split loses there, profiles/r02_hubs_sweep.txt).
+    Facebook's 64th column is in 9 % of the rows and the split loses there, profiles/r02_hubs_sweep.txt);
+    with the split (bf16) panel the count is then taken at engine.HUB_EXTEND_SHARE (Enron 192 columns).
     Multiples of 32 (the panel's width).  skewed: the Gram's waves take pair-balanced shares
     (engine.row_cuts)."""
     from grf_amd.dist import setup_phi
-    return eng.column_stats(setup_phi(eng, A_dev, m, p, L, f, seed=42), share)
+    return eng.column_stats(setup_phi(eng, A_dev, m, p, L, f, seed=42), share, extend=eng.hub_extend_share())
 
 
 def init_distributed(local_rank: int) -> int:

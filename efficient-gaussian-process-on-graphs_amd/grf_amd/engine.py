@@ -33,6 +33,10 @@ DEFAULT_BAND_WIDTH = 4096  # transpose band = one Gram tile (32 KB int64 LDS acc
 ROWS_BAND_WIDTH = 8192
 # hub-column split: columns in at least this share of Phi's rows go to the dense MFMA panel (hub_count)
 HUB_SHARE = 0.13
+# ... and once a graph has such columns, with the split panel (bf16 products: 3/8 of the fp32 MFMA's cost per
+# multiply-add) the columns down to this share as well: Enron 96 -> 192 columns, 7.52 -> 7.38 ms per K; 128 /
+# 256 columns 7.47 / 7.50 (profiles/r05_hub_sweep_split.txt); Facebook's 20 columns above 0.13 stay unsplit
+HUB_EXTEND_SHARE = 0.105
 # gram(method="auto"): the dense MFMA path up to this many rows, the sparse path above
 DENSE_GRAM_MAX_N = 4500  # measured crossover, profiles/r03_gram_crossover.txt
 # the banded transpose counts its buckets itself (grf_transpose_banded_self: no count atomics in the
@@ -844,15 +848,27 @@ class GRFEngine:
         return out[:, :n]
 
     @staticmethod
-    def column_stats(phi: DeviceCSR, share: float = HUB_SHARE) -> Tuple[int, bool]:
+    def column_stats(phi: DeviceCSR, share: float = HUB_SHARE,
+                     extend: Optional[float] = None) -> Tuple[int, bool]:
         """(hub_count, skewed) from one column count of Phi: skewed when the densest column holds at
-        least SKEW_RATIO times the mean column's entries (the policy of ``row_cuts``).  One host read."""
+        least SKEW_RATIO times the mean column's entries (the policy of ``row_cuts``).  extend: when at least
+        one panel width of columns reaches ``share``, the hub count is taken at this (lower) share instead
+        (``HUB_EXTEND_SHARE``, the split panel's).  One host read."""
         n = phi.n_cols
         if phi.nnz == 0 or n == 0:
             return 0, False
         c = torch.bincount(phi.idx[:phi.nnz].long(), minlength=n)
-        hubs, cmax = (int(x) for x in torch.stack([(c >= share * phi.n_rows).sum(), c.max()]).tolist())
-        return hubs // 32 * 32, cmax >= SKEW_RATIO * phi.nnz / n
+        low = share if extend is None else min(share, extend)
+        hubs, wide, cmax = (int(x) for x in torch.stack([(c >= share * phi.n_rows).sum(),
+                                                          (c >= low * phi.n_rows).sum(), c.max()]).tolist())
+        hubs = hubs // 32 * 32
+        if hubs and extend is not None:
+            hubs = wide // 32 * 32
+        return hubs, cmax >= SKEW_RATIO * phi.nnz / n
+
+    def hub_extend_share(self) -> Optional[float]:
+        """The panel's extension share for this engine's dense precision (None: the fp32 panel)."""
+        return HUB_EXTEND_SHARE if self.dense_precision == "split" else None
 
     @staticmethod
     def hub_count(phi: DeviceCSR, share: float = HUB_SHARE) -> int:
@@ -871,7 +887,7 @@ class GRFEngine:
         """Whole K on the sparse path exactly as the bench assembles it: the symmetric tiles + mirror,
         with the hub-column split when Phi has hub columns (``hub_count``)."""
         tr = self.transpose_banded(phi)
-        hubs, skewed = self.column_stats(phi)
+        hubs, skewed = self.column_stats(phi, extend=self.hub_extend_share())
         if hubs:
             return self.gram_sparse_sym_hubs(phi, tr, hubs, out=out, skewed=skewed)
         return self.gram_sparse_sym(phi, tr, out=out, skewed=skewed)
