@@ -38,7 +38,7 @@ HUB_SHARE = 0.13
 # 256 columns 7.47 / 7.50 (profiles/r05_hub_sweep_split.txt); Facebook's 20 columns above 0.13 stay unsplit
 HUB_EXTEND_SHARE = 0.105
 # gram(method="auto"): the dense MFMA path up to this many rows, the sparse path above
-DENSE_GRAM_MAX_N = 4500  # measured crossover, profiles/r03_gram_crossover.txt
+DENSE_GRAM_MAX_N = 4500  # measured crossover, profiles/r03_gram_crossover.txt (split Gram: r05_gram_crossover.txt)
 # the banded transpose counts its buckets itself (grf_transpose_banded_self: no count atomics in the
 # walk, no scan over every bucket); GRF_TRANSPOSE_SELF=0 restores the walk-counted plan (A/B)
 SELF_COUNT_TRANSPOSE = os.environ.get("GRF_TRANSPOSE_SELF", "1") != "0"
