@@ -870,18 +870,15 @@ class GRFEngine:
         """The panel's extension share for this engine's dense precision (None: the fp32 panel)."""
         return HUB_EXTEND_SHARE if self.dense_precision == "split" else None
 
-    @staticmethod
-    def hub_count(phi: DeviceCSR, share: float = HUB_SHARE) -> int:
-        """Hub columns worth the dense MFMA panel of the hub-column split: the columns of Phi present in
-        at least ``share`` of its rows, in multiples of 32 (the panel's width).  A column in c of the n
-        rows saves ~c^2 / 2 gathered records and costs n^2 / 2 MFMA multiply-adds, ~60x cheaper each,
-        so it pays from c / n ~ 1 / sqrt(60) = 0.13 (Enron 96 columns, C4 / Facebook 0:
-        profiles/r02_hubs_sweep.txt).  One host read."""
-        n = phi.n_cols
-        if phi.nnz == 0 or n == 0:
-            return 0
-        c = torch.bincount(phi.idx[:phi.nnz].long(), minlength=n)
-        return int((c >= share * phi.n_rows).sum().item()) // 32 * 32
+    def hub_count(self, phi: DeviceCSR, share: float = HUB_SHARE) -> int:
+        """Hub columns worth the dense MFMA panel of the hub-column split (the policy of ``gram_sparse_auto``
+        and the bench's --hubs auto): the columns of Phi present in at least ``share`` of its rows, in
+        multiples of 32 (the panel's width) -- with the split panel, once there are any, those down to
+        ``HUB_EXTEND_SHARE``.  A column in c of the n rows saves ~c^2 / 2 gathered records and costs n^2 / 2
+        MFMA multiply-adds, ~60x cheaper each on the fp32 panel, so it pays from c / n ~ 1 / sqrt(60) = 0.13
+        (profiles/r02_hubs_sweep.txt); the split panel's 3/8 of that cost moved Enron's best count from 96 to
+        192 columns (profiles/r05_hub_sweep_split.txt).  One host read."""
+        return self.column_stats(phi, share, extend=self.hub_extend_share())[0]
 
     def gram_sparse_auto(self, phi: DeviceCSR, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Whole K on the sparse path exactly as the bench assembles it: the symmetric tiles + mirror,
