@@ -1,4 +1,5 @@
-// grf_gram_dense.hip -- the dense path's Gram K = A A^T on the fp32 MFMA.
+// grf_gram_dense.hip -- the dense path's Gram K = A A^T on the MFMA: the fp32 instruction (grf_gram_dense_ws) and
+// the same product on the bf16 matrix cores from an exact three-plane split of A (grf_gram_dense_split, below).
 //
 // Reference: efficient_graph_gp/graph_kernels/fast_grf_kernel_general.py:38-39 (Phi = F f; K = Phi Phi^T,
 // a numpy dgemm); here A is the dense fp32 Phi (n x k_dim, row-major, zero-padded to lda).
