@@ -37,15 +37,17 @@ from grf_amd.graphs import er_graph_exact_edges, powerlaw_graph, snap_graph  # n
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh -> tools/pmc_summary.py), committed
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_summary.json")
+# ... and of the C5 workload (bench.py --workload c5; tools/gpu_steps.sh pmc step)
+PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "r05_c5_pmc_summary.json")
 DEFAULT_WORKLOAD = (100_000, 1_000_000, 128, 8, 0.1)
 
 
-def pmc_traffic(kernels):
+def pmc_traffic(kernels, path=PMC_SUMMARY):
     """HBM bytes per launch of the named kernels from the committed PMC summary
     (2 * FETCH_SIZE + WRITE_SIZE KiB, the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md)."""
     import json as _json
     try:
-        d = _json.load(open(PMC_SUMMARY))
+        d = _json.load(open(path))
     except (OSError, ValueError):
         return None
     total = 0.0
@@ -57,11 +59,11 @@ def pmc_traffic(kernels):
     return total
 
 
-def pmc_counter(kernel, counter):
+def pmc_counter(kernel, counter, path=PMC_SUMMARY):
     """One counter's per-launch value of the named kernel from the committed PMC summary (None if absent)."""
     import json as _json
     try:
-        d = _json.load(open(PMC_SUMMARY))
+        d = _json.load(open(path))
     except (OSError, ValueError):
         return None
     hits = [v for name, v in d.items() if name.split("<")[0].replace("void ", "") == kernel]
@@ -850,7 +852,10 @@ def main():
     sym = pl.mode == "sym"
     kernels = ["grf::gram_sparse_kernel", "grf::gram_mirror_swz_kernel"] if sym else ["grf::gram_sparse_kernel"]
     headline = (n, args.edges, m, L, p) == DEFAULT_WORKLOAD and args.graph == "er" and world == 1 and sym
-    traffic = pmc_traffic(kernels) if headline else None
+    # the committed PMC summary of this workload: the headline's, or C5's (one GPU)
+    pmc_path = PMC_SUMMARY if headline else (
+        PMC_SUMMARY_C5 if getattr(args, "workload", "") == "c5" and world == 1 else None)
+    traffic = pmc_traffic(kernels, pmc_path) if pmc_path else None
     # the walk kernel (phi_fused_kernel): per walk, E[moves] = (1-p)(1-(1-p)^(L-1))/p recorded moves,
     # each reading the current node's row bounds + the chosen entry's column and weight (SURVEY.md
     # §8d: 16 B per move), + the compact Phi row written (int32 column + fp32 value per entry)
@@ -858,12 +863,12 @@ def main():
     moves = walks * (1.0 - p) * (1.0 - (1.0 - p) ** (L - 1)) / p
     walk_alg = 16.0 * moves + 8.0 * local_nnz
     walk_achieved = walk_alg / (walk_ms * 1e-3) / 1e9
-    walk_traffic = pmc_traffic(["grf::phi_fused_kernel"]) if headline else None
+    walk_traffic = pmc_traffic(["grf::phi_fused_kernel"], pmc_path) if pmc_path else None
     # the walk's VALU issue rate from ONE rocprofv3 --pmc pass (SQ_INSTS_VALU and GRBM_GUI_ACTIVE counted
     # together, tools/pmc_passes.sh "sq"): wave-instructions per SIMD-cycle, the cycles of the dispatch being
     # GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs, MI355X_MICROARCH.md); no clock or timer involved
-    walk_valu = pmc_counter("grf::phi_fused_kernel", "SQ_INSTS_VALU") if headline else None
-    walk_gui = pmc_counter("grf::phi_fused_kernel", "GRBM_GUI_ACTIVE") if headline else None
+    walk_valu = pmc_counter("grf::phi_fused_kernel", "SQ_INSTS_VALU", pmc_path) if pmc_path else None
+    walk_gui = pmc_counter("grf::phi_fused_kernel", "GRBM_GUI_ACTIVE", pmc_path) if pmc_path else None
     walk_valu_rate = walk_valu / (walk_gui / 8.0 * N_SIMDS) if walk_valu and walk_gui else None
     wl = workload_name(args, A)
     if args.k_rows:
@@ -910,7 +915,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": (f"rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of the same kernels on this workload, "
-                                        f"{os.path.relpath(PMC_SUMMARY, ROOT)} (FETCH_SIZE x the calibrated factor "
+                                        f"{os.path.relpath(pmc_path or PMC_SUMMARY, ROOT)} (FETCH_SIZE x the calibrated factor "
                                         f"+ WRITE_SIZE; bytes per launch)")
                      if traffic is not None else None,
                      "kernel": "+".join(k.split("::")[1] for k in kernels), "kernel_ms": gram_avg,
@@ -924,7 +929,7 @@ def main():
                           "valu_insts_per_launch": walk_valu,
                           "gui_active_cycles_per_launch": walk_gui / 8.0 if walk_gui else None,
                           "valu_source": (f"one rocprofv3 --pmc pass of this workload (SQ_INSTS_VALU, GRBM_GUI_ACTIVE), "
-                                          f"{os.path.relpath(PMC_SUMMARY, ROOT)}: SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x "
+                                          f"{os.path.relpath(pmc_path or PMC_SUMMARY, ROOT)}: SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x "
                                           f"1024 SIMDs) against the measured 1 wave64 VALU instruction per 4 cycles per SIMD "
                                           f"(profiles/r04_valu_ceiling.txt; fp64 transcendentals take 16: a lower bound "
                                           f"of the VALU pipe's busy share)") if walk_valu_rate is not None else None,
