@@ -441,3 +441,28 @@ def test_gather_model_counts_bucket_line_visits():
                     want_rec += visits * pairs[b, k] * 12
             got = bench.gather_model(phi, tr, sym=sym)
             assert got[0] == want_lines and got[1] == want_rec, (unit, sym)
+
+
+def test_hub_column_policy_extension():
+    """engine.column_stats: columns in >= share of the rows, in panel widths of 32; with `extend` (the split
+    panel's HUB_EXTEND_SHARE) a graph that has a panel at `share` takes its columns down to `extend`, and a
+    graph without one stays unsplit (Enron 96 -> 192 columns, Facebook 0)."""
+    from grf_amd.engine import HUB_EXTEND_SHARE, HUB_SHARE, DeviceCSR, GRFEngine
+
+    def csr_with_column_counts(n_rows, counts):
+        cols = np.concatenate([np.full(c, k, np.int32) for k, c in enumerate(counts)])
+        ptr = torch.zeros(n_rows + 1, dtype=torch.int64)
+        ptr[-1] = len(cols)  # (only the column list and nnz are read)
+        return DeviceCSR(n_rows, len(counts), ptr, torch.from_numpy(cols), None, None, len(cols))
+
+    n = 1000
+    # 40 columns in 14 % of the rows, 40 more in 11 %, the rest in 1 %
+    counts = [140] * 40 + [110] * 40 + [10] * 200
+    phi = csr_with_column_counts(n, counts)
+    assert GRFEngine.column_stats(phi, HUB_SHARE)[0] == 32
+    assert GRFEngine.column_stats(phi, HUB_SHARE, extend=HUB_EXTEND_SHARE)[0] == 64
+    # fewer than one panel width at the gate share: no split, extension or not
+    counts = [140] * 20 + [110] * 60 + [10] * 200
+    phi = csr_with_column_counts(n, counts)
+    assert GRFEngine.column_stats(phi, HUB_SHARE)[0] == 0
+    assert GRFEngine.column_stats(phi, HUB_SHARE, extend=HUB_EXTEND_SHARE)[0] == 0
