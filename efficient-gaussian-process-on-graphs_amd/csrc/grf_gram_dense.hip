@@ -355,14 +355,14 @@ __device__ __forceinline__ Quarter tile_compute(const DenseArgs &a, float *lds, 
 // registers) into c and returns true.  Hand-off: slab stores -> every wave vmcnt(0) -> barrier -> agent
 // release -> ticket fetch_add; the last arriver resets the ticket, then agent acquire -> barrier -> loads.
 // `flag` is LDS the ring no longer uses (every wave is past its k-loop).
-template <int MF, int BK, typename SlabOf>
+template <int MF, int BK, int NW = 4, typename SlabOf>
 __device__ __forceinline__ bool split_combine(const DenseArgs &a,
                                               typename Layout<MF, BK>::acc_t (&c)[Layout<MF, BK>::NBLK]
                                                                                  [Layout<MF, BK>::NBLK],
                                               int32_t *ticket, int64_t pieces, int64_t me, SlabOf slab_of,
                                               int32_t *flag, int wave, int lane) {
     using L = Layout<MF, BK>;
-    constexpr int64_t kSlab = 4 * 16 * 64;  // float4 per piece: [4 waves][16 float4][64 lanes]
+    constexpr int64_t kSlab = NW * 16 * 64;  // float4 per piece: [NW waves][16 float4][64 lanes]
     f32x4v *mine = reinterpret_cast<f32x4v *>(a.slabs) + slab_of(me) * kSlab + wave * 16 * 64 + lane;
 #pragma unroll
     for (int j = 0; j < 16; ++j) mine[j * 64] = L::get(c, j);
@@ -714,6 +714,182 @@ __global__ __launch_bounds__(256, 2) void gram_split_sk_kernel(DenseArgs a) {
     }
 }
 
+// Wide workgroups for the split path (large n): 8 waves own a 256 x 128 item -- the row-block pair
+// (2p, 2p + 1) against column block j >= 2p -- each wave the same 64 x 64 quarter (2 x 2 blocks, c0 / c1) as
+// above.  A k-tile stages 256 + 128 rows (24 KiB) for 8 x 24 MFMAs instead of 256 rows for 4 x 24: 3 DMA
+// pieces per wave and k-tile instead of 4, 3/4 of the staged bytes per flop (the 128-tile split kernel is
+// bound by its LDS-DMA staging and its split VALU about equally: timing-only ablations in
+// profiles/r05_split_gram_ab.txt).  One workgroup per CU (96 KiB ring; 3 or 5 stages measured slower), 2 waves
+// per SIMD as before; stream-K over the items' k-tiles at every size.  A diagonal item (j = 2p or 2p + 1)
+// stages its B rows again although they are A rows: ~2.5 % of the items at C2.
+struct WideStage {
+    static constexpr int FA = 2 * kTile * 16, FB = kTile * 16, F = FA + FB;  // floats per stage
+    static constexpr int PW = F / 256 / 8;                                   // 1-KiB pieces per wave
+};
+static_assert(WideStage::PW * 256 * 8 == WideStage::F, "a stage is whole pieces over 8 waves");
+
+// item b (row-major over (row pair p, column block j >= 2 p)) -> (p, j); row pair p has nt - 2 p items
+__device__ __forceinline__ void item_coords(int64_t b, int64_t nt, int64_t &p, int64_t &j) {
+    auto first = [nt](int64_t r) { return r * (nt + 1) - r * r; };
+    const int64_t np = (nt + 1) / 2;
+    const double t = (double)(nt + 1);
+    int64_t i = (int64_t)((t - sqrt(t * t - 4.0 * (double)b)) * 0.5);
+    if (i < 0) i = 0;
+    if (i > np - 1) i = np - 1;
+    while (i > 0 && first(i) > b) --i;
+    while (i < np - 1 && first(i + 1) <= b) ++i;
+    p = i;
+    j = 2 * i + (b - first(i));
+}
+
+template <int NST, bool LIVE>
+__device__ __forceinline__ void kloop_wide(float *lds, const float *const *src, const int *dst, int64_t kb, int64_t ke,
+                                           const int *aoff, const int *boff, f32x16 (&c0)[2][2],
+                                           f32x16 (&c1)[2][2]) {
+    using L = Layout<32, 16>;
+    constexpr int G = WideStage::PW;
+    static_assert(G == 3, "the DMA placement below is written for 3 pieces per wave");
+    const int64_t nk = (ke - kb) / 16;
+    auto issue_part = [&](int64_t t, int q) {
+        const int64_t k0 = kb + (t < nk ? t : nk - 1) * 16;
+        dma16(src[q] + k0, lds + (int)(t % NST) * WideStage::F + dst[q]);
+    };
+    if (nk <= 0) return;
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+#pragma unroll
+        for (int q = 0; q < G; ++q) issue_part(t, q);
+    for (int64_t t = 0; t < nk; ++t) {
+        wait_vm<(NST - 2) * G>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if constexpr (!LIVE) {
+#pragma unroll
+            for (int q = 0; q < G; ++q) issue_part(t + NST - 1, q);
+        } else {
+            const float *As = lds + (int)(t % NST) * WideStage::F;
+            const char *pa = reinterpret_cast<const char *>(As);
+            const char *pb = reinterpret_cast<const char *>(As + WideStage::FA);
+            f32x4v ra[2][2], rb[2][2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    ra[x][g] = *reinterpret_cast<const f32x4v *>(pa + aoff[g] * 4 + x * L::XSTRIDE);
+                    rb[x][g] = *reinterpret_cast<const f32x4v *>(pb + boff[g] * 4 + x * L::XSTRIDE);
+                }
+            bf16x8 a[2][3], b[2][3];
+            split3(ra[0][0], ra[0][1], a[0][0], a[0][1], a[0][2]);
+            split3(rb[0][0], rb[0][1], b[0][0], b[0][1], b[0][2]);
+            __builtin_amdgcn_sched_barrier(0);
+            auto mf = [&](int x, int y, int s) {
+                if (s == 0) {
+                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][0], c0[x][y], 0, 0, 0);
+                    return;
+                }
+                constexpr int P[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
+                c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][P[s][0]], b[y][P[s][1]], c1[x][y], 0, 0, 0);
+            };
+            auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+            mf(0, 0, 0); split_pair<0>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
+            mf(0, 0, 1); split_pair<1>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
+            mf(0, 0, 2); split_pair<2>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
+            mf(0, 0, 3); split_pair<3>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
+            mf(0, 0, 4); issue_part(t + NST - 1, 0); fence();
+            mf(0, 0, 5); issue_part(t + NST - 1, 1); fence();
+            mf(0, 1, 0); split_pair<0>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
+            mf(0, 1, 1); split_pair<1>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
+            mf(0, 1, 2); split_pair<2>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
+            mf(0, 1, 3); split_pair<3>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
+            mf(0, 1, 4); issue_part(t + NST - 1, 2); fence();
+            mf(0, 1, 5);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) mf(1, 0, s);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) mf(1, 1, s);
+        }
+    }
+}
+
+template <int NST>
+__device__ __forceinline__ Quarter item_compute_wide(const DenseArgs &a, float *lds, int64_t item, int64_t kb,
+                                                     int64_t ke, int wave, int lane, f32x16 (&c)[2][2]) {
+    using L = Layout<32, 16>;
+    const int wm = wave >> 1, wn = wave & 1;
+    int64_t p, j;
+    item_coords(item, a.nt, p, j);
+    const int64_t m0 = 2 * p * kTile, n0 = j * kTile;
+    // piece P = wave PW + i of the stage: P < 16 the A image's (rows m0 ..), else the B image's (rows n0 ..)
+    constexpr int PA = WideStage::FA / 256;
+    const float *src[WideStage::PW];
+    int dst[WideStage::PW];
+#pragma unroll
+    for (int i = 0; i < WideStage::PW; ++i) {
+        const int P = wave * WideStage::PW + i;
+        const bool isA = P < PA;
+        const int pc = (isA ? P : P - PA) * 64 + lane;
+        const int row = pc / L::C, kc = (pc % L::C) ^ L::swz(row);
+        int64_t r = (isA ? m0 : n0) + row;
+        r = r < a.n ? r : a.n - 1;
+        src[i] = a.A + r * a.lda + 4 * kc;
+        dst[i] = isA ? P * 256 : WideStage::FA + (P - PA) * 256;
+    }
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        aoff[g] = L::off(wm * 64, 0, g, lane);
+        boff[g] = L::off(wn * 64, 0, g, lane);
+    }
+    const int64_t R = m0 + wm * 64, Cc = n0 + wn * 64;
+    Quarter q{R, Cc, R == Cc, R > Cc};
+    const bool live = !q.below && R < a.n && Cc < a.n;
+    f32x16 c0[2][2], c1[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            c0[x][y] = f32x16{};
+            c1[x][y] = f32x16{};
+        }
+    if (live) kloop_wide<NST, true>(lds, src, dst, kb, ke, aoff, boff, c0, c1);
+    else kloop_wide<NST, false>(lds, src, dst, kb, ke, aoff, boff, c0, c1);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) c[x][y] = c0[x][y] + c1[x][y];
+    return q;
+}
+
+// stream-K over the items laid end to end (units of one k-tile), as gram_split_sk_kernel over the tiles
+template <int NST>
+__global__ __launch_bounds__(512, 1) void gram_split_wide_kernel(DenseArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[NST * WideStage::F];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t U = a.sk_units, KT = a.sk_kt;
+    const int64_t u0 = (int64_t)blockIdx.x * U;
+    const int64_t u1 = u0 + U < a.sk_total ? u0 + U : a.sk_total;
+    for (int64_t u = u0; u < u1;) {
+        const int64_t item = u / KT, tb = item * KT, te = tb + KT;
+        const int64_t se = u1 < te ? u1 : te;
+        __syncthreads();
+        f32x16 c[2][2];
+        const Quarter q = item_compute_wide<NST>(a, lds, item, (u - tb) * 16, (se - tb) * 16, wave, lane, c);
+        bool write = true;
+        if (u != tb || se != te) {
+            const int64_t s0 = tb / U, s1 = (te - 1) / U;
+            const int64_t first = 2 * s0 + (tb == s0 * U ? 0 : 1);
+            write = split_combine<32, 16, 8>(
+                a, c, a.tickets + first, s1 - s0 + 1, blockIdx.x - s0,
+                [&](int64_t j) { return j == 0 ? first : 2 * (s0 + j); }, reinterpret_cast<int32_t *>(lds), wave,
+                lane);
+        }
+        if (write && !q.below && q.qr < a.n && q.qc < a.n)
+            write_quarter<32, 16>(a, c, q.qr, q.qc, q.diag, false, lane);
+        u = se;
+    }
+}
+
 constexpr int kCUs = 256;
 
 int env_int(const char *name, int dflt) {
@@ -787,6 +963,19 @@ SkPlan sk_plan(int64_t n, int64_t k_dim, int bk) {
     p.units = std::max<int64_t>(1, cdiv<int64_t>(p.total, slots));
     p.grid = cdiv<int64_t>(p.total, p.units);
     p.ws_bytes = kTicketBytes + (size_t)(2 * p.grid) * kTile * kTile * sizeof(float);
+    return p;
+}
+
+// The wide split kernel's stream-K plan: one 8-wave workgroup per CU, items of 256 x 128, slabs of 128 KiB
+SkPlan sk_plan_wide(int64_t n, int64_t k_dim) {
+    SkPlan p{};
+    const int64_t nt = cdiv<int64_t>(n, kTile), np = (nt + 1) / 2;
+    p.kt = cdiv<int64_t>(k_dim, 16);
+    p.total = (np * (nt + 1) - np * np) * p.kt;
+    const int64_t slots = std::min<int64_t>(kCUs, std::max<int64_t>(p.total, 1));
+    p.units = std::max<int64_t>(1, cdiv<int64_t>(p.total, slots));
+    p.grid = cdiv<int64_t>(p.total, p.units);
+    p.ws_bytes = kTicketBytes + (size_t)(2 * p.grid) * 2 * kTile * kTile * sizeof(float);
     return p;
 }
 
@@ -870,7 +1059,10 @@ int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float 
 
 
 // The split path: the fp32 path's workspace (tickets and slabs; the ticket block must be zero on first use)
-size_t dense_gram_split_workspace_bytes(int64_t n, int64_t k_dim) { return dense_gram_workspace_bytes(n, k_dim); }
+size_t dense_gram_split_workspace_bytes(int64_t n, int64_t k_dim) {
+    const size_t base = dense_gram_workspace_bytes(n, k_dim);
+    return n <= 0 ? base : std::max(base, sk_plan_wide(n, k_dim).ws_bytes);
+}
 
 // workspace NULL (the hub panel's upper_only call): whole tiles only, as dense_gram without one
 int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
@@ -898,6 +1090,24 @@ int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, 
     a.ldk = ldk;
     a.kpad = p.kpad;
     a.upper_only = upper_only ? 1 : 0;
+    // the wide workgroups (256 x 128 items) from 64 tile rows on (n > 8064): C2 (n = 10 000) 5.60 -> 5.12 ms,
+    // n = 16384 24.5 -> 22.7; equal at n = 6144, slower at C3 (0.148 -> 0.164: 132 items on 256 CUs, every one
+    // cut) -- profiles/r05_split_gram_ab.txt.  GRF_DENSE_WIDE (read per call, for A/B and tests): 0 never,
+    // 1 always, unset / -1 by that rule.
+    const int wide_env = env_int("GRF_DENSE_WIDE", -1);
+    const bool wide = wide_env == 1 || (wide_env != 0 && p.nt >= 64);
+    if (wide && workspace && !upper_only && p.kpad > 0) {
+        const SkPlan q = sk_plan_wide(n, k_dim);
+        GRF_REQUIRE_GRID(q.grid, 512, "gram_split_wide_kernel");
+        a.tickets = reinterpret_cast<int32_t *>(workspace);
+        a.slabs = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes);
+        a.sk_units = q.units;
+        a.sk_kt = q.kt;
+        a.sk_total = q.total;
+        gram_split_wide_kernel<kSplitNST><<<(unsigned)q.grid, 512, 0, st>>>(a);
+        GRF_CHECK_LAUNCH("gram_split_wide_kernel");
+        return GRF_OK;
+    }
     static const int sk_env = env_int("GRF_DENSE_SK", -1);
     const bool sk = workspace && (sk_env == 1 || (sk_env != 0 && p.tiles >= kCUs));
     if (!workspace) {

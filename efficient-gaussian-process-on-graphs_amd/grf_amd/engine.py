@@ -830,7 +830,7 @@ class GRFEngine:
         # workspace per stream, ZEROED when allocated (the kernel leaves the tickets zero after every
         # launch; an uninitialised block gave round 4's NaN, profiles/AB_LOG.md "dense-Gram NaN"), dropped
         # after a failed call so that no ticket a broken launch may have left is read again.  The split
-        # path's planes follow the ticket block and slabs in the same workspace.
+        # path sizes it for its own (wide-workgroup) slabs as well.
         need = int(self.lib.grf_gram_dense_split_workspace_bytes(n, k_dim) if split
                    else self.lib.grf_gram_dense_workspace_bytes(n, k_dim))
         stream = self.stream

@@ -592,10 +592,40 @@ def test_gram_dense_split_vs_fp64_and_fp32(eng, n, k):
     assert np.array_equal(eng.gram_dense(At, k, precision="split").cpu().numpy(), Ksn)
 
 
+@pytest.mark.parametrize("n,k", [(100, 37), (300, 900), (1153, 1153), (2708, 2708), (4200, 20), (4200, 1000),
+                                 (4500, 16)])
+def test_gram_dense_split_wide(eng, monkeypatch, n, k):
+    """The split Gram's wide workgroups (256 x 128 items, stream-K; the default from 64 tile rows on, forced
+    here with GRF_DENSE_WIDE=1 at small n): odd tile-row counts (the item's second row block past n), k of
+    one or two k-tiles (items cut at many slot boundaries), against fp64 within the fp32 path's bound, against
+    the 128-tile split kernel (GRF_DENSE_WIDE=0) within twice that bound, exactly symmetric, run-to-run
+    identical, tickets back at zero."""
+    import torch
+    lda = -(-k // 64) * 64
+    Ad = np.zeros((n, lda), np.float32)
+    r = np.random.default_rng(n * 7 + k)
+    v = (r.random((n, k)) * 10.0 ** r.uniform(-3, 1, (n, k))) * (r.random((n, k)) < 0.2)
+    v[1::2] *= np.sign(r.standard_normal((n // 2, k)))
+    Ad[:, :k] = v.astype(np.float32)
+    At = torch.from_numpy(Ad).to(eng.device)
+    monkeypatch.setenv("GRF_DENSE_WIDE", "1")
+    Kw = eng.gram_dense(At, k, precision="split").cpu().numpy()
+    Kw2 = eng.gram_dense(At, k, precision="split").cpu().numpy()
+    ws = eng._dense_ws[eng.stream.value]
+    assert int(ws[:4096].view(torch.int32).abs().sum()) == 0
+    monkeypatch.setenv("GRF_DENSE_WIDE", "0")
+    Kn = eng.gram_dense(At, k, precision="split").cpu().numpy()
+    ref = Ad.astype(np.float64) @ Ad.astype(np.float64).T
+    bound = np.abs(Ad).astype(np.float64) @ np.abs(Ad).astype(np.float64).T + 1e-30
+    assert (np.abs(Kw - ref) / bound).max() <= 1e-5
+    assert (np.abs(Kw.astype(np.float64) - Kn) / bound).max() <= 2e-5
+    assert np.isfinite(Kw).all() and np.array_equal(Kw, Kw.T) and np.array_equal(Kw, Kw2)
+
+
 def test_gram_dense_c2_size_stream_k(eng):
-    """the stream-K path at the bench's C2 size (n = k = 10 000, 3160 tiles over 512
-    slots: tiles cut at slot boundaries and summed through slabs) against fp64 on sampled rows, exactly
-    symmetric, run-to-run identical bits."""
+    """the stream-K path at the bench's C2 size (n = k = 10 000; the split Gram's wide
+    workgroups: 1600 items of 256 x 128 over 256 slots, items cut at slot boundaries and summed through
+    slabs) against fp64 on sampled rows, exactly symmetric, run-to-run identical bits."""
     import torch
     n = k = 10000
     lda = -(-k // 64) * 64
