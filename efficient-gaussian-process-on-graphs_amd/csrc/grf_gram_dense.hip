@@ -492,33 +492,46 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_sk_kernel(DenseArgs a) {
 // the two 16-B chunks the fp32 kernel reads for fragment groups 0 and 1 (Layout<32, 16>::off).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// 8 floats -> their three bf16 planes (round to nearest; every step exact)
-__device__ __forceinline__ void split3(f32x4v lo, f32x4v hi, bf16x8 &p0, bf16x8 &p1, bf16x8 &p2) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const float v = e < 4 ? lo[e] : hi[e - 4];
-        const __bf16 a0 = (__bf16)v;
-        const float r1 = v - (float)a0;
-        const __bf16 a1 = (__bf16)r1;
-        p0[e] = a0;
-        p1[e] = a1;
-        p2[e] = (__bf16)(r1 - (float)a1);
-    }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // a plane fragment as 4 packed bf16 pairs
+
+// Two floats -> one dword of each of their three planes: v_cvt_pk_bf16_f32 (round to nearest), each plane
+// unpacked from that pair (v_lshlrev / v_and; a per-element split converted every value twice), remainders
+// exact.  This file is built with -fno-slp-vectorize (Makefile): hipcc otherwise packs the subtractions into
+// v_pk_add_f32, which costs several issue slots beside MFMAs (MI355X_MICROARCH.md cycle constants) and
+// needs s_nops.  11 VALU per pair; the split kernels run 7-8 % faster with the same bits
+// (profiles/r05_split_gram_ab.txt, version 6).
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk(float x, float y) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){x, y}, bf16x2v));
+}
+__device__ __forceinline__ void split2(float x, float y, uint32_t &p0, uint32_t &p1, uint32_t &p2) {
+    p0 = cvt_pk(x, y);
+    const float rx = x - __builtin_bit_cast(float, p0 << 16);
+    const float ry = y - __builtin_bit_cast(float, p0 & 0xffff0000u);
+    p1 = cvt_pk(rx, ry);
+    const float sx = rx - __builtin_bit_cast(float, p1 << 16);
+    const float sy = ry - __builtin_bit_cast(float, p1 & 0xffff0000u);
+    p2 = cvt_pk(sx, sy);
 }
 
-// elements 2 i, 2 i + 1 of split3 (the same operations): a slice of one operand's split to place between MFMAs
+// elements 2 I, 2 I + 1 of 8 floats (lo, hi): a slice of one operand's split to place between MFMAs
 template <int I>
-__device__ __forceinline__ void split_pair(f32x4v lo, f32x4v hi, bf16x8 &p0, bf16x8 &p1, bf16x8 &p2) {
-#pragma unroll
-    for (int e = 2 * I; e < 2 * I + 2; ++e) {
-        const float v = e < 4 ? lo[e] : hi[e - 4];
-        const __bf16 a0 = (__bf16)v;
-        const float r1 = v - (float)a0;
-        const __bf16 a1 = (__bf16)r1;
-        p0[e] = a0;
-        p1[e] = a1;
-        p2[e] = (__bf16)(r1 - (float)a1);
-    }
+__device__ __forceinline__ void split_pair(f32x4v lo, f32x4v hi, u32x4 &p0, u32x4 &p1, u32x4 &p2) {
+    const f32x4v &v = I < 2 ? lo : hi;
+    uint32_t q0, q1, q2;
+    split2(v[2 * (I & 1)], v[2 * (I & 1) + 1], q0, q1, q2);
+    p0[I] = q0;
+    p1[I] = q1;
+    p2[I] = q2;
+}
+
+// 8 floats -> their three bf16 planes (round to nearest; every step exact)
+__device__ __forceinline__ void split3(f32x4v lo, f32x4v hi, u32x4 &p0, u32x4 &p1, u32x4 &p2) {
+    split_pair<0>(lo, hi, p0, p1, p2);
+    split_pair<1>(lo, hi, p0, p1, p2);
+    split_pair<2>(lo, hi, p0, p1, p2);
+    split_pair<3>(lo, hi, p0, p1, p2);
 }
 
 // The k-loop of one tile over [kb, ke) with the split products.  The ring, the DMA pieces (issue: all of
@@ -571,7 +584,7 @@ __device__ __forceinline__ void kloop_split(float *lds, const float *const *srcA
                     ra[x][g] = *reinterpret_cast<const f32x4v *>(pa + aoff[g] * 4 + x * L::XSTRIDE);
                     rb[x][g] = *reinterpret_cast<const f32x4v *>(pb + boff[g] * 4 + x * L::XSTRIDE);
                 }
-            bf16x8 a[2][3], b[2][3];
+            u32x4 a[2][3], b[2][3];
             // block (0, 0) needs A0 and B0 split; B1's and A1's splits (a pair of elements per MFMA) and the next
             // k-tile's DMA pieces go between the MFMAs of the blocks before them, in this order (sched_barrier
             // fences): VALU and VMEM issue in the MFMA shadows instead of ~110 VALU ahead of the first MFMA
@@ -580,11 +593,14 @@ __device__ __forceinline__ void kloop_split(float *lds, const float *const *srcA
             __builtin_amdgcn_sched_barrier(0);
             auto mf = [&](int x, int y, int s) {
                 if (s == 0) {
-                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][0], c0[x][y], 0, 0, 0);
+                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][0]),
+                                                                     __builtin_bit_cast(bf16x8, b[y][0]), c0[x][y], 0, 0, 0);
                     return;
                 }
                 constexpr int P[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
-                c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][P[s][0]], b[y][P[s][1]], c1[x][y], 0, 0, 0);
+                c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][P[s][0]]),
+                                                                 __builtin_bit_cast(bf16x8, b[y][P[s][1]]), c1[x][y],
+                                                                 0, 0, 0);
             };
             auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
             mf(0, 0, 0); split_pair<0>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
@@ -778,17 +794,20 @@ __device__ __forceinline__ void kloop_wide(float *lds, const float *const *src, 
                     ra[x][g] = *reinterpret_cast<const f32x4v *>(pa + aoff[g] * 4 + x * L::XSTRIDE);
                     rb[x][g] = *reinterpret_cast<const f32x4v *>(pb + boff[g] * 4 + x * L::XSTRIDE);
                 }
-            bf16x8 a[2][3], b[2][3];
+            u32x4 a[2][3], b[2][3];
             split3(ra[0][0], ra[0][1], a[0][0], a[0][1], a[0][2]);
             split3(rb[0][0], rb[0][1], b[0][0], b[0][1], b[0][2]);
             __builtin_amdgcn_sched_barrier(0);
             auto mf = [&](int x, int y, int s) {
                 if (s == 0) {
-                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][0], b[y][0], c0[x][y], 0, 0, 0);
+                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][0]),
+                                                                     __builtin_bit_cast(bf16x8, b[y][0]), c0[x][y], 0, 0, 0);
                     return;
                 }
                 constexpr int P[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
-                c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x][P[s][0]], b[y][P[s][1]], c1[x][y], 0, 0, 0);
+                c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][P[s][0]]),
+                                                                 __builtin_bit_cast(bf16x8, b[y][P[s][1]]), c1[x][y],
+                                                                 0, 0, 0);
             };
             auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
             mf(0, 0, 0); split_pair<0>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
