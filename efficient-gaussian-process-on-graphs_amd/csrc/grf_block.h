@@ -134,10 +134,12 @@ __device__ __forceinline__ KT bitonic_keep(KT a, KT o, bool take_min) {
 // u32 keys: the same keep as ONE v_med3_u32 against a per-stage selector (0: the minimum, ~0: the
 // maximum -- the median of {a, o, 0} is min(a, o), of {a, o, ~0} max(a, o)), instead of a min, a
 // max and a select per key
+// (written as min / max, which hipcc folds into v_med3_u32: an inline-asm v_med3_u32 left the scheduler
+// blind to it -- no interleaving of a stage's DPP moves ahead of its medians, and an s_nop before every
+// DPP move that read an asm result)
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
+    return __builtin_elementwise_min(__builtin_elementwise_max(a, b),
+                                     __builtin_elementwise_max(__builtin_elementwise_min(a, b), c));
 }
 template <typename KT>
 __device__ __forceinline__ KT bitonic_keep_sel(KT a, KT o, bool take_min, uint32_t sel) {

@@ -488,7 +488,7 @@ __global__ __launch_bounds__(256) void lap_row_group_kernel(int64_t n, const int
             dj[q] = dinv[need[q] ? col[q] : (valid ? i : 0)];
         }
     }
-    double ti;
+    double ti = 0.0;
     const bool need_i = insert && lap_pre(d, di, ti);
     double ui;
     const bool keep_i = lap_post(need_i, ti, di, ui);  // (dinv[i] is di)
