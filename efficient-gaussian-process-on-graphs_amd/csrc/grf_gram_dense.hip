@@ -505,33 +505,80 @@ typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t cvt_pk(float x, float y) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){x, y}, bf16x2v));
 }
-__device__ __forceinline__ void split2(float x, float y, uint32_t &p0, uint32_t &p1, uint32_t &p2) {
-    p0 = cvt_pk(x, y);
-    const float rx = x - __builtin_bit_cast(float, p0 << 16);
-    const float ry = y - __builtin_bit_cast(float, p0 & 0xffff0000u);
-    p1 = cvt_pk(rx, ry);
-    const float sx = rx - __builtin_bit_cast(float, p1 << 16);
-    const float sy = ry - __builtin_bit_cast(float, p1 & 0xffff0000u);
-    p2 = cvt_pk(sx, sy);
+// plane 0 of one fragment (8 floats lo, hi): four v_cvt_pk_bf16_f32
+__device__ __forceinline__ void plane0(const f32x4v &lo, const f32x4v &hi, u32x4 &p0) {
+    p0[0] = cvt_pk(lo[0], lo[1]);
+    p0[1] = cvt_pk(lo[2], lo[3]);
+    p0[2] = cvt_pk(hi[0], hi[1]);
+    p0[3] = cvt_pk(hi[2], hi[3]);
 }
 
-// elements 2 I, 2 I + 1 of 8 floats (lo, hi): a slice of one operand's split to place between MFMAs
+// pairs I, I + 1 of a fragment: the remainders after plane pq (exact; kept in place of the values) and their
+// next plane pn -- called with (p0, p1), then (p1, p2)
 template <int I>
-__device__ __forceinline__ void split_pair(f32x4v lo, f32x4v hi, u32x4 &p0, u32x4 &p1, u32x4 &p2) {
-    const f32x4v &v = I < 2 ? lo : hi;
-    uint32_t q0, q1, q2;
-    split2(v[2 * (I & 1)], v[2 * (I & 1) + 1], q0, q1, q2);
-    p0[I] = q0;
-    p1[I] = q1;
-    p2[I] = q2;
+__device__ __forceinline__ void next_plane2(f32x4v &lo, f32x4v &hi, const u32x4 &pq, u32x4 &pn) {
+#pragma unroll
+    for (int i = I; i < I + 2; ++i) {
+        f32x4v &v = i < 2 ? lo : hi;
+        const int e = 2 * (i & 1);
+        const float rx = v[e] - __builtin_bit_cast(float, pq[i] << 16);
+        const float ry = v[e + 1] - __builtin_bit_cast(float, pq[i] & 0xffff0000u);
+        v[e] = rx;
+        v[e + 1] = ry;
+        pn[i] = cvt_pk(rx, ry);
+    }
 }
 
-// 8 floats -> their three bf16 planes (round to nearest; every step exact)
-__device__ __forceinline__ void split3(f32x4v lo, f32x4v hi, u32x4 &p0, u32x4 &p1, u32x4 &p2) {
-    split_pair<0>(lo, hi, p0, p1, p2);
-    split_pair<1>(lo, hi, p0, p1, p2);
-    split_pair<2>(lo, hi, p0, p1, p2);
-    split_pair<3>(lo, hi, p0, p1, p2);
+// One k-tile of a wave's 2 x 2 blocks: fragments ra[x] (A block x), rb[y] (B block y) -> 6 products per
+// block.  Plane 0 of all four fragments first (16 conversions), so the four a0 b0 products start at once;
+// planes 1 and 2 (two pairs of one fragment per gap) and the next k-tile's DMA pieces (issue(0 .. 3)) go
+// between the MFMAs, each plane ready before the first product that reads it (sched_barrier fences).  Each
+// block's c1 still takes its five products in the order s = 1 .. 5, so the sums are bitwise unchanged.
+template <typename Issue>
+__device__ __forceinline__ void split_ktile(f32x4v (&ra)[2][2], f32x4v (&rb)[2][2], f32x16 (&c0)[2][2],
+                                            f32x16 (&c1)[2][2], Issue issue) {
+    u32x4 a[2][3], b[2][3];
+    plane0(ra[0][0], ra[0][1], a[0][0]);
+    plane0(rb[0][0], rb[0][1], b[0][0]);
+    plane0(ra[1][0], ra[1][1], a[1][0]);
+    plane0(rb[1][0], rb[1][1], b[1][0]);
+    __builtin_amdgcn_sched_barrier(0);
+    auto mf = [&](int x, int y, int s) {
+        if (s == 0) {
+            c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][0]),
+                                                             __builtin_bit_cast(bf16x8, b[y][0]), c0[x][y], 0, 0, 0);
+            return;
+        }
+        constexpr int P[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
+        c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][P[s][0]]),
+                                                         __builtin_bit_cast(bf16x8, b[y][P[s][1]]), c1[x][y], 0, 0, 0);
+    };
+    auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+    // (each line: the product, then the work that fits behind it; comments name what the product reads)
+    mf(0, 0, 0); next_plane2<0>(ra[0][0], ra[0][1], a[0][0], a[0][1]); fence();  // A0 p1
+    mf(0, 1, 0); next_plane2<2>(ra[0][0], ra[0][1], a[0][0], a[0][1]); fence();
+    mf(1, 0, 0); next_plane2<0>(rb[0][0], rb[0][1], b[0][0], b[0][1]); fence();  // B0 p1
+    mf(1, 1, 0); next_plane2<2>(rb[0][0], rb[0][1], b[0][0], b[0][1]); fence();
+    mf(0, 0, 1); next_plane2<0>(rb[1][0], rb[1][1], b[1][0], b[1][1]); fence();  // (A0 p0, B0 p1); B1 p1
+    mf(0, 0, 2); next_plane2<2>(rb[1][0], rb[1][1], b[1][0], b[1][1]); fence();  // (A0 p1, B0 p0)
+    mf(0, 1, 1); next_plane2<0>(ra[1][0], ra[1][1], a[1][0], a[1][1]); fence();  // (A0 p0, B1 p1); A1 p1
+    mf(0, 1, 2); next_plane2<2>(ra[1][0], ra[1][1], a[1][0], a[1][1]); fence();
+    mf(1, 0, 1); next_plane2<0>(ra[0][0], ra[0][1], a[0][1], a[0][2]); fence();  // (A1 p0, B0 p1); A0 p2
+    mf(1, 0, 2); next_plane2<2>(ra[0][0], ra[0][1], a[0][1], a[0][2]); fence();  // (A1 p1, B0 p0)
+    mf(1, 1, 1); next_plane2<0>(rb[0][0], rb[0][1], b[0][1], b[0][2]); fence();  // B0 p2
+    mf(1, 1, 2); next_plane2<2>(rb[0][0], rb[0][1], b[0][1], b[0][2]); fence();
+    mf(0, 0, 3); next_plane2<0>(rb[1][0], rb[1][1], b[1][1], b[1][2]); fence();  // (A0 p0, B0 p2); B1 p2
+    mf(0, 0, 4); next_plane2<2>(rb[1][0], rb[1][1], b[1][1], b[1][2]); fence();
+    mf(0, 0, 5); next_plane2<0>(ra[1][0], ra[1][1], a[1][1], a[1][2]); fence();  // (A0 p2, B0 p0); A1 p2
+    mf(0, 1, 3); next_plane2<2>(ra[1][0], ra[1][1], a[1][1], a[1][2]); fence();  // (A0 p0, B1 p2)
+    mf(0, 1, 4); issue(0); fence();
+    mf(0, 1, 5); issue(1); fence();
+    mf(1, 0, 3); issue(2); fence();
+    mf(1, 0, 4); issue(3); fence();
+    mf(1, 0, 5);
+    mf(1, 1, 3);
+    mf(1, 1, 4);
+    mf(1, 1, 5);
 }
 
 // The k-loop of one tile over [kb, ke) with the split products.  The ring, the DMA pieces (issue: all of
@@ -584,41 +631,7 @@ __device__ __forceinline__ void kloop_split(float *lds, const float *const *srcA
                     ra[x][g] = *reinterpret_cast<const f32x4v *>(pa + aoff[g] * 4 + x * L::XSTRIDE);
                     rb[x][g] = *reinterpret_cast<const f32x4v *>(pb + boff[g] * 4 + x * L::XSTRIDE);
                 }
-            u32x4 a[2][3], b[2][3];
-            // block (0, 0) needs A0 and B0 split; B1's and A1's splits (a pair of elements per MFMA) and the next
-            // k-tile's DMA pieces go between the MFMAs of the blocks before them, in this order (sched_barrier
-            // fences): VALU and VMEM issue in the MFMA shadows instead of ~110 VALU ahead of the first MFMA
-            split3(ra[0][0], ra[0][1], a[0][0], a[0][1], a[0][2]);
-            split3(rb[0][0], rb[0][1], b[0][0], b[0][1], b[0][2]);
-            __builtin_amdgcn_sched_barrier(0);
-            auto mf = [&](int x, int y, int s) {
-                if (s == 0) {
-                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][0]),
-                                                                     __builtin_bit_cast(bf16x8, b[y][0]), c0[x][y], 0, 0, 0);
-                    return;
-                }
-                constexpr int P[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
-                c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][P[s][0]]),
-                                                                 __builtin_bit_cast(bf16x8, b[y][P[s][1]]), c1[x][y],
-                                                                 0, 0, 0);
-            };
-            auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
-            mf(0, 0, 0); split_pair<0>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
-            mf(0, 0, 1); split_pair<1>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
-            mf(0, 0, 2); split_pair<2>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
-            mf(0, 0, 3); split_pair<3>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
-            mf(0, 0, 4); issue_part(t + NST - 1, 0); fence();
-            mf(0, 0, 5); issue_part(t + NST - 1, 1); fence();
-            mf(0, 1, 0); split_pair<0>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
-            mf(0, 1, 1); split_pair<1>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
-            mf(0, 1, 2); split_pair<2>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
-            mf(0, 1, 3); split_pair<3>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
-            mf(0, 1, 4); issue_part(t + NST - 1, 2); fence();
-            mf(0, 1, 5); issue_part(t + NST - 1, 3); fence();
-#pragma unroll
-            for (int s = 0; s < 6; ++s) mf(1, 0, s);
-#pragma unroll
-            for (int s = 0; s < 6; ++s) mf(1, 1, s);
+            split_ktile(ra, rb, c0, c1, [&](int q) { issue_part(t + NST - 1, q); });
         }
     }
 }
@@ -794,38 +807,7 @@ __device__ __forceinline__ void kloop_wide(float *lds, const float *const *src, 
                     ra[x][g] = *reinterpret_cast<const f32x4v *>(pa + aoff[g] * 4 + x * L::XSTRIDE);
                     rb[x][g] = *reinterpret_cast<const f32x4v *>(pb + boff[g] * 4 + x * L::XSTRIDE);
                 }
-            u32x4 a[2][3], b[2][3];
-            split3(ra[0][0], ra[0][1], a[0][0], a[0][1], a[0][2]);
-            split3(rb[0][0], rb[0][1], b[0][0], b[0][1], b[0][2]);
-            __builtin_amdgcn_sched_barrier(0);
-            auto mf = [&](int x, int y, int s) {
-                if (s == 0) {
-                    c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][0]),
-                                                                     __builtin_bit_cast(bf16x8, b[y][0]), c0[x][y], 0, 0, 0);
-                    return;
-                }
-                constexpr int P[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
-                c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][P[s][0]]),
-                                                                 __builtin_bit_cast(bf16x8, b[y][P[s][1]]), c1[x][y],
-                                                                 0, 0, 0);
-            };
-            auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
-            mf(0, 0, 0); split_pair<0>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
-            mf(0, 0, 1); split_pair<1>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
-            mf(0, 0, 2); split_pair<2>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
-            mf(0, 0, 3); split_pair<3>(rb[1][0], rb[1][1], b[1][0], b[1][1], b[1][2]); fence();
-            mf(0, 0, 4); issue_part(t + NST - 1, 0); fence();
-            mf(0, 0, 5); issue_part(t + NST - 1, 1); fence();
-            mf(0, 1, 0); split_pair<0>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
-            mf(0, 1, 1); split_pair<1>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
-            mf(0, 1, 2); split_pair<2>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
-            mf(0, 1, 3); split_pair<3>(ra[1][0], ra[1][1], a[1][0], a[1][1], a[1][2]); fence();
-            mf(0, 1, 4); issue_part(t + NST - 1, 2); fence();
-            mf(0, 1, 5);
-#pragma unroll
-            for (int s = 0; s < 6; ++s) mf(1, 0, s);
-#pragma unroll
-            for (int s = 0; s < 6; ++s) mf(1, 1, s);
+            split_ktile(ra, rb, c0, c1, [&](int q) { if (q < G) issue_part(t + NST - 1, q); });
         }
     }
 }
