@@ -326,8 +326,9 @@ def dense_gram_roofline(precision: str, flops: float, ms: float) -> dict:
     if precision == "split":
         return {"bound": "mfma", "achieved": SPLIT_PRODUCTS * tfs, "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": SPLIT_PRODUCTS * tfs / MFMA_BF16_PEAK_TFS, "traffic": None,
-                "kernel": "gram_split_mfma_kernel / gram_split_sk_kernel (fp32 LDS-DMA staging, exact three-plane "
-                          "bf16 split in registers, v_mfma_f32_32x32x16_bf16, 6 products per term)",
+                "kernel": "gram_split_mfma_kernel (128x128 tiles; n <= 8064) / gram_split_wide_kernel (256x128 "
+                          "items of 8 waves, stream-K) (fp32 LDS-DMA staging, exact three-plane bf16 split in "
+                          "registers, v_mfma_f32_32x32x16_bf16, 6 products per term)",
                 "kernel_ms": ms, "algorithmic_flops": flops, "bf16_flops": SPLIT_PRODUCTS * flops,
                 "fp32_equivalent_tflops": tfs, "fp32_equivalent_vs_fp32_peak": tfs / MFMA_F32_PEAK_TFS}
     return {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
