@@ -422,12 +422,13 @@ int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda,
  * a2), K = sum over the six plane products a_p b_q with p + q <= 2 on v_mfma_f32_32x32x16_bf16 (16x the
  * fp32 MFMA's rate), a0 b0 and the five corrections accumulated apart in fp32.  The dropped products are
  * below 2^-23 |a b| per term, so the error bound is the fp32 path's plus 2^-23 sum_k |A_ik A_jk|
- * (measured against fp64: tests/test_gpu_parity.py test_gram_dense_split_*).  Same tiles, stream-K /
- * split-K decomposition, symmetry and determinism as grf_gram_dense_ws.  Finite inputs below 2^128 (1 - 2^-9)
+ * (measured against fp64: tests/test_gpu_parity.py test_gram_dense_split_*).  Symmetry and determinism as
+ * grf_gram_dense_ws; from 64 tile rows on (n > 8064) 256 x 128 items of 8 waves on stream-K (bits then differ
+ * from the 128-tile decomposition's within the bound above; GRF_DENSE_WIDE=0 / 1 forces it off / on).  Finite inputs below 2^128 (1 - 2^-9)
  * in magnitude only: an entry whose sum involves an infinite or NaN value of A (or one that rounds to an
  * infinite bf16) is NaN, where grf_gram_dense_ws follows IEEE (+-inf where no 0 * inf occurs).  workspace (required):
- * grf_gram_dense_split_workspace_bytes(n, k_dim) bytes, 256-byte aligned, ZERO on first use (the first
- * part is grf_gram_dense_ws's ticket block and slabs, the rest the planes). */
+ * grf_gram_dense_split_workspace_bytes(n, k_dim) bytes, 256-byte aligned, ZERO on first use (the ticket
+ * block of grf_gram_dense_ws at the same place, then the partial tiles of either decomposition). */
 size_t grf_gram_dense_split_workspace_bytes(int64_t n, int64_t k_dim);
 int32_t grf_gram_dense_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                              void *workspace, size_t workspace_bytes, grf_stream_t stream);
