@@ -593,13 +593,14 @@ def test_gram_dense_split_vs_fp64_and_fp32(eng, n, k):
 
 
 @pytest.mark.parametrize("n,k", [(100, 37), (300, 900), (1153, 1153), (2708, 2708), (4200, 20), (4200, 1000),
-                                 (4500, 16)])
+                                 (4500, 16), (8200, 300)])
 def test_gram_dense_split_wide(eng, monkeypatch, n, k):
     """The split Gram's wide workgroups (256 x 128 items, stream-K; the default from 64 tile rows on, forced
     here with GRF_DENSE_WIDE=1 at small n): odd tile-row counts (the item's second row block past n), k of
     one or two k-tiles (items cut at many slot boundaries), against fp64 within the fp32 path's bound, against
     the 128-tile split kernel (GRF_DENSE_WIDE=0) within twice that bound, exactly symmetric, run-to-run
-    identical, tickets back at zero."""
+    identical, tickets back at zero; at n = 8200 (65 tile rows) the default takes the wide path (same bits as
+    forced)."""
     import torch
     lda = -(-k // 64) * 64
     Ad = np.zeros((n, lda), np.float32)
@@ -620,6 +621,9 @@ def test_gram_dense_split_wide(eng, monkeypatch, n, k):
     assert (np.abs(Kw - ref) / bound).max() <= 1e-5
     assert (np.abs(Kw.astype(np.float64) - Kn) / bound).max() <= 2e-5
     assert np.isfinite(Kw).all() and np.array_equal(Kw, Kw.T) and np.array_equal(Kw, Kw2)
+    monkeypatch.delenv("GRF_DENSE_WIDE")
+    Kd = eng.gram_dense(At, k, precision="split").cpu().numpy()
+    assert np.array_equal(Kd, Kw if -(-n // 128) >= 64 else Kn)
 
 
 def test_gram_dense_c2_size_stream_k(eng):
