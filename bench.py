@@ -378,6 +378,7 @@ def main_c3(args):
     n, m, L, p = W.shape[0], args.walks, args.length, args.p_halt
     f = diffusion_modulator(L, 1.0)
     Wt = torch.from_numpy(W).to(eng.device)
+    nnz_w = int(np.count_nonzero(W))  # (setup: sizes every step's walk matrix without a device count)
     gram_ev = []        # the Gram in the timed (pipelined) steps
     gram_ev_alone = []  # the Gram in the serial steps (nothing beside it): the roofline's time
     # the next step's front runs here beside this step's Gram (--side-priority high: the stream's workgroups
@@ -386,7 +387,7 @@ def main_c3(args):
     main = torch.cuda.current_stream(eng.device)
 
     def front():
-        G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY)
+        G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY, nnz_w=nnz_w)
         # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule, written straight into
         # the dense fp32 Phi the Gram reads (no compaction, no memset: grf_densify_padded)
         return eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False))
@@ -1173,7 +1174,7 @@ def mfma_leg(eng, args, steps: int = 20, workload: str = "c3"):
     W, wdesc, _ = dense_workload(workload)
     n, m, L, p = W.shape[0], args.walks, args.length, args.p_halt
     f = diffusion_modulator(L, 1.0)
-    G = eng.walk_matrix_dense(torch.from_numpy(W).to(eng.device), C.LAP_NUMPY)
+    G = eng.walk_matrix_dense(W, C.LAP_NUMPY)  # (host W: nnz counted on the host)
     dense = eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False))
     del G, W
     flops = 1.0 * n * (n + 1) * n

@@ -478,12 +478,13 @@ __global__ __launch_bounds__(256, WPE) void gram_dense_sk_kernel(DenseArgs a) {
 // of three bf16 values: a0 = bf16(a), a1 = bf16(a - a0), a2 = a - a0 - a1 (round to nearest: a has 24
 // significant bits, a0 and a1 take 8 each, so the last remainder has at most 8 and is a bf16 exactly;
 // values below ~2^-100 lose their last plane to the bf16 subnormal range).  a b = sum over p, q of a_p b_q;
-// the six products with p + q <= 2 are kept (the dropped three are below 2^-23 |a b| together), each exact
+// the six products with p + q <= 2 are kept (the dropped three: at most (2u^3 + u^4) |a b| = (2^-23 + 2^-32)
+// |a b| together, u = 2^-8), each exact
 // in the MFMA's fp32 arithmetic, summed on v_mfma_f32_32x32x16_bf16 -- 16x the fp32 MFMA's rate per clock,
 // so six of them cost 3/8 of the fp32 instruction's cycles per k.  The leading product a0 b0 is
 // accumulated on its own (c0) and the five corrections together (c1, 2^-8 of the magnitude), c0 + c1 at
 // the end: c0's rounding is the fp32 chain's, c1's 2^-8 of that, so the error bound stays the fp32 MFMA
-// path's plus 2^-23 sum |a_k b_k| for the dropped products.
+// path's plus (2^-23 + 2^-32) sum |a_k b_k| for the dropped products.
 //
 // Staging is the fp32 path's (the same LDS-DMA pieces, swizzled k-tiles of BK = 16 floats, 4-stage ring,
 // two workgroups per CU): the split is done in registers after the fragment reads, so the bytes staged

@@ -715,8 +715,7 @@ struct IntSum {  // per-lane exact-integer-sum state of numpy's shortcut (wave_n
 
 __global__ __launch_bounds__(256) void lapd_stage_kernel(int64_t n, const double *W, int32_t mode, PwPlan plan,
                                                          double *deg, double *dinv, int32_t *scnt, int32_t *scol,
-                                                         double *sval, uint64_t *flags, uint32_t *ticket,
-                                                         int32_t *err) {
+                                                         double *sval, uint64_t *flags, uint32_t *ticket) {
     __shared__ double sums[4][kPwPlanLeaves];
     __shared__ PwLeaf leaves[4][kPwLeaves];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -769,10 +768,7 @@ __global__ __launch_bounds__(256) void lapd_stage_kernel(int64_t n, const double
         else dinv[i] = 1.0 / sqrt(d > 0.0 ? d : 1.0);
         scnt[i] = st.cnt;
         flags[i] = 0;
-        if (i == 0) {
-            *ticket = 0u;
-            *err = 0;
-        }
+        if (i == 0) *ticket = 0u;
     }
 }
 
@@ -781,10 +777,11 @@ constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 
 
 // Decoupled look-back (R2 granules: the 8-byte word {status, value} is the whole hand-off, written and
 // polled by relaxed agent-scope atomics; cdna_hip_programming.md Guideline 16).  Publishes this row's
-// count, returns the exclusive prefix of the counts before it.  Bounded spins: after ~2^20 polls of an
-// unpublished word (a predecessor that never ran: impossible under the ticket order) *err is set and the
-// wave goes on (its row pointer is then wrong; the word is left for a debugger, the launch still ends).
-__device__ int64_t lookback(uint64_t *flags, int64_t i, int64_t c, int lane, int32_t *err) {
+// count, returns the exclusive prefix of the counts before it.  The spin on an unpublished word has no
+// bound: tiles take their tickets when they start, so every predecessor of a polling tile is resident (or
+// done) and publishes without waiting on anything later -- a bounded spin could only turn a slow
+// predecessor (preempted, or starved beside another queue) into a silently wrong row pointer.
+__device__ int64_t lookback(uint64_t *flags, int64_t i, int64_t c, int lane) {
     gu64_t *f = (gu64_t *)flags;
     if (lane == 0) __hip_atomic_store(f + i, (i == 0 ? kLbIncl : kLbAgg) | (uint64_t)c, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
@@ -794,14 +791,9 @@ __device__ int64_t lookback(uint64_t *flags, int64_t i, int64_t c, int lane, int
         const int64_t idx = pos - lane;
         uint64_t w = kLbIncl;  // (before row 0: an inclusive zero)
         if (idx >= 0) {
-            for (uint32_t spin = 0;; ++spin) {
+            for (;;) {
                 w = __hip_atomic_load(f + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((w >> 62) != 0) break;
-                if (spin > (1u << 20)) {
-                    *err = 1;
-                    w = kLbIncl;
-                    break;
-                }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -878,8 +870,7 @@ constexpr int kLapdTileRows = 64;
 __global__ __launch_bounds__(256) void lapd_emit_kernel(int64_t n, const double *W, int32_t mode, const double *deg,
                                                         const double *dinv, const int32_t *scnt, const int32_t *scol,
                                                         const double *sval, uint64_t *flags, uint32_t *ticket,
-                                                        int32_t *err, int64_t *l_ptr, int32_t *l_idx, double *l_val,
-                                                        int64_t l_cap) {
+                                                        int64_t *l_ptr, int32_t *l_idx, double *l_val, int64_t l_cap) {
     constexpr int R = kLapdTileRows;
     __shared__ int32_t s_seg[R + 1];  // items before row r (pairs + 1 diagonal item per staged row)
     __shared__ int32_t s_cnt[R];      // nonzeros of row r
@@ -972,7 +963,7 @@ __global__ __launch_bounds__(256) void lapd_emit_kernel(int64_t n, const double 
         s_nzp[lane + 1] = pz;
         if (lane == 0) s_nzp[0] = 0;
         const int64_t total = __shfl(inc, 63, 64);
-        const int64_t ex = lookback(flags, tile, total, lane, err);
+        const int64_t ex = lookback(flags, tile, total, lane);
         if (lane == 0) s_excl = ex;
     }
     __syncthreads();
@@ -1053,7 +1044,7 @@ size_t grf_laplacian_csr_workspace_bytes(int64_t n) {
 }
 
 // dense workspace: dinv [n] f64 | staged counts [n] i32 | staged columns [n x cap] i32 | staged values
-// [n x cap] f64 | look-back words [n] u64 | ticket + error word (256 B)
+// [n x cap] f64 | look-back words [n] u64 | ticket (256 B)
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 size_t grf_laplacian_dense_workspace_bytes(int64_t n) {
     const size_t nn = (size_t)(n > 0 ? n : 1);
@@ -1131,16 +1122,15 @@ int32_t grf_laplacian_dense(int64_t n, const double *W, int32_t mode, int64_t *l
     uint64_t *flags = (uint64_t *)w;
     w += al256(nn * sizeof(uint64_t));
     uint32_t *ticket = (uint32_t *)w;
-    int32_t *err = (int32_t *)(w + 16);
     PwPlan plan;
     if (!pw_plan_build(n, plan)) plan.nl = 0;
     const unsigned g = (unsigned)cdiv<int64_t>(n, 4);
     GRF_REQUIRE_GRID(g, 256, "lapd_stage_kernel");
-    lapd_stage_kernel<<<g, 256, 0, st>>>(n, W, mode, plan, deg, dinv, scnt, scol, sval, flags, ticket, err);
+    lapd_stage_kernel<<<g, 256, 0, st>>>(n, W, mode, plan, deg, dinv, scnt, scol, sval, flags, ticket);
     GRF_CHECK_LAUNCH("lapd_stage_kernel");
     const unsigned gt = (unsigned)cdiv<int64_t>(n, kLapdTileRows);
-    lapd_emit_kernel<<<gt, 256, 0, st>>>(n, W, mode, deg, dinv, scnt, scol, sval, flags, ticket, err, l_ptr, l_idx,
-                                        l_val, l_cap);
+    lapd_emit_kernel<<<gt, 256, 0, st>>>(n, W, mode, deg, dinv, scnt, scol, sval, flags, ticket, l_ptr, l_idx, l_val,
+                                        l_cap);
     GRF_CHECK_LAUNCH("lapd_emit_kernel");
     return GRF_OK;
 }

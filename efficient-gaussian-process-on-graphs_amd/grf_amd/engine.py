@@ -210,6 +210,8 @@ class GRFEngine:
         # cores (fp32-class error, 1.3-1.4x faster: profiles/r05_split_gram_error.txt, AB_LOG "split Gram") or
         # the 'fp32' matrix instruction
         self.dense_precision = os.environ.get("GRF_GRAM_DENSE_PRECISION", "split")
+        if self.dense_precision not in ("split", "fp32"):
+            raise ValueError(f"GRF_GRAM_DENSE_PRECISION must be 'split' or 'fp32', got {self.dense_precision!r}")
 
     # ------------------------------------------------------------ utilities
     @property
@@ -246,17 +248,30 @@ class GRFEngine:
         G.nnz_bound = cap  # (sizes the augmented walk matrix without reading nnz back)
         return G
 
-    def walk_matrix_dense(self, W, mode: int) -> DeviceCSR:
-        """Dense-input walk matrix (numpy Laplacian variants or the matrix itself) as CSR."""
-        Wt = torch.as_tensor(np.ascontiguousarray(W, dtype=np.float64) if not torch.is_tensor(W) else W)
+    def walk_matrix_dense(self, W, mode: int, nnz_w: Optional[int] = None) -> DeviceCSR:
+        """Dense-input walk matrix (numpy Laplacian variants or the matrix itself) as CSR.
+
+        Its capacity (and the augmented walk matrix sized from it, cached on the result) is nnz(W) + n
+        (the Laplacian adds at most the diagonal).  nnz(W) is counted on the host for a host W, taken
+        from ``nnz_w`` when the caller knows it (the bench counts its resident W once, at setup), else
+        bounded by n^2 while that is small (<= 2^26 entries: 0.8 GB of CSR) or counted on the device
+        (a torch reduction and a host round trip: 0.64 ms of C2's front, profiles/r05_c2_kernel_alone.txt)."""
+        host = not torch.is_tensor(W)
+        Wn = np.ascontiguousarray(W, dtype=np.float64) if host else None
+        Wt = torch.as_tensor(Wn) if host else W
         Wt = Wt.to(self.device, torch.float64).contiguous()
         n = Wt.shape[0]
         if Wt.dim() != 2 or Wt.shape[1] != n:
             raise ValueError("Adjacency matrix must be square.")
-        # walk-matrix capacity: nnz(W) + n; the bound n^2 up to 256 M entries (3 GB of CSR: capacity only,
-        # the kernels write the real entries) avoids counting -- a torch reduction over W and a host round
-        # trip per call, 0.64 ms of C2's 10k x 10k front (profiles/r05_c2_kernel_alone.txt)
-        cap = n * n if n * n <= (1 << 28) else int(torch.count_nonzero(Wt).item()) + n
+        if nnz_w is not None:
+            cap = min(int(nnz_w) + n, n * n)
+        elif host:
+            cap = int(np.count_nonzero(Wn)) + n
+        elif n * n <= (1 << 26):
+            cap = n * n
+        else:
+            cap = int(torch.count_nonzero(Wt).item()) + n
+        cap = max(cap, 1)
         lp, li, lv = self._empty(n + 1, torch.int64), self._empty(cap, torch.int32), self._empty(cap, torch.float64)
         deg = self._empty(n, torch.float64)
         ws = self._ws(self.lib.grf_laplacian_dense_workspace_bytes(n))
@@ -817,7 +832,7 @@ class GRFEngine:
     def gram_dense(self, dense_phi: torch.Tensor, k_dim: int, precision: Optional[str] = None) -> torch.Tensor:
         """K = A A^T of the dense fp32 Phi on the MFMA.  precision 'fp32': the fp32 matrix instruction
         (grf_gram_dense_ws); 'split': the same product on the bf16 matrix cores from an exact three-plane
-        split of A (grf_gram_dense_split, error bound the fp32 path's + 2^-23 sum |a b|); None: the engine's
+        split of A (grf_gram_dense_split, error bound the fp32 path's + (2^-23 + 2^-32) sum |a b|); None: the engine's
         ``dense_precision`` (GRF_GRAM_DENSE_PRECISION, default 'split')."""
         precision = precision or self.dense_precision
         if precision not in ("fp32", "split"):

@@ -137,11 +137,13 @@ def _square_symmetrised(K: torch.Tensor, i1: Optional[torch.Tensor], i2: Optiona
     """K(x1, x2) for equal-length index tensors that are different objects: where x1 and x2 hold the
     same values (decided on the device, no host read), the block is K(x, x) and is returned exactly
     symmetric as (K + K^T) / 2 -- what the symmetric path's mirrored tiles give up to the K tolerance;
-    otherwise K unchanged."""
+    otherwise K unchanged.  K (a fresh block) is updated in place with one temporary: lerp with a 0 / 1
+    weight returns its start or its end exactly (torch evaluates weight >= 0.5 as end - (end - start)(1 - w))."""
     if i1 is None or i2 is None or K.dim() != 2 or K.shape[0] != K.shape[1] or i1.shape != i2.shape:
         return K
-    same = torch.eq(i1, i2).all()
-    return torch.where(same, 0.5 * (K + K.t()), K)
+    same = torch.eq(i1, i2).all().to(K.dtype)
+    T = K + K.t()
+    return K.lerp_(T.mul_(0.5), same)
 
 
 def rowdot(eng: GRFEngine, A: DeviceCSR, rows_a: Optional[torch.Tensor], B: DeviceCSR,

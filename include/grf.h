@@ -420,8 +420,10 @@ int32_t grf_gram_dense_ws(int64_t n, int64_t k_dim, const float *A, int64_t lda,
                           void *workspace, size_t workspace_bytes, grf_stream_t stream);
 /* The same K on the bf16 matrix cores (ABI 6): A is split exactly into three bf16 planes (a = a0 + a1 +
  * a2), K = sum over the six plane products a_p b_q with p + q <= 2 on v_mfma_f32_32x32x16_bf16 (16x the
- * fp32 MFMA's rate), a0 b0 and the five corrections accumulated apart in fp32.  The dropped products are
- * below 2^-23 |a b| per term, so the error bound is the fp32 path's plus 2^-23 sum_k |A_ik A_jk|
+ * fp32 MFMA's rate), a0 b0 and the five corrections accumulated apart in fp32.  The dropped products
+ * |a1 b2| + |a2 b1| + |a2 b2| are at most (2u^3 + u^4) |a b| = (2^-23 + 2^-32) |a b| per term (bf16 unit
+ * roundoff u = 2^-8), so the error bound is the fp32 path's plus (2^-23 + 2^-32) sum_k |A_ik A_jk| for
+ * normal planes (an entry within 2^16 of the bf16 subnormal range can also lose its plane 2)
  * (measured against fp64: tests/test_gpu_parity.py test_gram_dense_split_*).  Symmetry and determinism as
  * grf_gram_dense_ws; from 64 tile rows on (n > 8064) 256 x 128 items of 8 waves on stream-K (bits then differ
  * from the 128-tile decomposition's within the bound above; GRF_DENSE_WIDE=0 / 1 forces it off / on).  Finite inputs below 2^128 (1 - 2^-9)

@@ -1417,13 +1417,13 @@ def test_bench_cols_at_headline_size_gloo(eng, world):
                "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
                "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--rank-turns",
                "--fingerprint-dir", fp_dir]
-        r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=800)
+        r = _run_beating(cmd, root, env, 800, f"c4_gloo_n{world}")
         assert r.returncode == 0, r.stderr[-3000:]
         line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
         out_dir = os.environ.get("GRF_TEST_OUT")
         if out_dir:
             os.makedirs(out_dir, exist_ok=True)
-            with open(os.path.join(out_dir, f"r05_bench_gloo_n{world}.json"), "w") as fh:
+            with open(os.path.join(out_dir, f"r06_bench_gloo_n{world}.json"), "w") as fh:
                 fh.write(json.dumps(line) + "\n")
         d = line["distributed"]
         assert line["n_gpus"] == world and d["backend"] == "gloo" and d["world_size"] == world
@@ -1439,6 +1439,136 @@ def test_bench_cols_at_headline_size_gloo(eng, world):
         assert fp["mode"] == "cols" and fp["shard"] == [b, e] and fp["cols_sym"] == (4 * (e - b) >= 100_000)
         h, sm = ref[(b, e, fp["cols_sym"])]
         assert fp["hash"] == h, f"rank {q} of {world}: K block bits differ from the one-GPU K"
+        assert abs(fp["sum"] - sm) <= 1e-12 * abs(sm), (q, fp["sum"], sm)
+
+
+def _run_beating(cmd, cwd, env, timeout, tag):
+    """subprocess.run(capture_output=True, text=True) that appends a line to $GRF_TEST_OUT/<tag>.beat every
+    30 s while the child runs (a long silent multi-rank run stays visibly alive to a hang watchdog)."""
+    import os
+    import subprocess
+    import tempfile
+    import time
+    out_dir = os.environ.get("GRF_TEST_OUT")
+    with tempfile.TemporaryFile("w+") as fo, tempfile.TemporaryFile("w+") as fe:
+        p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=fo, stderr=fe, text=True)
+        t0 = time.time()
+        while True:
+            try:
+                p.wait(timeout=30)
+                break
+            except subprocess.TimeoutExpired:
+                if time.time() - t0 > timeout:
+                    p.kill()
+                    p.wait()
+                    raise
+                if out_dir:
+                    os.makedirs(out_dir, exist_ok=True)
+                    with open(os.path.join(out_dir, f"{tag}.beat"), "a") as fh:
+                        fh.write(f"{time.time() - t0:.0f} s\n")
+        fo.seek(0)
+        fe.seek(0)
+        return subprocess.CompletedProcess(cmd, p.returncode, fo.read(), fe.read())
+
+
+_C5_REF_PRINTS = {}  # (b, kr_end) -> fingerprint of the one-GPU K's columns [b, kr_end) at C5
+
+
+def _c5_reference_prints(eng, blocks):
+    """Fingerprints of the one-GPU C5 column blocks K[:, b:kr_end] (N = 1M Chung-Lu power-law, seed 0,
+    m = 64, L = 8, p = 0.1, Philox seed 42).  Phi of all 1M nodes from ONE un-sharded walk (setup_phi, no
+    collective); each block from the transpose of its rows walked on their own (walk_phi src_begin /
+    src_end) in a different layout from the bench's -- 4096-row bands of packed pairs, not one
+    8192-row band of 32-B slots -- so only the exact fixed-point sums are shared (the Gram's bits do not
+    depend on the band width or the record layout).  Every row's shift from a pass over Phi's values."""
+    import torch
+    from grf_amd.dist import setup_phi
+    from grf_amd.engine import DeviceCSR
+    from grf_amd.graphs import powerlaw_graph
+    from tools.gram_hash import fingerprint
+    import bench
+    todo = [blk for blk in blocks if blk not in _C5_REF_PRINTS]
+    if not todo:
+        return _C5_REF_PRINTS
+    n, m, L, p = 1_000_000, 64, 8, 0.1
+    f = bench.diffusion_modulator(L, 1.0)
+    A = DeviceCSR.from_scipy(powerlaw_graph(n, 10.0, 2.5, seed=0), eng.device)
+    G = eng.laplacian(A)
+    phi = setup_phi(eng, A, m, p, L, f, seed=42)
+    shifts = eng.phi_row_shifts(phi)
+    for b, ke in todo:
+        loc = eng.compact(eng.walk_phi(G, m, p, L, f, seed=42, src_begin=b, src_end=ke, want64=False),
+                          want64=False)
+        tr = eng.transpose_banded(loc, 4096)
+        Kb = eng.gram_sparse_cols(phi, shifts, tr)
+        _C5_REF_PRINTS[(b, ke)] = fingerprint(Kb)
+        del Kb, tr, loc
+        torch.cuda.empty_cache()
+    del phi, shifts, G, A
+    torch.cuda.empty_cache()
+    return _C5_REF_PRINTS
+
+
+@pytest.mark.timeout(1100)
+@pytest.mark.parametrize("world,k_rows", [(2, 8192), (4, 8192), (8, 4096)])
+def test_bench_c5_cols_at_size_gloo(eng, world, k_rows):
+    """BASELINE config 5's multi-rank step at its full size -- bench.py --workload c5
+    --gpus W under torch.distributed.run (gloo, W ranks sharing the one GPU): N = 1M power-law, m = 64,
+    every rank walks 1M / W sources, the 176 M-entry Phi all-gather with its exact bound, the per-rank
+    slot transpose of rows [b, b + k_rows) and the column block K[:, b:b + k_rows] over all 1M rows.
+    World 8 takes 4096-column blocks: 8 x 32.8 GB of 8192-column blocks would not fit in the one GPU's
+    288 GB beside eight ranks' Phi (8 x 16.4 GB does).  Every rank's block must be bit-identical to the
+    same columns computed by one GPU from an un-sharded walk (_c5_reference_prints), its in-run K
+    check passes, and the line reports every rank's Gram time re-run alone (--rank-turns) and its
+    all-gather bytes.  GRF_TEST_OUT=<dir> keeps the line (profiles/r06_bench_c5_gloo_n<W>.json)."""
+    import json
+    import os
+    import shutil
+    import socket
+    import subprocess
+    import sys
+    import tempfile
+    from grf_amd.dist import shard_range
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = 1_000_000
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    fp_dir = tempfile.mkdtemp(prefix="grf_fp5_")
+    try:
+        env = dict(os.environ, GRF_DIST_BACKEND="gloo")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+               "--workload", "c5", "--k-rows", str(k_rows), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+               "--no-cpu-baseline", "--rank-turns", "--fingerprint-dir", fp_dir]
+        r = _run_beating(cmd, root, env, 1000, f"c5_gloo_n{world}")
+        if r.returncode != 0 and os.environ.get("GRF_TEST_OUT"):
+            with open(os.path.join(os.environ["GRF_TEST_OUT"], f"c5_gloo_n{world}.failed.log"), "w") as fh:
+                fh.write(r.stdout + "\n----- stderr -----\n" + r.stderr)
+        assert r.returncode == 0, r.stderr[-3000:]
+        line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+        out_dir = os.environ.get("GRF_TEST_OUT")
+        if out_dir:
+            os.makedirs(out_dir, exist_ok=True)
+            with open(os.path.join(out_dir, f"r06_bench_c5_gloo_n{world}.json"), "w") as fh:
+                fh.write(json.dumps(line) + "\n")
+        d = line["distributed"]
+        assert line["n_gpus"] == world and d["backend"] == "gloo" and d["world_size"] == world
+        assert line["config"]["n_nodes"] == n and line["config"]["walks_per_node"] == 64
+        assert line["unit"] == "K-rows/s" and line["config"]["k_rows_per_gpu"] == k_rows
+        assert line["parity"]["ok"] and len(line["parity"]["per_rank"]) == world
+        assert all(x > 0 for x in d["gram_ms_alone_per_rank"]) and all(x > 0 for x in d["gather_bytes_sent_per_rank"])
+        prints = [json.load(open(os.path.join(fp_dir, f"rank{q}.json"))) for q in range(world)]
+    finally:
+        shutil.rmtree(fp_dir, ignore_errors=True)
+    blocks = [(shard_range(n, q, world)[0], shard_range(n, q, world)[0] + k_rows) for q in range(world)]
+    ref = _c5_reference_prints(eng, blocks)
+    for q, fp in enumerate(prints):
+        b, e = shard_range(n, q, world)
+        assert fp["mode"] == "cols" and fp["shard"] == [b, e] and not fp["cols_sym"] and fp["k_rows"] == k_rows
+        h, sm = ref[blocks[q]]
+        assert fp["hash"] == h, f"rank {q} of {world}: C5 K block bits differ from the one-GPU block"
         assert abs(fp["sum"] - sm) <= 1e-12 * abs(sm), (q, fp["sum"], sm)
 
 
