@@ -28,6 +28,7 @@
 namespace grf {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t uint4_v __attribute__((ext_vector_type(4)));
 
 // The Gram tiles' K stores and the swizzled mirror's K loads: non-temporal (K is write-once and
 // larger than every cache).  -DGRF_GRAM_K_NT=0 builds them with the default policy (A/B build: the
@@ -119,6 +120,47 @@ __device__ inline int gram_propagate_ids(unsigned char *bid, int carry, int lane
     }
     (void)rep;
     reinterpret_cast<uint4 *>(bid)[lane] = make_uint4(w[0], w[1], w[2], w[3]);
+    return __builtin_amdgcn_readlane(max(run, before), 63);
+}
+
+// gram_propagate_ids over a chunk of 64 * 4 * NW positions (NW = 1, 2: 4 or 8 per lane, one LDS read and write
+// of 4 NW bytes): a short stream (C5's column-block tiles: ~235 pairs per wave) pays for the positions it has
+// instead of 1024 (the 16-byte form is ~110 VALU per lane and batch)
+template <int NW>
+__device__ inline int gram_propagate_ids_n(unsigned char *bid, int carry, int lane) {
+    uint32_t w[NW];
+    if constexpr (NW == 1) {
+        w[0] = reinterpret_cast<uint32_t *>(bid)[lane];
+    } else {
+        const uint2 x = reinterpret_cast<uint2 *>(bid)[lane];
+        w[0] = x.x;
+        w[1] = x.y;
+    }
+    int run = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            run = max(run, (int)((w[i] >> (8 * b)) & 0xffu));
+            o |= (uint32_t)run << (8 * b);
+        }
+        w[i] = o;
+    }
+    int before = __builtin_amdgcn_update_dpp(0, wave_incl_max(run), 0x138, 0xf, 0xf, false);  // wave_shr:1
+    before = max(before, carry);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t v = (w[i] >> (8 * b)) & 0xffu;
+            o |= (v > (uint32_t)before ? v : (uint32_t)before) << (8 * b);
+        }
+        w[i] = o;
+    }
+    if constexpr (NW == 1) reinterpret_cast<uint32_t *>(bid)[lane] = w[0];
+    else reinterpret_cast<uint2 *>(bid)[lane] = make_uint2(w[0], w[1]);
     return __builtin_amdgcn_readlane(max(run, before), 63);
 }
 
@@ -367,17 +409,23 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
             aval[h * 64 + lane] = av[h];
         }
         int carry = 0;
-        for (int32_t c0 = 0; c0 < total; c0 += kChunk) {
-            const int32_t cend = (total - c0) < kChunk ? total : c0 + kChunk;
+        // (chunks of 256 / 512 positions when the stream is that short: the propagation's VALU scales with it)
+        const int32_t chunk = total <= 256 ? 256 : total <= 512 ? 512 : kChunk;
+        for (int32_t c0 = 0; c0 < total; c0 += chunk) {
+            const int32_t cend = (total - c0) < chunk ? total : c0 + chunk;
             // bucket ids of the chunk: clear, mark every non-empty bucket's first position, propagate
-            reinterpret_cast<uint4 *>(bidv)[lane] = make_uint4(0u, 0u, 0u, 0u);
+            if (chunk == 256) reinterpret_cast<uint32_t *>(bidv)[lane] = 0u;
+            else if (chunk == 512) reinterpret_cast<uint2 *>(bidv)[lane] = make_uint2(0u, 0u);
+            else reinterpret_cast<uint4 *>(bidv)[lane] = make_uint4(0u, 0u, 0u, 0u);
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int h = 0; h < kV; ++h)
                 if (cnt[h] > 0 && excl[h] >= c0 && excl[h] < cend)
                     bidv[excl[h] - c0] = (unsigned char)(h * 64 + lane + 1);
             __builtin_amdgcn_wave_barrier();
-            carry = gram_propagate_ids(bidv, carry, lane);
+            carry = chunk == 256   ? gram_propagate_ids_n<1>(bidv, carry, lane)
+                    : chunk == 512 ? gram_propagate_ids_n<2>(bidv, carry, lane)
+                                   : gram_propagate_ids(bidv, carry, lane);
             __builtin_amdgcn_wave_barrier();
             int32_t w0 = c0;
             for (; w0 + 64 * kGramUnroll <= cend; w0 += 64 * kGramUnroll)
@@ -434,24 +482,17 @@ __global__ __launch_bounds__(64 * kWaves) void gram_sparse_kernel(
 }
 
 // ------------------------------------------------- pipelined column-block tiles (GRF_REC_SLOT buckets)
-// The column-block Gram of the slot layout (C5: 1M tiles K[i, 0:8192]) as ONE persistent workgroup per CU
-// that owns two 64 KB tile accumulators and splits its waves by role:
-//   * kG gather waves accumulate tile i (their i-th tile: blockIdx.x + i * gridDim.x) into acc[i & 1];
-//   * 4 store waves write tile i - 1 out of acc[(i - 1) & 1] (non-temporal) and zero it;
-// then one barrier (LDS only: `s_waitcnt lgkmcnt(0); s_barrier` -- no vmcnt wait, so neither role's
-// outstanding global operations are drained).  The split matters because vmcnt counts loads and stores
-// together in issue order: a wave that stored a tile would wait for those stores at its next load (the
-// round-3 persistent variant, AB_LOG), so no gather wave ever stores and no store wave ever loads (the tile's
-// shift reaches the store waves through LDS).  A tile's dependent chain (row pointers -> the wave's
-// nonzeros -> their slot headers -> record pairs) is software-pipelined over the tiles: at the start of
-// tile i the headers of tile i + 1, the nonzeros of tile i + 2 and the row pointers of tile i + 3 are issued
-// together, ahead of tile i's gathers, so a tile waits for about one HBM round trip instead of four
-// dependent ones.  (Issued after the gathers instead, their results would be waited for by the register
-// rotation between tiles.)  Same integer sums as gram_sparse_kernel: identical bits.
-constexpr int kPipeStoreWaves = 4;
-constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) alone (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait)
-constexpr int kPipeMaxG = 12;
-
+// The column-block Gram of the slot layout (C5: 1M tiles K[i, 0:8192]) as a persistent kernel of two
+// workgroups per CU (the LDS holds two 64 KB accumulators), each taking the tiles blockIdx.x + i gridDim.x in
+// turn: tile i's gathers, a barrier, tile i's write-out and zeroing, a barrier.  A tile's dependent chain (row
+// bounds -> the wave's nonzeros -> their slot headers -> record pairs) is software-pipelined over the tiles:
+// the headers of tile i + 1, the nonzeros of tile i + 2 and the bounds of tile i + 3 are issued at the start of
+// tile i, behind tile i - 1's K stores, so tile i's one wait covers the stores' completion, the prefetches and
+// its own gathers (vmcnt counts loads and stores together in issue order) -- about one round trip per tile,
+// against four dependent ones for gram_sparse_kernel -- while the CU's other workgroup overlaps it.  Same
+// integer sums: identical bits.  Measured and removed (profiles/r06_c5_gram_ab.txt, AB_LOG round 6): gather and
+// store waves split by role around double accumulators in one workgroup per CU; loader waves filling an LDS
+// ring with each tile's nonzeros and headers; a wave prefetching the nonzeros into L2.
 __device__ __forceinline__ void pipe_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 struct PipeNz {     // one tile's first batch of this wave's nonzeros (one per lane) and its bounds
@@ -462,77 +503,32 @@ struct PipeNz {     // one tile's first batch of this wave's nonzeros (one per l
     int64_t ws0;    // first nonzero of the share
 };
 
-template <int kG>
-__global__ __launch_bounds__(64 * (kG + kPipeStoreWaves)) void gram_slot_pipe_kernel(
+template <int kWv>
+__global__ __launch_bounds__(64 * kWv) void gram_slot_pipe_kernel(
     int64_t n_cols, int64_t row_begin, int64_t rows, int64_t W, int64_t t_rows, int64_t n_tiles,
     const int64_t *__restrict__ ptr, const int32_t *__restrict__ idx, const float *__restrict__ val,
     const unsigned char *__restrict__ t_rec, const int32_t *__restrict__ rowshift, float *__restrict__ K,
     int64_t ldk, int64_t ovf_base, int32_t ablate) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [2][W], s_sh[4], gather state
+    extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W], then the waves' stream state
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-    constexpr int kV = 2;  // stream buckets per nonzero: the slot's inline pairs, its overflow pairs
+    constexpr int kV = 2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t G = gridDim.x;
     const int64_t n_mine = (int64_t)blockIdx.x < n_tiles ? (n_tiles - 1 - (int64_t)blockIdx.x) / G + 1 : 0;
-    int32_t *s_sh = reinterpret_cast<int32_t *>(acc + 2 * W);
     u64x2 *acc2 = reinterpret_cast<u64x2 *>(acc);
     const u64x2 z2 = {0ull, 0ull};
-    for (int64_t q = tid; q < W; q += 64 * (kG + kPipeStoreWaves)) acc2[q] = z2;  // both buffers
-    pipe_barrier();
-
-    if (wave >= kG) {
-        // ---- store waves: tile i - 1 out of its buffer, the buffer zeroed for tile i + 1
-        const int stid = tid - 64 * kG;
-        constexpr int kST = 64 * kPipeStoreWaves;
-        for (int64_t i = 0; i <= n_mine; ++i) {
-            if (i >= 1 && ablate != 2) {
-                const int64_t t = (int64_t)blockIdx.x + (i - 1) * G, J = t / rows, r = t - J * rows, j0 = J * W;
-                const int64_t wlen = (t_rows - j0) < W ? (t_rows - j0) : W;
-                const int sh = s_sh[(i - 1) & 1];
-                unsigned long long *a = acc + ((i - 1) & 1) * W;
-                u64x2 *a2 = reinterpret_cast<u64x2 *>(a);
-                float *krow = K + r * ldk + j0;
-                int64_t done = 0;
-                if ((ldk & 3) == 0 && (j0 & 3) == 0) {
-                    const int64_t n4 = wlen / 4;
-                    f32x4 *k4 = reinterpret_cast<f32x4 *>(krow);
-                    for (int64_t q = stid; q < n4; q += kST) {
-                        const u64x2 x = a2[2 * q], y = a2[2 * q + 1];
-                        f32x4 o;
-                        o[0] = fx_to_float(x[0], sh);
-                        o[1] = fx_to_float(x[1], sh);
-                        o[2] = fx_to_float(y[0], sh);
-                        o[3] = fx_to_float(y[1], sh);
-                        GRF_K_STORE(o, &k4[q]);
-                        a2[2 * q] = z2;
-                        a2[2 * q + 1] = z2;
-                    }
-                    done = n4 * 4;
-                }
-                for (int64_t q = done + stid; q < wlen; q += kST) {
-                    krow[q] = fx_to_float(a[q], sh);
-                    a[q] = 0ull;
-                }
-            }
-            pipe_barrier();
-        }
-        return;
-    }
-
-    // ---- gather waves
-    unsigned char *st = reinterpret_cast<unsigned char *>(s_sh + 4) + wave * wave_state_bytes(kV);
+    for (int64_t q = tid; q < W / 2; q += 64 * kWv) acc2[q] = z2;
+    unsigned char *st = reinterpret_cast<unsigned char *>(acc + W) + wave * wave_state_bytes(kV);
     unsigned char *bidv = st;                                             // [kChunk]
     int32_t *tbase = reinterpret_cast<int32_t *>(st + kChunk);            // [64 kV]
     float *aval = reinterpret_cast<float *>(st + kChunk + 64 * kV * 4);  // [64 kV]
     const __amdgpu_buffer_rsrc_t rec_rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char *>(t_rec), (short)0, 0x7fffffff, 0x00020000);
-    auto tile_row = [&](int64_t i, int64_t &J) -> int64_t {  // (global row of my i-th tile, its band)
+    auto tile_row = [&](int64_t i, int64_t &J) -> int64_t {
         const int64_t t = (int64_t)blockIdx.x + i * G;
         J = t / rows;
         return row_begin + (t - J * rows);
     };
-    // stage 1: the row's bounds (lane 0: ptr[row], lane 1: ptr[row + 1]) and shift, by buffer loads (always
-    // vector memory: a scalar load would hold lgkmcnt, i.e. every LDS wait, until it returned)
     auto load_bounds = [&](int64_t i, int64_t &pv, int32_t &shv) {
         if (i >= n_mine) {
             pv = 0;
@@ -549,7 +545,6 @@ __global__ __launch_bounds__(64 * (kG + kPipeStoreWaves)) void gram_slot_pipe_ke
             __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(rowshift + row), (short)0, 4, 0x00020000);
         shv = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, 0u, 0, 0);
     };
-    // stage 2: the wave's share of the row and its first 64 nonzeros
     auto load_nz = [&](int64_t i, int64_t pv, int32_t shv, PipeNz &z) {
         if (i >= n_mine) {
             z = PipeNz{-1, 0.f, 0, 0, 0};
@@ -561,24 +556,22 @@ __global__ __launch_bounds__(64 * (kG + kPipeStoreWaves)) void gram_slot_pipe_ke
             return (int64_t)(((uint64_t)hi << 32) | lo);
         };
         const int64_t e0 = lane_i64(0), e1 = lane_i64(1);
-        const int64_t nnz = e1 - e0, share = (nnz + kG - 1) / kG;
+        const int64_t nnz = e1 - e0, share = (nnz + kWv - 1) / kWv;
         const int64_t s0 = wave * share < nnz ? wave * share : nnz, s1 = (wave + 1) * share < nnz ? (wave + 1) * share : nnz;
         const int64_t e = e0 + s0 + lane;
-        const bool ok = s0 + lane < s1 && lane < 64;
+        const bool ok = s0 + lane < s1;
         z.k = ok ? idx[e] : -1;
         z.a = ok ? val[e] : 0.f;
         z.sh = shv;
         z.nb = (int32_t)(s1 - s0);
         z.ws0 = e0 + s0;
     };
-    // stage 3: the slot headers {pairs, first overflow pair}
     auto load_hdr = [&](int64_t i, int32_t k) -> uint2 {
         if (i >= n_mine || k < 0) return make_uint2(0u, 0u);
         int64_t J;
         tile_row(i, J);
         return *reinterpret_cast<const uint2 *>(t_rec + 32 * (J * n_cols + k));
     };
-    // one batch of (at most) 64 nonzeros -> two stream buckets each
     auto run_batch = [&](const GramStream &gs, int64_t J, int32_t k, float a, uint2 d) {
         int32_t cnt[kV], excl[kV], t0[kV];
         const int32_t sb = (int32_t)(32 * (J * n_cols + (k >= 0 ? k : 0)));
@@ -600,24 +593,23 @@ __global__ __launch_bounds__(64 * (kG + kPipeStoreWaves)) void gram_slot_pipe_ke
             aval[h * 64 + lane] = a;
         }
         int carry = 0;
-        for (int32_t c0 = 0; c0 < total; c0 += kChunk) {
-            const int32_t cend = (total - c0) < kChunk ? total : c0 + kChunk;
-            reinterpret_cast<uint4 *>(bidv)[lane] = make_uint4(0u, 0u, 0u, 0u);
+        const int32_t chunk = total <= 256 ? 256 : total <= 512 ? 512 : kChunk;
+        for (int32_t c0 = 0; c0 < total; c0 += chunk) {
+            const int32_t cend = (total - c0) < chunk ? total : c0 + chunk;
+            if (chunk == 256) reinterpret_cast<uint32_t *>(bidv)[lane] = 0u;
+            else if (chunk == 512) reinterpret_cast<uint2 *>(bidv)[lane] = make_uint2(0u, 0u);
+            else reinterpret_cast<uint4 *>(bidv)[lane] = make_uint4(0u, 0u, 0u, 0u);
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int h = 0; h < kV; ++h)
                 if (cnt[h] > 0 && excl[h] >= c0 && excl[h] < cend) bidv[excl[h] - c0] = (unsigned char)(h * 64 + lane + 1);
             __builtin_amdgcn_wave_barrier();
-            carry = gram_propagate_ids(bidv, carry, lane);
+            carry = chunk == 256   ? gram_propagate_ids_n<1>(bidv, carry, lane)
+                    : chunk == 512 ? gram_propagate_ids_n<2>(bidv, carry, lane)
+                                   : gram_propagate_ids(bidv, carry, lane);
             __builtin_amdgcn_wave_barrier();
             int32_t w0 = c0;
-            // (every group ends with an explicit vmcnt(0) -- its adds waited for its gathers anyway -- so the
-            // compiler's wait insertion, which merges this loop's paths, never sees a gather still pending at
-            // the next group and never makes the first group wait vmcnt(0) for the prefetch loads)
-            for (; w0 + 64 * 8 <= cend; w0 += 64 * 8) {
-                gram_windows<8, 0>(gs, w0, c0, cend, lane);
-                __builtin_amdgcn_s_waitcnt(kWaitVm0);
-            }
+            for (; w0 + 64 * 8 <= cend; w0 += 64 * 8) gram_windows<8, 0>(gs, w0, c0, cend, lane);
             if (w0 < cend) {
                 switch ((cend - w0 + 63) >> 6) {
                     case 1: gram_windows<1, 1>(gs, w0, c0, cend, lane); break;
@@ -629,13 +621,10 @@ __global__ __launch_bounds__(64 * (kG + kPipeStoreWaves)) void gram_slot_pipe_ke
                     case 7: gram_windows<7, 1>(gs, w0, c0, cend, lane); break;
                     default: gram_windows<8, 1>(gs, w0, c0, cend, lane); break;
                 }
-                __builtin_amdgcn_s_waitcnt(kWaitVm0);
             }
             __builtin_amdgcn_wave_barrier();
         }
     };
-
-    // prologue: the stages of tiles 0 .. 2
     int64_t pv;
     int32_t shv;
     PipeNz T0, T1;
@@ -645,26 +634,19 @@ __global__ __launch_bounds__(64 * (kG + kPipeStoreWaves)) void gram_slot_pipe_ke
     load_bounds(1, pv, shv);
     load_nz(1, pv, shv, T1);
     load_bounds(2, pv, shv);
-    // (drained here, once: a load left pending into the loop makes the compiler's wait insertion assume any
-    // loop register may still be loading and wait vmcnt(0) wherever one is overwritten)
     __builtin_amdgcn_s_waitcnt(0);
-    for (int64_t i = 0; i <= n_mine; ++i) {
-        if (i < n_mine && ablate != 1) {
-            // the next tiles' stages, issued together ahead of this tile's gathers: headers of tile i + 1,
-            // nonzeros of i + 2, bounds of i + 3 (the gathers' in-order wait covers them, so the register
-            // rotation below never waits; the tile's chain is one HBM round trip beside its gathers)
-            const uint2 d1 = load_hdr(i + 1, T1.k);
-            PipeNz T2;
-            load_nz(i + 2, pv, shv, T2);
-            load_bounds(i + 3, pv, shv);
-            int64_t J;
-            tile_row(i, J);
-            if (wave == 0 && lane == 0) s_sh[i & 1] = T0.sh;
-            const GramStream gs{bidv, tbase, aval, rec_rs, reinterpret_cast<unsigned char *>(acc + (i & 1) * W),
-                                ldexp(1.0, T0.sh), 8};
+    pipe_barrier();
+    for (int64_t i = 0; i < n_mine; ++i) {
+        const uint2 d1 = load_hdr(i + 1, T1.k);
+        PipeNz T2;
+        load_nz(i + 2, pv, shv, T2);
+        load_bounds(i + 3, pv, shv);
+        int64_t J;
+        const int64_t row = tile_row(i, J);
+        if (ablate != 1) {
+            const GramStream gs{bidv, tbase, aval, rec_rs, reinterpret_cast<unsigned char *>(acc), ldexp(1.0, T0.sh), 8};
             run_batch(gs, J, T0.k, T0.a, d0);
-            // the rest of a share longer than 64 nonzeros (rows past 64 kG entries), batch by batch
-            for (int32_t g = 64; g < T0.nb; g += 64) {
+            for (int32_t g = 64; g < T0.nb; g += 64) {  // (a share past 64 nonzeros: batch by batch)
                 const int64_t e = T0.ws0 + g + lane;
                 const bool ok = g + lane < T0.nb;
                 const int32_t k = ok ? idx[e] : -1;
@@ -672,11 +654,38 @@ __global__ __launch_bounds__(64 * (kG + kPipeStoreWaves)) void gram_slot_pipe_ke
                 const uint2 d = k >= 0 ? *reinterpret_cast<const uint2 *>(t_rec + 32 * (J * n_cols + k)) : make_uint2(0u, 0u);
                 run_batch(gs, J, k, a, d);
             }
-            T0 = T1;
-            d0 = d1;
-            T1 = T2;
         }
         pipe_barrier();
+        // tile i out (non-temporal) and its accumulator zeroed
+        const int64_t r = row - row_begin, j0 = J * W;
+        const int64_t wlen = (t_rows - j0) < W ? (t_rows - j0) : W;
+        const int sh = T0.sh;
+        float *krow = K + r * ldk + j0;
+        int64_t done = 0;
+        if ((ldk & 3) == 0 && (j0 & 3) == 0) {
+            const int64_t n4 = wlen / 4;
+            f32x4 *k4 = reinterpret_cast<f32x4 *>(krow);
+            for (int64_t q = tid; q < n4; q += 64 * kWv) {
+                const u64x2 x = acc2[2 * q], y = acc2[2 * q + 1];
+                f32x4 o;
+                o[0] = fx_to_float(x[0], sh);
+                o[1] = fx_to_float(x[1], sh);
+                o[2] = fx_to_float(y[0], sh);
+                o[3] = fx_to_float(y[1], sh);
+                if (ablate != 2) GRF_K_STORE(o, &k4[q]);
+                acc2[2 * q] = z2;
+                acc2[2 * q + 1] = z2;
+            }
+            done = n4 * 4;
+        }
+        for (int64_t q = done + tid; q < wlen; q += 64 * kWv) {
+            if (ablate != 2) krow[q] = fx_to_float(acc[q], sh);
+            acc[q] = 0ull;
+        }
+        pipe_barrier();
+        T0 = T1;
+        d0 = d1;
+        T1 = T2;
     }
 }
 
@@ -887,8 +896,6 @@ static int32_t gram_balance(const GramTiles &tl, int32_t unit) {
     return (unit == GRF_REC_SLOT || tl.t_rows < 0) ? 1 : 0;
 }
 
-static bool pipe_lds_ok(size_t bytes) { return bytes <= 160 * 1024; }
-
 static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramTiles &tl, int64_t t_first,
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
                                  const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
@@ -900,36 +907,29 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
         GRF_REQUIRE(!t_split, GRF_EUNSUPPORTED, "gram: GRF_REC_SLOT has no split variant");
         GRF_REQUIRE(32 * slot_buckets < ((int64_t)1 << 30), GRF_EUNSUPPORTED,
                     "gram: GRF_REC_SLOT slots beyond 32-bit record offsets");
-        // column blocks (a whole launch of non-symmetric tiles over all columns): the pipelined persistent
-        // kernel (GRF_GRAM_PIPE=0: the tile-per-workgroup kernel below; GRF_GRAM_PIPE_G=12: 12 gather waves, 8 by
-        // default: C5 alone 11.32 vs 11.88 ms, profiles/r06_c5_gram_ab.txt)
-        // (read per call: the bit-identity test switches it between calls; GRF_GRAM_PIPE_ABLATE=1 / 2 are
-        // timing-only ablations -- no gathers / no K stores -- whose K is wrong)
-        const int pipe_g = [] {
+        // column blocks (a whole launch of non-symmetric tiles over all columns): the persistent software-pipelined
+        // kernel, GRF_GRAM_PIPE=0: the tile-per-workgroup kernel below (read per call: the bit-identity test
+        // switches it; GRF_GRAM_PIPE_ABLATE=1 / 2 are timing-only ablations -- no gathers / no K stores -- whose
+        // K is wrong; profiles/r06_c5_gram_ab.txt)
+        const bool pipe = [] {
             const char *e = getenv("GRF_GRAM_PIPE");
-            if (e && atoi(e) == 0) return 0;
-            const char *g = getenv("GRF_GRAM_PIPE_G");
-            return (g && atoi(g) == kPipeMaxG) ? kPipeMaxG : 8;
+            return !e || atoi(e) != 0;
         }();
         const int32_t ablate = [] {
             const char *e = getenv("GRF_GRAM_PIPE_ABLATE");
             return e ? (int32_t)atoi(e) : 0;
         }();
-        const size_t pipe_lds = (size_t)2 * tl.W * 8 + 16 + (size_t)pipe_g * wave_state_bytes(2);
-        if (pipe_g && !tl.sym && tl.t_rows >= 0 && !tl.add_k && tl.k_begin == 0 && tl.k_end == (int32_t)n_total &&
-            t_first == 0 && t_last == tl.total() && tl.J_off == 0 && pipe_lds_ok(pipe_lds)) {
+        if (pipe && !tl.sym && tl.t_rows >= 0 && !tl.add_k && tl.k_begin == 0 && tl.k_end == (int32_t)n_total &&
+            t_first == 0 && t_last == tl.total() && tl.J_off == 0) {
+            const size_t lds = gram_lds_bytes(tl.W, 8, 2);
             int dev = 0, n_cu = 0;
             GRF_CHECK_HIP(hipGetDevice(&dev));
             GRF_CHECK_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-            const int64_t grid = std::min<int64_t>(std::max(n_cu, 1), t_last);
-            if (pipe_g == 8)
-                gram_slot_pipe_kernel<8><<<(unsigned)grid, 64 * (8 + kPipeStoreWaves), pipe_lds, st>>>(
-                    n_total, row_begin, tl.rows, tl.W, tl.t_rows, t_last, ptr, idx, val,
-                    reinterpret_cast<const unsigned char *>(t_rec), t_rowshift, K, ldk, 32 * slot_buckets, ablate);
-            else
-                gram_slot_pipe_kernel<kPipeMaxG><<<(unsigned)grid, 64 * (kPipeMaxG + kPipeStoreWaves), pipe_lds, st>>>(
-                    n_total, row_begin, tl.rows, tl.W, tl.t_rows, t_last, ptr, idx, val,
-                    reinterpret_cast<const unsigned char *>(t_rec), t_rowshift, K, ldk, 32 * slot_buckets, ablate);
+            const int per_cu = (int)std::max<int64_t>(1, (int64_t)(160 * 1024) / (int64_t)lds);
+            const int64_t grid = std::min<int64_t>((int64_t)std::max(n_cu, 1) * per_cu, t_last);
+            gram_slot_pipe_kernel<8><<<(unsigned)grid, 512, lds, st>>>(
+                n_total, row_begin, tl.rows, tl.W, tl.t_rows, t_last, ptr, idx, val,
+                reinterpret_cast<const unsigned char *>(t_rec), t_rowshift, K, ldk, 32 * slot_buckets, ablate);
             GRF_CHECK_LAUNCH("gram_slot_pipe_kernel");
             return GRF_OK;
         }

@@ -6,7 +6,7 @@
 namespace grf {
 
 // ------------------------------------------------------------------ Philox
-__device__ inline void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                                      uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -24,31 +24,33 @@ __device__ inline void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint
     o0 = c0; o1 = c1; o2 = c2; o3 = c3;
 }
 
-// Lemire rejection tail (probability < deg / 2^32): words continue with x3 of
-// block 0, then blocks 1, 2, ... of the same (step, walk, source) counter.
-__device__ __noinline__ uint64_t philox_lemire_retry(uint32_t d, uint32_t thr, uint32_t x3, uint32_t l, uint32_t w,
-                                                     uint32_t s, uint32_t k0, uint32_t k1) {
-    uint64_t mm = (uint64_t)x3 * d;
-    if ((uint32_t)mm >= thr) return mm;
+// Lemire rejection tail of step l (probability < deg / 2^32): words from blocks 1, 2, ... of the step's own
+// counter (l, w, s, blk) -- block 0 of (j, w, s) is the step pair's main draw (philox_walk).
+__device__ __noinline__ uint64_t philox_lemire_retry(uint32_t d, uint32_t thr, uint32_t l, uint32_t w, uint32_t s,
+                                                     uint32_t k0, uint32_t k1) {
     for (uint32_t blk = 1;; ++blk) {
         uint32_t y[4];
         philox4x32_10(l, w, s, blk, k0, k1, y[0], y[1], y[2], y[3]);
         for (int i = 0; i < 4; ++i) {
-            mm = (uint64_t)y[i] * d;
+            const uint64_t mm = (uint64_t)y[i] * d;
             if ((uint32_t)mm >= thr) return mm;
         }
     }
 }
 
-// The halt test h < p of the 53-bit double h = (x0:x1 >> 11) 2^-53 as an integer compare: h < p <=> t < p 2^53
-// <=> t < ceil(p 2^53) for the integer t (p 2^53 is exact); 0 when p <= 0 or NaN (never halts).
+// The halt test of one 32-bit word x: halt iff x < ceil(p 2^32) (p 2^32 is exact; P(halt) = ceil(p 2^32) / 2^32,
+// within 2^-32 of p); 0 when p <= 0 or NaN (never halts), 2^32 when p >= 1 (always).
 __device__ inline uint64_t halt_threshold(double p) {
-    const double y = ceil(p * 9007199254740992.0);
-    return y > 0.0 ? (y < 9007199254740992.0 ? (uint64_t)y : (1ull << 53)) : 0ull;
+    const double y = ceil(p * 4294967296.0);
+    return y > 0.0 ? (y < 4294967296.0 ? (uint64_t)y : (1ull << 32)) : 0ull;
 }
-__device__ inline bool halts(uint32_t x0, uint32_t x1, uint64_t thr) {
-    return ((((uint64_t)x0 << 32) | x1) >> 11) < thr;
-}
+__device__ inline bool halts(uint32_t x, uint64_t thr) { return (uint64_t)x < thr; }
+
+// The words of step l: one Philox4x32-10 block (l / 2, w, s, 0) serves the step pair -- the even step halts on
+// x0 and picks its neighbour from x1, the odd step uses x2 and x3 -- so a walk of L recorded visits runs
+// ceil((L - 1) / 2) blocks (the last recorded visit draws nothing).  The walks below take the steps in pairs,
+// so the four words live in registers for one loop iteration (carried across iterations, with the block
+// computed on every other step, they went to scratch memory).
 
 // x / c correctly rounded without the IEEE divide sequence (v_div_scale x2, v_rcp_f64, 5 FMAs, v_div_fmas,
 // v_div_fixup per call): with y = RN(1 / c) (loop-invariant: computed once per walk) the quotient
@@ -92,9 +94,9 @@ __device__ inline double load_update(int rule, double load, Deg deg, double w, c
 
 // One Philox walk (source s, walk w) of at most L recorded visits: visit(l, node, load) is
 // called for the recorded steps l = 0, 1, ...; returns the number of recorded visits.
-// Per step: record (current node, load); stop at a zero-degree node or with probability
-// p_halt (53-bit double from words x0, x1 < p); otherwise move to neighbour Lemire(x2, deg)
-// and update the load by the importance weight deg * w / (1 - p).
+// Per step: record (current node, load); stop after the L-th visit, at a zero-degree node or with
+// probability p_halt (StepWords: halt word < ceil(p 2^32)); otherwise move to neighbour Lemire(pick
+// word, deg) and update the load by the importance weight deg * w / (1 - p).
 template <typename Visit>
 __device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const int32_t *__restrict__ g_idx,
                                       const double *__restrict__ g_val, int64_t s, uint32_t w, double p, int32_t L,
@@ -103,27 +105,36 @@ __device__ inline int32_t philox_walk(const int64_t *__restrict__ g_ptr, const i
     double load = 1.0;
     const uint64_t hthr = halt_threshold(p);
     const LoadKeep keep(p);
-    int32_t l = 0;
-    for (; l < L; ++l) {
-        visit(l, (int32_t)cur, load);
-        const int64_t rs = g_ptr[cur], deg = g_ptr[cur + 1] - rs;
-        if (deg == 0) return l + 1;
-        uint32_t x0, x1, x2, x3;
-        philox4x32_10((uint32_t)l, w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
-        if (halts(x0, x1, hthr)) return l + 1;
+    int64_t rs = g_ptr[s], deg = g_ptr[s + 1] - rs;
+    // one move of step l with halt word hw and neighbour word pw; false: the walk halts here
+    auto move = [&](int32_t l, uint32_t hw, uint32_t pw) -> bool {
+        if (halts(hw, hthr)) return false;
         const uint32_t d = (uint32_t)deg;
         uint32_t k = 0;
         if (d > 1) {
-            uint64_t mm = (uint64_t)x2 * d;
+            uint64_t mm = (uint64_t)pw * d;
             if ((uint32_t)mm < d) {
                 const uint32_t thr = (0u - d) % d;
-                if ((uint32_t)mm < thr) mm = philox_lemire_retry(d, thr, x3, (uint32_t)l, w, (uint32_t)s, k0, k1);
+                if ((uint32_t)mm < thr) mm = philox_lemire_retry(d, thr, (uint32_t)l, w, (uint32_t)s, k0, k1);
             }
             k = (uint32_t)(mm >> 32);
         }
         const double wt = g_val[rs + k];
         load = load_update(rule, load, deg, wt, keep);
         cur = g_idx[rs + k];
+        rs = g_ptr[cur];
+        deg = g_ptr[cur + 1] - rs;
+        return true;
+    };
+    for (int32_t l = 0; l < L; l += 2) {
+        visit(l, (int32_t)cur, load);
+        if (l == L - 1 || deg == 0) return l + 1;
+        uint32_t x0, x1, x2, x3;
+        philox4x32_10((uint32_t)l >> 1, w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
+        if (!move(l, x0, x1)) return l + 1;
+        visit(l + 1, (int32_t)cur, load);
+        if (l + 1 == L - 1 || deg == 0) return l + 2;
+        if (!move(l + 1, x2, x3)) return l + 2;
     }
     return L;
 }
@@ -164,20 +175,15 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
     const LoadKeep keep(p);
     int64_t rs = g_ptr[s];
     int64_t deg = g_ptr[s + 1] - rs;
-    int32_t l = 0;
-    for (; l < L; ++l) {
-        visit(l, (int32_t)cur, load);
-        if (deg == 0) return l + 1;
-        uint32_t x0, x1, x2, x3;
-        philox4x32_10((uint32_t)l, w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
-        if (halts(x0, x1, hthr)) return l + 1;
+    auto move = [&](int32_t l, uint32_t hw, uint32_t pw) -> bool {
+        if (halts(hw, hthr)) return false;
         const uint32_t d = (uint32_t)deg;
         uint32_t k = 0;
         if (d > 1) {
-            uint64_t mm = (uint64_t)x2 * d;
+            uint64_t mm = (uint64_t)pw * d;
             if ((uint32_t)mm < d) {
                 const uint32_t thr = (0u - d) % d;
-                if ((uint32_t)mm < thr) mm = philox_lemire_retry(d, thr, x3, (uint32_t)l, w, (uint32_t)s, k0, k1);
+                if ((uint32_t)mm < thr) mm = philox_lemire_retry(d, thr, (uint32_t)l, w, (uint32_t)s, k0, k1);
             }
             k = (uint32_t)(mm >> 32);
         }
@@ -198,6 +204,17 @@ __device__ inline int32_t philox_walk_aug(const int64_t *__restrict__ g_ptr, con
             rs = (int64_t)(uint32_t)a.y;
             deg = a.z;
         }
+        return true;
+    };
+    for (int32_t l = 0; l < L; l += 2) {
+        visit(l, (int32_t)cur, load);
+        if (l == L - 1 || deg == 0) return l + 1;
+        uint32_t x0, x1, x2, x3;
+        philox4x32_10((uint32_t)l >> 1, w, (uint32_t)s, 0u, k0, k1, x0, x1, x2, x3);
+        if (!move(l, x0, x1)) return l + 1;
+        visit(l + 1, (int32_t)cur, load);
+        if (l + 1 == L - 1 || deg == 0) return l + 2;
+        if (!move(l + 1, x2, x3)) return l + 2;
     }
     return L;
 }

@@ -26,7 +26,7 @@ RNG_PCG64, RNG_PHILOX = 0, 1
 LOAD_CUMULATIVE, LOAD_NONCUMULATIVE, LOAD_ABLATION = 0, 1, 2
 NORM_DIV, NORM_MUL_RECIP = 0, 1
 REC_LINE, REC_PACKED, REC_SLOT = 128, 12, 32
-ABI_VERSION = 6  # include/grf.h GRF_ABI_VERSION: argument lists change between revisions
+ABI_VERSION = 7  # include/grf.h GRF_ABI_VERSION: argument lists change between revisions
 
 
 class GrfWalkParams(ctypes.Structure):

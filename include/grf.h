@@ -54,7 +54,7 @@ enum grf_laplacian_mode {
 
 enum grf_rng {
     GRF_RNG_PCG64 = 0, /* numpy PCG64 stream replay, one sequential stream per chunk (reference-exact) */
-    GRF_RNG_PHILOX = 1 /* Philox4x32-10 keyed (seed), counter (step, walk, source, block)          */
+    GRF_RNG_PHILOX = 1 /* Philox4x32-10 keyed (seed), counter (step pair, walk, source, block)     */
 };
 
 enum grf_load_rule {
@@ -69,8 +69,8 @@ enum grf_norm {
 };
 
 /* The ABI revision of this header: grf_version() returns it, and a binding must refuse a library whose
- * revision differs (argument lists change between revisions). */
-#define GRF_ABI_VERSION 6
+ * revision differs (argument lists, or -- ABI 7 -- the GRF_RNG_PHILOX stream, change between revisions). */
+#define GRF_ABI_VERSION 7
 
 const char *grf_last_error(void);
 int32_t grf_version(void);
@@ -110,7 +110,10 @@ size_t grf_laplacian_dense_workspace_bytes(int64_t n);
  *   slot_node[(s - src_begin) * L * m + l * m + w] (int32, -1 = no visit),
  *   slot_load[same]                                   (float64)
  * for sources s in [src_begin, src_end).
- * RNG GRF_RNG_PHILOX: key = seed (64 bit).  Any [src_begin, src_end).
+ * RNG GRF_RNG_PHILOX: key = seed (64 bit).  Any [src_begin, src_end).  Block (l / 2, w, s, 0) of
+ *   Philox4x32-10 serves steps l = 2j, 2j + 1 of walk (s, w): the even step halts iff x0 < ceil(p 2^32)
+ *   and takes neighbour Lemire(x1, deg), the odd step uses x2 and x3; a Lemire rejection of step l
+ *   continues on blocks (l, w, s, 1), (l, w, s, 2), ...; the L-th recorded visit draws nothing.
  * RNG GRF_RNG_PCG64 : chunks = np.array_split(arange(n), n_chunks); chunk c is one
  *   numpy default_rng(seed + c) stream; [src_begin, src_end) must be a union of
  *   whole chunks (use grf_chunk_bounds). */

@@ -290,10 +290,19 @@ static void walk_pcg64_range(void *ctx, int64_t b, int64_t e) {
     for (int64_t ch = b; ch < e; ++ch) walk_pcg64_chunk((walk_ctx *)ctx, ch);
 }
 
-/* Philox walk of (s, wk): halt draw = 53-bit double from two words, neighbour
- * = 32-bit Lemire with rejection continuing on the same counter stream. */
+/* Philox walk of (s, wk), the engine's stream (csrc/grf_philox.h StepWords): one Philox4x32-10 block
+ * (l / 2, wk, s, 0) serves the step pair l = 2j, 2j + 1 -- the even step halts iff x0 < ceil(p 2^32) and
+ * picks its neighbour by 32-bit Lemire from x1, the odd step uses x2 and x3; a Lemire rejection of step l
+ * continues on blocks (l, wk, s, 1), (l, wk, s, 2), ...; the L-th recorded visit draws nothing. */
+static uint64_t halt_threshold32(double p) {
+    double y = ceil(p * 4294967296.0);
+    return y > 0.0 ? (y < 4294967296.0 ? (uint64_t)y : (1ull << 32)) : 0ull;
+}
 static void walk_philox_one(walk_ctx *c, int64_t s, int64_t wk) {
     const int64_t L = c->L, m = c->m;
+    const uint32_t k0 = (uint32_t)c->philox_seed, k1 = (uint32_t)(c->philox_seed >> 32);
+    const uint64_t hthr = halt_threshold32(c->p_halt);
+    uint32_t x[4] = {0, 0, 0, 0};
     int64_t cur = s;
     double load = 1.0;
     int64_t l = 0;
@@ -301,20 +310,25 @@ static void walk_philox_one(walk_ctx *c, int64_t s, int64_t wk) {
         int64_t slot = (s * L + l) * m + wk;
         c->slot_node[slot] = (int32_t)cur;
         c->slot_load[slot] = load;
+        if (l == L - 1) { ++l; break; }
         int64_t rs = c->indptr[cur], deg = c->indptr[cur + 1] - rs;
         if (deg == 0) { ++l; break; }
-        philox_stream ps = {(uint32_t)c->philox_seed, (uint32_t)(c->philox_seed >> 32), (uint32_t)l, (uint32_t)wk,
-                            (uint32_t)s, 0u, {0, 0, 0, 0}, 4};
-        uint32_t x0 = ps_next(&ps), x1 = ps_next(&ps);
-        double h = (double)((((uint64_t)x0 << 32) | x1) >> 11) * (1.0 / 9007199254740992.0);
-        if (h < c->p_halt) { ++l; break; }
+        if ((l & 1) == 0) {
+            uint32_t ctr[4] = {(uint32_t)(l >> 1), (uint32_t)wk, (uint32_t)s, 0u};
+            philox4x32_10(ctr, k0, k1, x);
+        }
+        uint32_t hw = (l & 1) ? x[2] : x[0], pw = (l & 1) ? x[3] : x[1];
+        if ((uint64_t)hw < hthr) { ++l; break; }
         uint32_t d = (uint32_t)deg, k = 0;
         if (d > 1) {
-            uint64_t mm = (uint64_t)ps_next(&ps) * d;
+            uint64_t mm = (uint64_t)pw * d;
             uint32_t left = (uint32_t)mm;
             if (left < d) {
                 uint32_t thr = (uint32_t)(0u - d) % d;
-                while (left < thr) { mm = (uint64_t)ps_next(&ps) * d; left = (uint32_t)mm; }
+                if (left < thr) {
+                    philox_stream ps = {k0, k1, (uint32_t)l, (uint32_t)wk, (uint32_t)s, 1u, {0, 0, 0, 0}, 4};
+                    while (left < thr) { mm = (uint64_t)ps_next(&ps) * d; left = (uint32_t)mm; }
+                }
             }
             k = (uint32_t)(mm >> 32);
         }

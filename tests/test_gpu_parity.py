@@ -1036,6 +1036,44 @@ def test_slot_transpose_gram_bit_identical(eng, graph):
                        eng.gram_sparse(phs, eng.transpose_banded(phs, 8192, rec_unit=C.REC_PACKED), 0, 2000))
 
 
+@pytest.mark.parametrize("pipe", ["1"])
+def test_gram_cols_pipelined_bit_identical(eng, pipe):
+    """The persistent, software-pipelined column-block Gram kernel for slot buckets (gram_slot_pipe_kernel, the
+    default) gives the tile-per-workgroup kernel's bits (GRF_GRAM_PIPE=0): m = 256 walks of up to 6 visits on a
+    degree-40 graph (rows of over 768 nonzeros, past 64 per gather wave: the batch-by-batch tail of a share),
+    one band (8192 columns), three bands with a ragged last one, a band width that is not a power of two, a
+    row range, and t_rows not a multiple of 4."""
+    import os
+
+    import torch
+    from grf_amd import _lib as C
+    n = 30001
+    A = er_graph(n, 40, 7)
+    G = eng.laplacian(A)
+    m, L = 256, 6
+    f = [1.0, -0.5, 0.125, -0.02, 0.003, -0.0004]
+    phi = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=3, want64=False), want64=False)
+    shift = eng.phi_row_shifts(phi)
+    assert int((phi.ptr[1:] - phi.ptr[:-1]).max()) > 64 * 12  # (shares past one batch of 64 per wave)
+    old = os.environ.get("GRF_GRAM_PIPE")
+    try:
+        for b, e, bw, rows in ((0, 8192, 8192, None), (5000, 25000, 8192, None), (101, 6101, 6016, None),
+                               (2000, 10190, 8192, (333, 29001)), (7, 8194, 8192, None)):
+            loc = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=3, src_begin=b, src_end=e, want64=False), want64=False)
+            ts = eng.transpose_banded(loc, bw, rec_unit=C.REC_SLOT)
+            r0, r1 = rows or (0, n)
+            os.environ["GRF_GRAM_PIPE"] = "0"
+            K0 = eng.gram_sparse_cols(phi, shift, ts, r0, r1).clone()
+            os.environ["GRF_GRAM_PIPE"] = pipe
+            K1 = eng.gram_sparse_cols(phi, shift, ts, r0, r1)
+            assert torch.equal(K0, K1), (pipe, b, e, bw, rows)
+    finally:
+        if old is None:
+            os.environ.pop("GRF_GRAM_PIPE", None)
+        else:
+            os.environ["GRF_GRAM_PIPE"] = old
+
+
 @pytest.mark.parametrize("unit", [128, 12])
 def test_transpose_wide_regions(eng, unit):
     """A graph large enough that the staged fill widens its column regions (n_rows * n_cols / (16 cr)
