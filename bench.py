@@ -326,9 +326,10 @@ def dense_gram_roofline(precision: str, flops: float, ms: float) -> dict:
     if precision == "split":
         return {"bound": "mfma", "achieved": SPLIT_PRODUCTS * tfs, "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": SPLIT_PRODUCTS * tfs / MFMA_BF16_PEAK_TFS, "traffic": None,
-                "kernel": "gram_split_mfma_kernel (128x128 tiles; n <= 8064) / gram_split_wide_kernel (256x128 "
-                          "items of 8 waves, stream-K) (fp32 LDS-DMA staging, exact three-plane bf16 split in "
-                          "registers, v_mfma_f32_32x32x16_bf16, 6 products per term)",
+                "kernel": "gram_split_mfma_kernel (128x128 tiles, fp32 LDS-DMA staging, the exact three-plane bf16 "
+                          "split in registers; n <= 8064) / gram_planes_wide_kernel (256x128 items of 8 waves, "
+                          "stream-K, the planes split once by the front and staged as they are) -- "
+                          "v_mfma_f32_32x32x16_bf16, 6 products per term",
                 "kernel_ms": ms, "algorithmic_flops": flops, "bf16_flops": SPLIT_PRODUCTS * flops,
                 "fp32_equivalent_tflops": tfs, "fp32_equivalent_vs_fp32_peak": tfs / MFMA_F32_PEAK_TFS}
     return {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
@@ -390,7 +391,11 @@ def main_c3(args):
         G = eng.walk_matrix_dense(Wt, C.LAP_NUMPY, nnz_w=nnz_w)
         # fused Philox walks -> Phi rows with the dense sampler's divide-by-m rule, written straight into
         # the dense fp32 Phi the Gram reads (no compaction, no memset: grf_densify_padded)
-        return eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False))
+        return eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False),
+                                  planes=use_planes)
+
+    # the split Gram's planes written by the front itself (grf_densify_padded_planes) where the planes path runs
+    use_planes = (args.gram_precision or eng.dense_precision) == "split" and eng.use_planes(n)
 
     def front_on_side():
         # independent of `main`: a front reads only the resident adjacency and writes fresh buffers
@@ -575,6 +580,9 @@ def main():
     ap.add_argument("--path", choices=["dense", "sparse"], default="dense",
                     help="c2: the reference's dense path (dense adjacency, MFMA Gram; default) or its sparse path "
                          "as BASELINE config 2 names it (CSR adjacency, fused walks, transpose, symmetric sparse Gram)")
+    ap.add_argument("--serial-steps", type=int, default=3,
+                    help="un-pipelined steps timed after the throughput steps (serial_ms_per_step, the walk kernel "
+                         "alone); 0 skips them (the all-reduce mode at the headline size under gloo: minutes per step)")
     ap.add_argument("--rank-turns", action="store_true",
                     help="N > 1: after the timed steps, re-run each rank's K assembly alone (ranks take turns between "
                          "barriers) and report gram_ms_alone_per_rank (the per-rank time of an unshared GPU when the "
@@ -653,10 +661,10 @@ def main():
         # one GPU, whole K: the next front beside the mirror; N > 1 row / column blocks: the next
         # front's collectives beside this step's Gram (the compute of a front beside a Gram gains
         # ~1 %: single-GPU row modes stay serial)
-        # K-row-block workloads (C5) on one GPU: the next front beside this step's column-block Gram
-        # (22.3 vs 22.9 ms per step, profiles/r02_c5_overlap.txt)
-        args.overlap = pl.mode == "sym" or (coll and pl.mode != "allreduce") or \
-            (pl.mode == "cols" and bool(args.k_rows))
+        # K-row-block workloads (C5) on one GPU: serial -- the column-block Gram is a persistent kernel
+        # holding every CU's LDS, so a front issued beside it only waits (16.68 vs 16.20 ms per step,
+        # profiles/r06_bench_c5.json; with the tile-per-workgroup Gram it gained 0.6 ms, r02_c5_overlap.txt)
+        args.overlap = pl.mode == "sym" or (coll and pl.mode != "allreduce")
     gram_ev = []  # (start, end) events around the K assembly of every timed step, read after the loop
     walk_ev = []  # (start, end) events around walk_phi in the serial-latency steps (kernel alone)
     last = [None]
@@ -765,6 +773,7 @@ def main():
     if coll:
         dist.barrier()
         D.GATHER_STATS = []  # HIP events around every Phi all-gather of the timed steps
+        D.ALLREDUCE_STATS = [] if pl.mode == "allreduce" else None  # ... and every bucketed K all-reduce
     t0 = time.perf_counter()
     run(args.steps, True)
     torch.cuda.synchronize()
@@ -773,6 +782,8 @@ def main():
     t = time.perf_counter() - t0
     gather_stats = D.GATHER_STATS or []
     D.GATHER_STATS = None
+    allreduce_stats = D.ALLREDUCE_STATS or []
+    D.ALLREDUCE_STATS = None
     if coll:
         from grf_amd.dist import check_gather_overflow
         check_gather_overflow(dev)  # (raises if a bounded all-gather truncated a rank's Phi)
@@ -782,16 +793,18 @@ def main():
     # latency of one un-pipelined step (reported beside the throughput; not part of `value`), with
     # the walk kernel timed alone there
     ov = args.overlap
-    args.overlap = False
-    run(1, False)  # (warm-up of the serial order)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    run(3, False, record_walk=True)
-    torch.cuda.synchronize()
-    serial_ms = 1000.0 * (time.perf_counter() - t1) / 3
-    args.overlap = ov
+    serial_ms = None
+    if args.serial_steps > 0:
+        args.overlap = False
+        run(1, False)  # (warm-up of the serial order)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        run(args.serial_steps, False, record_walk=True)
+        torch.cuda.synchronize()
+        serial_ms = 1000.0 * (time.perf_counter() - t1) / args.serial_steps
+        args.overlap = ov
     gram_ms = [a.elapsed_time(b_) for a, b_ in gram_ev]
-    walk_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in walk_ev]))
+    walk_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in walk_ev])) if walk_ev else 0.0
     gram_alone = rank_turns_gram_ms(eng, last[0], pl, K, coll, rank, world) if args.rank_turns else None
     if args.fingerprint_dir:
         # bit-level fingerprint of this rank's K block (tools/gram_hash.py), for the at-size multi-rank test
@@ -808,13 +821,15 @@ def main():
     coll_ms = float(np.mean([a.elapsed_time(b_) for a, b_, _, _ in gather_stats])) if gather_stats else 0.0
     coll_sent = float(np.mean([x for _, _, x, _ in gather_stats])) if gather_stats else 0.0
     coll_recv = float(np.mean([x for _, _, _, x in gather_stats])) if gather_stats else 0.0
+    ar_ms = float(np.mean([a.elapsed_time(b_) for a, b_, _ in allreduce_stats])) if allreduce_stats else 0.0
+    ar_bytes = float(np.mean([x for _, _, x in allreduce_stats])) if allreduce_stats else 0.0
     if coll:
         tt = torch.tensor([t, float(np.mean(gram_ms)), walk_ms], dtype=torch.float64, device=dev)
         dist_all_reduce(tt, op=dist.ReduceOp.MAX)
         t, gram_avg, walk_ms = (float(x) for x in tt.tolist())
         # every rank's Gram time, collective time and volume, and parity ratio (rank order)
         mine = torch.tensor([float(np.mean(gram_ms)), coll_ms, coll_sent, coll_recv, parity["max_ratio"],
-                             float(pl.e - pl.b), gram_alone or 0.0], dtype=torch.float64, device=dev)
+                             float(pl.e - pl.b), gram_alone or 0.0, ar_ms, ar_bytes], dtype=torch.float64, device=dev)
         allr = torch.zeros(world * mine.numel(), dtype=torch.float64, device=dev)
         allr[rank * mine.numel():(rank + 1) * mine.numel()] = mine
         dist_all_reduce(allr)
@@ -830,6 +845,11 @@ def main():
                      "gather_bytes_received_per_rank": [int(x) for x in per_rank[:, 3]],
                      "gather_note": "HIP events on the issuing stream around each step's Phi all-gather "
                                     "(the transfer + the wait for the slowest rank), mean over the timed steps"}
+        if pl.mode == "allreduce":
+            dist_info["allreduce_ms_per_rank"] = [float(x) for x in per_rank[:, 7]]
+            dist_info["allreduce_bytes_per_rank"] = [int(x) for x in per_rank[:, 8]]
+            dist_info["allreduce_note"] = ("HIP events on the issuing stream around each timed step's bucketed K "
+                                           "all-reduce (1 GiB buckets; under gloo staged through host memory)")
         if args.rank_turns:
             dist_info["gram_ms_alone_per_rank"] = [float(x) for x in per_rank[:, 6]]
             dist_info["gram_alone_note"] = ("each rank's K assembly (its column / row block from the last front) "
@@ -864,7 +884,7 @@ def main():
     walks = float(e - b) * m
     moves = walks * (1.0 - p) * (1.0 - (1.0 - p) ** (L - 1)) / p
     walk_alg = 16.0 * moves + 8.0 * local_nnz
-    walk_achieved = walk_alg / (walk_ms * 1e-3) / 1e9
+    walk_achieved = walk_alg / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else 0.0
     walk_traffic = pmc_traffic(["grf::phi_fused_kernel"], pmc_path) if pmc_path else None
     # the walk's VALU issue rate from ONE rocprofv3 --pmc pass (SQ_INSTS_VALU and GRBM_GUI_ACTIVE counted
     # together, tools/pmc_passes.sh "sq"): wave-instructions per SIMD-cycle, the cycles of the dispatch being
@@ -1178,14 +1198,17 @@ def mfma_leg(eng, args, steps: int = 20, workload: str = "c3"):
     dense = eng.densify_padded(eng.walk_phi(G, m, p, L, f, seed=42, norm=C.NORM_DIV, want64=False))
     del G, W
     flops = 1.0 * n * (n + 1) * n
+    # the split path's operand as the bench's front leaves it: the bf16 planes where the planes path runs
+    planes = eng.split_planes(dense, n) if eng.use_planes(n) else None
 
     def time_gram(prec):
+        op = planes if prec == "split" and planes is not None else dense
         for _ in range(3):
-            eng.gram_dense(dense, n, precision=prec)
+            eng.gram_dense(op, n, precision=prec)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         for _ in range(steps):
-            eng.gram_dense(dense, n, precision=prec)
+            eng.gram_dense(op, n, precision=prec)
         ev[1].record()
         ev[1].synchronize()
         return ev[0].elapsed_time(ev[1]) / steps

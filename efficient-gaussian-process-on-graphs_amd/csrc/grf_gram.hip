@@ -871,6 +871,12 @@ int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, 
                          void *workspace, size_t workspace_bytes, bool upper_only, grf_stream_t stream);
 int32_t dense_gram(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk, void *workspace,
                    size_t workspace_bytes, bool upper_only, grf_stream_t stream);
+int64_t planes_row_bytes(int64_t k_dim);
+int32_t split_planes(int64_t n, int64_t k_dim, const float *A, int64_t lda, void *P, int64_t ldp, grf_stream_t stream);
+int32_t densify_padded_planes(int64_t n_rows, int64_t cap, int64_t n_cols, const int32_t *cnt, const int32_t *idx,
+                              const float *val, void *P, int64_t ldp, grf_stream_t stream);
+int32_t dense_gram_planes(int64_t n, int64_t k_dim, const void *P, int64_t ldp, float *K, int64_t ldk,
+                          void *workspace, size_t workspace_bytes, grf_stream_t stream);
 
 }  // namespace grf
 
@@ -1295,6 +1301,23 @@ int32_t grf_gram_dense_split(int64_t n, int64_t k_dim, const float *A, int64_t l
 int32_t grf_gram_dense_split_upper(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                                    grf_stream_t stream) {
     return grf::dense_gram_split(n, k_dim, A, lda, K, ldk, nullptr, 0, true, stream);
+}
+
+int64_t grf_planes_row_bytes(int64_t k_dim) { return grf::planes_row_bytes(k_dim); }
+
+int32_t grf_split_planes(int64_t n, int64_t k_dim, const float *A, int64_t lda, void *P, int64_t ldp,
+                         grf_stream_t stream) {
+    return grf::split_planes(n, k_dim, A, lda, P, ldp, stream);
+}
+
+int32_t grf_densify_padded_planes(int64_t n_rows, int64_t cap, int64_t n_cols, const int32_t *cnt, const int32_t *idx,
+                                  const float *val, void *P, int64_t ldp, grf_stream_t stream) {
+    return grf::densify_padded_planes(n_rows, cap, n_cols, cnt, idx, val, P, ldp, stream);
+}
+
+int32_t grf_gram_dense_planes(int64_t n, int64_t k_dim, const void *P, int64_t ldp, float *K, int64_t ldk,
+                              void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    return grf::dense_gram_planes(n, k_dim, P, ldp, K, ldk, workspace, workspace_bytes, stream);
 }
 
 int32_t grf_densify_padded(int64_t n_rows, int64_t cap, int64_t n_cols, const int32_t *cnt, const int32_t *idx,

@@ -892,6 +892,235 @@ __global__ __launch_bounds__(512, 1) void gram_split_wide_kernel(DenseArgs a) {
     }
 }
 
+// ------------------------------------------------------------ the planes split once, by the producer
+// The wide split kernel above splits every staged k-tile again in registers (184 VALU per wave and k-tile,
+// ~2 ceil(n / 128) times per element).  Here A's three bf16 planes are written once (grf_split_planes, or the
+// dense front's grf_densify_padded_planes) and staged as they are: the k-loop issues fragment reads and MFMAs
+// only.  The planes are the in-register split's (the same cvt_pk / remainder sequence per element) and the
+// MFMAs run in the same order per block, so K is bit-identical to gram_split_wide_kernel's.
+// Plane layout P: row r, k-tile t (16 k) is 96 B at r ldp + 96 t: plane 0 of k = 16 t .. 16 t + 15 (bf16, k
+// order), then plane 1, then plane 2 -- six 16-B chunks c = 2 p + h (h: the k half a lane's MFMA operand takes).
+constexpr int kPlaneBytes = 96;  // one row's k-tile (3 planes x 16 bf16)
+
+__device__ __forceinline__ void split_chunk(f32x4v lo, f32x4v hi, u32x4 &p0, u32x4 &p1, u32x4 &p2) {
+    plane0(lo, hi, p0);
+    next_plane2<0>(lo, hi, p0, p1);
+    next_plane2<2>(lo, hi, p0, p1);
+    next_plane2<0>(lo, hi, p1, p2);
+    next_plane2<2>(lo, hi, p1, p2);
+}
+
+// one thread per (row, k-tile, half): 8 floats -> three 16-B plane chunks
+__global__ __launch_bounds__(256) void split_planes_kernel(int64_t n, int64_t kt, const float *__restrict__ A,
+                                                           int64_t lda, unsigned char *__restrict__ P, int64_t ldp) {
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (u >= n * kt * 2) return;
+    const int64_t r = u / (kt * 2), rem = u - r * kt * 2, t = rem >> 1, h = rem & 1;
+    const f32x4v *src = reinterpret_cast<const f32x4v *>(A + r * lda + 16 * t + 8 * h);
+    u32x4 p0, p1, p2;
+    split_chunk(src[0], src[1], p0, p1, p2);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(P + r * ldp + kPlaneBytes * t + 16 * h);
+    dst[0] = p0;
+    dst[2] = p1;
+    dst[4] = p2;
+}
+
+// the dense front's producer: the walk's padded rows straight to the planes (densify_padded_kernel's LDS
+// row, then the split of every 8-float chunk)
+__global__ __launch_bounds__(256) void densify_padded_planes_kernel(int64_t cap, const int32_t *__restrict__ cnt,
+                                                                    const int32_t *__restrict__ idx,
+                                                                    const float *__restrict__ val, int64_t kt,
+                                                                    unsigned char *__restrict__ P, int64_t ldp) {
+    extern __shared__ __attribute__((aligned(16))) float prow[];  // [16 kt]
+    const int64_t r = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int q4 = (int)(4 * kt);
+    for (int t = tid; t < q4; t += 256) reinterpret_cast<float4 *>(prow)[t] = float4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    const int64_t b = r * cap;
+    const int c = cnt[r];
+    for (int e = tid; e < c; e += 256) prow[idx[b + e]] = val[b + e];
+    __syncthreads();
+    for (int u = tid; u < (int)(2 * kt); u += 256) {
+        const f32x4v *src = reinterpret_cast<const f32x4v *>(prow + 8 * u);
+        u32x4 p0, p1, p2;
+        split_chunk(src[0], src[1], p0, p1, p2);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(P + r * ldp + kPlaneBytes * (u >> 1) + 16 * (u & 1));
+        dst[0] = p0;
+        dst[2] = p1;
+        dst[4] = p2;
+    }
+}
+
+// The wide items (256 x 128, 8 waves, stream-K) on the planes.  A stage is 256 + 128 rows of 96 B (36 KiB; 4
+// stages = 144 KiB, one workgroup per CU as the fp32-staged wide kernel): 36 1-KiB DMA pieces, piece P of wave w
+// for P = w + 8 i (i < 5; the four waves past piece 35 re-issue their first, the same bytes to the same place,
+// so every wave's in-flight count is 5 per k-tile).  LDS row image: row R's chunk c at R 96 + 16 (c ^ ((R >> 3)
+// & 1)) -- rows 8 apart differ in 96 B = 24 banks, so the swap of the halves of every 8th row's planes makes the
+// 16 rows of a ds_read_b128 phase hit 16 distinct 4-bank groups.
+struct PlaneStage {
+    static constexpr int RA = 2 * kTile, RB = kTile;
+    static constexpr int BA = RA * kPlaneBytes, BB = RB * kPlaneBytes, B = BA + BB;  // bytes
+    static constexpr int NP = B / 1024, G = (NP + 7) / 8;  // pieces per stage, per wave
+};
+static_assert(PlaneStage::B % 1024 == 0, "whole pieces");
+__device__ __forceinline__ uint32_t plane_lds_off(int row, int c) { return (uint32_t)(row * kPlaneBytes + 16 * (c ^ ((row >> 3) & 1))); }
+
+__device__ __forceinline__ void dma16b(const unsigned char *src, unsigned char *lds_piece) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)lds_piece, 16, 0, 0);
+}
+
+// one k-tile of a wave's 2 x 2 blocks from staged planes: a[x][p] / b[y][q] read from LDS, the six products
+// per block in split_ktile's order (c0: a0 b0; c1: (0,1) (1,0) (0,2) (1,1) (2,0)), the DMA pieces between
+// (a lane's chunk of block x, plane p sits at base + 32 rows x 96 B x + 32 p: rows 32 apart keep the swap bit,
+// ((row >> 3) & 1) = ((lane >> 3) & 1), so one base per operand and immediate offsets address all six)
+template <typename Issue>
+__device__ __forceinline__ void planes_ktile(const unsigned char *As, const unsigned char *Bs, uint32_t abase,
+                                             uint32_t bbase, f32x16 (&c0)[2][2], f32x16 (&c1)[2][2], Issue issue) {
+    u32x4 a[2][3], b[2][3];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            a[x][p] = *reinterpret_cast<const u32x4 *>(As + abase + 32 * kPlaneBytes * x + 32 * p);
+            b[x][p] = *reinterpret_cast<const u32x4 *>(Bs + bbase + 32 * kPlaneBytes * x + 32 * p);
+        }
+    auto mf = [&](int x, int y, int s) {
+        if (s == 0) {
+            c0[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][0]),
+                                                             __builtin_bit_cast(bf16x8, b[y][0]), c0[x][y], 0, 0, 0);
+            return;
+        }
+        constexpr int PQ[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
+        c1[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[x][PQ[s][0]]),
+                                                         __builtin_bit_cast(bf16x8, b[y][PQ[s][1]]), c1[x][y], 0, 0, 0);
+    };
+    auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+    mf(0, 0, 0); mf(0, 1, 0); mf(1, 0, 0); mf(1, 1, 0); fence();
+    mf(0, 0, 1); issue(0); fence();
+    mf(0, 0, 2); mf(0, 1, 1); fence();
+    mf(0, 1, 2); issue(1); fence();
+    mf(1, 0, 1); mf(1, 0, 2); fence();
+    mf(1, 1, 1); issue(2); fence();
+    mf(1, 1, 2); mf(0, 0, 3); fence();
+    mf(0, 0, 4); issue(3); fence();
+    mf(0, 0, 5); mf(0, 1, 3); fence();
+    mf(0, 1, 4); issue(4); fence();
+    mf(0, 1, 5);
+    mf(1, 0, 3);
+    mf(1, 0, 4);
+    mf(1, 0, 5);
+    mf(1, 1, 3);
+    mf(1, 1, 4);
+    mf(1, 1, 5);
+}
+
+template <int NST, bool LIVE>
+__device__ __forceinline__ void kloop_planes(unsigned char *lds, const unsigned char *const *src, const uint32_t *dst,
+                                             int64_t kb, int64_t ke, uint32_t abase, uint32_t bbase,
+                                             f32x16 (&c0)[2][2], f32x16 (&c1)[2][2]) {
+    constexpr int G = PlaneStage::G;
+    const int64_t nk = (ke - kb) / 16;
+    auto issue_part = [&](int64_t t, int q) {
+        const int64_t kt0 = kb / 16 + (t < nk ? t : nk - 1);
+        dma16b(src[q] + kPlaneBytes * kt0, lds + (int)(t % NST) * PlaneStage::B + dst[q]);
+    };
+    if (nk <= 0) return;
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+#pragma unroll
+        for (int q = 0; q < G; ++q) issue_part(t, q);
+    for (int64_t t = 0; t < nk; ++t) {
+        wait_vm<(NST - 2) * G>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if constexpr (!LIVE) {
+#pragma unroll
+            for (int q = 0; q < G; ++q) issue_part(t + NST - 1, q);
+        } else {
+            const unsigned char *As = lds + (int)(t % NST) * PlaneStage::B;
+            planes_ktile(As, As + PlaneStage::BA, abase, bbase, c0, c1,
+                         [&](int q) { if (q < G) issue_part(t + NST - 1, q); });
+        }
+    }
+}
+
+template <int NST>
+__device__ __forceinline__ Quarter item_compute_planes(const DenseArgs &a, const unsigned char *P, int64_t ldp,
+                                                       unsigned char *lds, int64_t item, int64_t kb, int64_t ke,
+                                                       int wave, int lane, f32x16 (&c)[2][2]) {
+    const int wm = wave >> 1, wn = wave & 1;
+    int64_t p, j;
+    item_coords(item, a.nt, p, j);
+    const int64_t m0 = 2 * p * kTile, n0 = j * kTile;
+    const unsigned char *src[PlaneStage::G];
+    uint32_t dst[PlaneStage::G];
+#pragma unroll
+    for (int i = 0; i < PlaneStage::G; ++i) {
+        int Pc = wave + 8 * i;
+        if (Pc >= PlaneStage::NP) Pc = wave;  // (the re-issued first piece)
+        const uint32_t off = (uint32_t)Pc * 1024u + 16u * (uint32_t)lane;  // this lane's LDS bytes in the stage
+        const bool isA = off < (uint32_t)PlaneStage::BA;
+        const uint32_t o = isA ? off : off - PlaneStage::BA;
+        const int R = (int)(o / kPlaneBytes), jj = (int)((o % kPlaneBytes) / 16);
+        const int cc = jj ^ ((R >> 3) & 1);  // the global chunk that lands here
+        int64_t r = (isA ? m0 : n0) + R;
+        r = r < a.n ? r : a.n - 1;
+        src[i] = P + r * ldp + 16 * cc;
+        dst[i] = off;
+    }
+    const uint32_t abase = plane_lds_off(wm * 64 + (lane & 31), lane >> 5);
+    const uint32_t bbase = plane_lds_off(wn * 64 + (lane & 31), lane >> 5);
+    const int64_t R = m0 + wm * 64, Cc = n0 + wn * 64;
+    Quarter q{R, Cc, R == Cc, R > Cc};
+    const bool live = !q.below && R < a.n && Cc < a.n;
+    f32x16 c0[2][2], c1[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            c0[x][y] = f32x16{};
+            c1[x][y] = f32x16{};
+        }
+    if (live) kloop_planes<NST, true>(lds, src, dst, kb, ke, abase, bbase, c0, c1);
+    else kloop_planes<NST, false>(lds, src, dst, kb, ke, abase, bbase, c0, c1);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) c[x][y] = c0[x][y] + c1[x][y];
+    return q;
+}
+
+template <int NST>
+__global__ __launch_bounds__(512, 1) void gram_planes_wide_kernel(DenseArgs a, const unsigned char *P, int64_t ldp) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NST * PlaneStage::B];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t U = a.sk_units, KT = a.sk_kt;
+    const int64_t u0 = (int64_t)blockIdx.x * U;
+    const int64_t u1 = u0 + U < a.sk_total ? u0 + U : a.sk_total;
+    for (int64_t u = u0; u < u1;) {
+        const int64_t item = u / KT, tb = item * KT, te = tb + KT;
+        const int64_t se = u1 < te ? u1 : te;
+        __syncthreads();
+        f32x16 c[2][2];
+        const Quarter q = item_compute_planes<NST>(a, P, ldp, lds, item, (u - tb) * 16, (se - tb) * 16, wave, lane, c);
+        bool write = true;
+        if (u != tb || se != te) {
+            const int64_t s0 = tb / U, s1 = (te - 1) / U;
+            const int64_t first = 2 * s0 + (tb == s0 * U ? 0 : 1);
+            write = split_combine<32, 16, 8>(
+                a, c, a.tickets + first, s1 - s0 + 1, blockIdx.x - s0,
+                [&](int64_t j) { return j == 0 ? first : 2 * (s0 + j); }, reinterpret_cast<int32_t *>(lds), wave,
+                lane);
+        }
+        if (write && !q.below && q.qr < a.n && q.qc < a.n)
+            write_quarter<32, 16>(a, c, q.qr, q.qc, q.diag, false, lane);
+        u = se;
+    }
+}
+
 constexpr int kCUs = 256;
 
 int env_int(const char *name, int dflt) {
@@ -1138,6 +1367,79 @@ int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, 
     a.n_split = p.n_split;
     gram_split_mfma_kernel<<<(unsigned)items, 256, 0, st>>>(a);
     GRF_CHECK_LAUNCH("gram_split_mfma_kernel");
+    return GRF_OK;
+}
+
+// ---- the planes path
+int64_t planes_row_bytes(int64_t k_dim) { return cdiv<int64_t>(k_dim, 16) * kPlaneBytes; }
+
+int32_t split_planes(int64_t n, int64_t k_dim, const float *A, int64_t lda, void *P, int64_t ldp, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && k_dim >= 0 && (n == 0 || (A && P)), GRF_EINVAL, "grf_split_planes: bad arguments");
+    const int64_t kt = cdiv<int64_t>(k_dim, 16);
+    GRF_REQUIRE(lda >= 16 * kt && lda % 4 == 0 && ((uintptr_t)A & 15) == 0, GRF_EINVAL,
+                "grf_split_planes: lda must cover k_dim rounded up to 16 (zero-padded), A 16-byte aligned");
+    GRF_REQUIRE(ldp >= kt * kPlaneBytes && ldp % 16 == 0 && ((uintptr_t)P & 15) == 0, GRF_EINVAL,
+                "grf_split_planes: ldp must cover %lld bytes, a multiple of 16, P 16-byte aligned",
+                (long long)(kt * kPlaneBytes));
+    const int64_t work = n * kt * 2;
+    if (work == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(cdiv<int64_t>(work, 256), 256, "split_planes_kernel");
+    split_planes_kernel<<<(unsigned)cdiv<int64_t>(work, 256), 256, 0, S(stream)>>>(
+        n, kt, A, lda, reinterpret_cast<unsigned char *>(P), ldp);
+    GRF_CHECK_LAUNCH("split_planes_kernel");
+    return GRF_OK;
+}
+
+int32_t densify_padded_planes(int64_t n_rows, int64_t cap, int64_t n_cols, const int32_t *cnt, const int32_t *idx,
+                              const float *val, void *P, int64_t ldp, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && cap >= 1 && n_cols >= 0 && (n_rows == 0 || (cnt && idx && val && P)), GRF_EINVAL,
+                "grf_densify_padded_planes: bad arguments");
+    const int64_t kt = cdiv<int64_t>(n_cols, 16);
+    GRF_REQUIRE(ldp >= kt * kPlaneBytes && ldp % 16 == 0 && ((uintptr_t)P & 15) == 0, GRF_EINVAL,
+                "grf_densify_padded_planes: ldp must cover %lld bytes, a multiple of 16, P 16-byte aligned",
+                (long long)(kt * kPlaneBytes));
+    GRF_REQUIRE(16 * kt * (int64_t)sizeof(float) <= 160 * 1024, GRF_EUNSUPPORTED,
+                "grf_densify_padded_planes: a row of %lld floats does not fit one CU's LDS", (long long)(16 * kt));
+    if (n_rows == 0) return GRF_OK;
+    GRF_REQUIRE_GRID(n_rows, 256, "densify_padded_planes_kernel");
+    densify_padded_planes_kernel<<<(unsigned)n_rows, 256, (size_t)(16 * kt) * sizeof(float), S(stream)>>>(
+        cap, cnt, idx, val, kt, reinterpret_cast<unsigned char *>(P), ldp);
+    GRF_CHECK_LAUNCH("densify_padded_planes_kernel");
+    return GRF_OK;
+}
+
+// K from the planes on the wide items (stream-K at every size); workspace as dense_gram_split's
+int32_t dense_gram_planes(int64_t n, int64_t k_dim, const void *P, int64_t ldp, float *K, int64_t ldk,
+                          void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n >= 0 && k_dim >= 0 && K && ldk >= n && (n == 0 || P), GRF_EINVAL, "grf_gram_dense_planes: bad arguments");
+    GRF_REQUIRE(ldp >= planes_row_bytes(k_dim) && ldp % 16 == 0 && ((uintptr_t)P & 15) == 0, GRF_EINVAL,
+                "grf_gram_dense_planes: ldp must cover the k-tiles' planes, a multiple of 16, P 16-byte aligned");
+    GRF_REQUIRE(ldk % 4 == 0 && ((uintptr_t)K & 15) == 0, GRF_EINVAL,
+                "grf_gram_dense_planes: ldk must be a multiple of 4 and K 16-byte aligned");
+    if (n == 0 || k_dim == 0) {
+        if (n) GRF_CHECK_HIP(hipMemset2DAsync(K, (size_t)ldk * sizeof(float), 0, (size_t)n * sizeof(float), (size_t)n,
+                                              S(stream)));
+        return GRF_OK;
+    }
+    GRF_REQUIRE(workspace && ((uintptr_t)workspace & 255) == 0 &&
+                    workspace_bytes >= dense_gram_split_workspace_bytes(n, k_dim),
+                GRF_EINVAL, "grf_gram_dense_planes: workspace too small or not 256-byte aligned");
+    DenseArgs a{};
+    a.K = K;
+    a.n = n;
+    a.nt = cdiv<int64_t>(n, kTile);
+    a.ldk = ldk;
+    a.kpad = cdiv<int64_t>(k_dim, 16) * 16;
+    const SkPlan q = sk_plan_wide(n, k_dim);
+    GRF_REQUIRE_GRID(q.grid, 512, "gram_planes_wide_kernel");
+    a.tickets = reinterpret_cast<int32_t *>(workspace);
+    a.slabs = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes);
+    a.sk_units = q.units;
+    a.sk_kt = q.kt;
+    a.sk_total = q.total;
+    gram_planes_wide_kernel<kSplitNST><<<(unsigned)q.grid, 512, 0, S(stream)>>>(
+        a, reinterpret_cast<const unsigned char *>(P), ldp);
+    GRF_CHECK_LAUNCH("gram_planes_wide_kernel");
     return GRF_OK;
 }
 

@@ -120,6 +120,10 @@ SIGNATURES = {
     "grf_gram_dense_split_upper": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "grf_densify": (_i32, [_i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "grf_densify_padded": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "grf_planes_row_bytes": (_i64, [_i64]),
+    "grf_split_planes": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "grf_densify_padded_planes": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "grf_gram_dense_planes": (_i32, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
     # the GPyTorch surface's feature algebra (step_* are host arrays of device pointers)
     "grf_phi_steps_csr_count": (_i32, [_i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "grf_phi_steps_csr_fill": (_i32, [_i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),

@@ -357,6 +357,11 @@ def gather_phi(engine, local, count_ws=None, group=None, band_width=None, shards
     return DeviceCSR(n, n, ptr, idx, None, val32, int(idx.numel()))
 
 
+# (bench.py --mode allreduce): when a list, every bucketed K all-reduce appends (start event, end event, bytes
+# reduced by this rank) -- HIP events on the issuing stream around the whole bucket loop
+ALLREDUCE_STATS: Optional[list] = None
+
+
 def allreduce_buckets(t: torch.Tensor, bucket_bytes: int = 1 << 30, group=None) -> torch.Tensor:
     """In-place sum of a (possibly row-padded, row-strided) 2-D tensor over the ranks, one
     contiguous row bucket of at most ``bucket_bytes`` per collective (bounds RCCL's staging)."""
@@ -364,8 +369,16 @@ def allreduce_buckets(t: torch.Tensor, bucket_bytes: int = 1 << 30, group=None) 
         return t  # (one rank in an initialised group still runs the collectives: the RCCL rehearsal)
     rows_per = max(1, bucket_bytes // max(1, t.stride(0) * t.element_size()))
     base = t.as_strided((t.shape[0], t.stride(0)), (t.stride(0), 1)) if t.dim() == 2 else t.view(-1, 1)
+    start = None
+    if ALLREDUCE_STATS is not None and torch.cuda.is_available() and t.is_cuda:
+        start = torch.cuda.Event(enable_timing=True)
+        start.record()
     for r0 in range(0, base.shape[0], rows_per):
         all_reduce(base[r0:r0 + rows_per], group=group)
+    if start is not None:
+        end = torch.cuda.Event(enable_timing=True)
+        end.record()
+        ALLREDUCE_STATS.append((start, end, int(base.numel() * base.element_size())))
     return t
 
 

@@ -193,6 +193,21 @@ def choose_rec_unit(nnz: int, n_rows: int, n_cols: int, band_width: int) -> int:
     return C.REC_LINE if per_bucket >= 8.0 else C.REC_PACKED
 
 
+class DensePlanes:
+    """The dense Phi as the split Gram's three bf16 planes (include/grf.h grf_split_planes): ``P`` uint8
+    [n x row bytes] on the device, ``n`` rows, ``k_dim`` columns."""
+
+    def __init__(self, P: torch.Tensor, n: int, k_dim: int):
+        self.P, self.n, self.k_dim = P, int(n), int(k_dim)
+
+    @property
+    def shape(self):
+        return (self.n, self.k_dim)
+
+    def record_stream(self, stream):
+        self.P.record_stream(stream)
+
+
 class GRFEngine:
     """All device work for one GPU.  ``device`` is a torch device (``cuda:N``)."""
 
@@ -817,17 +832,44 @@ class GRFEngine:
                 "grf_densify")
         return out
 
-    def densify_padded(self, rows: PaddedRows) -> torch.Tensor:
+    def densify_padded(self, rows: PaddedRows, planes: bool = False):
         """The dense fp32 Phi (zero-padded lda, as ``densify``) straight from the walk's padded rows, no
-        compaction (grf_densify_padded); rows too wide for one CU's LDS take compact + densify."""
+        compaction (grf_densify_padded); rows too wide for one CU's LDS take compact + densify.
+        planes: the split Gram's three bf16 planes instead (``DensePlanes``, grf_densify_padded_planes), for
+        ``gram_dense``'s planes path."""
         n = rows.n_rows
         lda = max(64, -(-rows.n_cols // 64) * 64)
+        if planes and rows.val32 is not None and -(-rows.n_cols // 16) * 64 <= 160 * 1024:
+            ldp = int(self.lib.grf_planes_row_bytes(rows.n_cols))
+            P = torch.empty((n, ldp), dtype=torch.uint8, device=self.device)
+            C.check(self.lib.grf_densify_padded_planes(n, rows.cap, rows.n_cols, _p(rows.cnt), _p(rows.idx),
+                                                       _p(rows.val32), _p(P), ldp, self.stream),
+                    "grf_densify_padded_planes")
+            return DensePlanes(P, n, rows.n_cols)
         if rows.val32 is None or lda * 4 > 160 * 1024:
-            return self.densify(self.compact(rows, want64=False, sync_free=True))
+            out = self.densify(self.compact(rows, want64=False, sync_free=True))
+            return self.split_planes(out, rows.n_cols) if planes else out
         out = torch.empty((n, lda), dtype=torch.float32, device=self.device)
         C.check(self.lib.grf_densify_padded(n, rows.cap, rows.n_cols, _p(rows.cnt), _p(rows.idx), _p(rows.val32),
                                             _p(out), lda, self.stream), "grf_densify_padded")
-        return out
+        return self.split_planes(out, rows.n_cols) if planes else out
+
+    @staticmethod
+    def use_planes(n: int) -> bool:
+        """The split Gram on pre-split planes (grf_gram_dense_planes): opt-in, GRF_DENSE_PLANES=1 (read per call).
+        Measured slower than the split in registers: staging three bf16 planes moves 1.5x the fp32 bytes and the
+        Gram is bound by its staging, not by the split's VALU -- C2 Gram 4.64 -> 5.62 ms, C3 (wide items) 0.144 ->
+        0.156 ms (profiles/r06_dense_planes_ab.txt); the same K bits."""
+        return os.environ.get("GRF_DENSE_PLANES") == "1"
+
+    def split_planes(self, dense_phi: torch.Tensor, k_dim: int) -> "DensePlanes":
+        """The dense fp32 Phi's three bf16 planes, split once (grf_split_planes)."""
+        n = dense_phi.shape[0]
+        ldp = int(self.lib.grf_planes_row_bytes(k_dim))
+        P = torch.empty((n, ldp), dtype=torch.uint8, device=self.device)
+        C.check(self.lib.grf_split_planes(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(P), ldp, self.stream),
+                "grf_split_planes")
+        return DensePlanes(P, n, k_dim)
 
     def gram_dense(self, dense_phi: torch.Tensor, k_dim: int, precision: Optional[str] = None) -> torch.Tensor:
         """K = A A^T of the dense fp32 Phi on the MFMA.  precision 'fp32': the fp32 matrix instruction
@@ -838,6 +880,12 @@ class GRFEngine:
         if precision not in ("fp32", "split"):
             raise ValueError(f"unknown dense Gram precision {precision!r}")
         split = precision == "split"
+        planes = isinstance(dense_phi, DensePlanes)
+        if planes and not split:
+            raise ValueError("gram_dense: the bf16 planes take precision 'split'")
+        if split and not planes and self.use_planes(dense_phi.shape[0]):
+            dense_phi = self.split_planes(dense_phi, k_dim)  # (the split once, then the planes' k-loop)
+            planes = True
         n = dense_phi.shape[0]
         ldk = self.leading_dim(n)
         out = torch.empty((n, ldk), dtype=torch.float32, device=self.device)
@@ -855,8 +903,12 @@ class GRFEngine:
             ws = cache[stream.value] = torch.zeros(max(need, 16), dtype=torch.uint8, device=self.device)
         fn = self.lib.grf_gram_dense_split if split else self.lib.grf_gram_dense_ws
         try:
-            C.check(fn(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, _p(ws), ws.numel(), stream),
-                    "grf_gram_dense_split" if split else "grf_gram_dense_ws")
+            if planes:
+                C.check(self.lib.grf_gram_dense_planes(n, k_dim, _p(dense_phi.P), dense_phi.P.stride(0), _p(out), ldk,
+                                                       _p(ws), ws.numel(), stream), "grf_gram_dense_planes")
+            else:
+                C.check(fn(n, k_dim, _p(dense_phi), dense_phi.stride(0), _p(out), ldk, _p(ws), ws.numel(), stream),
+                        "grf_gram_dense_split" if split else "grf_gram_dense_ws")
         except Exception:
             cache.pop(stream.value, None)
             raise

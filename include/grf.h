@@ -440,6 +440,22 @@ int32_t grf_gram_dense_split(int64_t n, int64_t k_dim, const float *A, int64_t l
 /* grf_gram_dense_upper on the split products (ABI 6): the hub-column split's panel. */
 int32_t grf_gram_dense_split_upper(int64_t n, int64_t k_dim, const float *A, int64_t lda, float *K, int64_t ldk,
                                    grf_stream_t stream);
+/* The split's three bf16 planes written once (ABI 7): P row r holds, per k-tile t of 16, 96 bytes at
+ * r ldp + 96 t -- plane 0 of k = 16 t .. 16 t + 15 (bf16, k order), plane 1, plane 2 -- the planes
+ * grf_gram_dense_split forms in registers for every staged k-tile.  ldp >= grf_planes_row_bytes(k_dim)
+ * (= 96 ceil(k_dim / 16)), a multiple of 16.  grf_split_planes reads A (zero-padded to 16 ceil(k_dim / 16)
+ * columns, as grf_gram_dense_split requires); grf_densify_padded_planes writes them straight from the walk's
+ * padded rows (grf_densify_padded's arguments, n_cols = k_dim).  grf_gram_dense_planes: K = A A^T from them on
+ * the 256 x 128 wide workgroups with nothing but fragment reads and MFMAs in the k-loop -- bit-identical to
+ * grf_gram_dense_split's wide path (the same planes, the same products in the same order); workspace as
+ * grf_gram_dense_split's (grf_gram_dense_split_workspace_bytes, ZERO on first use). */
+int64_t grf_planes_row_bytes(int64_t k_dim);
+int32_t grf_split_planes(int64_t n, int64_t k_dim, const float *A, int64_t lda, void *P, int64_t ldp,
+                         grf_stream_t stream);
+int32_t grf_densify_padded_planes(int64_t n_rows, int64_t cap, int64_t n_cols, const int32_t *cnt, const int32_t *idx,
+                                  const float *val, void *P, int64_t ldp, grf_stream_t stream);
+int32_t grf_gram_dense_planes(int64_t n, int64_t k_dim, const void *P, int64_t ldp, float *K, int64_t ldk,
+                              void *workspace, size_t workspace_bytes, grf_stream_t stream);
 
 /* CSR (float32) -> dense float32 [n_rows x lda], zero filled. */
 int32_t grf_densify(int64_t n_rows, const int64_t *ptr, const int32_t *idx, const float *val, float *out,

@@ -1610,6 +1610,48 @@ def test_bench_c5_cols_at_size_gloo(eng, world, k_rows):
         assert abs(fp["sum"] - sm) <= 1e-12 * abs(sm), (q, fp["sum"], sm)
 
 
+@pytest.mark.timeout(1500)
+def test_bench_allreduce_at_headline_size_gloo():
+    """the north star's literal multi-GPU option -- per-rank partial K over an inner slice
+    of Phi's columns, summed by a bucketed all-reduce on the final kernel matrix -- once at the headline size
+    (C4: N = 100k, 1M edges, m = 128): two gloo ranks on the one GPU, each holding the whole 40 GB K, one timed
+    step, no serial steps (host-staged all-reduces of 40 GB take minutes).  The in-run check holds every
+    rank's K to the K tolerance of Phi Phi^T (K 1 and K v over all 10^10 entries against the gathered Phi) --
+    not bit-identity: fp32 partials are added in the collective's order.  The line reports every rank's
+    all-reduce time and bytes.  GRF_TEST_OUT=<dir> keeps it (profiles/r06_bench_allreduce_gloo_n2.json)."""
+    import json
+    import os
+    import socket
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, GRF_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--mode", "allreduce", "--steps", "1", "--warmup", "1", "--serial-steps", "0",
+           "--no-cpu-baseline"]
+    r = _run_beating(cmd, root, env, 1400, "allreduce_gloo_n2")
+    out_dir = os.environ.get("GRF_TEST_OUT")
+    if r.returncode != 0 and out_dir:
+        with open(os.path.join(out_dir, "allreduce_gloo_n2.failed.log"), "w") as fh:
+            fh.write(r.stdout + "\n----- stderr -----\n" + r.stderr)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        with open(os.path.join(out_dir, "r06_bench_allreduce_gloo_n2.json"), "w") as fh:
+            fh.write(json.dumps(line) + "\n")
+    d = line["distributed"]
+    assert line["n_gpus"] == 2 and d["backend"] == "gloo" and d["world_size"] == 2
+    assert line["config"]["n_nodes"] == 100_000 and line["config"]["walks_per_node"] == 128
+    assert line["parity"]["ok"] and len(line["parity"]["per_rank"]) == 2, line["parity"]
+    assert all(x > 0 for x in d["allreduce_ms_per_rank"])
+    assert all(x >= 100_000 * 100_000 * 4 for x in d["allreduce_bytes_per_rank"])
+
+
 @pytest.mark.parametrize("mode", ["cols", "rows", "allreduce"])
 def test_bench_multi_gpu_path_on_rccl_one_rank(mode):
     """The N > 1 bench step on RCCL itself (backend "nccl"), one rank on the one-GPU box
@@ -1688,3 +1730,42 @@ def test_compaction_row_stats_give_same_shifts(eng):
     assert torch.equal(a.ptr, b.ptr) and torch.equal(a.idx[:nnz], b.idx[:nnz])
     assert torch.equal(a.val32[:nnz], b.val32[:nnz])
     assert torch.equal(eng.phi_row_shifts(a), eng.phi_row_shifts(b))
+
+
+@pytest.mark.parametrize("n,k", [(1000, 1000), (3001, 2708), (8193, 777), (300, 17)])
+def test_gram_dense_planes_bit_identical(eng, n, k):
+    """The split Gram on planes written once (grf_split_planes / grf_densify_padded_planes +
+    grf_gram_dense_planes) gives the in-register split's wide path (GRF_DENSE_WIDE=1) the same K bits: the same
+    planes, the same six products per block in the same order; odd n, k not a multiple of 16, a single tile
+    row.  The fused producer's planes equal the separate split's, byte for byte."""
+    import os
+
+    import torch
+    g = torch.Generator(device="cpu").manual_seed(n + k)
+    A = torch.zeros((n, max(64, -(-k // 64) * 64)), dtype=torch.float32)
+    vals = torch.randn((n, k), generator=g) * torch.rand((n, k), generator=g).pow(3)
+    A[:, :k] = torch.where(torch.rand((n, k), generator=g) < 0.3, vals, torch.zeros_like(vals))
+    A = A.to(eng.device)
+    old = {v: os.environ.get(v) for v in ("GRF_DENSE_WIDE", "GRF_DENSE_PLANES")}
+    try:
+        os.environ["GRF_DENSE_WIDE"] = "1"
+        os.environ["GRF_DENSE_PLANES"] = "0"
+        Kw = eng.gram_dense(A, k, precision="split").clone()
+        P = eng.split_planes(A, k)
+        Kp = eng.gram_dense(P, k, precision="split")
+        assert torch.equal(Kw, Kp), float((Kw - Kp).abs().max())
+        os.environ["GRF_DENSE_PLANES"] = "1"
+        assert torch.equal(eng.gram_dense(A, k, precision="split"), Kw)  # (split inside gram_dense)
+    finally:
+        for v, x in old.items():
+            if x is None:
+                os.environ.pop(v, None)
+            else:
+                os.environ[v] = x
+    # the fused producer: padded walk rows straight to the planes
+    Ad = er_graph(n, 6, 5)
+    G = eng.laplacian(Ad)
+    rows = eng.walk_phi(G, 16, 0.2, 4, [1.0, -0.5, 0.25, -0.125], seed=3, want64=False)
+    Pf = eng.densify_padded(rows, planes=True)
+    Ps = eng.split_planes(eng.densify_padded(rows), n)
+    assert torch.equal(Pf.P, Ps.P)
