@@ -36,9 +36,9 @@ from grf_amd.graphs import er_graph_exact_edges, powerlaw_graph, snap_graph  # n
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh -> tools/pmc_summary.py), committed
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_pmc_summary.json")
 # ... and of the C5 workload (bench.py --workload c5; tools/gpu_steps.sh pmc step)
-PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "r05_c5_pmc_summary.json")
+PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "r06_c5_pmc_summary.json")
 DEFAULT_WORKLOAD = (100_000, 1_000_000, 128, 8, 0.1)
 
 
