@@ -328,8 +328,8 @@ def dense_gram_roofline(precision: str, flops: float, ms: float) -> dict:
                 "frac": SPLIT_PRODUCTS * tfs / MFMA_BF16_PEAK_TFS, "traffic": None,
                 "kernel": "gram_split_mfma_kernel (128x128 tiles, fp32 LDS-DMA staging, the exact three-plane bf16 "
                           "split in registers; n <= 8064) / gram_planes_wide_kernel (256x128 items of 8 waves, "
-                          "stream-K, the planes split once by the front and staged as they are) -- "
-                          "v_mfma_f32_32x32x16_bf16, 6 products per term",
+                          "XCD-ordered whole-item rounds + stream-K, the planes split once by the front and staged "
+                          "as they are) -- v_mfma_f32_32x32x16_bf16, 6 products per term",
                 "kernel_ms": ms, "algorithmic_flops": flops, "bf16_flops": SPLIT_PRODUCTS * flops,
                 "fp32_equivalent_tflops": tfs, "fp32_equivalent_vs_fp32_peak": tfs / MFMA_F32_PEAK_TFS}
     return {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",

@@ -655,6 +655,12 @@ __global__ __launch_bounds__(64 * kWv) void gram_slot_pipe_kernel(
                 run_batch(gs, J, k, a, d);
             }
         }
+        // Every load of this tile and the prefetches issued at its start is complete here in practice (the
+        // gathers' last window waited for them: vmcnt is in order), but the wait-count pass cannot see it through
+        // the data-dependent batch loops, so it would guard the next tile's uses of the prefetched registers with a
+        // vmcnt(0) behind this tile's K stores -- a store round trip per tile before the next one's loads issue.
+        // Said explicitly here, before the stores, the stores stay in flight into the next tile.
+        __builtin_amdgcn_s_waitcnt(0);
         pipe_barrier();
         // tile i out (non-temporal) and its accumulator zeroed
         const int64_t r = row - row_begin, j0 = J * W;

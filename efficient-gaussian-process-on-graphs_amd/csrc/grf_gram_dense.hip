@@ -63,6 +63,8 @@ struct DenseArgs {
     int32_t n_split;   // pieces per split tile (the tiles from n_whole on)
     int32_t upper_only;  // write only K[row][col] of the computed tiles (the hub panel's seed)
     int64_t sk_units, sk_kt, sk_total;  // stream-K: k-tile units per slot, per tile, in all
+    int64_t dp_rounds;  // wide kernels: rounds of whole items before the stream-K units [dp_rounds grid kt, total)
+    int32_t xcd_slots;  // wide kernels: number the slots XCD-contiguously (grid a multiple of 8)
 };
 
 // Fragment layout of one wave's 64 x 64 quarter.
@@ -862,34 +864,58 @@ __device__ __forceinline__ Quarter item_compute_wide(const DenseArgs &a, float *
     return q;
 }
 
-// stream-K over the items laid end to end (units of one k-tile), as gram_split_sk_kernel over the tiles
-template <int NST>
-__global__ __launch_bounds__(512, 1) void gram_split_wide_kernel(DenseArgs a) {
-    __shared__ __attribute__((aligned(16))) float lds[NST * WideStage::F];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int64_t U = a.sk_units, KT = a.sk_kt;
-    const int64_t u0 = (int64_t)blockIdx.x * U;
+// The wide kernels' schedule.  Slot s of the grid G (one workgroup per CU) takes whole items in rounds -- round r's
+// item r G + s -- then an equal share of the k-tile units of the items left, stream-K (split items summed in piece
+// order by the last piece, as gram_split_sk_kernel over the tiles).  With xcd_slots the slots are numbered
+// XCD-contiguously: workgroups are dealt round-robin over the 8 XCDs, so slot = (b mod 8) (G / 8) + b / 8 gives
+// the 32 CUs of one XCD 32 consecutive items of a round -- mostly one row pair against consecutive column blocks --
+// which start together and run the same k-loop, so each k-tile of the shared A rows comes from HBM once per XCD and
+// hits that XCD's L2 for the other CUs (the items of a round also share their B column blocks across XCDs, in the
+// Infinity Cache).  item(it, kb, ke, c) computes k range [kb, ke) of item `it` into c and returns its Quarter.
+template <class ItemFn>
+__device__ __forceinline__ void wide_schedule(const DenseArgs &a, int32_t *lds_scratch, int wave, int lane,
+                                              ItemFn &&item_fn) {
+    const int64_t G = gridDim.x, b = blockIdx.x;
+    const int64_t slot = a.xcd_slots ? (b & 7) * (G >> 3) + (b >> 3) : b;
+    const int64_t KT = a.sk_kt;
+    for (int64_t r = 0; r < a.dp_rounds; ++r) {
+        __syncthreads();
+        f32x16 c[2][2];
+        const Quarter q = item_fn(r * G + slot, (int64_t)0, KT * 16, c);
+        if (!q.below && q.qr < a.n && q.qc < a.n) write_quarter<32, 16>(a, c, q.qr, q.qc, q.diag, false, lane);
+    }
+    const int64_t U = a.sk_units, base = a.dp_rounds * G * KT;
+    const int64_t u0 = base + slot * U;
     const int64_t u1 = u0 + U < a.sk_total ? u0 + U : a.sk_total;
     for (int64_t u = u0; u < u1;) {
         const int64_t item = u / KT, tb = item * KT, te = tb + KT;
         const int64_t se = u1 < te ? u1 : te;
         __syncthreads();
         f32x16 c[2][2];
-        const Quarter q = item_compute_wide<NST>(a, lds, item, (u - tb) * 16, (se - tb) * 16, wave, lane, c);
+        const Quarter q = item_fn(item, (u - tb) * 16, (se - tb) * 16, c);
         bool write = true;
         if (u != tb || se != te) {
-            const int64_t s0 = tb / U, s1 = (te - 1) / U;
-            const int64_t first = 2 * s0 + (tb == s0 * U ? 0 : 1);
+            const int64_t s0 = (tb - base) / U, s1 = (te - 1 - base) / U;
+            const int64_t first = 2 * s0 + (tb - base == s0 * U ? 0 : 1);
             write = split_combine<32, 16, 8>(
-                a, c, a.tickets + first, s1 - s0 + 1, blockIdx.x - s0,
-                [&](int64_t j) { return j == 0 ? first : 2 * (s0 + j); }, reinterpret_cast<int32_t *>(lds), wave,
-                lane);
+                a, c, a.tickets + first, s1 - s0 + 1, slot - s0,
+                [&](int64_t j) { return j == 0 ? first : 2 * (s0 + j); }, lds_scratch, wave, lane);
         }
         if (write && !q.below && q.qr < a.n && q.qc < a.n)
             write_quarter<32, 16>(a, c, q.qr, q.qc, q.diag, false, lane);
         u = se;
     }
+}
+
+template <int NST>
+__global__ __launch_bounds__(512, 1) void gram_split_wide_kernel(DenseArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[NST * WideStage::F];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    wide_schedule(a, reinterpret_cast<int32_t *>(lds), wave, lane,
+                  [&](int64_t item, int64_t kb, int64_t ke, f32x16 (&c)[2][2]) {
+                      return item_compute_wide<NST>(a, lds, item, kb, ke, wave, lane, c);
+                  });
 }
 
 // ------------------------------------------------------------ the planes split once, by the producer
@@ -1097,28 +1123,10 @@ __global__ __launch_bounds__(512, 1) void gram_planes_wide_kernel(DenseArgs a, c
     __shared__ __attribute__((aligned(16))) unsigned char lds[NST * PlaneStage::B];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int64_t U = a.sk_units, KT = a.sk_kt;
-    const int64_t u0 = (int64_t)blockIdx.x * U;
-    const int64_t u1 = u0 + U < a.sk_total ? u0 + U : a.sk_total;
-    for (int64_t u = u0; u < u1;) {
-        const int64_t item = u / KT, tb = item * KT, te = tb + KT;
-        const int64_t se = u1 < te ? u1 : te;
-        __syncthreads();
-        f32x16 c[2][2];
-        const Quarter q = item_compute_planes<NST>(a, P, ldp, lds, item, (u - tb) * 16, (se - tb) * 16, wave, lane, c);
-        bool write = true;
-        if (u != tb || se != te) {
-            const int64_t s0 = tb / U, s1 = (te - 1) / U;
-            const int64_t first = 2 * s0 + (tb == s0 * U ? 0 : 1);
-            write = split_combine<32, 16, 8>(
-                a, c, a.tickets + first, s1 - s0 + 1, blockIdx.x - s0,
-                [&](int64_t j) { return j == 0 ? first : 2 * (s0 + j); }, reinterpret_cast<int32_t *>(lds), wave,
-                lane);
-        }
-        if (write && !q.below && q.qr < a.n && q.qc < a.n)
-            write_quarter<32, 16>(a, c, q.qr, q.qc, q.diag, false, lane);
-        u = se;
-    }
+    wide_schedule(a, reinterpret_cast<int32_t *>(lds), wave, lane,
+                  [&](int64_t item, int64_t kb, int64_t ke, f32x16 (&c)[2][2]) {
+                      return item_compute_planes<NST>(a, P, ldp, lds, item, kb, ke, wave, lane, c);
+                  });
 }
 
 constexpr int kCUs = 256;
@@ -1184,6 +1192,8 @@ DensePlan dense_plan(int64_t n, int64_t k_dim, int bk) {
 struct SkPlan {
     int64_t kt, total, units, grid;
     size_t ws_bytes;
+    int64_t dp_rounds;  // (wide plan) whole-item rounds before the stream-K units
+    int32_t xcd_slots;  // (wide plan) XCD-contiguous slot numbering
 };
 SkPlan sk_plan(int64_t n, int64_t k_dim, int bk) {
     SkPlan p{};
@@ -1197,15 +1207,29 @@ SkPlan sk_plan(int64_t n, int64_t k_dim, int bk) {
     return p;
 }
 
-// The wide split kernel's stream-K plan: one 8-wave workgroup per CU, items of 256 x 128, slabs of 128 KiB
+// The wide kernels' plan: one 8-wave workgroup per CU, items of 256 x 128, slabs of 128 KiB.  From two items per
+// slot on, whole-item rounds in XCD-contiguous slot order (wide_schedule) and stream-K over the rest; a rest below
+// G / 4 items would cut each of its items into more than 4 pieces, so one round joins it.  GRF_DENSE_XCD=0 (read
+// per call, A/B): stream-K over every item, slots in launch order (round 5's schedule).
 SkPlan sk_plan_wide(int64_t n, int64_t k_dim) {
     SkPlan p{};
     const int64_t nt = cdiv<int64_t>(n, kTile), np = (nt + 1) / 2;
+    const int64_t items = np * (nt + 1) - np * np;
     p.kt = cdiv<int64_t>(k_dim, 16);
-    p.total = (np * (nt + 1) - np * np) * p.kt;
-    const int64_t slots = std::min<int64_t>(kCUs, std::max<int64_t>(p.total, 1));
-    p.units = std::max<int64_t>(1, cdiv<int64_t>(p.total, slots));
-    p.grid = cdiv<int64_t>(p.total, p.units);
+    p.total = items * p.kt;
+    const bool xcd = env_int("GRF_DENSE_XCD", 1) != 0;
+    if (xcd && items >= 2 * kCUs) {
+        p.grid = kCUs;
+        p.dp_rounds = items / p.grid;
+        const int64_t rest = items - p.dp_rounds * p.grid;
+        if (rest > 0 && rest < p.grid / 4) --p.dp_rounds;
+        p.units = std::max<int64_t>(1, cdiv<int64_t>(p.total - p.dp_rounds * p.grid * p.kt, p.grid));
+        p.xcd_slots = 1;
+    } else {
+        const int64_t slots = std::min<int64_t>(kCUs, std::max<int64_t>(p.total, 1));
+        p.units = std::max<int64_t>(1, cdiv<int64_t>(p.total, slots));
+        p.grid = cdiv<int64_t>(p.total, p.units);
+    }
     p.ws_bytes = kTicketBytes + (size_t)(2 * p.grid) * 2 * kTile * kTile * sizeof(float);
     return p;
 }
@@ -1335,6 +1359,8 @@ int32_t dense_gram_split(int64_t n, int64_t k_dim, const float *A, int64_t lda, 
         a.sk_units = q.units;
         a.sk_kt = q.kt;
         a.sk_total = q.total;
+        a.dp_rounds = q.dp_rounds;
+        a.xcd_slots = q.xcd_slots;
         gram_split_wide_kernel<kSplitNST><<<(unsigned)q.grid, 512, 0, st>>>(a);
         GRF_CHECK_LAUNCH("gram_split_wide_kernel");
         return GRF_OK;
@@ -1437,6 +1463,8 @@ int32_t dense_gram_planes(int64_t n, int64_t k_dim, const void *P, int64_t ldp, 
     a.sk_units = q.units;
     a.sk_kt = q.kt;
     a.sk_total = q.total;
+    a.dp_rounds = q.dp_rounds;
+    a.xcd_slots = q.xcd_slots;
     gram_planes_wide_kernel<kSplitNST><<<(unsigned)q.grid, 512, 0, S(stream)>>>(
         a, reinterpret_cast<const unsigned char *>(P), ldp);
     GRF_CHECK_LAUNCH("gram_planes_wide_kernel");

@@ -38,16 +38,21 @@ __device__ inline double pw_leaf(const double *a, int64_t n) {
     return res;
 }
 
-// numpy pairwise_sum_DOUBLE, recursion unrolled onto an explicit stack
-__device__ double np_pairwise(const double *a, int64_t n) {
+// The recursion's explicit stack lives in LDS (one per wave, used by lane 0 only): a per-lane array in
+// registers would be dynamically indexed, i.e. private (scratch) memory -- 2.5 KB per lane, which the runtime
+// must back for every wave the device can hold at each launch of every kernel reaching this code.
+// Depth: a frame of m > 128 values splits into halves of <= m / 2 + 8, so 64 frames cover any int64 n.
+constexpr int kPwDepth = 64;
+struct PwFrame { int64_t off, n; double left; int32_t state; };
+
+// numpy pairwise_sum_DOUBLE, recursion unrolled onto the explicit stack `st`
+__device__ double np_pairwise(const double *a, int64_t n, PwFrame *st) {
     if (n <= 128) return pw_leaf(a, n);
-    struct Frame { int64_t off, n; int state; double left; };
-    Frame st[64];
     int sp = 0;
-    st[0] = {0, n, 0, 0.0};
+    st[0] = {0, n, 0.0, 0};
     double ret = 0.0;
     while (sp >= 0) {
-        Frame &f = st[sp];
+        PwFrame &f = st[sp];
         if (f.n <= 128) {
             ret = pw_leaf(a + f.off, f.n);
             --sp;
@@ -57,12 +62,12 @@ __device__ double np_pairwise(const double *a, int64_t n) {
         n2 -= n2 % 8;
         if (f.state == 0) {
             f.state = 1;
-            st[sp + 1] = {f.off, n2, 0, 0.0};
+            st[sp + 1] = {f.off, n2, 0.0, 0};
             ++sp;
         } else if (f.state == 1) {
             f.left = ret;
             f.state = 2;
-            st[sp + 1] = {f.off + n2, f.n - n2, 0, 0.0};
+            st[sp + 1] = {f.off + n2, f.n - n2, 0.0, 0};
             ++sp;
         } else {
             ret = f.left + ret;
@@ -75,14 +80,20 @@ __device__ double np_pairwise(const double *a, int64_t n) {
 // numpy pairwise_sum_DOUBLE of a[0 .. n) by one wave, bit for bit: the recursion's leaves (runs
 // of <= 128 values, split points n2 = n/2 - (n/2) % 8) are listed by lane 0, summed by the 64 lanes
 // in parallel with the leaf's own 8-accumulator order, and combined by lane 0 in the recursion's
-// order.  `leaf` is per-wave LDS scratch for kPwLeaves leaves; longer inputs fall back to lane 0.
+// order.  `ws` is the wave's LDS: kPwLeaves leaves and the stack; longer inputs fall back to lane 0.
 // Every lane returns the sum.  (A hub row of thousands of entries, or a dense row, no longer
 // costs one lane thousands of dependent adds.)
 constexpr int kPwLeaves = 128;
 struct PwLeaf { int64_t off; int64_t n; double sum; };
+struct PwScratch {
+    PwLeaf leaf[kPwLeaves];
+    PwFrame st[kPwDepth];
+};
 
-__device__ double wave_np_pairwise(const double *a, int64_t n, PwLeaf *leaf) {
+__device__ double wave_np_pairwise(const double *a, int64_t n, PwScratch *ws) {
     const int lane = threadIdx.x & 63;
+    PwLeaf *leaf = ws->leaf;
+    PwFrame *st = ws->st;
     if (n <= 128) {
         // one leaf: lanes 0..7 own the accumulators r_j (a[j], a[j + 8], ...), then the fixed tree
         double r = 0.0;
@@ -125,12 +136,11 @@ __device__ double wave_np_pairwise(const double *a, int64_t n, PwLeaf *leaf) {
     // list the leaves (lane 0, the recursion's explicit stack), left to right
     int32_t nl = 0;
     if (lane == 0) {
-        int64_t so[64], sn[64];
         int sp = 0;
-        so[0] = 0;
-        sn[0] = n;
+        st[0].off = 0;
+        st[0].n = n;
         while (sp >= 0) {
-            const int64_t o = so[sp], m = sn[sp];
+            const int64_t o = st[sp].off, m = st[sp].n;
             --sp;
             if (m <= 128) {
                 if (nl < kPwLeaves) leaf[nl] = PwLeaf{o, m, 0.0};
@@ -140,28 +150,30 @@ __device__ double wave_np_pairwise(const double *a, int64_t n, PwLeaf *leaf) {
             int64_t n2 = m / 2;
             n2 -= n2 % 8;
             // push right then left: the left subtree's leaves come first
-            ++sp; so[sp] = o + n2; sn[sp] = m - n2;
-            ++sp; so[sp] = o; sn[sp] = n2;
+            ++sp;
+            st[sp].off = o + n2;
+            st[sp].n = m - n2;
+            ++sp;
+            st[sp].off = o;
+            st[sp].n = n2;
         }
     }
     nl = __shfl(nl, 0, 64);
+    __builtin_amdgcn_wave_barrier();
     if (nl > kPwLeaves) {
-        const double t = lane == 0 ? np_pairwise(a, n) : 0.0;
+        const double t = lane == 0 ? np_pairwise(a, n, st) : 0.0;
         return __shfl(t, 0, 64);
     }
-    __builtin_amdgcn_wave_barrier();
     for (int l = lane; l < nl; l += 64) leaf[l].sum = pw_leaf(a + leaf[l].off, leaf[l].n);
     __builtin_amdgcn_wave_barrier();
     // combine in the recursion's order (lane 0): the same stack machine with leaf sums in order
     double total = 0.0;
     if (lane == 0) {
-        struct Frame { int64_t n; int state; double left; };
-        Frame st[64];
         int sp = 0, next = 0;
-        st[0] = {n, 0, 0.0};
+        st[0] = {0, n, 0.0, 0};
         double ret = 0.0;
         while (sp >= 0) {
-            Frame &f = st[sp];
+            PwFrame &f = st[sp];
             if (f.n <= 128) {
                 ret = leaf[next++].sum;
                 --sp;
@@ -171,12 +183,12 @@ __device__ double wave_np_pairwise(const double *a, int64_t n, PwLeaf *leaf) {
             n2 -= n2 % 8;
             if (f.state == 0) {
                 f.state = 1;
-                st[sp + 1] = {n2, 0, 0.0};
+                st[sp + 1] = {0, n2, 0.0, 0};
                 ++sp;
             } else if (f.state == 1) {
                 f.left = ret;
                 f.state = 2;
-                st[sp + 1] = {f.n - n2, 0, 0.0};
+                st[sp + 1] = {0, f.n - n2, 0.0, 0};
                 ++sp;
             } else {
                 ret = f.left + ret;
@@ -185,6 +197,7 @@ __device__ double wave_np_pairwise(const double *a, int64_t n, PwLeaf *leaf) {
         }
         total = ret;
     }
+    __builtin_amdgcn_wave_barrier();
     return __shfl(total, 0, 64);
 }
 
@@ -192,11 +205,11 @@ __device__ double wave_np_pairwise(const double *a, int64_t n, PwLeaf *leaf) {
 // degrees a_ii... : deg = a0 + pairwise(rest) per row (np.add.reduceat), one wave per row
 __global__ __launch_bounds__(256) void lap_deg_kernel(int64_t n, const int64_t *ptr, const double *val, double *deg,
                                                       double *dinv) {
-    __shared__ PwLeaf leaves[4][kPwLeaves];
+    __shared__ PwScratch leaves[4];
     const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
     const int64_t b = ptr[i], e = ptr[i + 1];
-    const double rest = e - b > 1 ? wave_np_pairwise(val + b + 1, e - b - 1, leaves[threadIdx.x >> 6]) : 0.0;
+    const double rest = e - b > 1 ? wave_np_pairwise(val + b + 1, e - b - 1, &leaves[threadIdx.x >> 6]) : 0.0;
     if ((threadIdx.x & 63) == 0) {
         const double d = e > b ? val[b] + rest : 0.0;
         deg[i] = d;
@@ -292,7 +305,7 @@ constexpr int kLeafPer = 16;  // 128 (one numpy leaf) / 8 lanes
 __global__ __launch_bounds__(256) void lap_deg_group_kernel(int64_t n, const int64_t *__restrict__ ptr,
                                                             const double *__restrict__ val, double *__restrict__ deg,
                                                             double *__restrict__ dinv) {
-    __shared__ PwLeaf leaves[4][kPwLeaves];
+    __shared__ PwScratch leaves[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
     const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 8;
     if (r0 >= n) return;
@@ -355,7 +368,7 @@ __global__ __launch_bounds__(256) void lap_deg_group_kernel(int64_t n, const int
         const int gg = (__ffsll((long long)todo) - 1) >> 3;
         todo &= todo - 1;
         const int64_t ii = r0 + gg, bb = ptr[ii], ee = ptr[ii + 1];
-        const double rr = wave_np_pairwise(val + bb + 1, ee - bb - 1, leaves[wave]);
+        const double rr = wave_np_pairwise(val + bb + 1, ee - bb - 1, &leaves[wave]);
         if (lane == 0) {
             const double d = val[bb] + rr;
             deg[ii] = d;
@@ -632,7 +645,9 @@ static bool pw_plan_build(int64_t n, PwPlan &p) {
     return true;
 }
 
-__device__ double plan_row_sum(const double *a, const PwPlan &plan, double *sums, int lane) {
+// (stk: the wave's LDS stack of the combine, kPwPlanLeaves doubles -- not a per-lane array, which would be
+// private memory)
+__device__ double plan_row_sum(const double *a, const PwPlan &plan, double *sums, double *stk, int lane) {
     const int g = lane >> 3, j = lane & 7;
     for (int l0 = 0; l0 < plan.nl; l0 += 8) {
         const int l = l0 + g;
@@ -659,7 +674,6 @@ __device__ double plan_row_sum(const double *a, const PwPlan &plan, double *sums
     __builtin_amdgcn_wave_barrier();
     double d = 0.0;
     if (lane == 0) {
-        double stk[32];
         int sp = -1;
         for (int t = 0; t < plan.nprog; ++t) {
             const int tok = plan.prog[t];
@@ -716,8 +730,8 @@ struct IntSum {  // per-lane exact-integer-sum state of numpy's shortcut (wave_n
 __global__ __launch_bounds__(256) void lapd_stage_kernel(int64_t n, const double *W, int32_t mode, PwPlan plan,
                                                          double *deg, double *dinv, int32_t *scnt, int32_t *scol,
                                                          double *sval, uint64_t *flags, uint32_t *ticket) {
-    __shared__ double sums[4][kPwPlanLeaves];
-    __shared__ PwLeaf leaves[4][kPwLeaves];
+    __shared__ double sums[4][kPwPlanLeaves], stk[4][kPwPlanLeaves];
+    __shared__ PwScratch leaves[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t i = (int64_t)blockIdx.x * 4 + wave;  // one wave per row
     if (i >= n) return;
@@ -760,7 +774,7 @@ __global__ __launch_bounds__(256) void lapd_stage_kernel(int64_t n, const double
         // every partial sum of any order is an exact integer (< 2^53): the recursion's result, bit for bit
         d = wave_sum(is.s);
     } else {
-        d = plan.nl > 0 ? plan_row_sum(a, plan, sums[wave], lane) : wave_np_pairwise(a, n, leaves[wave]);
+        d = plan.nl > 0 ? plan_row_sum(a, plan, sums[wave], stk[wave], lane) : wave_np_pairwise(a, n, &leaves[wave]);
     }
     if (lane == 0) {
         deg[i] = d;

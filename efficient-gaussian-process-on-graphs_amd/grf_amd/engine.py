@@ -856,11 +856,17 @@ class GRFEngine:
 
     @staticmethod
     def use_planes(n: int) -> bool:
-        """The split Gram on pre-split planes (grf_gram_dense_planes): opt-in, GRF_DENSE_PLANES=1 (read per call).
-        Measured slower than the split in registers: staging three bf16 planes moves 1.5x the fp32 bytes and the
-        Gram is bound by its staging, not by the split's VALU -- C2 Gram 4.64 -> 5.62 ms, C3 (wide items) 0.144 ->
-        0.156 ms (profiles/r06_dense_planes_ab.txt); the same K bits."""
-        return os.environ.get("GRF_DENSE_PLANES") == "1"
+        """The split Gram on pre-split bf16 planes (grf_gram_dense_planes) where the wide kernels run (from 64 tile
+        rows on, n > 8064; GRF_DENSE_WIDE=0 turns it off with them): with the wide kernels' XCD-ordered whole-item
+        rounds the staged k-tiles are L2 / Infinity-Cache hits, so staging the planes' 1.5x bytes costs less than
+        the split's VALU -- C2 Gram 4.40 -> 4.01 ms (profiles/r06_dense_xcd_ab.txt; before those rounds the planes
+        were staging-bound and slower, r06_dense_planes_ab.txt).  Below, the 128-tile kernel splits in registers
+        (C3: the wide planes kernel 0.156 vs 0.127 ms).  GRF_DENSE_PLANES (read per call): 1 always, 0 never.
+        Same K bits either way."""
+        env = os.environ.get("GRF_DENSE_PLANES")
+        if env in ("0", "1"):
+            return env == "1"
+        return -(-int(n) // 128) >= 64 and os.environ.get("GRF_DENSE_WIDE") != "0"
 
     def split_planes(self, dense_phi: torch.Tensor, k_dim: int) -> "DensePlanes":
         """The dense fp32 Phi's three bf16 planes, split once (grf_split_planes)."""

@@ -626,6 +626,38 @@ def test_gram_dense_split_wide(eng, monkeypatch, n, k):
     assert np.array_equal(Kd, Kw if -(-n // 128) >= 64 else Kn)
 
 
+@pytest.mark.parametrize("planes", ["1", "0"])
+@pytest.mark.parametrize("n,k", [(8192, 300), (10000, 160), (11520, 64)])
+def test_gram_dense_wide_xcd_rounds(eng, monkeypatch, n, k, planes):
+    """The wide kernels' whole-item rounds in XCD-contiguous slot order, then stream-K over the rest
+    (sk_plan_wide): 1056 items (a rest of 32 < 64 joins a round: 3 rounds + 288 items cut), 1600 (C2's count:
+    6 rounds + 64 items cut in four) and 2070 (7 rounds + 278); the planes kernel (the default here) and the
+    in-register split (GRF_DENSE_PLANES=0); against fp64 within the fp32 path's bound, against round 5's
+    stream-K-only schedule (GRF_DENSE_XCD=0) within twice that bound, exactly symmetric, run-to-run identical,
+    tickets back at zero."""
+    import torch
+    monkeypatch.setenv("GRF_DENSE_PLANES", planes)
+    lda = -(-k // 64) * 64
+    g = torch.Generator(device=eng.device).manual_seed(n + k)
+    A = torch.zeros((n, lda), dtype=torch.float32, device=eng.device)
+    A[:, :k] = torch.rand((n, k), device=eng.device, generator=g) * (
+        torch.rand((n, k), device=eng.device, generator=g) < 0.3)
+    K1 = eng.gram_dense(A, k, precision="split")
+    K2 = eng.gram_dense(A, k, precision="split")
+    ws = eng._dense_ws[eng.stream.value]
+    assert int(ws[:4096].view(torch.int32).abs().sum()) == 0
+    assert torch.equal(K1, K2) and torch.equal(K1, K1.t()) and bool(torch.isfinite(K1).all())
+    monkeypatch.setenv("GRF_DENSE_XCD", "0")
+    K0 = eng.gram_dense(A, k, precision="split")
+    monkeypatch.delenv("GRF_DENSE_XCD")
+    rows = torch.arange(0, n, 61, device=eng.device)
+    Ad = A[:, :k].double()
+    ref = Ad[rows] @ Ad.t()
+    bound = 1e-5 * (Ad[rows].abs() @ Ad.abs().t()) + 1e-30
+    assert float(((K1[rows].double() - ref).abs() / bound).max()) <= 1.0
+    assert float(((K1[rows].double() - K0[rows].double()).abs() / bound).max()) <= 2.0
+
+
 def test_gram_dense_c2_size_stream_k(eng):
     """the stream-K path at the bench's C2 size (n = k = 10 000; the split Gram's wide
     workgroups: 1600 items of 256 x 128 over 256 slots, items cut at slot boundaries and summed through
