@@ -35,7 +35,7 @@ def main():
             m["hbm_bytes_per_launch"] = 2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024
         if "TCC_HIT_sum" in m:
             m["l2_hit_rate"] = m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
-        res[k.split("(")[0]] = m
+        res[k.replace("(anonymous namespace)::", "").split("(")[0]] = m
     json.dump(res, sys.stdout, indent=1, sort_keys=True)
     print()
 
