@@ -1001,7 +1001,7 @@ __device__ __forceinline__ void dma16b(const unsigned char *src, unsigned char *
 // per block in split_ktile's order (c0: a0 b0; c1: (0,1) (1,0) (0,2) (1,1) (2,0)), the DMA pieces between
 // (a lane's chunk of block x, plane p sits at base + 32 rows x 96 B x + 32 p: rows 32 apart keep the swap bit,
 // ((row >> 3) & 1) = ((lane >> 3) & 1), so one base per operand and immediate offsets address all six)
-template <typename Issue>
+template <bool SIX = false, typename Issue>
 __device__ __forceinline__ void planes_ktile(const unsigned char *As, const unsigned char *Bs, uint32_t abase,
                                              uint32_t bbase, f32x16 (&c0)[2][2], f32x16 (&c1)[2][2], Issue issue) {
     u32x4 a[2][3], b[2][3];
@@ -1034,6 +1034,10 @@ __device__ __forceinline__ void planes_ktile(const unsigned char *As, const unsi
     mf(0, 0, 5); mf(0, 1, 3); fence();
     mf(0, 1, 4); issue(4); fence();
     mf(0, 1, 5);
+    if constexpr (SIX) {  // (the 128-tile kernel's sixth piece)
+        issue(5);
+        fence();
+    }
     mf(1, 0, 3);
     mf(1, 0, 4);
     mf(1, 0, 5);
@@ -1127,6 +1131,123 @@ __global__ __launch_bounds__(512, 1) void gram_planes_wide_kernel(DenseArgs a, c
                   [&](int64_t item, int64_t kb, int64_t ke, f32x16 (&c)[2][2]) {
                       return item_compute_planes<NST>(a, P, ldp, lds, item, kb, ke, wave, lane, c);
                   });
+}
+
+// The 128-tile kernel on the planes (n <= 8064, where the wide items leave CUs idle): the in-register split
+// kernel's work items (gram_split_mfma_kernel: tiles cut into k-slices, pieces summed by the last) with stages of
+// 128 + 128 rows of 96 B (24 KiB; 3 stages = 72 KiB, two workgroups per CU), 24 1-KiB DMA pieces per k-tile, piece
+// P of wave w for P = w + 4 i (i < 6; a diagonal tile stages A alone: 12 pieces, 3 per wave), the fragment reads
+// and MFMAs of planes_ktile.  Same products in the same order as the in-register kernel: the same K bits.
+struct PlaneTileStage {
+    static constexpr int BA = kTile * kPlaneBytes, B = 2 * BA;  // bytes: the A image, then the B image
+    static constexpr int G = B / 1024 / 4, GD = BA / 1024 / 4;  // pieces per wave and k-tile (off / on the diagonal)
+};
+static_assert(PlaneTileStage::BA % 4096 == 0 && PlaneTileStage::G == 6, "whole pieces, six per wave");
+constexpr int kPlaneTileNST = 3;
+
+template <int NST, bool DIAG, bool LIVE>
+__device__ __forceinline__ void kloop_planes_tile(unsigned char *lds, const unsigned char *const *src,
+                                                  const uint32_t *dst, int64_t kb, int64_t ke, uint32_t abase,
+                                                  uint32_t bbase, f32x16 (&c0)[2][2], f32x16 (&c1)[2][2]) {
+    constexpr int G = DIAG ? PlaneTileStage::GD : PlaneTileStage::G;
+    const int64_t nk = (ke - kb) / 16;
+    auto issue_part = [&](int64_t t, int q) {
+        const int64_t kt0 = kb / 16 + (t < nk ? t : nk - 1);
+        dma16b(src[q] + kPlaneBytes * kt0, lds + (int)(t % NST) * PlaneTileStage::B + dst[q]);
+    };
+    if (nk <= 0) return;
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+#pragma unroll
+        for (int q = 0; q < G; ++q) issue_part(t, q);
+    for (int64_t t = 0; t < nk; ++t) {
+        wait_vm<(NST - 2) * G>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if constexpr (!LIVE) {
+#pragma unroll
+            for (int q = 0; q < G; ++q) issue_part(t + NST - 1, q);
+        } else {
+            const unsigned char *As = lds + (int)(t % NST) * PlaneTileStage::B;
+            const unsigned char *Bs = DIAG ? As : As + PlaneTileStage::BA;
+            planes_ktile<true>(As, Bs, abase, bbase, c0, c1, [&](int q) { if (q < G) issue_part(t + NST - 1, q); });
+        }
+    }
+}
+
+__device__ __forceinline__ Quarter tile_compute_planes(const DenseArgs &a, const unsigned char *P, int64_t ldp,
+                                                       unsigned char *lds, int64_t tile, int64_t kb, int64_t ke,
+                                                       int wave, int lane, f32x16 (&c)[2][2]) {
+    const int wm = wave >> 1, wn = wave & 1;
+    int64_t bi, bj;
+    tile_coords(tile, a.nt, bi, bj);
+    const int64_t m0 = bi * kTile, n0 = bj * kTile;
+    const bool diag = bi == bj;
+    const unsigned char *src[PlaneTileStage::G];
+    uint32_t dst[PlaneTileStage::G];
+#pragma unroll
+    for (int i = 0; i < PlaneTileStage::G; ++i) {
+        const uint32_t off = (uint32_t)(wave + 4 * i) * 1024u + 16u * (uint32_t)lane;  // this lane's stage bytes
+        const bool isA = off < (uint32_t)PlaneTileStage::BA;
+        const uint32_t o = isA ? off : off - PlaneTileStage::BA;
+        const int R = (int)(o / kPlaneBytes), jj = (int)((o % kPlaneBytes) / 16);
+        const int cc = jj ^ ((R >> 3) & 1);  // the global chunk that lands here
+        int64_t r = (isA ? m0 : n0) + R;
+        r = r < a.n ? r : a.n - 1;
+        src[i] = P + r * ldp + 16 * cc;
+        dst[i] = off;
+    }
+    const uint32_t abase = plane_lds_off(wm * 64 + (lane & 31), lane >> 5);
+    const uint32_t bbase = plane_lds_off(wn * 64 + (lane & 31), lane >> 5);
+    Quarter q{m0 + wm * 64, n0 + wn * 64, diag, diag && wn < wm};
+    const bool live = !q.below && q.qr < a.n && q.qc < a.n;
+    f32x16 c0[2][2], c1[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            c0[x][y] = f32x16{};
+            c1[x][y] = f32x16{};
+        }
+    constexpr int NST = kPlaneTileNST;
+    if (diag) {
+        if (live) kloop_planes_tile<NST, true, true>(lds, src, dst, kb, ke, abase, bbase, c0, c1);
+        else kloop_planes_tile<NST, true, false>(lds, src, dst, kb, ke, abase, bbase, c0, c1);
+    } else {
+        if (live) kloop_planes_tile<NST, false, true>(lds, src, dst, kb, ke, abase, bbase, c0, c1);
+        else kloop_planes_tile<NST, false, false>(lds, src, dst, kb, ke, abase, bbase, c0, c1);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) c[x][y] = c0[x][y] + c1[x][y];
+    return q;
+}
+
+__global__ __launch_bounds__(256, 2) void gram_planes_tile_kernel(DenseArgs a, const unsigned char *P, int64_t ldp) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kPlaneTileNST * PlaneTileStage::B];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t w = blockIdx.x;
+    int64_t tile, slice = 0, pieces = 1;
+    if (w < a.n_whole) {
+        tile = w;
+    } else {
+        tile = a.n_whole + (w - a.n_whole) / a.n_split;
+        slice = (w - a.n_whole) % a.n_split;
+        pieces = a.n_split;
+    }
+    const int64_t kb = pieces > 1 ? slice * a.k_split : 0;
+    const int64_t ke = pieces > 1 ? (kb + a.k_split < a.kpad ? kb + a.k_split : a.kpad) : a.kpad;
+    f32x16 c[2][2];
+    const Quarter q = tile_compute_planes(a, P, ldp, lds, tile, kb, ke, wave, lane, c);
+    if (pieces > 1) {
+        const int64_t u = tile - a.n_whole;
+        if (!split_combine<32, 16>(a, c, a.tickets + u, pieces, slice, [&](int64_t s) { return u * pieces + s; },
+                                   reinterpret_cast<int32_t *>(lds), wave, lane))
+            return;
+    }
+    tile_write<32, 16>(a, c, q, wave, lane);
 }
 
 constexpr int kCUs = 256;
@@ -1434,7 +1555,7 @@ int32_t densify_padded_planes(int64_t n_rows, int64_t cap, int64_t n_cols, const
     return GRF_OK;
 }
 
-// K from the planes on the wide items (stream-K at every size); workspace as dense_gram_split's
+// K from the planes: the wide items from 64 tile rows on, else the 128-tile kernel; workspace as dense_gram_split's
 int32_t dense_gram_planes(int64_t n, int64_t k_dim, const void *P, int64_t ldp, float *K, int64_t ldk,
                           void *workspace, size_t workspace_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n >= 0 && k_dim >= 0 && K && ldk >= n && (n == 0 || P), GRF_EINVAL, "grf_gram_dense_planes: bad arguments");
@@ -1456,6 +1577,24 @@ int32_t dense_gram_planes(int64_t n, int64_t k_dim, const void *P, int64_t ldp, 
     a.nt = cdiv<int64_t>(n, kTile);
     a.ldk = ldk;
     a.kpad = cdiv<int64_t>(k_dim, 16) * 16;
+    // the wide items from 64 tile rows on (the split path's rule, GRF_DENSE_WIDE as there), else 128-tiles
+    const int wide_env = env_int("GRF_DENSE_WIDE", -1);
+    if (!(wide_env == 1 || (wide_env != 0 && a.nt >= 64))) {
+        const DensePlan p = dense_plan(n, k_dim, 16);
+        const int64_t split_tiles = p.tiles - p.n_whole;
+        const int64_t items = p.n_whole + split_tiles * p.n_split;
+        GRF_REQUIRE_GRID(items, 256, "gram_planes_tile_kernel");
+        a.tickets = split_tiles > 0 ? reinterpret_cast<int32_t *>(workspace) : nullptr;
+        a.slabs = split_tiles > 0 ? reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + kTicketBytes)
+                                  : nullptr;
+        a.n_whole = p.n_whole;
+        a.k_split = p.k_split;
+        a.n_split = p.n_split;
+        gram_planes_tile_kernel<<<(unsigned)items, 256, 0, S(stream)>>>(a, reinterpret_cast<const unsigned char *>(P),
+                                                                         ldp);
+        GRF_CHECK_LAUNCH("gram_planes_tile_kernel");
+        return GRF_OK;
+    }
     const SkPlan q = sk_plan_wide(n, k_dim);
     GRF_REQUIRE_GRID(q.grid, 512, "gram_planes_wide_kernel");
     a.tickets = reinterpret_cast<int32_t *>(workspace);

@@ -860,9 +860,9 @@ class GRFEngine:
         rows on, n > 8064; GRF_DENSE_WIDE=0 turns it off with them): with the wide kernels' XCD-ordered whole-item
         rounds the staged k-tiles are L2 / Infinity-Cache hits, so staging the planes' 1.5x bytes costs less than
         the split's VALU -- C2 Gram 4.40 -> 4.01 ms (profiles/r06_dense_xcd_ab.txt; before those rounds the planes
-        were staging-bound and slower, r06_dense_planes_ab.txt).  Below, the 128-tile kernel splits in registers
-        (C3: the wide planes kernel 0.156 vs 0.127 ms).  GRF_DENSE_PLANES (read per call): 1 always, 0 never.
-        Same K bits either way."""
+        were staging-bound and slower, r06_dense_planes_ab.txt).  Below, the 128-tile kernel splits in registers:
+        its planes twin (gram_planes_tile_kernel) measured equal at C3 (0.133 ms both: that Gram is bound by neither
+        the split nor the staged bytes).  GRF_DENSE_PLANES (read per call): 1 always, 0 never.  Same K bits."""
         env = os.environ.get("GRF_DENSE_PLANES")
         if env in ("0", "1"):
             return env == "1"

@@ -658,6 +658,37 @@ def test_gram_dense_wide_xcd_rounds(eng, monkeypatch, n, k, planes):
     assert float(((K1[rows].double() - K0[rows].double()).abs() / bound).max()) <= 2.0
 
 
+@pytest.mark.parametrize("n,k", [(2708, 2708), (1000, 1000), (300, 17), (4000, 500)])
+def test_gram_dense_planes_tile_kernel(eng, monkeypatch, n, k):
+    """The 128-tile kernel on the planes (gram_planes_tile_kernel, below 64 tile rows): below 256 tiles the
+    in-register split runs the same work items (gram_split_mfma_kernel), so the bits are identical (C3's size
+    among them); from 256 tiles on the in-register path is stream-K (other k pieces): within twice the fp32
+    path's bound of it.  Both within the bound of fp64, exactly symmetric, run-to-run identical, tickets zero."""
+    import torch
+    lda = -(-k // 64) * 64
+    g = torch.Generator(device=eng.device).manual_seed(n * 3 + k)
+    A = torch.zeros((n, lda), dtype=torch.float32, device=eng.device)
+    A[:, :k] = torch.randn((n, k), device=eng.device, generator=g) * (
+        torch.rand((n, k), device=eng.device, generator=g) < 0.3)
+    monkeypatch.setenv("GRF_DENSE_PLANES", "0")
+    K0 = eng.gram_dense(A, k, precision="split").clone()
+    monkeypatch.setenv("GRF_DENSE_PLANES", "1")
+    K1 = eng.gram_dense(A, k, precision="split").clone()
+    K2 = eng.gram_dense(A, k, precision="split")
+    ws = eng._dense_ws[eng.stream.value]
+    assert int(ws[:4096].view(torch.int32).abs().sum()) == 0
+    assert torch.equal(K1, K2) and torch.equal(K1, K1.t()) and bool(torch.isfinite(K1).all())
+    tiles = (-(-n // 128)) * (-(-n // 128) + 1) // 2
+    Ad = A[:, :k].double()
+    rows = torch.arange(0, n, 7, device=eng.device)
+    bound = 1e-5 * (Ad[rows].abs() @ Ad.abs().t()) + 1e-30
+    assert float(((K1[rows].double() - Ad[rows] @ Ad.t()).abs() / bound).max()) <= 1.0
+    if tiles < 256:
+        assert torch.equal(K0, K1), float((K0 - K1).abs().max())
+    else:
+        assert float(((K1[rows].double() - K0[rows].double()).abs() / bound).max()) <= 2.0
+
+
 def test_gram_dense_c2_size_stream_k(eng):
     """the stream-K path at the bench's C2 size (n = k = 10 000; the split Gram's wide
     workgroups: 1600 items of 256 x 128 over 256 slots, items cut at slot boundaries and summed through
