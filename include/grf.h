@@ -445,10 +445,11 @@ int32_t grf_gram_dense_split_upper(int64_t n, int64_t k_dim, const float *A, int
  * grf_gram_dense_split forms in registers for every staged k-tile.  ldp >= grf_planes_row_bytes(k_dim)
  * (= 96 ceil(k_dim / 16)), a multiple of 16.  grf_split_planes reads A (zero-padded to 16 ceil(k_dim / 16)
  * columns, as grf_gram_dense_split requires); grf_densify_padded_planes writes them straight from the walk's
- * padded rows (grf_densify_padded's arguments, n_cols = k_dim).  grf_gram_dense_planes: K = A A^T from them on
- * the 256 x 128 wide workgroups with nothing but fragment reads and MFMAs in the k-loop -- bit-identical to
- * grf_gram_dense_split's wide path (the same planes, the same products in the same order); workspace as
- * grf_gram_dense_split's (grf_gram_dense_split_workspace_bytes, ZERO on first use). */
+ * padded rows (grf_densify_padded's arguments, n_cols = k_dim).  grf_gram_dense_planes: K = A A^T from them with
+ * nothing but fragment reads and MFMAs in the k-loop, on grf_gram_dense_split's decomposition for the size (the
+ * 256 x 128 wide workgroups from 64 tile rows on, GRF_DENSE_WIDE as there; else the 128-tiles with their k-slices)
+ * and bit-identical to it wherever both take the same work items (the same planes, the same products in the same
+ * order); workspace as grf_gram_dense_split's (grf_gram_dense_split_workspace_bytes, ZERO on first use). */
 int64_t grf_planes_row_bytes(int64_t k_dim);
 int32_t grf_split_planes(int64_t n, int64_t k_dim, const float *A, int64_t lda, void *P, int64_t ldp,
                          grf_stream_t stream);
