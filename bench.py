@@ -90,6 +90,21 @@ def auto_hubs(eng, A_dev, m, p, L, f, share: float = 0.13):
     return eng.column_stats(setup_phi(eng, A_dev, m, p, L, f, seed=42), share, extend=eng.hub_extend_share())
 
 
+def _device_tensors(obj, depth: int = 3):
+    """The CUDA tensors held by a front (its attributes, theirs, ... to ``depth`` levels; the engine skipped)."""
+    import torch
+
+    from grf_amd.engine import GRFEngine
+    if torch.is_tensor(obj):
+        return [obj] if obj.is_cuda else []
+    if depth == 0 or obj is None or isinstance(obj, (GRFEngine, int, float, str, bool)):
+        return []
+    out = []
+    for v in (vars(obj).values() if hasattr(obj, "__dict__") else []):
+        out += _device_tensors(v, depth - 1)
+    return out
+
+
 def init_distributed(local_rank: int) -> int:
     """One process per GPU over RCCL (backend "nccl").  GRF_DIST_BACKEND=gloo rehearses the same
     multi-process path with several ranks on one GPU (device tensors staged through host memory
@@ -730,14 +745,10 @@ def main():
     def back_on_main(frd, record, after_gram=None):
         fr, done = frd
         main.wait_event(done)
-        # every device buffer the front allocated on `side` (Phi, the transpose, the row cuts, ...) is
-        # used on `main`: recorded there, so the allocator does not hand it out before `main` is done
-        for obj in vars(fr).values():
-            if obj is None:
-                continue
-            for v in ([obj] if torch.is_tensor(obj) else vars(obj).values() if hasattr(obj, "__dict__") else []):
-                if torch.is_tensor(v) and v.is_cuda:
-                    v.record_stream(main)
+        # every device buffer the front allocated on `side` (Phi -- CSR or padded rows --, the transpose, the row
+        # cuts, ...) is used on `main`: recorded there, so the allocator does not hand it out before `main` is done
+        for v in _device_tensors(fr):
+            v.record_stream(main)
         back(fr, record, after_gram)
 
     def run(steps: int, record: bool, record_walk: bool = False):

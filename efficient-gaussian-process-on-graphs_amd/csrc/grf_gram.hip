@@ -508,7 +508,7 @@ __global__ __launch_bounds__(64 * kWv) void gram_slot_pipe_kernel(
     int64_t n_cols, int64_t row_begin, int64_t rows, int64_t W, int64_t t_rows, int64_t n_tiles,
     const int64_t *__restrict__ ptr, const int32_t *__restrict__ idx, const float *__restrict__ val,
     const unsigned char *__restrict__ t_rec, const int32_t *__restrict__ rowshift, float *__restrict__ K,
-    int64_t ldk, int64_t ovf_base, int32_t ablate) {
+    int64_t ldk, int64_t ovf_base, int32_t ablate, int64_t pad_cap, const int32_t *__restrict__ pad_cnt) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];  // [W], then the waves' stream state
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     constexpr int kV = 2;
@@ -529,23 +529,33 @@ __global__ __launch_bounds__(64 * kWv) void gram_slot_pipe_kernel(
         J = t / rows;
         return row_begin + (t - J * rows);
     };
-    auto load_bounds = [&](int64_t i, int64_t &pv, int32_t &shv) {
+    // the row bounds: from the CSR row pointers (lanes 0 / 1: ptr[row], ptr[row + 1]), or with pad_cap > 0 from
+    // padded rows (row r's pad_cnt[r] entries at r pad_cap: the walk's output, no compaction) -- the count kept
+    // as loaded (pc) and combined only in load_nz, so no ALU op waits on the load here
+    auto load_bounds = [&](int64_t i, int64_t &pv, int32_t &pc, int32_t &shv) {
         if (i >= n_mine) {
             pv = 0;
+            pc = 0;
             shv = 0;
             return;
         }
         int64_t J;
         const int64_t row = tile_row(i, J);
-        const __amdgpu_buffer_rsrc_t rp =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(ptr + row), (short)0, 16, 0x00020000);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rp, (uint32_t)(lane & 1) * 8u, 0, 0);
-        pv = (int64_t)(((uint64_t)v[1] << 32) | v[0]);
+        if (pad_cap > 0) {
+            const __amdgpu_buffer_rsrc_t rc =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(pad_cnt + row), (short)0, 4, 0x00020000);
+            pc = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rc, 0u, 0, 0);
+        } else {
+            const __amdgpu_buffer_rsrc_t rp =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(ptr + row), (short)0, 16, 0x00020000);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rp, (uint32_t)(lane & 1) * 8u, 0, 0);
+            pv = (int64_t)(((uint64_t)v[1] << 32) | v[0]);
+        }
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(rowshift + row), (short)0, 4, 0x00020000);
         shv = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, 0u, 0, 0);
     };
-    auto load_nz = [&](int64_t i, int64_t pv, int32_t shv, PipeNz &z) {
+    auto load_nz = [&](int64_t i, int64_t pv, int32_t pc, int32_t shv, PipeNz &z) {
         if (i >= n_mine) {
             z = PipeNz{-1, 0.f, 0, 0, 0};
             return;
@@ -555,7 +565,15 @@ __global__ __launch_bounds__(64 * kWv) void gram_slot_pipe_kernel(
             const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)pv >> 32), l);
             return (int64_t)(((uint64_t)hi << 32) | lo);
         };
-        const int64_t e0 = lane_i64(0), e1 = lane_i64(1);
+        int64_t e0, e1;
+        if (pad_cap > 0) {
+            int64_t J;
+            e0 = tile_row(i, J) * pad_cap;
+            e1 = e0 + (int64_t)__builtin_amdgcn_readlane(pc, 0);
+        } else {
+            e0 = lane_i64(0);
+            e1 = lane_i64(1);
+        }
         const int64_t nnz = e1 - e0, share = (nnz + kWv - 1) / kWv;
         const int64_t s0 = wave * share < nnz ? wave * share : nnz, s1 = (wave + 1) * share < nnz ? (wave + 1) * share : nnz;
         const int64_t e = e0 + s0 + lane;
@@ -625,22 +643,22 @@ __global__ __launch_bounds__(64 * kWv) void gram_slot_pipe_kernel(
             __builtin_amdgcn_wave_barrier();
         }
     };
-    int64_t pv;
-    int32_t shv;
+    int64_t pv = 0;
+    int32_t pc = 0, shv;
     PipeNz T0, T1;
-    load_bounds(0, pv, shv);
-    load_nz(0, pv, shv, T0);
+    load_bounds(0, pv, pc, shv);
+    load_nz(0, pv, pc, shv, T0);
     uint2 d0 = load_hdr(0, T0.k);
-    load_bounds(1, pv, shv);
-    load_nz(1, pv, shv, T1);
-    load_bounds(2, pv, shv);
+    load_bounds(1, pv, pc, shv);
+    load_nz(1, pv, pc, shv, T1);
+    load_bounds(2, pv, pc, shv);
     __builtin_amdgcn_s_waitcnt(0);
     pipe_barrier();
     for (int64_t i = 0; i < n_mine; ++i) {
         const uint2 d1 = load_hdr(i + 1, T1.k);
         PipeNz T2;
-        load_nz(i + 2, pv, shv, T2);
-        load_bounds(i + 3, pv, shv);
+        load_nz(i + 2, pv, pc, shv, T2);
+        load_bounds(i + 3, pv, pc, shv);
         int64_t J;
         const int64_t row = tile_row(i, J);
         if (ablate != 1) {
@@ -912,7 +930,8 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
                                  int64_t t_last, const int64_t *ptr, const int32_t *idx, const float *val,
                                  const uint32_t *t_desc, const void *t_rec, int32_t unit, const int32_t *t_rowshift,
                                  float *K, int64_t ldk, hipStream_t st, const void *t_split = nullptr,
-                                 int64_t slot_buckets = 0, const int32_t *row_cuts = nullptr) {
+                                 int64_t slot_buckets = 0, const int32_t *row_cuts = nullptr, int64_t pad_cap = 0,
+                                 const int32_t *pad_cnt = nullptr) {
     if (unit == GRF_REC_SLOT) {
         // the slot layout: 8-wave tiles (one batch of 64 nonzeros per wave: two stream buckets each),
         // the default unroll and exact tails; the overflow pairs follow the slot_buckets slots
@@ -931,8 +950,11 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
             const char *e = getenv("GRF_GRAM_PIPE_ABLATE");
             return e ? (int32_t)atoi(e) : 0;
         }();
-        if (pipe && !tl.sym && tl.t_rows >= 0 && !tl.add_k && tl.k_begin == 0 && tl.k_end == (int32_t)n_total &&
-            t_first == 0 && t_last == tl.total() && tl.J_off == 0) {
+        const bool pipe_ok = !tl.sym && tl.t_rows >= 0 && !tl.add_k && tl.k_begin == 0 &&
+                             tl.k_end == (int32_t)n_total && t_first == 0 && t_last == tl.total() && tl.J_off == 0;
+        GRF_REQUIRE(pad_cap == 0 || pipe_ok, GRF_EUNSUPPORTED,
+                    "gram: padded rows need the pipelined column-block kernel (a whole non-symmetric launch)");
+        if ((pipe || pad_cap > 0) && pipe_ok) {
             const size_t lds = gram_lds_bytes(tl.W, 8, 2);
             int dev = 0, n_cu = 0;
             GRF_CHECK_HIP(hipGetDevice(&dev));
@@ -941,7 +963,8 @@ static int32_t gram_tiles_launch(int64_t n_total, int64_t row_begin, const GramT
             const int64_t grid = std::min<int64_t>((int64_t)std::max(n_cu, 1) * per_cu, t_last);
             gram_slot_pipe_kernel<8><<<(unsigned)grid, 512, lds, st>>>(
                 n_total, row_begin, tl.rows, tl.W, tl.t_rows, t_last, ptr, idx, val,
-                reinterpret_cast<const unsigned char *>(t_rec), t_rowshift, K, ldk, 32 * slot_buckets, ablate);
+                reinterpret_cast<const unsigned char *>(t_rec), t_rowshift, K, ldk, 32 * slot_buckets, ablate, pad_cap,
+                pad_cnt);
             GRF_CHECK_LAUNCH("gram_slot_pipe_kernel");
             return GRF_OK;
         }
@@ -1190,8 +1213,8 @@ static int32_t gram_sparse_cols_impl(int64_t n_cols, int64_t row_begin, int64_t 
                                      const int32_t *idx, const float *val, const int32_t *row_shift, int64_t t_rows,
                                      int64_t sym_row0, int64_t band_width, int32_t rec_unit, const uint32_t *t_desc,
                                      const void *t_rec, const void *t_split, float *K, int64_t ldk,
-                                     grf_stream_t stream) {
-    GRF_REQUIRE(n_cols > 0 && 0 <= row_begin && row_begin <= row_end && ptr && idx && val && row_shift &&
+                                     grf_stream_t stream, int64_t pad_cap = 0, const int32_t *pad_cnt = nullptr) {
+    GRF_REQUIRE(n_cols > 0 && 0 <= row_begin && row_begin <= row_end && (ptr || pad_cnt) && idx && val && row_shift &&
                     t_rows >= 0 && t_desc && t_rec && K && ldk >= t_rows,
                 GRF_EINVAL, "grf_gram_sparse_cols: bad arguments");
     GRF_REQUIRE(band_width >= 64 && band_width % 64 == 0 && band_width <= 8192, GRF_EUNSUPPORTED,
@@ -1210,7 +1233,8 @@ static int32_t gram_sparse_cols_impl(int64_t n_cols, int64_t row_begin, int64_t 
         GramTiles tl{r1 - r0, band_width, nb, sym, 0, (int32_t)n_cols};
         tl.t_rows = t_rows;
         return gram_tiles_launch(n_cols, r0, tl, 0, tl.total(), ptr, idx, val, t_desc, t_rec, rec_unit, row_shift,
-                                 K + (r0 - row_begin) * ldk, ldk, st, sym ? t_split : nullptr, nb * n_cols);
+                                 K + (r0 - row_begin) * ldk, ldk, st, sym ? t_split : nullptr, nb * n_cols, nullptr,
+                                 pad_cap, pad_cnt);
     };
     if (sym_row0 < 0) return launch(row_begin, row_end, false);
     // Phi_B = Phi[sym_row0, sym_row0 + t_rows): the square K[B, B] is symmetric and its bands start at
@@ -1231,6 +1255,15 @@ int32_t grf_gram_sparse_cols(int64_t n_cols, int64_t row_begin, int64_t row_end,
     (void)workspace_bytes;
     return gram_sparse_cols_impl(n_cols, row_begin, row_end, ptr, idx, val, row_shift, t_rows, sym_row0, band_width,
                                  rec_unit, t_desc, t_rec, t_split, K, ldk, stream);
+}
+
+int32_t grf_gram_sparse_cols_padded(int64_t n_cols, int64_t row_begin, int64_t row_end, int64_t cap,
+                                    const int32_t *cnt, const int32_t *idx, const float *val, const int32_t *row_shift,
+                                    int64_t t_rows, int64_t band_width, const uint32_t *t_desc, const void *t_rec,
+                                    float *K, int64_t ldk, grf_stream_t stream) {
+    GRF_REQUIRE(cap >= 1 && cnt, GRF_EINVAL, "grf_gram_sparse_cols_padded: bad padded rows");
+    return gram_sparse_cols_impl(n_cols, row_begin, row_end, nullptr, idx, val, row_shift, t_rows, -1, band_width,
+                                 GRF_REC_SLOT, t_desc, t_rec, nullptr, K, ldk, stream, cap, cnt);
 }
 
 int32_t grf_gram_sparse_kslice(int64_t n_total, int64_t row_begin, int64_t row_end, int64_t k_begin, int64_t k_end,

@@ -1267,6 +1267,22 @@ int32_t grf_phi_row_shifts_stats(int64_t n_rows, const void *stats, float *maxab
     return GRF_OK;
 }
 
+int32_t grf_phi_row_shifts_rows(int64_t n_rows, const float *row_max, const double *row_sum, float *maxabs,
+                                int32_t *row_shift, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && row_max && row_sum && maxabs && row_shift, GRF_EINVAL,
+                "grf_phi_row_shifts_rows: bad arguments");
+    hipStream_t st = S(stream);
+    GRF_CHECK_HIP(hipMemsetAsync(maxabs, 0, sizeof(float), st));
+    if (n_rows == 0) return GRF_OK;
+    tr_maxabs_kernel<<<1, 1024, 0, st>>>(n_rows, row_max, maxabs);  // (the max of the row maxima: exact)
+    GRF_CHECK_LAUNCH("tr_maxabs_kernel");
+    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 256), 256, "tr_rowshift_kernel");
+    tr_rowshift_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 256), 256, 0, st>>>(n_rows, row_max, row_sum, maxabs,
+                                                                            row_shift);
+    GRF_CHECK_LAUNCH("tr_rowshift_kernel");
+    return GRF_OK;
+}
+
 int32_t grf_phi_row_shifts(int64_t n_rows, const int64_t *ptr, const float *val, float *maxabs, int32_t *row_shift,
                            void *workspace, size_t workspace_bytes, grf_stream_t stream) {
     GRF_REQUIRE(n_rows >= 0 && ptr && val && maxabs && row_shift && workspace, GRF_EINVAL,

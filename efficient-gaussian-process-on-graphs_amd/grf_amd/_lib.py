@@ -26,7 +26,7 @@ RNG_PCG64, RNG_PHILOX = 0, 1
 LOAD_CUMULATIVE, LOAD_NONCUMULATIVE, LOAD_ABLATION = 0, 1, 2
 NORM_DIV, NORM_MUL_RECIP = 0, 1
 REC_LINE, REC_PACKED, REC_SLOT = 128, 12, 32
-ABI_VERSION = 7  # include/grf.h GRF_ABI_VERSION: argument lists change between revisions
+ABI_VERSION = 8  # include/grf.h GRF_ABI_VERSION: argument lists change between revisions
 
 
 class GrfWalkParams(ctypes.Structure):
@@ -65,6 +65,8 @@ SIGNATURES = {
     "grf_walk_aug_bytes": (_sz, [_i64]),
     "grf_walk_phi": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32, _i64,
                              _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
+    "grf_walk_phi_stats": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32,
+                                   _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
     "grf_phi_fused": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_scan_workspace_bytes": (_sz, [_i64]),
@@ -82,6 +84,9 @@ SIGNATURES = {
     "grf_phi_row_shifts_workspace_bytes": (_sz, [_i64]),
     "grf_phi_row_shifts": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_phi_row_shifts_stats": (_i32, [_i64, _vp, _vp, _vp, _vp]),
+    "grf_phi_row_shifts_rows": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp]),
+    "grf_gram_sparse_cols_padded": (_i32, [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64,
+                                           _vp]),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),
     "grf_gram_mirror": (_i32, [_i64, _vp, _i64, _i64, _vp]),
     "grf_gram_sparse_upper": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,

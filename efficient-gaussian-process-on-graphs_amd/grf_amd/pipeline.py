@@ -24,13 +24,19 @@ from typing import Callable, List, Optional, Tuple
 import numpy as np
 import torch
 
-from .engine import DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, SELF_COUNT_TRANSPOSE, DeviceCSR, GRFEngine, cols_band_width
+from . import _lib as C
+from .engine import (DEFAULT_BAND_WIDTH, ROWS_BAND_WIDTH, SELF_COUNT_TRANSPOSE, DeviceCSR, GRFEngine, PaddedRows,
+                     cols_band_width)
 
 # column blocks with sparse buckets take the GRF_REC_SLOT transpose (GRF_REC_SLOTS=0: packed pairs, A/B)
 SLOTS_DEFAULT = os.environ.get("GRF_REC_SLOTS", "1") == "1"
 # one GPU, column blocks: the compaction leaves the rows' Gram shift statistics (GRF_COMPACT_STATS=0: a
 # separate pass over Phi's values, A/B)
 COMPACT_STATS = os.environ.get("GRF_COMPACT_STATS", "1") == "1"
+# one GPU, column blocks (C5): Phi stays the walk's padded rows -- the column-block Gram and the row shifts read
+# them directly and only the block's own rows are compacted for its transpose (GRF_PADDED_PHI=0: the whole
+# compaction, A/B)
+PADDED_PHI = os.environ.get("GRF_PADDED_PHI", "1") == "1"
 # pipelined whole K with the hub-column split: the next front starts beside the hub panel's MFMA Gram,
 # not at the mirror (Enron 8.66-8.68 -> 8.13-8.23 ms per K, profiles/r03_hub_early_front_ab.txt;
 # GRF_HUB_EARLY_FRONT=0: at the mirror)
@@ -133,6 +139,31 @@ class Front:
     row_shift: Optional[torch.Tensor] = None  # "cols": every row's fixed-point shift
 
 
+class PaddedPhi:
+    """Phi as the walk's padded rows (``rows``: row r's entries at r * cap, no compaction), for the K assembly
+    of one GPU's column block; every other attribute is the compacted CSR's, built on first use (checks and
+    tests, outside the timed steps)."""
+
+    def __init__(self, eng: GRFEngine, rows: PaddedRows):
+        self.eng, self.rows, self._csr = eng, rows, None
+
+    @property
+    def csr(self) -> DeviceCSR:
+        if self._csr is None:
+            self._csr = self.eng.compact(self.rows, want64=False, want32=True)
+        return self._csr
+
+    def __getattr__(self, name):
+        if name in ("eng", "rows", "_csr"):
+            raise AttributeError(name)
+        return getattr(self.csr, name)
+
+
+def phi_csr(phi) -> DeviceCSR:
+    """A front's Phi as a CSR (compacting padded rows on first use)."""
+    return phi.csr if isinstance(phi, PaddedPhi) else phi
+
+
 def alloc_k(eng: GRFEngine, pl: StepPlan) -> torch.Tensor:
     """The resident K buffer of one step (reused across steps)."""
     if pl.mode == "cols":
@@ -150,6 +181,18 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
         # the transpose of the block's rows alone (no count all-reduce, a 1/N-size transpose); the
         # walk counts its buckets when the block is all of the rank's rows
         fused = pl.kr_end == e and not SELF_COUNT_TRANSPOSE
+        if PADDED_PHI and not pl.collective and b == 0 and not fused and not pl.cols_sym and SLOTS_DEFAULT:
+            # one GPU: Phi as padded rows with their Gram statistics from the walk (no compaction of all of
+            # Phi); the block's rows [0, block_rows) compacted for their transpose
+            rows = eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e, want64=False,
+                                stats=True)
+            head = PaddedRows(rows.cnt[:pl.block_rows], rows.idx, None, rows.val32, rows.cap, rows.n_cols)
+            blk = eng.compact(head, want64=False, want32=True, sync_free=True)
+            tr = eng.transpose_banded(blk, pl.band_width, nnz_bound=pl.block_rows * pl.rows_cap, slots=True)
+            # (the padded Gram reads slot buckets; denser blocks take line buckets and the compacted Phi)
+            phi = PaddedPhi(eng, rows) if tr.rec_unit == C.REC_SLOT else \
+                eng.compact(rows, want64=False, want32=True, sync_free=True)
+            return Front(phi, tr, phi, eng.phi_row_shifts(rows))
         tws = eng.transpose_workspace(pl.block_rows, n, pl.band_width) if fused else None
         local = eng.compact(eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e,
                                          count_ws=tws, band_width=pl.band_width if fused else 0, count_origin=b,
@@ -208,7 +251,8 @@ def k_assembly(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, *,
     from .dist import allreduce_buckets
 
     if pl.mode == "cols":
-        eng.gram_sparse_cols(fr.phi, fr.row_shift, fr.tr, out=K, sym_row0=pl.b if pl.cols_sym else None)
+        phi = fr.phi.rows if isinstance(fr.phi, PaddedPhi) else fr.phi
+        eng.gram_sparse_cols(phi, fr.row_shift, fr.tr, out=K, sym_row0=pl.b if pl.cols_sym else None)
     elif pl.mode == "allreduce":
         eng.gram_sparse_kslice(fr.phi, fr.tr, pl.b, pl.e, out=K)  # all rows, inner slice [b, e)
         allreduce_buckets(K[:, :pl.n], group=pl.group)
@@ -268,7 +312,7 @@ def k_block_check(eng: GRFEngine, fr: Front, pl: StepPlan, K: torch.Tensor, seed
         3e-5 |Phi_A| (|Phi_B|^T |u|) + 1e-12 max|Phi| max_i max_k |Phi_ik| sum|u| + 1e-7 |want|.
     Returns {"max_ratio": max |got - want| / bound (<= 1 passes), ...}.  Reads K once (chunked)."""
     n = pl.n
-    phi = fr.phi
+    phi = phi_csr(fr.phi)
     if pl.mode == "cols":
         A_rows, B_rows = None, torch.arange(pl.b, pl.kr_end, device=eng.device)
         Kv = K[:, :pl.block_rows]                      # n x |B|

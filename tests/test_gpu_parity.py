@@ -1137,6 +1137,61 @@ def test_gram_cols_pipelined_bit_identical(eng, pipe):
             os.environ["GRF_GRAM_PIPE"] = old
 
 
+def test_gram_cols_padded_rows_bit_identical(eng):
+    """Phi as the walk's padded rows (grf_walk_phi_stats + grf_phi_row_shifts_rows + grf_gram_sparse_cols_padded:
+    one GPU's C5 block with no compaction of Phi) gives the compacted path's bits: the row statistics and shifts,
+    and K[r0:r1, B] for the same blocks as test_gram_cols_pipelined_bit_identical (rows past 64 per gather wave, a
+    ragged last band, a band width that is not a power of two, a row range); the padded rows themselves, compacted,
+    are the plain walk's Phi.  Then the pipeline's one-GPU column-block step both ways (GRF_PADDED_PHI)."""
+    import torch
+    from grf_amd import _lib as C
+    from grf_amd import pipeline as P
+    from grf_amd.engine import DeviceCSR
+    n = 30001
+    A = er_graph(n, 40, 7)
+    G = eng.laplacian(A)
+    m, L = 256, 6
+    f = [1.0, -0.5, 0.125, -0.02, 0.003, -0.0004]
+    rows = eng.walk_phi(G, m, 0.1, L, f, seed=3, want64=False, stats=True)
+    phi = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=3, want64=False), want64=False)
+    shift = eng.phi_row_shifts(phi)
+    shift_p = eng.phi_row_shifts(rows)
+    assert torch.equal(shift, shift_p)
+    cp = eng.compact(rows, want64=False)
+    assert torch.equal(cp.ptr, phi.ptr) and torch.equal(cp.idx[:phi.nnz], phi.idx[:phi.nnz])
+    assert torch.equal(cp.val32[:phi.nnz], phi.val32[:phi.nnz])
+    for b, e, bw, rr in ((0, 8192, 8192, None), (5000, 25000, 8192, None), (101, 6101, 6016, None),
+                         (2000, 10190, 8192, (333, 29001)), (7, 8194, 8192, None)):
+        loc = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=3, src_begin=b, src_end=e, want64=False), want64=False)
+        ts = eng.transpose_banded(loc, bw, rec_unit=C.REC_SLOT)
+        r0, r1 = rr or (0, n)
+        K0 = eng.gram_sparse_cols(phi, shift, ts, r0, r1).clone()
+        K1 = eng.gram_sparse_cols(rows, shift_p, ts, r0, r1)
+        assert torch.equal(K0, K1), (b, e, bw, rr)
+    # the pipeline's step (plan_step cols mode, one GPU: C5's shape at 600k nodes, slot buckets) with and
+    # without the padded front
+    from grf_amd.graphs import powerlaw_graph
+    A2 = powerlaw_graph(600_000, 10.0, 2.5, seed=1)
+    pl = P.plan_step(600_000, 64, 8, 0.1, np.array([1.0, -0.5, 0.125, -0.02, 0.003, -0.0004, 1e-5, -1e-6]),
+                     k_rows=8192)
+    assert pl.mode == "cols"
+    Ad = DeviceCSR.from_scipy(A2, eng.device)
+    old = P.PADDED_PHI
+    try:
+        P.PADDED_PHI = False
+        Ka, fra = P.kernel_step(eng, Ad, pl)
+        Ka = Ka.clone()
+        P.PADDED_PHI = True
+        Kb, frb = P.kernel_step(eng, Ad, pl)
+        assert isinstance(frb.phi, P.PaddedPhi) and not isinstance(fra.phi, P.PaddedPhi)
+        assert torch.equal(P.k_view(Ka, pl), P.k_view(Kb, pl))
+        assert torch.equal(fra.row_shift, frb.row_shift)
+        assert torch.equal(fra.phi.ptr, frb.phi.ptr)
+        assert P.k_block_check(eng, frb, pl, Kb)["max_ratio"] <= 1.0
+    finally:
+        P.PADDED_PHI = old
+
+
 @pytest.mark.parametrize("unit", [128, 12])
 def test_transpose_wide_regions(eng, unit):
     """A graph large enough that the staged fill widens its column regions (n_rows * n_cols / (16 cr)
