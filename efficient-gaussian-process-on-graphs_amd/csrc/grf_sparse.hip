@@ -461,15 +461,18 @@ __global__ __launch_bounds__(1024) void tr_maxabs_kernel(int64_t n, const float 
 // Per-row max / sum of |values| over a whole CSR (one wave per row, the loop order of the
 // transpose's binning kernel) and each workgroup's max: the Gram row shifts of rows that are not
 // in the transpose (the column-block Gram of the multi-GPU path).
+// (cap > 0: padded rows instead -- row r's cnt[r] entries at r cap, ptr unused; the same sums)
 __global__ __launch_bounds__(256) void phi_row_stats_kernel(int64_t n_rows, const int64_t *ptr, const float *val,
-                                                            float *wg_max, float *row_max, double *row_sum) {
+                                                            float *wg_max, float *row_max, double *row_sum,
+                                                            int64_t cap = 0, const int32_t *cnt = nullptr) {
     __shared__ float red[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t r = (int64_t)blockIdx.x * 4 + wave;
     float mx = 0.f;
     if (r < n_rows) {
         double sm = 0.0;
-        for (int64_t e = ptr[r] + lane; e < ptr[r + 1]; e += 64) {
+        const int64_t e0 = cap > 0 ? r * cap : ptr[r], e1 = cap > 0 ? r * cap + cnt[r] : ptr[r + 1];
+        for (int64_t e = e0 + lane; e < e1; e += 64) {
             const float a = fabsf(val[e]);
             mx = fmaxf(mx, a);
             sm += (double)a;
@@ -1267,16 +1270,24 @@ int32_t grf_phi_row_shifts_stats(int64_t n_rows, const void *stats, float *maxab
     return GRF_OK;
 }
 
-int32_t grf_phi_row_shifts_rows(int64_t n_rows, const float *row_max, const double *row_sum, float *maxabs,
-                                int32_t *row_shift, grf_stream_t stream) {
-    GRF_REQUIRE(n_rows >= 0 && row_max && row_sum && maxabs && row_shift, GRF_EINVAL,
-                "grf_phi_row_shifts_rows: bad arguments");
+int32_t grf_phi_row_shifts_padded(int64_t n_rows, int64_t cap, const int32_t *cnt, const float *val, float *maxabs,
+                                  int32_t *row_shift, void *workspace, size_t workspace_bytes, grf_stream_t stream) {
+    GRF_REQUIRE(n_rows >= 0 && cap >= 1 && cnt && val && maxabs && row_shift && workspace, GRF_EINVAL,
+                "grf_phi_row_shifts_padded: bad arguments");
+    GRF_REQUIRE(workspace_bytes >= grf_phi_row_shifts_workspace_bytes(n_rows), GRF_EINVAL,
+                "grf_phi_row_shifts_padded: workspace too small");
     hipStream_t st = S(stream);
     GRF_CHECK_HIP(hipMemsetAsync(maxabs, 0, sizeof(float), st));
     if (n_rows == 0) return GRF_OK;
-    tr_maxabs_kernel<<<1, 1024, 0, st>>>(n_rows, row_max, maxabs);  // (the max of the row maxima: exact)
+    float *row_max, *wg_max;
+    double *row_sum;
+    row_stats_layout(workspace, n_rows, row_max, row_sum, wg_max);
+    const int64_t nwg = cdiv<int64_t>(n_rows, 4);
+    GRF_REQUIRE_GRID(nwg, 256, "phi_row_stats_kernel");
+    phi_row_stats_kernel<<<(unsigned)nwg, 256, 0, st>>>(n_rows, nullptr, val, wg_max, row_max, row_sum, cap, cnt);
+    GRF_CHECK_LAUNCH("phi_row_stats_kernel");
+    tr_maxabs_kernel<<<1, 1024, 0, st>>>(nwg, wg_max, maxabs);
     GRF_CHECK_LAUNCH("tr_maxabs_kernel");
-    GRF_REQUIRE_GRID(cdiv<int64_t>(n_rows, 256), 256, "tr_rowshift_kernel");
     tr_rowshift_kernel<<<(unsigned)cdiv<int64_t>(n_rows, 256), 256, 0, st>>>(n_rows, row_max, row_sum, maxabs,
                                                                             row_shift);
     GRF_CHECK_LAUNCH("tr_rowshift_kernel");

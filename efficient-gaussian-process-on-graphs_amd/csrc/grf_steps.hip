@@ -161,8 +161,7 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
                                                         int32_t *__restrict__ phi_cnt, int32_t *__restrict__ phi_idx,
                                                         double *__restrict__ phi_val, float *__restrict__ phi_val32,
                                                         int32_t *__restrict__ t_count, int64_t band_width,
-                                                        int64_t n_cols, int64_t count_row0, int32_t sort_lds,
-                                                        float *__restrict__ row_max, double *__restrict__ row_sum) {
+                                                        int64_t n_cols, int64_t count_row0, int32_t sort_lds) {
     // LDS: ld [E] loads by slot (later the compacted step values), fl [Lf] the modulator,
     // scratch (2 x 16 ints), key [P] the sorted keys (later the compacted step keys).  32-bit
     // keys when (node, step, walk) fits 32 bits (C4 / C5): half the sort's LDS traffic and a
@@ -342,7 +341,6 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
     }
     int32_t total;
     int32_t rank = block_exclusive_scan_fast<int32_t>(emit, scratch + 16, &total);
-    const int32_t rank_first = rank;
     const int64_t obase = s * cap;
 #pragma unroll
     for (int qq = 0; qq < kPer; ++qq) {
@@ -358,39 +356,6 @@ __global__ __launch_bounds__(256) void phi_fused_kernel(int64_t m, int32_t L, in
         }
     }
     if (tid == 0) phi_cnt[s] = total < cap ? total : (int32_t)cap;
-    if (row_max) {
-        // the row's Gram statistics as phi_row_stats_kernel takes them from the compacted row (entry e summed by
-        // lane e % 64 in increasing e, then wave_sum; the max of |value|): grf_phi_row_shifts' bits with no pass
-        // over the rows (|value| staged by position in the freed load array)
-        const int32_t kept = total < cap ? total : (int32_t)cap;
-        float *av = reinterpret_cast<float *>(ld);  // [kept <= E]
-        __syncthreads();
-        int32_t r = rank_first;
-#pragma unroll
-        for (int qq = 0; qq < kPer; ++qq) {
-            if (pn_[qq] >= 0) {
-                if (r < cap) av[r] = fabsf((float)pv_[qq]);
-                ++r;
-            }
-        }
-        __syncthreads();
-        if (tid < 64) {
-            float mx = 0.f;
-            double sm = 0.0;
-            for (int32_t e = tid; e < kept; e += 64) {
-                const float a = av[e];
-                mx = fmaxf(mx, a);
-                sm += (double)a;
-            }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-            sm = wave_sum<double>(sm);
-            if (tid == 0) {
-                row_max[s] = mx;
-                row_sum[s] = sm;
-            }
-        }
-    }
 }
 
 // ---------------------------------------------- augmented walk matrix (philox_walk_aug)
@@ -524,8 +489,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
                                 int32_t rule, uint64_t seed,
                                 int64_t src_begin, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
                                 int32_t *phi_idx, double *phi_val, float *phi_val32, int32_t *t_count,
-                                int64_t band_width, int64_t n_cols, hipStream_t st, int64_t count_row0 = 0,
-                                float *row_max = nullptr, double *row_sum = nullptr) {
+                                int64_t band_width, int64_t n_cols, hipStream_t st, int64_t count_row0 = 0) {
     GRF_REQUIRE(norm == GRF_NORM_DIV || norm == GRF_NORM_MUL_RECIP, GRF_EINVAL, "grf_phi_fused: bad norm");
     GRF_REQUIRE(n_f >= 0 && (n_f == 0 || f), GRF_EINVAL, "grf_phi_fused: bad modulator");
     GRF_REQUIRE(m * (int64_t)L <= 4096, GRF_EUNSUPPORTED, "grf_phi_fused: needs walks_per_node * L <= 4096");
@@ -569,7 +533,7 @@ static int32_t phi_fused_launch(bool walk, int64_t n_src, int64_t m, int32_t L, 
         m, L, norm, P, wbits, lbits, slot_node, slot_load, g_ptr, g_idx, g_val,                                   \
         reinterpret_cast<const unsigned char *>(g_aug), p_halt, rule, (uint32_t)seed,                               \
         (uint32_t)(seed >> 32), src_begin, f, Lf, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, t_count, band_width, \
-        n_cols, count_row0, sort_lds, row_max, row_sum)
+        n_cols, count_row0, sort_lds)
 #define GRF_PHI_LAUNCH_KT(W, K, KT) GRF_PHI_LAUNCH_KTT(W, K, KT, 0)
 #define GRF_PHI_LAUNCH(W, K)                                                                                      \
     do {                                                                                                          \
@@ -607,11 +571,11 @@ int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const i
                             n_f, phi_cap, phi_cnt, phi_idx, phi_val, phi_val32, nullptr, 1, 0, S(stream));
 }
 
-static int32_t walk_phi_impl(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
-                             const void *g_aug, const grf_walk_params *params, int64_t src_begin, int64_t src_end,
-                             int32_t norm, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
-                             int32_t *phi_idx, double *phi_val, float *phi_val32, int32_t *t_count, int64_t band_width,
-                             int64_t count_row0, float *row_max, double *row_sum, grf_stream_t stream) {
+int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
+                     const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
+                     int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
+                     float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
+                     grf_stream_t stream) {
     GRF_REQUIRE(params != nullptr, GRF_EINVAL, "grf_walk_phi: params is NULL");
     const grf_walk_params P = *params;
     GRF_REQUIRE(n >= 0 && g_ptr && phi_cnt && phi_idx && (phi_val || phi_val32), GRF_EINVAL,
@@ -632,28 +596,7 @@ static int32_t walk_phi_impl(int64_t n, const int64_t *g_ptr, const int32_t *g_i
     GRF_REQUIRE(!g_aug || ((uintptr_t)g_aug & 31) == 0, GRF_EINVAL, "grf_walk_phi: g_aug must be 32-byte aligned");
     return phi_fused_launch(true, src_end - src_begin, P.walks_per_node, P.max_walk_length, norm, nullptr, nullptr,
                             g_ptr, g_idx, g_val, g_aug, P.p_halt, P.load_rule, P.seed, src_begin, f, n_f, phi_cap, phi_cnt,
-                            phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream), count_row0, row_max,
-                            row_sum);
-}
-
-int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, const void *g_aug,
-                     const grf_walk_params *params, int64_t src_begin, int64_t src_end, int32_t norm, const double *f,
-                     int32_t n_f, int64_t phi_cap, int32_t *phi_cnt, int32_t *phi_idx, double *phi_val,
-                     float *phi_val32, int32_t *t_count, int64_t band_width, int64_t count_row0,
-                     grf_stream_t stream) {
-    return walk_phi_impl(n, g_ptr, g_idx, g_val, g_aug, params, src_begin, src_end, norm, f, n_f, phi_cap, phi_cnt,
-                         phi_idx, phi_val, phi_val32, t_count, band_width, count_row0, nullptr, nullptr, stream);
-}
-
-int32_t grf_walk_phi_stats(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
-                           const void *g_aug, const grf_walk_params *params, int64_t src_begin, int64_t src_end,
-                           int32_t norm, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
-                           int32_t *phi_idx, double *phi_val, float *phi_val32, int32_t *t_count, int64_t band_width,
-                           int64_t count_row0, float *row_max, double *row_sum, grf_stream_t stream) {
-    GRF_REQUIRE(row_max && row_sum && phi_val32, GRF_EINVAL,
-                "grf_walk_phi_stats: row_max, row_sum and phi_val32 are required");
-    return walk_phi_impl(n, g_ptr, g_idx, g_val, g_aug, params, src_begin, src_end, norm, f, n_f, phi_cap, phi_cnt,
-                         phi_idx, phi_val, phi_val32, t_count, band_width, count_row0, row_max, row_sum, stream);
+                            phi_idx, phi_val, phi_val32, t_count, band_width, n, S(stream), count_row0);
 }
 
 size_t grf_walk_aug_bytes(int64_t nnz) { return kAugHeader + (size_t)(nnz > 0 ? nnz : 0) * sizeof(AugRec); }

@@ -65,8 +65,6 @@ SIGNATURES = {
     "grf_walk_aug_bytes": (_sz, [_i64]),
     "grf_walk_phi": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32, _i64,
                              _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
-    "grf_walk_phi_stats": (_i32, [_i64, _vp, _vp, _vp, _vp, ctypes.POINTER(GrfWalkParams), _i64, _i64, _i32, _vp, _i32,
-                                   _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
     "grf_phi_fused": (_i32, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "grf_scan_counts": (_i32, [_i64, _vp, _vp, _vp, _sz, _vp]),
     "grf_scan_workspace_bytes": (_sz, [_i64]),
@@ -84,7 +82,7 @@ SIGNATURES = {
     "grf_phi_row_shifts_workspace_bytes": (_sz, [_i64]),
     "grf_phi_row_shifts": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_phi_row_shifts_stats": (_i32, [_i64, _vp, _vp, _vp, _vp]),
-    "grf_phi_row_shifts_rows": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp]),
+    "grf_phi_row_shifts_padded": (_i32, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "grf_gram_sparse_cols_padded": (_i32, [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64,
                                            _vp]),
     "grf_gram_sparse_sym": (_i32, [_i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp]),

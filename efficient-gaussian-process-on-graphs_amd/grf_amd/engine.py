@@ -157,8 +157,6 @@ class PaddedRows:
     val32: Optional[torch.Tensor]  # float32 [n_rows * cap]
     cap: int
     n_cols: int
-    row_max: Optional[torch.Tensor] = None  # float32 [n_rows]: the rows' Gram statistics (walk_phi(stats=True))
-    row_sum: Optional[torch.Tensor] = None  # float64 [n_rows]
 
     @property
     def n_rows(self):
@@ -374,14 +372,12 @@ class GRFEngine:
                  seed: int = 42, load_rule: int = C.LOAD_CUMULATIVE, norm: int = C.NORM_MUL_RECIP,
                  src_begin: int = 0, src_end: Optional[int] = None, want32: bool = True,
                  count_ws: Optional[torch.Tensor] = None, band_width: int = 0, use_aug: bool = True,
-                 count_origin: int = 0, want64: bool = True, stats: bool = False) -> PaddedRows:
+                 count_origin: int = 0, want64: bool = True) -> PaddedRows:
         """Philox walks straight to Phi rows (one kernel; identical to walk + features).
 
         count_ws: a zeroed transpose workspace (``transpose_workspace``) in which the kernel also
         counts the banded transpose's buckets, for ``transpose_banded(..., counted_ws=...)``;
-        count_origin: the transposed matrix's first row (0: all of Phi; src_begin: these rows alone).
-        stats: also every row's Gram statistics (grf_walk_phi_stats), for ``phi_row_shifts`` of the padded
-        rows with no compaction."""
+        count_origin: the transposed matrix's first row (0: all of Phi; src_begin: these rows alone)."""
         n = G.n_rows
         src_end = n if src_end is None else src_end
         m, L = int(walks_per_node), int(max_walk_length)
@@ -398,16 +394,6 @@ class GRFEngine:
         v32 = self._empty(ns * cap, torch.float32) if want32 else None
         prm = C.GrfWalkParams(m, float(p_halt), L, int(load_rule), C.RNG_PHILOX, 0, 1, int(seed) & 0xFFFFFFFFFFFFFFFF)
         aug = self.walk_aug(G) if use_aug else None
-        if stats:
-            if v32 is None:
-                raise ValueError("walk_phi: stats need want32")
-            rmax = self._empty(max(ns, 1), torch.float32)
-            rsum = self._empty(max(ns, 1), torch.float64)
-            C.check(self.lib.grf_walk_phi_stats(n, _p(G.ptr), _p(G.idx), _p(G.val), _p(aug), ctypes.byref(prm),
-                                                src_begin, src_end, norm, _p(ft), ft.numel(), cap, _p(cnt), _p(idx),
-                                                _p(val), _p(v32), _p(count_ws), int(band_width), int(count_origin),
-                                                _p(rmax), _p(rsum), self.stream), "grf_walk_phi_stats")
-            return PaddedRows(cnt, idx, val, v32, cap, n, rmax[:ns], rsum[:ns])
         C.check(self.lib.grf_walk_phi(n, _p(G.ptr), _p(G.idx), _p(G.val), _p(aug), ctypes.byref(prm), src_begin,
                                       src_end,
                                       norm, _p(ft), ft.numel(), cap, _p(cnt), _p(idx), _p(val), _p(v32),
@@ -651,11 +637,12 @@ class GRFEngine:
         n = phi.n_rows
         shift = self._empty(max(n, 1), torch.int32)
         mx = self._empty(1, torch.float32)
-        if isinstance(phi, PaddedRows):
-            if phi.row_max is None:
-                raise ValueError("phi_row_shifts: padded rows need walk_phi(stats=True)")
-            C.check(self.lib.grf_phi_row_shifts_rows(n, _p(phi.row_max), _p(phi.row_sum), _p(mx), _p(shift),
-                                                     self.stream), "grf_phi_row_shifts_rows")
+        if isinstance(phi, PaddedRows):  # (the walk's rows, not compacted: grf_phi_row_shifts_padded)
+            if phi.val32 is None:
+                raise ValueError("phi_row_shifts: padded rows need their float32 values")
+            ws = self._ws(self.lib.grf_phi_row_shifts_workspace_bytes(n))
+            C.check(self.lib.grf_phi_row_shifts_padded(n, phi.cap, _p(phi.cnt), _p(phi.val32), _p(mx), _p(shift),
+                                                       _p(ws), ws.numel(), self.stream), "grf_phi_row_shifts_padded")
             return shift
         st = getattr(phi, "row_stats", None)
         if st is not None:  # (left by compact(..., stats=True): same bits, no pass over the values)

@@ -182,10 +182,9 @@ def front(eng: GRFEngine, A_dev: DeviceCSR, pl: StepPlan) -> Front:
         # walk counts its buckets when the block is all of the rank's rows
         fused = pl.kr_end == e and not SELF_COUNT_TRANSPOSE
         if PADDED_PHI and not pl.collective and b == 0 and not fused and not pl.cols_sym and SLOTS_DEFAULT:
-            # one GPU: Phi as padded rows with their Gram statistics from the walk (no compaction of all of
-            # Phi); the block's rows [0, block_rows) compacted for their transpose
-            rows = eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e, want64=False,
-                                stats=True)
+            # one GPU: Phi stays the walk's padded rows (no compaction of all of Phi; the row shifts from one
+            # pass over them); the block's rows [0, block_rows) compacted for their transpose
+            rows = eng.walk_phi(G, pl.m, pl.p_halt, pl.L, pl.f, seed=pl.seed, src_begin=b, src_end=e, want64=False)
             head = PaddedRows(rows.cnt[:pl.block_rows], rows.idx, None, rows.val32, rows.cap, rows.n_cols)
             blk = eng.compact(head, want64=False, want32=True, sync_free=True)
             tr = eng.transpose_banded(blk, pl.band_width, nnz_bound=pl.block_rows * pl.rows_cap, slots=True)

@@ -70,7 +70,7 @@ enum grf_norm {
 
 /* The ABI revision of this header: grf_version() returns it, and a binding must refuse a library whose
  * revision differs (argument lists, or -- ABI 7 -- the GRF_RNG_PHILOX stream, change between revisions;
- * ABI 8 added grf_walk_phi_stats, grf_phi_row_shifts_rows and grf_gram_sparse_cols_padded). */
+ * ABI 8 added grf_phi_row_shifts_padded and grf_gram_sparse_cols_padded). */
 #define GRF_ABI_VERSION 8
 
 const char *grf_last_error(void);
@@ -195,15 +195,6 @@ int32_t grf_walk_phi(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, cons
 int32_t grf_walk_aug(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val, void *g_aug,
                      grf_stream_t stream);
 size_t grf_walk_aug_bytes(int64_t nnz);
-/* grf_walk_phi plus the Gram row statistics of every row written (ABI 8): row_max[s] = max |value| and
- * row_sum[s] = the fp64 sum of |value| in grf_phi_row_shifts' order, for the row of source src_begin + s as
- * stored (float32 values, phi_val32 required) -- so grf_phi_row_shifts_rows gives the row shifts of the
- * padded rows bit for bit without compacting them. */
-int32_t grf_walk_phi_stats(int64_t n, const int64_t *g_ptr, const int32_t *g_idx, const double *g_val,
-                           const void *g_aug, const grf_walk_params *params, int64_t src_begin, int64_t src_end,
-                           int32_t norm, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
-                           int32_t *phi_idx, double *phi_val, float *phi_val32, int32_t *t_count, int64_t band_width,
-                           int64_t count_row0, float *row_max, double *row_sum, grf_stream_t stream);
 int32_t grf_phi_fused(int64_t n_src, int64_t m, int32_t L, int32_t norm, const int32_t *slot_node,
                       const double *slot_load, const double *f, int32_t n_f, int64_t phi_cap, int32_t *phi_cnt,
                       int32_t *phi_idx, double *phi_val, float *phi_val32, grf_stream_t stream);
@@ -393,9 +384,10 @@ int32_t grf_phi_row_shifts(int64_t n_rows, const int64_t *ptr, const float *val,
  * (one pass over the values fewer; identical bits). */
 int32_t grf_phi_row_shifts_stats(int64_t n_rows, const void *stats, float *maxabs, int32_t *row_shift,
                                  grf_stream_t stream);
-/* The same shifts from per-row statistics (grf_walk_phi_stats' row_max / row_sum; ABI 8). */
-int32_t grf_phi_row_shifts_rows(int64_t n_rows, const float *row_max, const double *row_sum, float *maxabs,
-                                int32_t *row_shift, grf_stream_t stream);
+/* The same shifts of padded rows (ABI 8): row r's cnt[r] entries at val[r * cap ...) (grf_walk_phi's output, not
+ * compacted); workspace as grf_phi_row_shifts'. */
+int32_t grf_phi_row_shifts_padded(int64_t n_rows, int64_t cap, const int32_t *cnt, const float *val, float *maxabs,
+                                  int32_t *row_shift, void *workspace, size_t workspace_bytes, grf_stream_t stream);
 /* grf_gram_sparse_cols from Phi as padded rows (ABI 8): row r's cnt[r] entries at idx / val [r * cap, ...) for
  * every row r < row_end (grf_walk_phi's output over sources [0, row_end), not compacted), Phi_B's transpose in
  * GRF_REC_SLOT buckets, no symmetric square; the pipelined column-block kernel (bit-identical to the CSR path

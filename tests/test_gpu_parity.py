@@ -1138,8 +1138,8 @@ def test_gram_cols_pipelined_bit_identical(eng, pipe):
 
 
 def test_gram_cols_padded_rows_bit_identical(eng):
-    """Phi as the walk's padded rows (grf_walk_phi_stats + grf_phi_row_shifts_rows + grf_gram_sparse_cols_padded:
-    one GPU's C5 block with no compaction of Phi) gives the compacted path's bits: the row statistics and shifts,
+    """Phi as the walk's padded rows (grf_phi_row_shifts_padded + grf_gram_sparse_cols_padded: one GPU's C5
+    block with no compaction of Phi) gives the compacted path's bits: the row shifts,
     and K[r0:r1, B] for the same blocks as test_gram_cols_pipelined_bit_identical (rows past 64 per gather wave, a
     ragged last band, a band width that is not a power of two, a row range); the padded rows themselves, compacted,
     are the plain walk's Phi.  Then the pipeline's one-GPU column-block step both ways (GRF_PADDED_PHI)."""
@@ -1152,7 +1152,7 @@ def test_gram_cols_padded_rows_bit_identical(eng):
     G = eng.laplacian(A)
     m, L = 256, 6
     f = [1.0, -0.5, 0.125, -0.02, 0.003, -0.0004]
-    rows = eng.walk_phi(G, m, 0.1, L, f, seed=3, want64=False, stats=True)
+    rows = eng.walk_phi(G, m, 0.1, L, f, seed=3, want64=False)
     phi = eng.compact(eng.walk_phi(G, m, 0.1, L, f, seed=3, want64=False), want64=False)
     shift = eng.phi_row_shifts(phi)
     shift_p = eng.phi_row_shifts(rows)
