@@ -472,10 +472,17 @@ __global__ __launch_bounds__(256) void phi_row_stats_kernel(int64_t n_rows, cons
     if (r < n_rows) {
         double sm = 0.0;
         const int64_t e0 = cap > 0 ? r * cap : ptr[r], e1 = cap > 0 ? r * cap + cnt[r] : ptr[r + 1];
-        for (int64_t e = e0 + lane; e < e1; e += 64) {
-            const float a = fabsf(val[e]);
-            mx = fmaxf(mx, a);
-            sm += (double)a;
+        for (int64_t e = e0 + lane; e < e1; e += 256) {  // (up to four loads in flight, summed in e order)
+            float a[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = e + 64 * q < e1 ? fabsf(val[e + 64 * q]) : 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (e + 64 * q < e1) {
+                    mx = fmaxf(mx, a[q]);
+                    sm += (double)a[q];
+                }
+            }
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
